@@ -1,0 +1,71 @@
+"""ctypes binding of ``libdino_ingest.so`` (the C ABI of ``include/dino_ingest.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).
+There is no fallback: if it is missing or a GPU is absent, every call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+from .params import DinoAugConfig, DinoLimits
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "libdino_ingest.so"
+
+DINO_OK = 0
+IMG_STATUS = {0: "ok", -1: "corrupt", -2: "truncated", -3: "bad-data", -4: "too-large",
+              1: "unsupported", 2: "multi-scan"}
+
+_lib = None
+
+
+class DinoError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library; raise loudly when it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise DinoError(f"{LIB_PATH} not found: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                        "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    vp, i32, i64, u64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
+    sig = {
+        "dino_abi_version": (i32, []),
+        "dino_last_error": (ctypes.c_char_p, []),
+        "dino_ctx_create": (i32, [ctypes.c_int, ctypes.POINTER(DinoLimits), ctypes.POINTER(vp)]),
+        "dino_ctx_destroy": (i32, [vp]),
+        "dino_decode": (i32, [vp, vp, vp, i32, vp, vp]),
+        "dino_copy_rgb": (i32, [vp, i32, vp, vp]),
+        "dino_sample_params": (i32, [vp, ctypes.POINTER(DinoAugConfig), u64, u64, vp, vp]),
+        "dino_augment": (i32, [vp, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(vp), vp]),
+        "dino_run_batch": (i32, [vp, vp, vp, i32, ctypes.POINTER(DinoAugConfig), u64, u64, vp,
+                                 ctypes.POINTER(vp), vp, vp]),
+        "dino_masks": (i32, [i32, i32, i32, i32, i32, dbl, dbl, i32, vp, vp, vp, vp]),
+        "dino_bf16_to_fp8": (i32, [vp, vp, i64, vp]),
+        "dino_debug_region": (i32, [vp, i32, i32, vp, i64, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != DINO_OK:
+        msg = load().dino_last_error().decode(errors="replace")
+        raise DinoError(f"{what} failed ({rc}): {msg}")
+
+
+def exported_symbols() -> list[str]:
+    return ["dino_abi_version", "dino_last_error", "dino_ctx_create", "dino_ctx_destroy", "dino_decode",
+            "dino_copy_rgb", "dino_sample_params", "dino_augment", "dino_run_batch", "dino_masks",
+            "dino_bf16_to_fp8", "dino_debug_region"]

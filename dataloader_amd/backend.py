@@ -1,0 +1,194 @@
+"""``MI355XBackend`` — drop-in peer of ``CPUBackend`` / ``DALIBackend``.
+
+Satisfies the structural ``BackendProtocol`` of reference
+``src/dino_loader/backends/protocol.py:18-69`` so that
+``DINODataLoader(..., backend=MI355XBackend())`` (reference loader.py:431-436)
+runs Stage 3 on the GPU.  Method-by-method:
+
+* ``name`` / ``supports_fp8`` / ``supports_gpu``     protocol.py:22-29
+* ``build_shard_cache``   -> in-process LRU (Stage 1 stays host-side; cpu.py:86-145)
+* ``build_pipeline``      -> :class:`MI355XAugPipeline` (dispatch as cpu.py:649-709;
+  DinoV2 multi-crop only — Eval/LeJEPA/User specs raise TypeError)
+* ``build_pipeline_iterator`` -> :class:`MI355XPipelineIterator` (cpu.py:711-722)
+* ``build_h2d_stream``    -> outputs are already device-resident: identity transfer
+  that orders the consumer stream after the producer (memory.py:131-165 semantics)
+* ``build_fp8_formatter`` -> HIP bf16->E4M3 cast (memory.py:168-214, scale 1)
+* ``init_distributed``    -> rank bookkeeping only (no collective on this path)
+"""
+
+from __future__ import annotations
+
+import contextlib
+import threading
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Any
+
+import torch
+
+from . import _lib
+from .pipeline import MI355XAugPipeline, MI355XPipelineIterator
+
+
+class InProcessShardCache:
+    """LRU of whole shard files in process memory (same contract as cpu.py:86-145)."""
+
+    def __init__(self, job_id: str = "mi355x", node_master: bool = True, max_gb: float = 1.0,
+                 prefetch_window: int = 4, timeout_s: float = 30.0, warn_threshold: float = 0.85) -> None:
+        self._max_bytes = int(max_gb * (1 << 30))
+        self._lru: OrderedDict[str, bytes] = OrderedDict()
+        self._total = 0
+        self._lock = threading.Lock()
+
+    def prefetch(self, shard_path: str) -> None:
+        """No-op (no async prefetch in-process)."""
+
+    def get(self, shard_path: str) -> bytes:
+        with self._lock:
+            if shard_path in self._lru:
+                self._lru.move_to_end(shard_path)
+                return self._lru[shard_path]
+        with open(shard_path, "rb") as f:
+            data = f.read()
+        with self._lock:
+            while self._lru and self._total + len(data) > self._max_bytes:
+                _, old = self._lru.popitem(last=False)
+                self._total -= len(old)
+            self._lru[shard_path] = data
+            self._total += len(data)
+        return data
+
+    @contextlib.contextmanager
+    def get_view(self, shard_path: str):
+        yield memoryview(self.get(shard_path))
+
+    @property
+    def utilisation(self) -> float:
+        if self._max_bytes == 0:
+            return 0.0
+        with self._lock:
+            return self._total / self._max_bytes
+
+
+class DeviceH2DStream:
+    """Stage-4 transfer for device-resident views: no copy, only stream ordering."""
+
+    def __init__(self, device: torch.device, topo: Any = None) -> None:
+        self._device = torch.device(device)
+
+    @contextlib.contextmanager
+    def transfer(self, batch: dict[str, list[torch.Tensor]]):
+        yield self.send(batch)
+
+    def send(self, batch: dict[str, list[torch.Tensor]]) -> dict[str, list[torch.Tensor]]:
+        return {k: [t if t.device == self._device else t.to(self._device, non_blocking=True) for t in v]
+                for k, v in batch.items()}
+
+    def wait(self) -> None:
+        """Views are produced on the current stream: nothing to wait for."""
+
+
+class HipFP8Formatter:
+    """bf16 -> float8_e4m3fn with scale 1 (TE ``cast_to_fp8`` semantics, memory.py:193-214)."""
+
+    def quantise(self, tensor: torch.Tensor) -> torch.Tensor:
+        assert tensor.dtype not in (torch.float8_e4m3fn, torch.float8_e5m2), "already FP8"
+        import ctypes
+
+        src = tensor.to(torch.bfloat16).contiguous()
+        out = torch.empty(src.shape, dtype=torch.float8_e4m3fn, device=src.device)
+        lib = _lib.load()
+        stream = ctypes.c_void_p(torch.cuda.current_stream(src.device).cuda_stream)
+        _lib.check(lib.dino_bf16_to_fp8(ctypes.c_void_p(src.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                        src.numel(), stream), "dino_bf16_to_fp8")
+        return out
+
+
+@dataclass
+class ClusterTopology:
+    label: str = "MI355X-xGMI"
+    gpus_per_node: int = 8
+    has_pcie: bool = True
+    has_infiniband: bool = False
+
+    @property
+    def is_nvl72(self) -> bool:
+        return False
+
+    @property
+    def is_grace_blackwell(self) -> bool:
+        return False
+
+
+@dataclass
+class DistribEnv:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    local_world_size: int = 1
+    topology: ClusterTopology | None = None
+
+    def __post_init__(self) -> None:
+        if self.topology is None:
+            self.topology = ClusterTopology()
+
+
+def _is_dinov2_spec(spec: Any) -> bool:
+    return type(spec).__name__ == "DinoV2AugSpec" and hasattr(spec, "aug_cfg")
+
+
+class MI355XBackend:
+    """Backend whose Stage 3 runs as HIP kernels on an MI355X (gfx950)."""
+
+    def __init__(self, max_image_dim: int = 8192, workspace_bytes: int = 0) -> None:
+        self._max_image_dim = max_image_dim
+        self._workspace_bytes = workspace_bytes
+
+    @property
+    def name(self) -> str:
+        return "mi355x"
+
+    @property
+    def supports_fp8(self) -> bool:
+        return True
+
+    @property
+    def supports_gpu(self) -> bool:
+        return True
+
+    def build_shard_cache(self, job_id: str = "mi355x", node_master: bool = True, max_gb: float = 1.0,
+                          prefetch_window: int = 4, timeout_s: float = 30.0, warn_threshold: float = 0.85,
+                          **kwargs: Any) -> InProcessShardCache:
+        return InProcessShardCache(job_id, node_master, max_gb, prefetch_window, timeout_s, warn_threshold)
+
+    def build_pipeline(self, source: Any, aug_spec: Any, pipeline_cfg: Any, specs: Any = None) -> MI355XAugPipeline:
+        if not _is_dinov2_spec(aug_spec):
+            raise TypeError(f"MI355XBackend: unsupported aug_spec type {type(aug_spec).__name__}.")
+        out = pipeline_cfg.output_dtype
+        if getattr(pipeline_cfg, "dali_fp8_output", False) or getattr(aug_spec, "fp8_output", False):
+            out = "fp8"
+        return MI355XAugPipeline(
+            source=source,
+            aug_cfg=aug_spec.aug_cfg,
+            batch_size=getattr(source, "_batch_size", 1),
+            resolution_src=getattr(source, "_resolution_src", None),
+            seed=pipeline_cfg.seed,
+            out_dtype=out,
+            device=pipeline_cfg.device_id,
+            max_image_dim=self._max_image_dim,
+            workspace_bytes=self._workspace_bytes,
+        )
+
+    def build_pipeline_iterator(self, pipeline: Any, aug_spec: Any, output_map: list[str],
+                                batch_size: int) -> MI355XPipelineIterator:
+        return MI355XPipelineIterator(pipeline, output_map, batch_size)
+
+    def build_h2d_stream(self, device: Any, topo: Any) -> DeviceH2DStream:
+        return DeviceH2DStream(device, topo)
+
+    def build_fp8_formatter(self) -> HipFP8Formatter:
+        return HipFP8Formatter()
+
+    def init_distributed(self, rank: int = 0, world_size: int = 1, local_rank: int = 0, local_world_size: int = 1,
+                         force_topology: str | None = None) -> DistribEnv:
+        return DistribEnv(rank, world_size, local_rank, local_world_size)

@@ -1,0 +1,144 @@
+"""Configuration objects the hot path reads, mirroring the reference's API.
+
+Field names, defaults and meaning follow reference ``src/dino_loader/config.py``
+(``NormStats`` :32-98, ``PipelineConfig`` :146-208, ``DINOAugConfig`` :216-313)
+and ``augmentation.py`` (``DinoV2AugSpec`` :245-286), so objects built for the
+reference loader can be handed to :class:`~dataloader_amd.backend.MI355XBackend`
+unchanged (the backend only duck-types the attributes below).
+"""
+
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+from typing import Any
+
+import numpy as np
+
+
+@dataclass(frozen=True)
+class NormStats:
+    mean: tuple = (0.485, 0.456, 0.406)
+    std: tuple = (0.229, 0.224, 0.225)
+
+    def __post_init__(self):
+        if any(s <= 0.0 for s in self.std):
+            raise ValueError(f"NormStats.std must be strictly positive, got {self.std}.")
+
+
+@dataclass(frozen=True)
+class PipelineConfig:
+    num_threads: int = 8
+    device_id: int = 0
+    hw_decoder_load: float = 0.90
+    cpu_queue: int = 16
+    gpu_queue: int = 6
+    seed: int = 0
+    fuse_normalization: bool = True
+    dali_fp8_output: bool = False
+    output_dtype: str = "bf16"
+
+
+@dataclass
+class DINOAugConfig:
+    global_crop_size: int = 224
+    local_crop_size: int = 96
+    n_global_crops: int = 2
+    n_local_crops: int = 8
+    global_crops_scale: tuple = (0.32, 1.0)
+    local_crops_scale: tuple = (0.05, 0.32)
+    blur_prob_global1: float = 1.0
+    blur_prob_global2: float = 0.1
+    blur_prob_local: float = 0.5
+    solarize_prob: float = 0.2
+    color_jitter_prob: float = 0.8
+    grayscale_prob: float = 0.2
+    blur_sigma_min: float = 0.1
+    blur_sigma_max: float = 2.0
+    brightness: float = 0.8
+    contrast: float = 0.8
+    saturation: float = 0.8
+    hue: float = 0.2
+    flip_prob: float = 0.5
+    preserve_aspect_ratio: bool = True
+    resolution_schedule: list = field(default_factory=list)
+    max_global_crop_size: int = 0
+    max_local_crop_size: int = 0
+    mean: tuple = (0.485, 0.456, 0.406)
+    std: tuple = (0.229, 0.224, 0.225)
+
+    def __post_init__(self):
+        if self.max_global_crop_size == 0:
+            self.max_global_crop_size = self.global_crop_size
+        if self.max_local_crop_size == 0:
+            self.max_local_crop_size = self.local_crop_size
+        if self.resolution_schedule:
+            self.resolution_schedule = sorted(self.resolution_schedule, key=lambda x: x[0])
+            if any(e < 0 for e, _ in self.resolution_schedule):
+                raise ValueError("DINOAugConfig: resolution_schedule epochs must be >= 0")
+
+    @property
+    def n_views(self) -> int:
+        return self.n_global_crops + self.n_local_crops
+
+    @property
+    def norm_stats(self) -> NormStats:
+        return NormStats(mean=self.mean, std=self.std)
+
+    def crop_size_at_epoch(self, epoch: int) -> int:
+        size = self.global_crop_size
+        for e, s in self.resolution_schedule:
+            if epoch >= e:
+                size = s
+        return size
+
+
+@dataclass
+class DinoV2AugSpec:
+    aug_cfg: DINOAugConfig = field(default_factory=DINOAugConfig)
+    fuse_normalization: bool = True
+    fp8_output: bool = False
+
+    @property
+    def output_map(self) -> list[str]:
+        return [f"view_{i}" for i in range(self.aug_cfg.n_views)]
+
+    @property
+    def norm_stats(self) -> NormStats:
+        return self.aug_cfg.norm_stats
+
+    @property
+    def initial_global_size(self) -> int:
+        return self.aug_cfg.global_crop_size
+
+    @property
+    def initial_local_size(self) -> int:
+        return self.aug_cfg.local_crop_size
+
+    @property
+    def supports_masking(self) -> bool:
+        return True
+
+    @property
+    def n_views(self) -> int:
+        return self.aug_cfg.n_views
+
+    def split_views(self, views: list[Any]) -> tuple[list[Any], list[Any]]:
+        n = self.aug_cfg.n_global_crops
+        return views[:n], views[n:]
+
+
+class ResolutionSource:
+    """Thread-safe (global, local) crop size holder (reference sources/resolution.py:23-71)."""
+
+    def __init__(self, global_size: int, local_size: int) -> None:
+        self._g, self._l = global_size, local_size
+        self._lock = threading.Lock()
+
+    def set(self, global_size: int, local_size: int) -> None:
+        with self._lock:
+            self._g, self._l = global_size, local_size
+
+    def __call__(self):
+        with self._lock:
+            return np.array(self._g, dtype=np.int32), np.array(self._l, dtype=np.int32)

@@ -1,0 +1,224 @@
+// capi.hip — the C ABI declared in include/dino_ingest.h.
+//
+// A dino_ctx owns the device-side descriptors and two workspaces sized once
+// from dino_limits (the pre-allocation ceilings of reference config.py:236-237):
+// the decode workspace (destuffed entropy bytes, DCT coefficients, component
+// planes, RGB images) and the augment workspace (horizontal-pass rows and
+// resize coefficient tables).  Nothing is allocated per call and no call
+// blocks the host: every entry point only enqueues work on the given stream.
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "kernels.hpp"
+
+using namespace dino;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), fmt, a, b);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s: %s", where, hipGetErrorString(e));
+  g_err = buf;
+  return DINO_EHIP;
+}
+}  // namespace
+
+struct dino_ctx {
+  int device = 0;
+  dino_limits lim{};
+  ImgDesc* d_desc = nullptr;
+  uint8_t* d_ws = nullptr;
+  int64_t ws_size = 0;
+  uint8_t* d_aws = nullptr;
+  int64_t aws_size = 0;
+  ViewPlan* d_plan = nullptr;
+  dino_view_params* d_params = nullptr;
+  uint8_t* d_gcrop = nullptr;
+  void** d_view_ptrs = nullptr;
+  int32_t last_batch = -1;
+};
+
+extern "C" {
+
+int dino_abi_version(void) { return DINO_ABI_VERSION; }
+
+const char* dino_last_error(void) { return g_err.c_str(); }
+
+int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
+  if (!out || !limits) return fail(DINO_EINVAL, "dino_ctx_create: null argument%s%lld");
+  *out = nullptr;
+  dino_limits L = *limits;
+  if (L.max_batch <= 0 || L.max_views <= 0 || L.max_crop_size <= 0)
+    return fail(DINO_EINVAL, "dino_ctx_create: max_batch/max_views/max_crop_size must be > 0%s%lld");
+  if (L.max_image_dim <= 0) L.max_image_dim = 8192;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  dino_ctx* c = new dino_ctx();
+  c->device = device;
+  c->lim = L;
+  // decode workspace: default 16 MiB per image of the batch (a 1600x2133 JPEG needs ~26 MiB,
+  // a 640x480 one ~2.4 MiB; images that do not fit are reported DINO_IMG_TOO_LARGE)
+  c->ws_size = L.workspace_bytes > 0 ? L.workspace_bytes : (int64_t)L.max_batch * (16ll << 20);
+  c->aws_size = (int64_t)L.max_batch * L.max_views * ((int64_t)L.max_crop_size * 3 * 1024 + (256ll << 10));
+  const int64_t nrec = (int64_t)L.max_batch * L.max_views;
+  if ((e = hipMalloc(&c->d_desc, sizeof(ImgDesc) * L.max_batch)) != hipSuccess ||
+      (e = hipMalloc(&c->d_ws, c->ws_size)) != hipSuccess || (e = hipMalloc(&c->d_aws, c->aws_size)) != hipSuccess ||
+      (e = hipMalloc(&c->d_plan, sizeof(ViewPlan) * nrec)) != hipSuccess ||
+      (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess ||
+      (e = hipMalloc(&c->d_view_ptrs, sizeof(void*) * L.max_views)) != hipSuccess) {
+    dino_ctx_destroy(c);
+    return hip_fail(e, "dino_ctx_create: hipMalloc");
+  }
+  if (L.max_crop_size > kMaxLdsCropSize) {
+    int64_t gb = (int64_t)L.max_batch * L.max_views * 3 * L.max_crop_size * L.max_crop_size;
+    if ((e = hipMalloc(&c->d_gcrop, gb)) != hipSuccess) {
+      dino_ctx_destroy(c);
+      return hip_fail(e, "dino_ctx_create: hipMalloc(gcrop)");
+    }
+  }
+  *out = c;
+  return DINO_OK;
+}
+
+int dino_ctx_destroy(dino_ctx* c) {
+  if (!c) return DINO_OK;
+  (void)hipFree(c->d_desc);
+  (void)hipFree(c->d_ws);
+  (void)hipFree(c->d_aws);
+  (void)hipFree(c->d_plan);
+  (void)hipFree(c->d_params);
+  (void)hipFree(c->d_gcrop);
+  (void)hipFree(c->d_view_ptrs);
+  delete c;
+  return DINO_OK;
+}
+
+int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch, int32_t* d_info,
+                void* stream) {
+  if (!c || !d_bytes || !d_offsets) return fail(DINO_EINVAL, "dino_decode: null argument%s%lld");
+  if (batch < 0 || batch > c->lim.max_batch)
+    return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
+  hipStream_t s = (hipStream_t)stream;
+  DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size};
+  hipError_t e = launch_decode(a, s);
+  if (e != hipSuccess) return hip_fail(e, "dino_decode");
+  if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
+  c->last_batch = batch;
+  return DINO_OK;
+}
+
+int dino_copy_rgb(dino_ctx* c, int32_t index, uint8_t* d_rgb, void* stream) {
+  if (!c || !d_rgb || index < 0 || index >= c->last_batch) return fail(DINO_EINVAL, "dino_copy_rgb: bad index%s%lld");
+  hipError_t e = launch_copy_rgb(c->d_desc, index, c->d_ws, d_rgb, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_copy_rgb");
+}
+
+static int check_cfg(const dino_ctx* c, const dino_aug_config* cfg) {
+  if (!cfg) return fail(DINO_EINVAL, "null dino_aug_config%s%lld");
+  const int nv = cfg->n_global + cfg->n_local;
+  if (cfg->n_global < 0 || cfg->n_local < 0 || nv <= 0 || nv > c->lim.max_views)
+    return fail(DINO_EINVAL, "view count %s%lld outside [1, max_views]", "", nv);
+  if (cfg->global_size <= 4 || cfg->local_size <= 4 || cfg->global_size > c->lim.max_crop_size ||
+      cfg->local_size > c->lim.max_crop_size)
+    return fail(DINO_EINVAL, "crop size outside (4, max_crop_size]%s%lld");
+  if (cfg->out_dtype < DINO_OUT_BF16 || cfg->out_dtype > DINO_OUT_FP8_E4M3)
+    return fail(DINO_EINVAL, "unknown out_dtype %s%lld", "", cfg->out_dtype);
+  return DINO_OK;
+}
+
+int dino_sample_params(dino_ctx* c, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
+                       dino_view_params* d_params, void* stream) {
+  if (!c || !d_params) return fail(DINO_EINVAL, "dino_sample_params: null argument%s%lld");
+  if (c->last_batch < 0) return fail(DINO_EINVAL, "dino_sample_params: no decoded batch%s%lld");
+  int r = check_cfg(c, cfg);
+  if (r) return r;
+  hipError_t e = launch_params(c->d_desc, c->last_batch, *cfg, seed, batch_index, d_params, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_sample_params");
+}
+
+int dino_augment(dino_ctx* c, const dino_aug_config* cfg, const dino_view_params* d_params, void* const* d_views,
+                 void* stream) {
+  if (!c || !d_params || !d_views) return fail(DINO_EINVAL, "dino_augment: null argument%s%lld");
+  if (c->last_batch < 0) return fail(DINO_EINVAL, "dino_augment: no decoded batch%s%lld");
+  int r = check_cfg(c, cfg);
+  if (r) return r;
+  const int nv = cfg->n_global + cfg->n_local;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = hipMemcpyAsync(c->d_view_ptrs, d_views, sizeof(void*) * nv, hipMemcpyHostToDevice, s);
+  if (e != hipSuccess) return hip_fail(e, "dino_augment(view ptrs)");
+  AugmentArgs a{c->d_desc, c->last_batch, d_params, c->d_plan, c->d_ws, c->d_aws, c->aws_size, c->d_gcrop,
+                (void* const*)c->d_view_ptrs, *cfg};
+  e = launch_augment(a, s);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_augment");
+}
+
+int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,
+                   const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index, dino_view_params* d_params_out,
+                   void* const* d_views, int32_t* d_info, void* stream) {
+  if (!c) return fail(DINO_EINVAL, "dino_run_batch: null ctx%s%lld");
+  int r = check_cfg(c, cfg);
+  if (r) return r;
+  if ((r = dino_decode(c, d_bytes, d_offsets, batch, d_info, stream))) return r;
+  dino_view_params* prm = d_params_out ? d_params_out : c->d_params;
+  if ((r = dino_sample_params(c, cfg, seed, batch_index, prm, stream))) return r;
+  return dino_augment(c, cfg, prm, d_views, stream);
+}
+
+int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,
+               int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
+               uint32_t* d_py_state, uint32_t* d_np_state, uint8_t* d_out, void* stream) {
+  if (height <= 0 || width <= 0 || n_masks < 0 || !d_py_state || !d_np_state || (!d_out && n_masks))
+    return fail(DINO_EINVAL, "dino_masks: bad arguments%s%lld");
+  if (num_masking_patches < 0 || num_masking_patches > height * width)
+    return fail(DINO_EINVAL, "dino_masks: num_masking_patches %s%lld out of range", "", num_masking_patches);
+  if (n_masks == 0) return DINO_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, sizeof(int32_t) * height * width, s);
+  if (e != hipSuccess) return hip_fail(e, "dino_masks(scratch)");
+  e = launch_masks(height, width, num_masking_patches, min_num_patches, max_num_patches, log_aspect_min,
+                   log_aspect_max, n_masks, d_py_state, d_np_state, d_out, scratch, s);
+  (void)hipFreeAsync(scratch, s);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_masks");
+}
+
+int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream) {
+  if (!c || !d_dst || index < 0 || index >= c->last_batch) return fail(DINO_EINVAL, "dino_debug_region: bad args%s%lld");
+  hipStream_t s = (hipStream_t)stream;
+  ImgDesc d;
+  hipError_t e = hipMemcpyAsync(&d, c->d_desc + index, sizeof(ImgDesc), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "dino_debug_region");
+  const void* src = nullptr;
+  int64_t n = 0;
+  switch (region) {
+    case 0: src = c->d_desc + index; n = sizeof(ImgDesc); break;
+    case 1: src = c->d_ws + d.ent_off; n = d.ent_len; break;
+    case 2: src = c->d_ws + d.coef_off; n = d.coef_bytes; break;
+    case 3: src = c->d_ws + d.plane_off; n = d.rgb_off - d.plane_off; break;
+    case 4: src = c->d_ws + d.rgb_off; n = (int64_t)d.width * d.height * 3; break;
+    default: return fail(DINO_EINVAL, "dino_debug_region: region %s%lld", "", region);
+  }
+  if (d.status != 0 && region != 0) return fail(DINO_EINVAL, "dino_debug_region: image status %s%lld", "", d.status);
+  if (n > max_bytes) n = max_bytes;
+  e = hipMemcpyAsync(d_dst, src, n, hipMemcpyDeviceToDevice, s);
+  return e == hipSuccess ? (int)0 : hip_fail(e, "dino_debug_region");
+}
+
+int dino_bf16_to_fp8(const uint16_t* d_in, uint8_t* d_out, int64_t n, void* stream) {
+  if ((!d_in || !d_out) && n > 0) return fail(DINO_EINVAL, "dino_bf16_to_fp8: null argument%s%lld");
+  hipError_t e = launch_bf16_to_fp8(d_in, d_out, n, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_bf16_to_fp8");
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// common.hpp — internal types shared by the host+device code of the ingest path.
+//
+// Every function in the *.hpp files of this directory is __host__ __device__:
+// the HIP kernels (kernels.hip) call them per lane, and the test-only host
+// emulator (tests/emu/emu.cpp) calls the very same code to check it against
+// Pillow on the CPU.  Arithmetic that must match Pillow/libjpeg bit for bit is
+// written without FMA contraction (the library is built with -ffp-contract=off).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dino_ingest.h"
+
+#define DHD __host__ __device__ __forceinline__
+
+namespace dino {
+
+constexpr int kMaxComp = 3;
+constexpr int kMaxBlocksPerMcu = 10;   // libjpeg D_MAX_BLOCKS_IN_MCU
+constexpr int kLookBits = 9;           // Huffman lookahead table bits
+
+enum ColorSpace : int32_t { kGray = 0, kYCbCr = 1, kRGB = 2 };
+
+struct CompDesc {
+  int32_t id, h, v, tq, td, ta;
+  int32_t bw, bh;        // coefficient block grid actually coded (incl. MCU padding)
+  int32_t dw, dh;        // libjpeg downsampled_width / downsampled_height
+  int64_t coef_off;      // byte offset of block (0,0) inside the image's coefficient area
+  int64_t plane_off;     // byte offset of the sample plane (pitch bw*8) inside the plane area
+};
+
+// Per-image descriptor written by k_parse / k_plan, read by every later stage.
+struct ImgDesc {
+  int32_t status;
+  int32_t width, height, ncomp, color;
+  int32_t max_h, max_v;
+  int32_t mcus_x, mcus_y, blocks_per_mcu;
+  int32_t restart_interval;
+  int32_t scan_off;        // entropy-coded data start, relative to the image's first byte
+  int32_t scan_len;        // raw bytes from scan_off to the end of the image buffer
+  int32_t n_rst_max;       // restart markers expected for a well-formed stream
+  int32_t huff_off[8];     // DC 0-3, AC 0-3: offset of the 16 BITS bytes (HUFFVAL follows), -1 absent
+  uint8_t mcu_comp[kMaxBlocksPerMcu];
+  uint8_t mcu_bx[kMaxBlocksPerMcu];
+  uint8_t mcu_by[kMaxBlocksPerMcu];
+  uint8_t pad0[2];
+  uint16_t qt[4][64];      // quant tables, natural order
+  CompDesc comp[kMaxComp];
+  int32_t total_blocks;    // MCUs * blocks_per_mcu
+  // filled by k_plan (byte offsets into the ctx workspace)
+  int64_t base;            // start of this image's chunk
+  int64_t ent_off, rst_off, coef_off, plane_off, rgb_off, htmp_off, rcoef_off;
+  int64_t coef_bytes;
+  // filled by k_destuff
+  int32_t ent_len;         // destuffed entropy bytes
+  int32_t n_rst;           // RST markers found
+  int32_t terminated;      // a terminating marker (EOI/other) was found
+  int32_t pad1;
+};
+
+// Bytes of resize-coefficient scratch reserved per view: bounds + int32 taps, both axes.
+DHD int64_t rcoef_stride_bytes(int out_size, int max_dim) {
+  // ksize = 2*ceil(support*scale)+1 with support 2 and scale <= max_dim/out
+  int k = 2 * ((2 * max_dim + out_size - 1) / out_size) + 3;
+  return (int64_t)2 * out_size * (k + 2) * 4;
+}
+
+DHD int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace dino

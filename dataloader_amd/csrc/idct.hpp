@@ -1,0 +1,194 @@
+// idct.hpp — libjpeg-turbo jidctint.c jpeg_idct_islow (CONST_BITS 13,
+// PASS1_BITS 2) with libjpeg's post-IDCT range-limit table semantics.  This is
+// the DCT method Pillow's decoder uses (default JDCT_ISLOW); the SIMD versions
+// in libjpeg-turbo are bit-exact with this C formulation.
+#pragma once
+
+#include "common.hpp"
+
+namespace dino {
+
+constexpr int kConstBits = 13;
+constexpr int kPass1Bits = 2;
+constexpr int32_t F0_298 = 2446, F0_390 = 3196, F0_541 = 4433, F0_765 = 6270, F0_899 = 7373,
+                  F1_175 = 9633, F1_501 = 12299, F1_847 = 15137, F1_961 = 16069, F2_053 = 16819,
+                  F2_562 = 20995, F3_072 = 25172;
+
+template <typename T>
+DHD int32_t descale(T x, int n) { return (int32_t)((x + ((T)1 << (n - 1))) >> n); }
+
+// IDCT_range_limit(cinfo)[x & RANGE_MASK] for 8-bit samples (jdmaster.c prepare_range_limit_table).
+DHD uint8_t range_limit_idct(int32_t x) {
+  int32_t i = x & 1023;
+  if (i < 128) return (uint8_t)(i + 128);
+  if (i < 512) return 255;
+  if (i < 896) return 0;
+  return (uint8_t)(i - 896);
+}
+
+// One 1-D pass of the islow butterfly on 8 inputs.  d0..d7 are the (dequantized
+// in pass 1) coefficients of one column/row; writes 8 results before descale.
+// T = int64_t reproduces libjpeg's JLONG arithmetic for any input; T = int32_t is
+// exact whenever every input magnitude is <= kIslow32Bound (worst-case sum of the
+// butterfly's constants is 178219, and 178219 * 11000 + 2^17 < 2^31).
+constexpr int32_t kIslow32Bound = 11000;
+
+template <typename T>
+struct Islow8 {
+  T t10, t11, t12, t13, t0, t1, t2, t3;
+};
+
+template <typename T>
+DHD Islow8<T> islow_core(T d0, T d1, T d2, T d3, T d4, T d5, T d6, T d7) {
+  Islow8<T> r;
+  // even part
+  T z2 = d2, z3 = d6;
+  T z1 = (z2 + z3) * F0_541;
+  T tmp2 = z1 + z3 * (-F1_847);
+  T tmp3 = z1 + z2 * F0_765;
+  T tmp0 = (d0 + d4) * (1 << kConstBits);
+  T tmp1 = (d0 - d4) * (1 << kConstBits);
+  r.t10 = tmp0 + tmp3;
+  r.t13 = tmp0 - tmp3;
+  r.t11 = tmp1 + tmp2;
+  r.t12 = tmp1 - tmp2;
+  // odd part
+  tmp0 = d7;
+  tmp1 = d5;
+  tmp2 = d3;
+  tmp3 = d1;
+  z1 = tmp0 + tmp3;
+  z2 = tmp1 + tmp2;
+  z3 = tmp0 + tmp2;
+  T z4 = tmp1 + tmp3;
+  T z5 = (z3 + z4) * F1_175;
+  tmp0 = tmp0 * F0_298;
+  tmp1 = tmp1 * F2_053;
+  tmp2 = tmp2 * F3_072;
+  tmp3 = tmp3 * F1_501;
+  z1 = z1 * (-F0_899);
+  z2 = z2 * (-F2_562);
+  z3 = z3 * (-F1_961);
+  z4 = z4 * (-F0_390);
+  z3 += z5;
+  z4 += z5;
+  r.t0 = tmp0 + z1 + z3;
+  r.t1 = tmp1 + z2 + z4;
+  r.t2 = tmp2 + z2 + z3;
+  r.t3 = tmp3 + z1 + z4;
+  return r;
+}
+
+// coef: 64 quantized coefficients (natural order, int16); q: quant table (natural
+// order, read as ISLOW_MULT_TYPE = short like jddctmgr.c).  out: 8x8 samples, row pitch `pitch`.
+template <typename T, typename OutT>
+DHD void idct_islow_t(const int16_t* coef, const uint16_t* q, OutT* out, int64_t pitch) {
+  int32_t ws[64];
+  for (int c = 0; c < 8; ++c) {
+    T d[8];
+    for (int r = 0; r < 8; ++r) d[r] = (T)((int32_t)coef[r * 8 + c] * (int32_t)(int16_t)q[r * 8 + c]);
+    Islow8<T> t = islow_core<T>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+    const int sh = kConstBits - kPass1Bits;
+    ws[0 * 8 + c] = descale(t.t10 + t.t3, sh);
+    ws[7 * 8 + c] = descale(t.t10 - t.t3, sh);
+    ws[1 * 8 + c] = descale(t.t11 + t.t2, sh);
+    ws[6 * 8 + c] = descale(t.t11 - t.t2, sh);
+    ws[2 * 8 + c] = descale(t.t12 + t.t1, sh);
+    ws[5 * 8 + c] = descale(t.t12 - t.t1, sh);
+    ws[3 * 8 + c] = descale(t.t13 + t.t0, sh);
+    ws[4 * 8 + c] = descale(t.t13 - t.t0, sh);
+  }
+  for (int r = 0; r < 8; ++r) {
+    const int32_t* w = ws + r * 8;
+    Islow8<T> t = islow_core<T>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+    const int sh = kConstBits + kPass1Bits + 3;
+    OutT* o = out + r * pitch;
+    o[0] = range_limit_idct(descale(t.t10 + t.t3, sh));
+    o[7] = range_limit_idct(descale(t.t10 - t.t3, sh));
+    o[1] = range_limit_idct(descale(t.t11 + t.t2, sh));
+    o[6] = range_limit_idct(descale(t.t11 - t.t2, sh));
+    o[2] = range_limit_idct(descale(t.t12 + t.t1, sh));
+    o[5] = range_limit_idct(descale(t.t12 - t.t1, sh));
+    o[3] = range_limit_idct(descale(t.t13 + t.t0, sh));
+    o[4] = range_limit_idct(descale(t.t13 - t.t0, sh));
+  }
+}
+
+// Exact for all inputs: 64-bit reference arithmetic.
+template <typename OutT>
+DHD void idct_islow(const int16_t* coef, const uint16_t* q, OutT* out, int64_t pitch) {
+  idct_islow_t<int64_t>(coef, q, out, pitch);
+}
+
+DHD int32_t iabs32(int32_t x) { return x < 0 ? -x : x; }
+
+// Same result as idct_islow; each pass runs in int32 when its inputs are within
+// kIslow32Bound (always, for valid 8-bit JPEG data) and in int64 otherwise.
+template <typename OutT>
+DHD void idct_islow_fast(const int16_t* coef, const uint16_t* q, OutT* out, int64_t pitch) {
+  int32_t d[64];
+  int32_t m = 0;
+  for (int i = 0; i < 64; ++i) {
+    d[i] = (int32_t)coef[i] * (int32_t)(int16_t)q[i];
+    int32_t a = iabs32(d[i]);
+    m = a > m ? a : m;
+  }
+  int32_t ws[64];
+  const int sh1 = kConstBits - kPass1Bits;
+  for (int c = 0; c < 8; ++c) {
+    if (m <= kIslow32Bound) {
+      Islow8<int32_t> t = islow_core<int32_t>(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c]);
+      ws[0 * 8 + c] = descale(t.t10 + t.t3, sh1);
+      ws[7 * 8 + c] = descale(t.t10 - t.t3, sh1);
+      ws[1 * 8 + c] = descale(t.t11 + t.t2, sh1);
+      ws[6 * 8 + c] = descale(t.t11 - t.t2, sh1);
+      ws[2 * 8 + c] = descale(t.t12 + t.t1, sh1);
+      ws[5 * 8 + c] = descale(t.t12 - t.t1, sh1);
+      ws[3 * 8 + c] = descale(t.t13 + t.t0, sh1);
+      ws[4 * 8 + c] = descale(t.t13 - t.t0, sh1);
+    } else {
+      Islow8<int64_t> t = islow_core<int64_t>(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c]);
+      ws[0 * 8 + c] = descale(t.t10 + t.t3, sh1);
+      ws[7 * 8 + c] = descale(t.t10 - t.t3, sh1);
+      ws[1 * 8 + c] = descale(t.t11 + t.t2, sh1);
+      ws[6 * 8 + c] = descale(t.t11 - t.t2, sh1);
+      ws[2 * 8 + c] = descale(t.t12 + t.t1, sh1);
+      ws[5 * 8 + c] = descale(t.t12 - t.t1, sh1);
+      ws[3 * 8 + c] = descale(t.t13 + t.t0, sh1);
+      ws[4 * 8 + c] = descale(t.t13 - t.t0, sh1);
+    }
+  }
+  int32_t m2 = 0;
+  for (int i = 0; i < 64; ++i) {
+    int32_t a = iabs32(ws[i]);
+    m2 = a > m2 ? a : m2;
+  }
+  const int sh2 = kConstBits + kPass1Bits + 3;
+  for (int r = 0; r < 8; ++r) {
+    const int32_t* w = ws + r * 8;
+    OutT* o = out + r * pitch;
+    if (m2 <= kIslow32Bound) {
+      Islow8<int32_t> t = islow_core<int32_t>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+      o[0] = range_limit_idct(descale(t.t10 + t.t3, sh2));
+      o[7] = range_limit_idct(descale(t.t10 - t.t3, sh2));
+      o[1] = range_limit_idct(descale(t.t11 + t.t2, sh2));
+      o[6] = range_limit_idct(descale(t.t11 - t.t2, sh2));
+      o[2] = range_limit_idct(descale(t.t12 + t.t1, sh2));
+      o[5] = range_limit_idct(descale(t.t12 - t.t1, sh2));
+      o[3] = range_limit_idct(descale(t.t13 + t.t0, sh2));
+      o[4] = range_limit_idct(descale(t.t13 - t.t0, sh2));
+    } else {
+      Islow8<int64_t> t = islow_core<int64_t>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+      o[0] = range_limit_idct(descale(t.t10 + t.t3, sh2));
+      o[7] = range_limit_idct(descale(t.t10 - t.t3, sh2));
+      o[1] = range_limit_idct(descale(t.t11 + t.t2, sh2));
+      o[6] = range_limit_idct(descale(t.t11 - t.t2, sh2));
+      o[2] = range_limit_idct(descale(t.t12 + t.t1, sh2));
+      o[5] = range_limit_idct(descale(t.t12 - t.t1, sh2));
+      o[3] = range_limit_idct(descale(t.t13 + t.t0, sh2));
+      o[4] = range_limit_idct(descale(t.t13 - t.t0, sh2));
+    }
+  }
+}
+
+}  // namespace dino

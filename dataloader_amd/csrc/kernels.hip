@@ -1,0 +1,805 @@
+// kernels.hip — the gfx950 kernels of the DINO Stage-3 ingest path.
+//
+// Decode half (one JPEG per workgroup where the work is serial per image):
+//   k_parse     1 lane / image      marker parse -> ImgDesc
+//   k_plan      1 workgroup         per-image workspace offsets (prefix sum), capacity check
+//   k_destuff   256 lanes / image   0xFF00 unstuffing + RSTn removal (block compaction)
+//   k_huffman   256 lanes / image   self-synchronising speculative Huffman decode
+//   k_idct      lanes over blocks   islow IDCT (int32 fast path, int64 exact fallback)
+//   k_color     lanes over pixels   fancy upsampling + YCbCr->RGB
+// Augment half (per view):
+//   k_params    1 lane / view       Philox draw of the view record (optional)
+//   k_vplan     1 workgroup         per-view scratch offsets
+//   k_rcoeffs   lanes over outputs  Pillow bicubic coefficient tables (both axes)
+//   k_hresize   lanes over pixels   horizontal pass (crop rows -> S columns, u8)
+//   k_augment   1 workgroup / view  vertical pass -> LDS planes -> jitter -> gray
+//                                   -> blur + solarize + normalize -> NCHW output
+// Plus k_masks (iBOT) and k_bf16_to_fp8 (Stage 5).
+#include "augment.hpp"
+#include "color.hpp"
+#include "huffman.hpp"
+#include "idct.hpp"
+#include "jpeg_parse.hpp"
+#include "kernels.hpp"
+#include "mask.hpp"
+#include "sampler.hpp"
+
+namespace dino {
+
+// ---------------------------------------------------------------------------
+// k_parse
+// ---------------------------------------------------------------------------
+__global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets, int B,
+                        int max_dim, ImgDesc* __restrict__ desc) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  int64_t off = offsets[i], len = offsets[i + 1] - off;
+  ImgDesc d;
+  if (len <= 0) {
+    d.status = DINO_IMG_CORRUPT;
+    d.width = d.height = d.ncomp = 0;
+  } else {
+    parse_jpeg(bytes + off, len, max_dim, &d);
+  }
+  desc[i] = d;
+}
+
+// ---------------------------------------------------------------------------
+// k_plan: exclusive scan of per-image chunk sizes (single workgroup of 1024)
+// ---------------------------------------------------------------------------
+__device__ int64_t image_chunk_bytes(const ImgDesc& d, int64_t* ent, int64_t* rst, int64_t* coef, int64_t* plane,
+                                     int64_t* rgb) {
+  if (d.status != DINO_IMG_OK) {
+    *ent = *rst = *coef = *plane = *rgb = 0;
+    return 0;
+  }
+  *ent = align16((int64_t)d.scan_len + 64);
+  *rst = align16(4 * ((int64_t)d.n_rst_max + 1));
+  *coef = align16(d.coef_bytes);
+  int64_t p = 0;
+  for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
+  *plane = align16(p);
+  *rgb = align16((int64_t)d.width * d.height * 3 + 16);
+  return *ent + *rst + *coef + *plane + *rgb;
+}
+
+__global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (B + 1023) / 1024;
+  int64_t local = 0;
+  for (int k = 0; k < per; ++k) {
+    int i = t * per + k;
+    if (i < B) {
+      int64_t a, b, c, d2, e;
+      local += image_chunk_bytes(desc[i], &a, &b, &c, &d2, &e);
+    }
+  }
+  part[t] = local;
+  __syncthreads();
+  for (int s = 1; s < 1024; s <<= 1) {  // Hillis-Steele inclusive scan
+    int64_t v = t >= s ? part[t - s] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t base = part[t] - local;
+  for (int k = 0; k < per; ++k) {
+    int i = t * per + k;
+    if (i >= B) continue;
+    ImgDesc& d = desc[i];
+    int64_t ent, rst, coef, plane, rgb;
+    int64_t sz = image_chunk_bytes(d, &ent, &rst, &coef, &plane, &rgb);
+    if (sz == 0) continue;
+    if (base + sz > ws_size) {
+      d.status = DINO_IMG_TOO_LARGE;
+    } else {
+      d.base = base;
+      d.ent_off = base;
+      d.rst_off = d.ent_off + ent;
+      d.coef_off = d.rst_off + rst;
+      d.plane_off = d.coef_off + coef;
+      d.rgb_off = d.plane_off + plane;
+    }
+    base += sz;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_destuff: one workgroup (256 lanes) per image
+// ---------------------------------------------------------------------------
+constexpr int kDestuffThreads = 256;
+
+__device__ __forceinline__ int classify_ff(const uint8_t* r, int n, int k) {
+  // for r[k] == 0xFF: 0 keep (FF00), 1 RST, 2 fill (FFFF), 3 terminating marker, 4 truncated (last byte)
+  if (k + 1 >= n) return 4;
+  int nx = r[k + 1];
+  if (nx == 0x00) return 0;
+  if (nx >= 0xD0 && nx <= 0xD7) return 1;
+  if (nx == 0xFF) return 2;
+  return 3;
+}
+
+__global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __restrict__ bytes,
+                                                             const int64_t* __restrict__ offsets,
+                                                             ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  __shared__ int s_end, s_term;
+  __shared__ int s_cnt[kDestuffThreads], s_rcnt[kDestuffThreads];
+  const int img = blockIdx.x, t = threadIdx.x;
+  ImgDesc* d = &desc[img];
+  if (d->status != DINO_IMG_OK) return;
+  const uint8_t* r = bytes + offsets[img] + d->scan_off;
+  const int n = d->scan_len;
+  uint8_t* out = ws + d->ent_off;
+  int32_t* rst = (int32_t*)(ws + d->rst_off);
+  const int chunk = (n + kDestuffThreads - 1) / kDestuffThreads;
+  const int k0 = t * chunk, k1 = min(n, k0 + chunk);
+  if (t == 0) {
+    s_end = n;
+    s_term = 0;
+  }
+  __syncthreads();
+  // pass 1: first terminating marker
+  for (int k = k0; k < k1; ++k) {
+    if (r[k] == 0xFF) {
+      int c = classify_ff(r, n, k);
+      if (c >= 3) {
+        atomicMin(&s_end, k);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  const int E = s_end;
+  if (t == 0) s_term = (E < n) && classify_ff(r, n, E) == 3;
+  // pass 2: counts
+  int cnt = 0, rc = 0;
+  const int e1 = min(k1, E);
+  for (int k = k0; k < e1; ++k) {
+    int v = r[k];
+    if (v == 0xFF) {
+      int c = classify_ff(r, n, k);
+      cnt += (c == 0);
+      rc += (c == 1);
+    } else if (!(k > 0 && r[k - 1] == 0xFF)) {
+      ++cnt;
+    }
+  }
+  s_cnt[t] = cnt;
+  s_rcnt[t] = rc;
+  __syncthreads();
+  for (int s = 1; s < kDestuffThreads; s <<= 1) {
+    int a = t >= s ? s_cnt[t - s] : 0, b = t >= s ? s_rcnt[t - s] : 0;
+    __syncthreads();
+    s_cnt[t] += a;
+    s_rcnt[t] += b;
+    __syncthreads();
+  }
+  int o = s_cnt[t] - cnt, ro = s_rcnt[t] - rc;
+  const int nrst_cap = d->n_rst_max + 1;
+  for (int k = k0; k < e1; ++k) {
+    int v = r[k];
+    if (v == 0xFF) {
+      int c = classify_ff(r, n, k);
+      if (c == 0) out[o++] = 0xFF;
+      else if (c == 1) {
+        if (ro < nrst_cap) rst[ro] = o;
+        ++ro;
+      }
+    } else if (!(k > 0 && r[k - 1] == 0xFF)) {
+      out[o++] = (uint8_t)v;
+    }
+  }
+  __syncthreads();
+  const int total = s_cnt[kDestuffThreads - 1];
+  // zero padding for word reads past the end
+  for (int k = total + t; k < total + 64 && k < n + 64; k += kDestuffThreads) out[k] = 0;
+  if (t == 0) {
+    d->ent_len = total;
+    d->n_rst = s_rcnt[kDestuffThreads - 1];
+    d->terminated = s_term;
+    if (!s_term) d->status = DINO_IMG_TRUNCATED;
+    else if (d->restart_interval > 0 && d->n_rst < d->n_rst_max - 1) d->status = DINO_IMG_BADDATA;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_huffman: one workgroup (256 lanes) per image
+// ---------------------------------------------------------------------------
+constexpr int kHuffThreads = 256;
+constexpr int kMinSubBits = 2048;
+constexpr int kBlkStride = 68;  // int16 per lane block buffer (136 B: 8-byte aligned, 2-way banks)
+
+struct HuffLds {
+  ImgDesc sd;
+  HuffTable tab[6];
+  HState S[kHuffThreads];
+  RangeOut R[kHuffThreads];
+  int32_t blk0[kHuffThreads];
+  int32_t pred[kHuffThreads][kMaxComp];
+  int16_t blkbuf[kHuffThreads * kBlkStride];
+  int32_t bad;
+};
+
+struct LdsSink {
+  int16_t* blk;
+  int16_t* coef;  // image coefficient area (global)
+  const ImgDesc* d;
+  __device__ void zero() {
+    uint64_t* p = (uint64_t*)blk;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = 0;
+  }
+  __device__ void set(int i, int16_t v) { blk[i] = v; }
+  __device__ void flush(int32_t b) {
+    int bpm = d->blocks_per_mcu;
+    int m = b / bpm, c = b - m * bpm;
+    int ci = d->mcu_comp[c];
+    const CompDesc& cd = d->comp[ci];
+    int one = d->ncomp == 1;
+    int bx = (m % d->mcus_x) * (one ? 1 : cd.h) + d->mcu_bx[c];
+    int by = (m / d->mcus_x) * (one ? 1 : cd.v) + d->mcu_by[c];
+    uint64_t* dst = (uint64_t*)(coef + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64);
+    const uint64_t* src = (const uint64_t*)blk;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dst[i] = src[i];
+  }
+};
+
+__global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restrict__ bytes,
+                                                          const int64_t* __restrict__ offsets,
+                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
+  ImgDesc& sd = L.sd;
+  const int img = blockIdx.x, t = threadIdx.x;
+  if (t == 0) sd = desc[img];
+  __syncthreads();
+  if (sd.status != DINO_IMG_OK) return;
+  const uint8_t* p = bytes + offsets[img];
+  // ---- tables: derived (6 lanes), then lookahead (all lanes)
+  if (t == 0) L.bad = 0;
+  __syncthreads();
+  if (t < 2 * sd.ncomp) {
+    int c = t >> 1, ac = t & 1;
+    int slot = ac ? 3 + c : c;
+    int off = ac ? sd.huff_off[4 + sd.comp[c].ta] : sd.huff_off[sd.comp[c].td];
+    if (!huff_build_derived(p + off, !ac, &L.tab[slot])) atomicOr(&L.bad, 1);
+  }
+  __syncthreads();
+  if (L.bad) {
+    if (t == 0) desc[img].status = DINO_IMG_CORRUPT;
+    return;
+  }
+  for (int e = t; e < 6 * (1 << kLookBits); e += kHuffThreads) {
+    int slot = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
+    int c = slot % 3;
+    if (c < sd.ncomp) L.tab[slot].look[idx] = huff_look_entry(&L.tab[slot], idx);
+  }
+  __syncthreads();
+  HuffImage im;
+  for (int c = 0; c < kMaxComp; ++c) {
+    im.dc[c] = &L.tab[c];
+    im.ac[c] = &L.tab[3 + c];
+  }
+  for (int i = 0; i < kMaxBlocksPerMcu; ++i) im.mcu_comp[i] = sd.mcu_comp[i];
+  im.blocks_per_mcu = sd.blocks_per_mcu;
+  const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
+  LdsSink sink;
+  sink.blk = L.blkbuf + t * kBlkStride;
+  sink.coef = (int16_t*)(ws + sd.coef_off);
+  sink.d = &sd;
+
+  if (sd.restart_interval > 0) {
+    // ---- restart intervals are independent: one lane per segment
+    const int32_t* rst = (const int32_t*)(ws + sd.rst_off);
+    const int nseg = sd.n_rst_max;
+    const int per = sd.restart_interval * sd.blocks_per_mcu;
+    for (int k = t; k < nseg; k += kHuffThreads) {
+      uint32_t start = k == 0 ? 0u : (uint32_t)rst[k - 1] * 8u;
+      BitReader sb{words, k + 1 < nseg ? (uint32_t)rst[k] : (uint32_t)sd.ent_len};
+      int32_t pred[kMaxComp] = {0, 0, 0};
+      int first = k * per, last = min(first + per, sd.total_blocks);
+      decode_write(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+    }
+    return;
+  }
+  // ---- speculative self-synchronising decode
+  const BitReader br{words, (uint32_t)sd.ent_len};
+  const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
+  int n = (int)((nbits + kMinSubBits - 1) / kMinSubBits);
+  n = n < 1 ? 1 : (n > kHuffThreads ? kHuffThreads : n);
+  uint32_t sub = (nbits + n - 1) / n;
+  sub = (sub + 31) & ~31u;
+  if (sub == 0) sub = 32;
+  const bool active = t < n;
+  const uint32_t my_end_range = (t == n - 1) ? nbits : (uint32_t)(t + 1) * sub;
+  const uint32_t my_end_write = (t == n - 1) ? 0xFFFFFFFFu : (uint32_t)(t + 1) * sub;
+  if (active) {
+    HState s0{(uint32_t)t * sub, 0, 0};
+    L.S[t] = s0;
+    L.R[t] = decode_range(br, im, s0, my_end_range);
+  }
+  for (int round = 0; round < kHuffThreads + 1; ++round) {
+    HState want;
+    bool redo = false;
+    if (active && t >= 1) {
+      want = L.R[t - 1].end;
+      redo = !hstate_eq(want, L.S[t]);
+    }
+    __syncthreads();
+    if (redo) {
+      L.S[t] = want;
+      L.R[t] = decode_range(br, im, want, my_end_range);
+    }
+    if (!__syncthreads_or(redo ? 1 : 0)) break;
+  }
+  // prefix sums of blocks and DC differences (serial over <= 256 lanes)
+  if (t == 0) {
+    int32_t b = 0, pr[kMaxComp] = {0, 0, 0};
+    for (int i = 0; i < n; ++i) {
+      L.blk0[i] = b;
+      for (int c = 0; c < kMaxComp; ++c) L.pred[i][c] = pr[c];
+      b += L.R[i].nblk;
+      for (int c = 0; c < kMaxComp; ++c) pr[c] += L.R[i].dcsum[c];
+    }
+  }
+  __syncthreads();
+  if (active) {
+    int32_t pred[kMaxComp] = {L.pred[t][0], L.pred[t][1], L.pred[t][2]};
+    decode_write(br, im, L.S[t], my_end_write, L.blk0[t], sd.total_blocks, pred, sink);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_idct: grid (gx, B); lanes over the 8x8 blocks of one image
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  const ImgDesc& d = desc[blockIdx.y];
+  if (d.status != DINO_IMG_OK) return;
+  int64_t nb[kMaxComp], tot = 0;
+  for (int c = 0; c < kMaxComp; ++c) {
+    nb[c] = c < d.ncomp ? (int64_t)d.comp[c].bw * d.comp[c].bh : 0;
+    tot += nb[c];
+  }
+  const int16_t* coef = (const int16_t*)(ws + d.coef_off);
+  uint8_t* planes = ws + d.plane_off;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < tot; g += (int64_t)gridDim.x * blockDim.x) {
+    int c = 0;
+    int64_t k = g;
+    while (k >= nb[c]) {
+      k -= nb[c];
+      ++c;
+    }
+    const CompDesc& cd = d.comp[c];
+    int by = (int)(k / cd.bw), bx = (int)(k - (int64_t)by * cd.bw);
+    const int16_t* src = coef + cd.coef_off / 2 + k * 64;
+    int16_t blk[64];
+    const int4* s4 = (const int4*)src;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ((int4*)blk)[i] = s4[i];
+    uint8_t out[64];
+    idct_islow_fast(blk, d.qt[cd.tq], out, 8);
+    const int pitch = cd.bw * 8;
+    uint8_t* dst = planes + cd.plane_off + (int64_t)by * 8 * pitch + bx * 8;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) *(uint64_t*)(dst + (int64_t)r * pitch) = *(const uint64_t*)(out + r * 8);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_color: grid (gx, B); lanes over output pixels
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  const ImgDesc& d = desc[blockIdx.y];
+  if (d.status != DINO_IMG_OK) return;
+  PlaneView pv[kMaxComp];
+  for (int c = 0; c < d.ncomp; ++c) {
+    const CompDesc& cd = d.comp[c];
+    pv[c].p = ws + d.plane_off + cd.plane_off;
+    pv[c].pitch = cd.bw * 8;
+    pv[c].dw = cd.dw;
+    pv[c].dh = cd.dh;
+    pv[c].hf = d.max_h / cd.h;
+    pv[c].vf = d.max_v / cd.v;
+    pv[c].method = upsample_method(pv[c].hf, pv[c].vf, cd.dw);
+  }
+  uint8_t* rgb = ws + d.rgb_off;
+  const int W = d.width;
+  const int64_t npx = (int64_t)W * d.height;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (int64_t)gridDim.x * blockDim.x) {
+    int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
+    uint8_t* o = rgb + i * 3;
+    if (d.ncomp == 1) {
+      uint8_t v = (uint8_t)upsample_at(pv[0], x, y);
+      o[0] = o[1] = o[2] = v;
+    } else {
+      int a = upsample_at(pv[0], x, y), b = upsample_at(pv[1], x, y), c = upsample_at(pv[2], x, y);
+      if (d.color == kYCbCr) {
+        ycc_to_rgb(a, b, c, o);
+      } else {
+        o[0] = (uint8_t)a;
+        o[1] = (uint8_t)b;
+        o[2] = (uint8_t)c;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Augment half
+// ---------------------------------------------------------------------------
+__global__ void k_params(const ImgDesc* __restrict__ desc, int B, dino_aug_config cfg, uint64_t seed,
+                         uint64_t batch_index, dino_view_params* __restrict__ out) {
+  const int nv = cfg.n_global + cfg.n_local;
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * nv) return;
+  int b = i / nv, v = i - b * nv;
+  const ImgDesc& d = desc[b];
+  int ok = d.status == DINO_IMG_OK;
+  sample_view(cfg, seed, batch_index, b, v, ok ? d.width : 1, ok ? d.height : 1, ok, &out[i]);
+}
+
+__device__ void view_sizes(const dino_view_params& p, int ok, int64_t* htmp, int64_t* rcoef, int32_t* kh, int32_t* kv) {
+  const int S = p.out_size;
+  *kh = ok && p.crop_w != S ? resample_ksize(p.crop_w, S) : 0;
+  *kv = ok && p.crop_h != S ? resample_ksize(p.crop_h, S) : 0;
+  *htmp = (*kh) ? align16((int64_t)p.crop_h * S * 3) : 0;
+  *rcoef = ok ? align16((int64_t)S * (4 + *kh + *kv) * 4) : 0;
+}
+
+// Host-supplied records are validated before any kernel indexes memory with them.
+__device__ bool params_valid(const dino_view_params& p, const ImgDesc& d, int S) {
+  if (p.out_size != S) return false;
+  if (p.crop_top < 0 || p.crop_left < 0 || p.crop_h < 1 || p.crop_w < 1) return false;
+  if ((int64_t)p.crop_top + p.crop_h > d.height || (int64_t)p.crop_left + p.crop_w > d.width) return false;
+  if (p.blur && (p.ksize < 1 || p.ksize > 15 || (p.ksize & 1) == 0 || !(p.sigma > 0.0))) return false;
+  for (int k = 0; k < 4; ++k)
+    if (p.order[k] > 3) return false;
+  return true;
+}
+
+__global__ void __launch_bounds__(1024) k_vplan(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                                int B, int nv, int n_global, int gsize, int lsize, int64_t aws_size,
+                                                ViewPlan* __restrict__ plan) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x, N = B * nv;
+  const int per = (N + 1023) / 1024;
+  int64_t local = 0;
+  for (int k = 0; k < per; ++k) {
+    int i = t * per + k;
+    if (i < N) {
+      int64_t a, b;
+      int32_t c, e;
+      const ImgDesc& d = desc[i / nv];
+      int S = (i % nv) < n_global ? gsize : lsize;
+      view_sizes(prm[i], d.status == DINO_IMG_OK && params_valid(prm[i], d, S), &a, &b, &c, &e);
+      local += a + b;
+    }
+  }
+  part[t] = local;
+  __syncthreads();
+  for (int s = 1; s < 1024; s <<= 1) {
+    int64_t v = t >= s ? part[t - s] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t base = part[t] - local;
+  for (int k = 0; k < per; ++k) {
+    int i = t * per + k;
+    if (i >= N) continue;
+    const ImgDesc& d = desc[i / nv];
+    int S = (i % nv) < n_global ? gsize : lsize;
+    int ok = d.status == DINO_IMG_OK && params_valid(prm[i], d, S);
+    int64_t a, b;
+    int32_t kh, kv;
+    view_sizes(prm[i], ok, &a, &b, &kh, &kv);
+    ViewPlan vp;
+    vp.ok = ok && (base + a + b <= aws_size);
+    vp.kh = kh;
+    vp.kv = kv;
+    vp.htmp_off = base;
+    vp.rcoef_off = base + a;
+    plan[i] = vp;
+    base += a + b;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restrict__ prm, const ViewPlan* __restrict__ plan,
+                                                 int nv, int v0, uint8_t* __restrict__ aws) {
+  const int i = blockIdx.y * nv + v0 + blockIdx.x;
+  const ViewPlan vp = plan[i];
+  if (!vp.ok) return;
+  const dino_view_params p = prm[i];
+  const int S = p.out_size;
+  int32_t* base = (int32_t*)(aws + vp.rcoef_off);
+  int32_t* hb = base;                 // [S][2]
+  int32_t* vb = base + 2 * S;         // [S][2]
+  int32_t* ht = base + 4 * S;         // [S][kh]
+  int32_t* vt = ht + (int64_t)S * vp.kh;
+  for (int x = threadIdx.x; x < S; x += blockDim.x) {
+    if (vp.kh) resample_coeffs_one(p.crop_w, S, x, vp.kh, &hb[2 * x], &hb[2 * x + 1], ht + (int64_t)x * vp.kh);
+    if (vp.kv) resample_coeffs_one(p.crop_h, S, x, vp.kv, &vb[2 * x], &vb[2 * x + 1], vt + (int64_t)x * vp.kv);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                                 const ViewPlan* __restrict__ plan, int nv, int v0,
+                                                 const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
+  const int b = blockIdx.z;
+  const int i = b * nv + v0 + blockIdx.y;
+  const ViewPlan vp = plan[i];
+  if (!vp.ok || !vp.kh) return;
+  const dino_view_params p = prm[i];
+  const ImgDesc& d = desc[b];
+  const int S = p.out_size, W = d.width;
+  const int32_t* base = (const int32_t*)(aws + vp.rcoef_off);
+  CoefView cv{base, base + 4 * S, vp.kh};
+  SrcView src{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  uint8_t* tmp = aws + vp.htmp_off;
+  const int64_t total = (int64_t)p.crop_h * S;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
+    uint8_t* o = tmp + e * 3;
+    o[0] = hresize_at(src, cv, r, x, 0);
+    o[1] = hresize_at(src, cv, r, x, 1);
+    o[2] = hresize_at(src, cv, r, x, 2);
+  }
+}
+
+template <typename OutT>
+__device__ __forceinline__ void store_out(OutT* out, int64_t o, float f);
+template <>
+__device__ __forceinline__ void store_out<uint16_t>(uint16_t* out, int64_t o, float f) {
+  out[o] = f32_to_bf16(f);
+}
+template <>
+__device__ __forceinline__ void store_out<float>(float* out, int64_t o, float f) {
+  out[o] = f;
+}
+template <>
+__device__ __forceinline__ void store_out<uint8_t>(uint8_t* out, int64_t o, float f) {
+  out[o] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f)));
+}
+
+// One workgroup per (view, image).  crop: 3 planes of S*S u8 (LDS when it fits,
+// otherwise a global scratch slice).
+template <typename OutT, bool kLdsCrop>
+__global__ void __launch_bounds__(512) k_augment(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                                 const ViewPlan* __restrict__ plan, int nv, int v0,
+                                                 const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws,
+                                                 uint8_t* __restrict__ gcrop, void* const* __restrict__ views,
+                                                 dino_aug_config cfg, int S) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  AugLdsHead& H = *reinterpret_cast<AugLdsHead*>(smem);
+  float* s_k1 = H.k1;
+  float* s_k2 = H.k2;
+  uint32_t& s_lsum = H.lsum;
+  const int b = blockIdx.y, v = v0 + blockIdx.x;
+  const int i = b * nv + v;
+  const dino_view_params p = prm[i];
+  const ViewPlan vp = plan[i];  // vp.ok implies p.out_size == S and an in-bounds crop
+  const int64_t N = (int64_t)S * S;
+  OutT* out = (OutT*)views[v] + (int64_t)b * 3 * N;
+  const int t = threadIdx.x, nt = blockDim.x;
+  if (!vp.ok) {  // reference cpu.py:253: undecodable -> zeros
+    for (int64_t e = t; e < 3 * N; e += nt) out[e] = (OutT)0;
+    return;
+  }
+  const ImgDesc& d = desc[b];
+  uint8_t* crop = kLdsCrop ? smem + sizeof(AugLdsHead) : gcrop + ((int64_t)b * gridDim.x + blockIdx.x) * 3 * N;
+  uint8_t *R = crop, *G = crop + N, *Bp = crop + 2 * N;
+  const JitterPlan jp = make_jitter_plan(p);
+  const int hd = hue_delta(p.hue);
+  const int W = d.width;
+  const bool need_h = vp.kh != 0, need_v = vp.kv != 0;
+  const int32_t* cbase = (const int32_t*)(aws + vp.rcoef_off);
+  CoefView cvv{cbase + 2 * S, cbase + 4 * S + (int64_t)S * vp.kh, vp.kv};
+  SrcView src = need_h ? SrcView{aws + vp.htmp_off, (int64_t)S * 3}
+                       : SrcView{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  if (t == 0) s_lsum = 0;
+  if (p.blur && t == 0) gaussian_kernel1d(p.ksize, p.sigma, s_k1);
+  __syncthreads();
+  if (p.blur && t < p.ksize * p.ksize) s_k2[t] = s_k1[t / p.ksize] * s_k1[t % p.ksize];
+  // pass A: vertical resample (+flip), ColorJitter ops before contrast, L sum
+  uint32_t lsum = 0;
+  for (int64_t e = t; e < N; e += nt) {
+    int y = (int)(e / S), x = (int)(e - (int64_t)y * S);
+    int r, g, bb;
+    if (need_v) {
+      r = vresize_at(src, cvv, y, x, 0);
+      g = vresize_at(src, cvv, y, x, 1);
+      bb = vresize_at(src, cvv, y, x, 2);
+    } else {
+      const uint8_t* q = src.base + (int64_t)y * src.pitch + (int64_t)x * 3;
+      r = q[0];
+      g = q[1];
+      bb = q[2];
+    }
+    jitter_stage0(jp, r, g, bb, p, hd);
+    int xo = p.flip ? S - 1 - x : x;
+    int64_t o = (int64_t)y * S + xo;
+    R[o] = (uint8_t)r;
+    G[o] = (uint8_t)g;
+    Bp[o] = (uint8_t)bb;
+    if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
+  }
+  if (jp.has_contrast) {
+    for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
+    if ((t & 63) == 0) atomicAdd(&s_lsum, lsum);
+  }
+  __syncthreads();
+  // pass B: contrast with the crop's mean, later ops, grayscale
+  if (p.jitter || p.gray) {
+    const int cmean = contrast_mean_from_sum(s_lsum, N);
+    for (int64_t e = t; e < N; e += nt) {
+      int r = R[e], g = G[e], bb = Bp[e];
+      jitter_stage1(jp, r, g, bb, p, cmean, hd);
+      R[e] = (uint8_t)r;
+      G[e] = (uint8_t)g;
+      Bp[e] = (uint8_t)bb;
+    }
+    __syncthreads();
+  }
+  // final pass: blur + solarize + normalize + cast, NCHW
+  const float m0 = cfg.mean[0], m1 = cfg.mean[1], m2 = cfg.mean[2];
+  const float d0 = cfg.std[0], d1 = cfg.std[1], d2 = cfg.std[2];
+  for (int64_t e = t; e < 3 * N; e += nt) {
+    int ch = (int)(e / N);
+    int64_t pix = e - (int64_t)ch * N;
+    int y = (int)(pix / S), x = (int)(pix - (int64_t)y * S);
+    const uint8_t* pl = crop + (int64_t)ch * N;
+    int val = p.blur ? blur_at(pl, S, y, x, s_k2, p.ksize) : pl[pix];
+    if (p.solarize) val = solarize_u8(val);
+    float mean = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
+    float sd = ch == 0 ? d0 : (ch == 1 ? d1 : d2);
+    store_out<OutT>(out, e, u8_normalize(val, mean, sd));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// iBOT masks: one lane runs the (inherently sequential) generator
+// ---------------------------------------------------------------------------
+__global__ void k_masks(MaskParams mp, int n, uint32_t* __restrict__ py_state, uint32_t* __restrict__ np_state,
+                        uint8_t* __restrict__ out, int32_t* __restrict__ scratch) {
+  __shared__ MtState py, np;
+  if (threadIdx.x != 0) return;
+  mt_load(py, py_state);
+  mt_load(np, np_state);
+  for (int k = 0; k < n; ++k) gen_mask(mp, py, np, out + (int64_t)k * mp.H * mp.W, scratch);
+  mt_store(py, py_state);
+  mt_store(np, np_state);
+}
+
+__global__ void k_bf16_to_fp8(const uint16_t* __restrict__ in, uint8_t* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = f32_to_fp8e4m3(bf16_to_f32(in[i]));
+}
+
+// copy of one decoded image out of the workspace (tests / debug)
+__global__ void k_copy_rgb(const ImgDesc* __restrict__ desc, int idx, const uint8_t* __restrict__ ws,
+                           uint8_t* __restrict__ dst) {
+  const ImgDesc& d = desc[idx];
+  if (d.status != DINO_IMG_OK) return;
+  const int64_t n = (int64_t)d.width * d.height * 3;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = ws[d.rgb_off + i];
+}
+
+__global__ void k_info(const ImgDesc* __restrict__ desc, int B, int32_t* __restrict__ info) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const ImgDesc& d = desc[i];
+  info[4 * i + 0] = d.status;
+  info[4 * i + 1] = d.width;
+  info[4 * i + 2] = d.height;
+  info[4 * i + 3] = d.ncomp;
+}
+
+
+}  // namespace dino
+
+// ===========================================================================
+// Launchers
+// ===========================================================================
+namespace dino {
+
+static int huff_lds_bytes() { return (int)((sizeof(HuffLds) + 15) & ~(size_t)15); }
+
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
+  const int B = a.batch;
+  if (B <= 0) return hipSuccess;
+  k_parse<<<(B + 63) / 64, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc);
+  k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size);
+  k_destuff<<<B, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huffman), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        huff_lds_bytes());
+    attr_set = true;
+  }
+  k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws);
+  k_idct<<<dim3(32, B), 256, 0, s>>>(a.desc, a.ws);
+  k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_params(const ImgDesc* desc, int batch, const dino_aug_config& cfg, uint64_t seed,
+                         uint64_t batch_index, dino_view_params* out, hipStream_t s) {
+  const int n = batch * (cfg.n_global + cfg.n_local);
+  if (n <= 0) return hipSuccess;
+  k_params<<<(n + 63) / 64, 64, 0, s>>>(desc, batch, cfg, seed, batch_index, out);
+  return hipGetLastError();
+}
+
+template <typename OutT>
+static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, int S, hipStream_t s) {
+  const int B = a.batch, nv = a.cfg.n_global + a.cfg.n_local;
+  if (nvc <= 0) return hipSuccess;
+  k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws);
+  k_hresize<<<dim3(8, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws);
+  const int threads = S >= 128 ? 512 : 256;
+  if (S <= kMaxLdsCropSize) {
+    const int lds = (int)sizeof(AugLdsHead) + 3 * S * S;
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_augment<OutT, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    k_augment<OutT, true><<<dim3(nvc, B), threads, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.gcrop,
+                                                           a.d_views, a.cfg, S);
+  } else {
+    if (!a.gcrop) return hipErrorInvalidValue;
+    k_augment<OutT, false><<<dim3(nvc, B), threads, sizeof(AugLdsHead), s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
+                                                                            a.aws, a.gcrop, a.d_views, a.cfg, S);
+  }
+  return hipGetLastError();
+}
+
+template <typename OutT>
+static hipError_t launch_augment_t(const AugmentArgs& a, hipStream_t s) {
+  hipError_t e = launch_augment_class<OutT>(a, 0, a.cfg.n_global, a.cfg.global_size, s);
+  if (e != hipSuccess) return e;
+  return launch_augment_class<OutT>(a, a.cfg.n_global, a.cfg.n_local, a.cfg.local_size, s);
+}
+
+hipError_t launch_augment(const AugmentArgs& a, hipStream_t s) {
+  const int B = a.batch, nv = a.cfg.n_global + a.cfg.n_local;
+  if (B <= 0 || nv <= 0) return hipSuccess;
+  k_vplan<<<1, 1024, 0, s>>>(a.desc, a.params, B, nv, a.cfg.n_global, a.cfg.global_size, a.cfg.local_size,
+                             a.aws_size, a.plan);
+  switch (a.cfg.out_dtype) {
+    case DINO_OUT_FP32:
+      return launch_augment_t<float>(a, s);
+    case DINO_OUT_FP8_E4M3:
+      return launch_augment_t<uint8_t>(a, s);
+    default:
+      return launch_augment_t<uint16_t>(a, s);
+  }
+}
+
+hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_t s) {
+  if (batch <= 0) return hipSuccess;
+  k_info<<<(batch + 63) / 64, 64, 0, s>>>(desc, batch, info);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s) {
+  k_copy_rgb<<<256, 256, 0, s>>>(desc, idx, ws, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,
+                        uint32_t* np, uint8_t* out, int32_t* scratch, hipStream_t s) {
+  MaskParams mp{H, W, target, minp, maxp, la0, la1};
+  k_masks<<<1, 64, 0, s>>>(mp, n, py, np, out, scratch);
+  return hipGetLastError();
+}
+
+hipError_t launch_bf16_to_fp8(const uint16_t* in, uint8_t* out, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  k_bf16_to_fp8<<<(unsigned)blocks, 256, 0, s>>>(in, out, n);
+  return hipGetLastError();
+}
+
+}  // namespace dino

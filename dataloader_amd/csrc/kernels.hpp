@@ -1,0 +1,61 @@
+// kernels.hpp — launch interface between the C ABI (capi.hip) and kernels.hip.
+#pragma once
+
+#include "common.hpp"
+
+namespace dino {
+
+// Per-(image, view) scratch placement, written by k_vplan.
+struct ViewPlan {
+  int64_t htmp_off;   // horizontal-pass rows (crop_h x S x 3 u8) in the augment workspace
+  int64_t rcoef_off;  // resize coefficient tables
+  int32_t kh, kv;     // taps per output of the horizontal / vertical pass (0 = pass skipped)
+  int32_t ok;         // image decoded and scratch available
+  int32_t pad;
+};
+
+// Dynamic-LDS header of k_augment (kept in the dynamic region so its base stays 16-B aligned).
+struct AugLdsHead {
+  float k1[16];
+  float k2[256];
+  uint32_t lsum;
+  uint32_t pad[3];
+};
+
+// Largest S whose three u8 planes fit next to the header in 160 KiB of LDS.
+constexpr int kMaxLdsCropSize = 233;
+
+struct DecodeArgs {
+  const uint8_t* bytes;
+  const int64_t* offsets;
+  int32_t batch;
+  int32_t max_dim;
+  ImgDesc* desc;
+  uint8_t* ws;
+  int64_t ws_size;
+};
+
+struct AugmentArgs {
+  const ImgDesc* desc;
+  int32_t batch;
+  const dino_view_params* params;
+  ViewPlan* plan;
+  const uint8_t* ws;
+  uint8_t* aws;
+  int64_t aws_size;
+  uint8_t* gcrop;          // global crop scratch for S > kMaxLdsCropSize (may be null otherwise)
+  void* const* d_views;    // device array of n_views output pointers
+  dino_aug_config cfg;
+};
+
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_params(const ImgDesc* desc, int batch, const dino_aug_config& cfg, uint64_t seed,
+                         uint64_t batch_index, dino_view_params* out, hipStream_t s);
+hipError_t launch_augment(const AugmentArgs& a, hipStream_t s);
+hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_t s);
+hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s);
+hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,
+                        uint32_t* np, uint8_t* out, int32_t* scratch, hipStream_t s);
+hipError_t launch_bf16_to_fp8(const uint16_t* in, uint8_t* out, int64_t n, hipStream_t s);
+
+}  // namespace dino

@@ -1,0 +1,138 @@
+"""Device-side engine: one ``dino_ctx`` per GPU plus torch-owned I/O buffers.
+
+``IngestEngine`` is the thin Python layer over the C ABI.  torch provides the
+device memory for inputs/outputs and the stream; every heavy step runs in the
+HIP kernels of ``libdino_ingest.so``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, VIEW_PARAMS_DTYPE, DinoLimits
+
+_TORCH_OUT = {OUT_BF16: torch.bfloat16, OUT_FP32: torch.float32, OUT_FP8_E4M3: torch.float8_e4m3fn}
+
+
+def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_handle(device: torch.device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def pack_jpegs(jpegs, pin: bool = True) -> tuple[torch.Tensor, torch.Tensor]:
+    """Pack a list of JPEG byte strings / uint8 arrays into one host buffer + int64 offsets[B+1]."""
+    lens = np.fromiter((len(j) for j in jpegs), dtype=np.int64, count=len(jpegs))
+    offsets = np.zeros(len(jpegs) + 1, dtype=np.int64)
+    np.cumsum(lens, out=offsets[1:])
+    total = int(offsets[-1])
+    buf = torch.empty(max(total, 1) + 16, dtype=torch.uint8, pin_memory=pin)
+    view = buf.numpy()
+    for j, o, n in zip(jpegs, offsets[:-1], lens):
+        view[o:o + n] = np.frombuffer(j, dtype=np.uint8) if isinstance(j, (bytes, bytearray, memoryview)) else j
+    return buf, torch.from_numpy(offsets)
+
+
+class IngestEngine:
+    """Owns a ``dino_ctx`` (decode + augment workspaces sized from the limits)."""
+
+    def __init__(self, device: int | torch.device = 0, max_batch: int = 512, max_views: int = 10,
+                 max_crop_size: int = 224, max_image_dim: int = 8192, workspace_bytes: int = 0):
+        self.lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise _lib.DinoError("IngestEngine needs a ROCm GPU (torch.cuda.is_available() is False); "
+                                 "there is no CPU fallback")
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self.limits = DinoLimits(max_batch, max_views, max_crop_size, max_image_dim, workspace_bytes)
+        self._ctx = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.dino_ctx_create(self.device.index or 0, ctypes.byref(self.limits),
+                                                ctypes.byref(self._ctx)), "dino_ctx_create")
+        self.last_batch = 0
+
+    # ------------------------------------------------------------------ decode
+    def decode(self, d_bytes: torch.Tensor, d_offsets: torch.Tensor, batch: int,
+               info: torch.Tensor | None = None) -> torch.Tensor:
+        if info is None:
+            info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
+        _lib.check(self.lib.dino_decode(self._ctx, _ptr(d_bytes), _ptr(d_offsets), batch, _ptr(info),
+                                        _stream_handle(self.device)), "dino_decode")
+        self.last_batch = batch
+        return info
+
+    def copy_rgb(self, index: int, width: int, height: int) -> torch.Tensor:
+        out = torch.zeros(height, width, 3, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.dino_copy_rgb(self._ctx, index, _ptr(out), _stream_handle(self.device)),
+                   "dino_copy_rgb")
+        return out
+
+    def debug_region(self, index: int, region: int, nbytes: int) -> torch.Tensor:
+        out = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.dino_debug_region(self._ctx, index, region, _ptr(out), nbytes,
+                                              _stream_handle(self.device)), "dino_debug_region")
+        return out
+
+    # ----------------------------------------------------------------- augment
+    def sample_params(self, cfg, seed: int, batch_index: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        n = self.last_batch * (cfg.n_global + cfg.n_local)
+        if out is None:
+            out = torch.empty(n * VIEW_PARAMS_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.dino_sample_params(self._ctx, ctypes.byref(cfg), seed & (2**64 - 1), batch_index,
+                                               _ptr(out), _stream_handle(self.device)), "dino_sample_params")
+        return out
+
+    def alloc_views(self, cfg, batch: int) -> list[torch.Tensor]:
+        dt = _TORCH_OUT[cfg.out_dtype]
+        sizes = [cfg.global_size] * cfg.n_global + [cfg.local_size] * cfg.n_local
+        return [torch.empty(batch, 3, s, s, dtype=dt, device=self.device) for s in sizes]
+
+    def augment(self, cfg, params: torch.Tensor, views: list[torch.Tensor] | None = None) -> list[torch.Tensor]:
+        if views is None:
+            views = self.alloc_views(cfg, self.last_batch)
+        ptrs = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
+        _lib.check(self.lib.dino_augment(self._ctx, ctypes.byref(cfg), _ptr(params), ptrs,
+                                         _stream_handle(self.device)), "dino_augment")
+        return views
+
+    def run_batch(self, d_bytes, d_offsets, batch: int, cfg, seed: int, batch_index: int,
+                  views: list[torch.Tensor] | None = None, params_out: torch.Tensor | None = None,
+                  info: torch.Tensor | None = None):
+        if views is None:
+            views = self.alloc_views(cfg, batch)
+        if info is None:
+            info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
+        ptrs = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
+        pp = _ptr(params_out) if params_out is not None else ctypes.c_void_p(0)
+        _lib.check(self.lib.dino_run_batch(self._ctx, _ptr(d_bytes), _ptr(d_offsets), batch, ctypes.byref(cfg),
+                                           seed & (2**64 - 1), batch_index, pp, ptrs, _ptr(info),
+                                           _stream_handle(self.device)), "dino_run_batch")
+        self.last_batch = batch
+        return views, info
+
+    def close(self) -> None:
+        if self._ctx:
+            torch.cuda.synchronize(self.device)
+            self.lib.dino_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def params_from_device(t: torch.Tensor) -> np.ndarray:
+    """Device param buffer -> numpy structured array of dino_view_params."""
+    return t.cpu().numpy().view(VIEW_PARAMS_DTYPE)
+
+
+def params_to_device(arr: np.ndarray, device) -> torch.Tensor:
+    raw = np.ascontiguousarray(arr, dtype=VIEW_PARAMS_DTYPE).view(np.uint8)
+    return torch.from_numpy(raw.copy()).to(device)

@@ -1,0 +1,152 @@
+/*
+ * dino_ingest.h — C ABI of the MI355X-native DINO Stage-3 ingest backend.
+ *
+ * This is the drop-in boundary for the reference's CPU hot path: everything
+ * that ``CPUBackend``'s ``CPUAugPipeline.run_one_batch`` does per batch
+ * (reference src/dino_loader/backends/cpu.py:309-367 — decode, random-resized
+ * crop x N views, colour jitter, grayscale, gaussian blur, solarize,
+ * normalize+cast) plus the iBOT mask generator (reference
+ * src/dino_loader/masking.py:148-172) and the Stage-5 FP8 cast (reference
+ * src/dino_loader/memory.py:193-214), as plain-pointer entry points.
+ *
+ * Conventions
+ *  - Every entry point returns int status: DINO_OK (0) or a negative DINO_E*;
+ *    dino_last_error() gives a thread-local message.  No C++ exception crosses
+ *    the ABI.
+ *  - Pointers named d_* are device (HBM) pointers; "stream" is a hipStream_t
+ *    passed as void*.  All work is enqueued on that stream; nothing blocks the
+ *    host unless stated.
+ *  - One dino_ctx per device; a ctx is not thread-safe (callers serialise),
+ *    several ctx may run concurrently on different devices/streams.
+ *  - Per-image status codes (d_status[i]): 0 ok, <0 the reference would have
+ *    raised inside Image.open/convert (cpu.py:250-253) -> zero-filled output,
+ *    >0 valid JPEG flavour this decoder does not implement (progressive,
+ *    arithmetic, 12-bit, CMYK, multi-scan) -> zero-filled output.
+ */
+#ifndef DINO_INGEST_H
+#define DINO_INGEST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DINO_ABI_VERSION 1
+
+/* return codes */
+#define DINO_OK 0
+#define DINO_EINVAL (-1)
+#define DINO_ENOMEM (-2)
+#define DINO_EHIP (-3)
+#define DINO_ECAPACITY (-4)
+
+/* per-image status codes */
+#define DINO_IMG_OK 0
+#define DINO_IMG_CORRUPT (-1)        /* not a JPEG / malformed header / bad table */
+#define DINO_IMG_TRUNCATED (-2)      /* entropy data ends before the last MCU, no EOI */
+#define DINO_IMG_BADDATA (-3)        /* libjpeg would error (bad sampling, MCU too large) */
+#define DINO_IMG_TOO_LARGE (-4)      /* exceeds ctx limits / workspace */
+#define DINO_IMG_UNSUPPORTED 1       /* progressive / arithmetic / lossless / 12-bit / CMYK */
+#define DINO_IMG_MULTISCAN 2         /* sequential JPEG with non-interleaved multi-scan */
+
+/* output dtypes */
+#define DINO_OUT_BF16 0
+#define DINO_OUT_FP32 1
+#define DINO_OUT_FP8_E4M3 2
+
+typedef struct dino_ctx dino_ctx;
+
+/* Pre-allocation ceilings (reference config.py:236-237 max_*_crop_size). */
+typedef struct dino_limits {
+  int32_t max_batch;           /* images per call */
+  int32_t max_views;           /* views per image (n_global + n_local) */
+  int32_t max_crop_size;       /* largest S of any view */
+  int32_t max_image_dim;       /* largest JPEG width or height accepted */
+  int64_t workspace_bytes;     /* decode workspace (HBM); 0 -> default */
+} dino_limits;
+
+/* Augmentation hyper-parameters (reference DINOAugConfig, config.py:243-272). */
+typedef struct dino_aug_config {
+  int32_t n_global, n_local;
+  int32_t global_size, local_size;
+  float global_scale[2], local_scale[2];
+  float blur_prob_global1, blur_prob_global2, blur_prob_local;
+  float solarize_prob, color_jitter_prob, grayscale_prob, flip_prob;
+  float blur_sigma_min, blur_sigma_max;
+  float brightness, contrast, saturation, hue;
+  float mean[3], std[3];
+  int32_t out_dtype;           /* DINO_OUT_* */
+  int32_t reserved;
+} dino_aug_config;
+
+/* Every random decision of one (sample, view) — reference cpu.py:172-267.
+ * 64 bytes, layout shared with dataloader_amd/params.py (numpy dtype). */
+typedef struct dino_view_params {
+  int32_t crop_top, crop_left, crop_h, crop_w;   /* RandomResizedCrop (i, j, h, w) */
+  int32_t out_size;                              /* S */
+  uint8_t flip, jitter, gray, blur;
+  uint8_t solarize, pad0[3];
+  uint8_t order[4];                              /* ColorJitter op order 0=B 1=C 2=S 3=H */
+  float brightness, contrast, saturation, hue;   /* ColorJitter factors */
+  double sigma;                                  /* blur sigma */
+  int32_t ksize;                                 /* blur kernel size */
+  int32_t pad1;
+} dino_view_params;
+
+/* Library / context */
+int dino_abi_version(void);
+const char* dino_last_error(void);
+int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out);
+int dino_ctx_destroy(dino_ctx* ctx);
+
+/* Stage 3, decode half: JPEG bytes -> RGB planes kept in the ctx workspace.
+ * d_bytes: packed JPEG bytes, d_offsets: int64[batch+1] byte offsets.
+ * d_info (nullable): int32[batch][4] = {status, width, height, components}. */
+int dino_decode(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,
+                int32_t* d_info, void* stream);
+
+/* Copy decoded image i (HWC uint8 RGB, pitch = width*3) to d_rgb (debug / tests). */
+int dino_copy_rgb(dino_ctx* ctx, int32_t index, uint8_t* d_rgb, void* stream);
+
+/* Sample view params on device (counter-based Philox keyed by seed, batch_index,
+ * sample, view) for the last decoded batch; writes batch*n_views records. */
+int dino_sample_params(dino_ctx* ctx, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
+                       dino_view_params* d_params, void* stream);
+
+/* Stage 3, augment half: for every image of the last decoded batch and every view v,
+ * write views[v] = [batch, 3, S_v, S_v] (dtype cfg->out_dtype, NCHW contiguous).
+ * views: HOST array of n_views DEVICE pointers (copied into the ctx before return).
+ * d_params: batch*n_views records (sample-major). Zero-fills images with status != 0. */
+int dino_augment(dino_ctx* ctx, const dino_aug_config* cfg, const dino_view_params* d_params,
+                 void* const* views, void* stream);
+
+/* One call = decode + sample params + augment (CPUAugPipeline.run_one_batch).
+ * d_params_out (nullable) receives the sampled records. */
+int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,
+                   const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
+                   dino_view_params* d_params_out, void* const* views, int32_t* d_info,
+                   void* stream);
+
+/* iBOT block masks (reference MaskingGenerator.__call__, masking.py:148-172).
+ * d_py_state: uint32[625] = CPython random.getstate() words + index;
+ * d_np_state: uint32[625] = numpy RandomState MT19937 key + pos.
+ * Both are advanced in place, exactly as n_masks sequential gen() calls would.
+ * d_out: bool/uint8 [n_masks, height*width]. */
+int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,
+               int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
+               uint32_t* d_py_state, uint32_t* d_np_state, uint8_t* d_out, void* stream);
+
+/* Debug / test introspection of the last decoded batch: copy image `index`'s
+ * region (0 descriptor, 1 destuffed entropy bytes, 2 DCT coefficients,
+ * 3 component planes, 4 RGB) into d_dst (<= max_bytes).  Synchronises the stream. */
+int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream);
+
+/* Stage-5 cast (reference FP8Formatter.quantise, memory.py:193-214, scale 1):
+ * bf16 -> OCP float8_e4m3fn, round-to-nearest-even, saturating. */
+int dino_bf16_to_fp8(const uint16_t* d_in, uint8_t* d_out, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DINO_INGEST_H */

@@ -1,0 +1,318 @@
+// Host models of the kernels' phase structure — TEST INFRASTRUCTURE ONLY.
+// Each function below mirrors one kernel of dataloader_amd/csrc/kernels.hip with
+// plain loops over lanes / threads, calling the same per-lane device functions.
+#pragma once
+
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../dataloader_amd/csrc/augment.hpp"
+#include "../../dataloader_amd/csrc/color.hpp"
+#include "../../dataloader_amd/csrc/huffman.hpp"
+#include "../../dataloader_amd/csrc/idct.hpp"
+#include "../../dataloader_amd/csrc/jpeg_parse.hpp"
+
+namespace dino {
+
+// ---- k_destuff (sequential statement of the same classification) ----------
+struct Destuffed {
+  std::vector<uint8_t> bytes;   // padded with zeros to a multiple of 4 + 8
+  std::vector<int32_t> rst;     // destuffed byte offset where each restart segment starts
+  int32_t len = 0;
+  int32_t terminated = 0;
+};
+
+inline Destuffed model_destuff(const uint8_t* r, int n) {
+  Destuffed d;
+  int E = n;
+  for (int k = 0; k < n; ++k) {
+    if (r[k] != 0xFF) continue;
+    int nx = k + 1 < n ? r[k + 1] : -1;
+    if (nx == 0x00 || (nx >= 0xD0 && nx <= 0xD7) || nx == 0xFF) continue;
+    E = k;
+    d.terminated = nx >= 0;
+    break;
+  }
+  for (int k = 0; k < E; ++k) {
+    if (r[k] == 0xFF) {
+      int nx = k + 1 < n ? r[k + 1] : -1;
+      if (nx == 0x00) d.bytes.push_back(0xFF);
+      else if (nx >= 0xD0 && nx <= 0xD7) d.rst.push_back((int32_t)d.bytes.size());
+      // fill byte: dropped
+    } else if (k > 0 && r[k - 1] == 0xFF) {
+      // second byte of FF00 / FFDx: dropped
+    } else {
+      d.bytes.push_back(r[k]);
+    }
+  }
+  d.len = (int32_t)d.bytes.size();
+  while (d.bytes.size() % 4) d.bytes.push_back(0);
+  for (int i = 0; i < 8; ++i) d.bytes.push_back(0);
+  return d;
+}
+
+struct CoefSink {
+  int16_t blk[64];
+  const ImgDesc* d;
+  int16_t* coef;  // image coefficient area
+  void zero() { memset(blk, 0, sizeof(blk)); }
+  void set(int i, int16_t v) { blk[i] = v; }
+  void flush(int32_t b) {
+    int m = b / d->blocks_per_mcu, c = b % d->blocks_per_mcu;
+    int ci = d->mcu_comp[c];
+    const CompDesc& cd = d->comp[ci];
+    int bx = (m % d->mcus_x) * (d->ncomp == 1 ? 1 : cd.h) + d->mcu_bx[c];
+    int by = (m / d->mcus_x) * (d->ncomp == 1 ? 1 : cd.v) + d->mcu_by[c];
+    memcpy(coef + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64, blk, 128);
+  }
+};
+
+inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* [6] */, HuffImage& im) {
+  for (int c = 0; c < d.ncomp; ++c) {
+    if (!huff_build_derived(p + d.huff_off[d.comp[c].td], true, &tabs[c])) return false;
+    if (!huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &tabs[3 + c])) return false;
+    for (int i = 0; i < (1 << kLookBits); ++i) {
+      tabs[c].look[i] = huff_look_entry(&tabs[c], i);
+      tabs[3 + c].look[i] = huff_look_entry(&tabs[3 + c], i);
+    }
+    im.dc[c] = &tabs[c];
+    im.ac[c] = &tabs[3 + c];
+  }
+  for (int i = 0; i < kMaxBlocksPerMcu; ++i) im.mcu_comp[i] = d.mcu_comp[i];
+  im.blocks_per_mcu = d.blocks_per_mcu;
+  return true;
+}
+
+// ---- k_huffman, speculative mode: phases 1..4 over `lanes` lanes ------------
+inline void model_huffman_spec(const BitReader& br, const HuffImage& im, uint32_t nbits, int total_blocks, int lanes,
+                               CoefSink& sink, int32_t* stats) {
+  int n = lanes;
+  uint32_t sub = (nbits + n - 1) / n;
+  sub = (sub + 31) & ~31u;
+  if (sub == 0) sub = 32;
+  std::vector<HState> S(n);
+  std::vector<RangeOut> R(n);
+  auto endof = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
+  for (int i = 0; i < n; ++i) {
+    S[i] = HState{(uint32_t)i * sub, 0, 0};
+    R[i] = decode_range(br, im, S[i], i == n - 1 ? nbits : endof(i));
+  }
+  int rounds = 0, redone = 0;
+  for (;;) {
+    std::vector<HState> want(n);
+    for (int i = 1; i < n; ++i) want[i] = R[i - 1].end;
+    bool any = false;
+    for (int i = 1; i < n; ++i) {
+      if (!hstate_eq(want[i], S[i])) {
+        S[i] = want[i];
+        R[i] = decode_range(br, im, S[i], i == n - 1 ? nbits : endof(i));
+        any = true;
+        ++redone;
+      }
+    }
+    ++rounds;
+    if (!any) break;
+  }
+  int32_t blk0 = 0, pred[kMaxComp] = {0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    int32_t p[kMaxComp] = {pred[0], pred[1], pred[2]};
+    decode_write(br, im, S[i], endof(i), blk0, total_blocks, p, sink);
+    blk0 += R[i].nblk;
+    for (int c = 0; c < kMaxComp; ++c) pred[c] += R[i].dcsum[c];
+  }
+  if (stats) {
+    stats[0] = rounds;
+    stats[1] = redone;
+    stats[2] = n;
+  }
+}
+
+struct StageCapture {
+  std::vector<uint8_t> ent;
+  std::vector<int16_t> coef;
+  std::vector<uint8_t> planes;
+  ImgDesc desc;
+};
+
+inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes, uint8_t* out_rgb, int32_t* stats,
+                             StageCapture* cap = nullptr) {
+  ImgDesc d;
+  if (parse_jpeg(p, len, 1 << 16, &d) != DINO_IMG_OK) return d.status;
+  Destuffed ds = model_destuff(p + d.scan_off, d.scan_len);
+  if (cap) {
+    cap->desc = d;
+    cap->ent.assign(ds.bytes.begin(), ds.bytes.begin() + ds.len);
+  }
+  if (!ds.terminated) return DINO_IMG_TRUNCATED;
+  HuffTable tabs[6];
+  HuffImage im;
+  if (!model_tables(p, d, tabs, im)) return DINO_IMG_CORRUPT;
+  std::vector<int16_t> coef(d.coef_bytes / 2, 0);
+  CoefSink sink;
+  sink.d = &d;
+  sink.coef = coef.data();
+  BitReader br{(const uint32_t*)ds.bytes.data(), (uint32_t)ds.len};
+  if (d.restart_interval > 0) {
+    int nseg = d.n_rst_max;
+    if ((int)ds.rst.size() < nseg - 1) return DINO_IMG_BADDATA;
+    int per = d.restart_interval * d.blocks_per_mcu;
+    for (int k = 0; k < nseg; ++k) {
+      uint32_t start = k == 0 ? 0 : (uint32_t)ds.rst[k - 1] * 8;
+      BitReader sb{br.words, k + 1 < nseg ? (uint32_t)ds.rst[k] : (uint32_t)ds.len};
+      int32_t pred[kMaxComp] = {0, 0, 0};
+      int first = k * per, last = std::min(first + per, d.total_blocks);
+      decode_write(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+    }
+  } else if (mode == 0) {
+    int32_t pred[kMaxComp] = {0, 0, 0};
+    decode_write(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, sink);
+  } else {
+    model_huffman_spec(br, im, (uint32_t)ds.len * 8, d.total_blocks, lanes, sink, stats);
+  }
+  if (cap) cap->coef = coef;
+  // k_idct
+  std::vector<uint8_t> planes;
+  int64_t psz = 0;
+  for (int c = 0; c < d.ncomp; ++c) psz += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
+  planes.resize(psz);
+  for (int c = 0; c < d.ncomp; ++c) {
+    const CompDesc& cd = d.comp[c];
+    int pitch = cd.bw * 8;
+    for (int by = 0; by < cd.bh; ++by)
+      for (int bx = 0; bx < cd.bw; ++bx)
+        idct_islow_fast(coef.data() + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64, d.qt[cd.tq],
+                   planes.data() + cd.plane_off + (int64_t)by * 8 * pitch + bx * 8, pitch);
+  }
+  if (cap) cap->planes = planes;
+  // k_color
+  PlaneView pv[kMaxComp];
+  for (int c = 0; c < d.ncomp; ++c) {
+    const CompDesc& cd = d.comp[c];
+    pv[c].p = planes.data() + cd.plane_off;
+    pv[c].pitch = cd.bw * 8;
+    pv[c].dw = cd.dw;
+    pv[c].dh = cd.dh;
+    pv[c].hf = d.max_h / cd.h;
+    pv[c].vf = d.max_v / cd.v;
+    pv[c].method = upsample_method(pv[c].hf, pv[c].vf, cd.dw);
+  }
+  for (int y = 0; y < d.height; ++y)
+    for (int x = 0; x < d.width; ++x) {
+      uint8_t* o = out_rgb + ((int64_t)y * d.width + x) * 3;
+      if (d.ncomp == 1) {
+        o[0] = o[1] = o[2] = (uint8_t)upsample_at(pv[0], x, y);
+      } else {
+        int a = upsample_at(pv[0], x, y), b = upsample_at(pv[1], x, y), c = upsample_at(pv[2], x, y);
+        if (d.color == kYCbCr) {
+          ycc_to_rgb(a, b, c, o);
+        } else {
+          o[0] = (uint8_t)a;
+          o[1] = (uint8_t)b;
+          o[2] = (uint8_t)c;
+        }
+      }
+    }
+  return DINO_IMG_OK;
+}
+
+// ---- k_rcoeffs + k_hresize + k_augment for one view ---------------------------
+struct ViewModel {
+  std::vector<int32_t> hb, ht, vb, vt;
+  int kh = 0, kv = 0;
+  std::vector<uint8_t> tmp;  // horizontal pass output, crop_h x S x 3
+};
+
+inline void model_coeffs(int in_size, int S, std::vector<int32_t>& b, std::vector<int32_t>& t, int& k) {
+  k = resample_ksize(in_size, S);
+  b.assign(2 * S, 0);
+  t.assign((size_t)S * k, 0);
+  for (int x = 0; x < S; ++x) resample_coeffs_one(in_size, S, x, k, &b[2 * x], &b[2 * x + 1], &t[(size_t)x * k]);
+}
+
+// Resized + flipped crop, planar u8 [3][S][S].
+inline void model_resize_planar(const uint8_t* rgb, int W, int H, const dino_view_params& p, uint8_t* planes) {
+  const int S = p.out_size;
+  const bool need_h = p.crop_w != S, need_v = p.crop_h != S;
+  SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  ViewModel vm;
+  if (need_h) {
+    model_coeffs(p.crop_w, S, vm.hb, vm.ht, vm.kh);
+    CoefView cv{vm.hb.data(), vm.ht.data(), vm.kh};
+    vm.tmp.assign((size_t)p.crop_h * S * 3, 0);
+    for (int r = 0; r < p.crop_h; ++r)
+      for (int x = 0; x < S; ++x)
+        for (int ch = 0; ch < 3; ++ch) vm.tmp[((size_t)r * S + x) * 3 + ch] = hresize_at(src, cv, r, x, ch);
+    src = SrcView{vm.tmp.data(), (int64_t)S * 3};
+  }
+  if (need_v) model_coeffs(p.crop_h, S, vm.vb, vm.vt, vm.kv);
+  CoefView cvv{vm.vb.data(), vm.vt.data(), vm.kv};
+  for (int y = 0; y < S; ++y)
+    for (int x = 0; x < S; ++x) {
+      int xo = p.flip ? S - 1 - x : x;
+      for (int ch = 0; ch < 3; ++ch) {
+        uint8_t v = need_v ? vresize_at(src, cvv, y, x, ch) : src.base[(int64_t)y * src.pitch + (int64_t)x * 3 + ch];
+        planes[(size_t)ch * S * S + (size_t)y * S + xo] = v;
+      }
+    }
+}
+
+inline int host_model_resized_crop(const uint8_t* rgb, int W, int H, const dino_view_params& p, uint8_t* out_hwc) {
+  const int S = p.out_size;
+  std::vector<uint8_t> pl((size_t)3 * S * S);
+  model_resize_planar(rgb, W, H, p, pl.data());
+  for (int i = 0; i < S * S; ++i)
+    for (int ch = 0; ch < 3; ++ch) out_hwc[(size_t)i * 3 + ch] = pl[(size_t)ch * S * S + i];
+  return 0;
+}
+
+inline int host_model_augment(const uint8_t* rgb, int W, int H, const dino_view_params& p, const float* mean,
+                              const float* stdv, int out_dtype, void* out) {
+  const int S = p.out_size;
+  const int64_t N = (int64_t)S * S;
+  std::vector<uint8_t> pl((size_t)3 * N);
+  model_resize_planar(rgb, W, H, p, pl.data());
+  uint8_t *R = pl.data(), *G = R + N, *B = G + N;
+  JitterPlan jp = make_jitter_plan(p);
+  int hd = hue_delta(p.hue);
+  uint64_t lsum = 0;
+  for (int64_t i = 0; i < N; ++i) {  // pass A: ops before contrast + L sum
+    int r = R[i], g = G[i], b = B[i];
+    jitter_stage0(jp, r, g, b, p, hd);
+    R[i] = (uint8_t)r;
+    G[i] = (uint8_t)g;
+    B[i] = (uint8_t)b;
+    lsum += (uint64_t)rgb_to_l(r, g, b);
+  }
+  int cmean = contrast_mean_from_sum(lsum, N);
+  for (int64_t i = 0; i < N; ++i) {  // pass B: contrast, later ops, grayscale
+    int r = R[i], g = G[i], b = B[i];
+    jitter_stage1(jp, r, g, b, p, cmean, hd);
+    R[i] = (uint8_t)r;
+    G[i] = (uint8_t)g;
+    B[i] = (uint8_t)b;
+  }
+  float k1[16], k2[256];
+  int ks = p.ksize;
+  if (p.blur) {
+    gaussian_kernel1d(ks, p.sigma, k1);
+    for (int a = 0; a < ks; ++a)
+      for (int b = 0; b < ks; ++b) k2[a * ks + b] = k1[a] * k1[b];
+  }
+  for (int ch = 0; ch < 3; ++ch)
+    for (int y = 0; y < S; ++y)
+      for (int x = 0; x < S; ++x) {
+        const uint8_t* plane = pl.data() + (size_t)ch * N;
+        int v = p.blur ? blur_at(plane, S, y, x, k2, ks) : plane[(size_t)y * S + x];
+        if (p.solarize) v = solarize_u8(v);
+        float f = u8_normalize(v, mean[ch], stdv[ch]);
+        size_t o = (size_t)ch * N + (size_t)y * S + x;
+        if (out_dtype == DINO_OUT_BF16) ((uint16_t*)out)[o] = f32_to_bf16(f);
+        else if (out_dtype == DINO_OUT_FP32) ((float*)out)[o] = f;
+        else ((uint8_t*)out)[o] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f)));
+      }
+  return 0;
+}
+
+}  // namespace dino
