@@ -1,0 +1,283 @@
+#!/usr/bin/env python
+"""Stage-3 throughput benchmark (BASELINE.json metric).
+
+One step = the full Stage-3 hot path over one batch of ``--batch`` JPEGs whose
+bytes are already resident in HBM: decode (parse, destuff, Huffman, IDCT,
+upsample+colour) + 10 views (2x224^2 + 8x96^2: random-resized crop, flip,
+colour jitter, grayscale, blur, solarize, normalize -> bf16 NCHW) — reference
+``CPUAugPipeline.run_one_batch`` (cpu.py:309-367).
+
+Workload (BASELINE.json configs[1]): per GPU, a 50 000-image dataset of
+synthetic textured 640x480 q85 4:2:0 JPEGs resident in HBM (``--unique``
+distinct encodes tiled to ``--images``), batch 512.  Multi-GPU: one process per
+GPU (torchrun), each rank with its own images and seed (seed + rank), no
+collective on the data path; a barrier + MAX over ranks brackets the timed
+region (weak scaling).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import random
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from multiprocessing import get_context
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "images/sec decode+10-crop, device-resident (JPEG bytes in HBM), 1/2/4/8 GPU"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def _gen_one(args):
+    w, h, seed, mixed = args
+    from dataloader_amd.synthetic import encode_jpeg, textured_rgb
+    rng = np.random.default_rng(seed)
+    if mixed:
+        short = int(rng.integers(224, 1601))
+        aspect = float(rng.uniform(0.75, 4.0 / 3.0))
+        long_ = max(short, int(round(short * max(aspect, 1.0 / aspect))))
+        w, h = (long_, short) if rng.random() < 0.5 else (short, long_)
+    return encode_jpeg(textured_rgb(w, h, rng), quality=85)
+
+
+def make_unique(n: int, w: int, h: int, base_seed: int, mixed: bool, procs: int) -> list[bytes]:
+    # 'spawn': never fork a process that may already hold a HIP context
+    jobs = [(w, h, base_seed * 100003 + k, mixed) for k in range(n)]
+    with get_context("spawn").Pool(max(1, procs)) as pool:
+        return pool.map(_gen_one, jobs, chunksize=4)
+
+
+def jpeg_meta(j: bytes):
+    import io
+
+    from PIL import Image
+    im = Image.open(io.BytesIO(j))
+    return im.size
+
+
+def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int) -> dict:
+    """Per-image algorithmic bytes of the path and of each kernel's interface."""
+    s_jpeg = float(np.mean([len(j) for j in jpegs]))
+    dims = [jpeg_meta(j) for j in jpegs]
+    px = float(np.mean([w * h for w, h in dims]))
+    # 4:2:0 coefficient count: luma + 2 quarter-size chroma, padded to 16x16 MCUs
+    blocks = float(np.mean([((w + 15) // 16) * ((h + 15) // 16) * 6 for w, h in dims]))
+    out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
+    return {
+        "path": s_jpeg + out,                       # S_jpeg + 1 044 480 B (bf16)
+        "k_destuff": 2 * s_jpeg,
+        "k_huffman": s_jpeg + blocks * 128,          # entropy bytes in, int16 coefficients out
+        "k_idct": blocks * 128 + blocks * 64,
+        "k_color": blocks * 64 + px * 3,
+        "k_hresize": None,
+        "k_augment_global": out_bytes * 3 * n_g * g * g,   # output write floor
+        "k_augment_local": out_bytes * 3 * n_l * l * l,
+        "s_jpeg": s_jpeg,
+        "pixels": px,
+    }
+
+
+def cpu_baseline(jpegs, seconds: float, batch: int = 32) -> dict:
+    """Reference-faithful CPUBackend restatement timed on this host's cores (oracle, kind 'port')."""
+    import torch
+
+    from oracle import cpu_ref
+    torch.set_num_threads(1)
+    workers = min(batch, os.cpu_count() or 4, 16)             # cpu.py:286, 303-306
+    cfg = cpu_ref.AugCfg()
+    table = cpu_ref.view_table(cfg)
+    gen = torch.Generator().manual_seed(0)
+    rnd = random.Random(0)
+
+    def sample(j):
+        img = cpu_ref.decode_rgb(j)
+        w, h = img.size
+        outs = []
+        for spec in table:                                     # decode per view, as cpu.py:251
+            p = cpu_ref.draw_params_like_cpubackend(w, h, spec, cfg, gen, rnd)
+            outs.append(cpu_ref.augment_one(j, p))
+        return outs
+
+    done = 0
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        k = 0
+        while True:
+            b = [jpegs[(k * batch + i) % len(jpegs)] for i in range(batch)]
+            res = list(ex.map(sample, b))
+            _ = [torch.stack([r[v] for r in res]) for v in range(len(table))]
+            done += batch
+            k += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "images/s", "cores": workers, "kind": "port",
+            "sample": f"{done} images ({batch}/batch) of the same synthetic JPEG pool, CPUBackend restatement "
+                      f"(PIL+torch), decode per view, ThreadPoolExecutor({workers}), {dt:.1f}s"}
+
+
+def load_traffic(kernel: str):
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None
+    try:
+        d = json.loads(f.read_text())
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:  # noqa: BLE001
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--images", type=int, default=50000)
+    ap.add_argument("--unique", type=int, default=256)
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600}")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--h2d", action="store_true", help="also time the H2D-inclusive rate (pinned host bytes)")
+    ap.add_argument("--kernel-json", default="", help="write per-kernel times here (rank 0)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    # synthetic data first, before anything initialises the GPU in this process
+    procs = min(16, os.cpu_count() or 4)
+    uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs)
+
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dataloader_amd.config import DINOAugConfig
+    from dataloader_amd.engine import pack_jpegs
+    from dataloader_amd.pipeline import MI355XAugPipeline
+    from dataloader_amd.sharding import rank_seed
+
+    n_img = args.images
+    jpegs = [uniq[i % len(uniq)] for i in range(n_img)]
+    host_buf, offsets = pack_jpegs(jpegs, pin=True)
+    d_bytes = host_buf.to(dev)
+    d_off = offsets.to(dev)
+    torch.cuda.synchronize()
+
+    cfg = DINOAugConfig()
+    B = args.batch
+    pipe = MI355XAugPipeline(None, cfg, B, seed=rank_seed(1234, rank), out_dtype=args.dtype, device=local_rank,
+                             max_image_dim=4096 if args.mixed else 2048)
+    views = pipe.engine.alloc_views(pipe._cfg(cfg.global_crop_size, cfg.local_crop_size), B)
+    n_batches = n_img // B
+
+    def step(k: int):
+        s = (k % n_batches) * B
+        pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    st = pipe.last_status()
+    if (st != 0).any():
+        raise RuntimeError(f"decode failures in warmup batch: {np.unique(st, return_counts=True)}")
+    pipe.engine.set_timing(True)
+    pipe.engine.kernel_times()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    ktimes = pipe.engine.kernel_times()
+    pipe.engine.set_timing(False)
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    h2d_rate = None
+    if args.h2d:
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for k in range(args.steps):
+            s = (k % n_batches) * B
+            base = int(offsets[s])
+            nbytes = int(offsets[s + B]) - base
+            hb = host_buf[base:base + nbytes].to(dev, non_blocking=True)
+            ho = (offsets[s:s + B + 1] - base).to(dev, non_blocking=True)
+            pipe.run_device_batch(hb, ho, B, views=views)
+        torch.cuda.synchronize()
+        h2d_rate = args.steps * B / (time.perf_counter() - t1)
+
+    value = world * args.steps * B / dt
+    out_bytes = {"bf16": 2, "fp8": 1, "fp32": 4}[args.dtype]
+    ab = algorithmic_bytes(uniq, cfg.global_crop_size, cfg.local_crop_size, cfg.n_global_crops,
+                           cfg.n_local_crops, out_bytes)
+    per_kernel = {k: {"avg_ms": (ms / n if n else 0.0), "launches": n, "total_ms": ms} for k, (ms, n) in ktimes.items()}
+    dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
+    dom_bytes = ab.get(dom)
+    roof = None
+    if dom_bytes:
+        bytes_launch = dom_bytes * B
+        achieved = bytes_launch / (per_kernel[dom]["avg_ms"] * 1e-3) / 1e9
+        traffic = load_traffic(dom)
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": dom,
+                "algorithmic_bytes_per_launch": int(bytes_launch)}
+    ms_step = dt / args.steps * 1e3
+    path_gbs = ab["path"] * B * world / (dt / args.steps) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(uniq, args.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": ("C3 mixed short side 224-1600" if args.mixed else
+                                    f"C2 {args.images} synthetic {args.width}x{args.height} q85 4:2:0 JPEGs "
+                                    "resident in HBM") + f", 2x224^2+8x96^2 views, {args.dtype} out",
+                       "global_batch": B * world, "batch_per_gpu": B, "parallelism": f"dp{world}",
+                       "mean_jpeg_bytes": round(ab["s_jpeg"]), "out_dtype": args.dtype},
+            "roofline": roof,
+            "path_roofline": {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
+                              "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5)},
+            "kernels_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in per_kernel.items()},
+            "cpu_baseline": cpu,
+        }
+        if h2d_rate is not None:
+            line["h2d_inclusive_images_per_s"] = round(h2d_rate, 1)
+        print(json.dumps(line), flush=True)
+        if args.kernel_json:
+            Path(args.kernel_json).write_text(json.dumps(per_kernel, indent=1))
+    pipe.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

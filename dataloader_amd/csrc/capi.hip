@@ -44,8 +44,9 @@ struct dino_ctx {
   ViewPlan* d_plan = nullptr;
   dino_view_params* d_params = nullptr;
   uint8_t* d_gcrop = nullptr;
-  void** d_view_ptrs = nullptr;
   int32_t last_batch = -1;
+  KernelTimer* timer = nullptr;
+  KernelTimer* tm() { return timer && timer->enabled ? timer : nullptr; }
 };
 
 extern "C" {
@@ -74,8 +75,7 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
   if ((e = hipMalloc(&c->d_desc, sizeof(ImgDesc) * L.max_batch)) != hipSuccess ||
       (e = hipMalloc(&c->d_ws, c->ws_size)) != hipSuccess || (e = hipMalloc(&c->d_aws, c->aws_size)) != hipSuccess ||
       (e = hipMalloc(&c->d_plan, sizeof(ViewPlan) * nrec)) != hipSuccess ||
-      (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess ||
-      (e = hipMalloc(&c->d_view_ptrs, sizeof(void*) * L.max_views)) != hipSuccess) {
+      (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess) {
     dino_ctx_destroy(c);
     return hip_fail(e, "dino_ctx_create: hipMalloc");
   }
@@ -98,7 +98,10 @@ int dino_ctx_destroy(dino_ctx* c) {
   (void)hipFree(c->d_plan);
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_gcrop);
-  (void)hipFree(c->d_view_ptrs);
+  if (c->timer) {
+    c->timer->destroy();
+    delete c->timer;
+  }
   delete c;
   return DINO_OK;
 }
@@ -110,7 +113,7 @@ int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, i
     return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
   hipStream_t s = (hipStream_t)stream;
   DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size};
-  hipError_t e = launch_decode(a, s);
+  hipError_t e = launch_decode(a, s, c->tm());
   if (e != hipSuccess) return hip_fail(e, "dino_decode");
   if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
   c->last_batch = batch;
@@ -142,7 +145,8 @@ int dino_sample_params(dino_ctx* c, const dino_aug_config* cfg, uint64_t seed, u
   if (c->last_batch < 0) return fail(DINO_EINVAL, "dino_sample_params: no decoded batch%s%lld");
   int r = check_cfg(c, cfg);
   if (r) return r;
-  hipError_t e = launch_params(c->d_desc, c->last_batch, *cfg, seed, batch_index, d_params, (hipStream_t)stream);
+  hipError_t e = launch_params(c->d_desc, c->last_batch, *cfg, seed, batch_index, d_params, (hipStream_t)stream,
+                                c->tm());
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_sample_params");
 }
 
@@ -153,12 +157,14 @@ int dino_augment(dino_ctx* c, const dino_aug_config* cfg, const dino_view_params
   int r = check_cfg(c, cfg);
   if (r) return r;
   const int nv = cfg->n_global + cfg->n_local;
+  if (nv > kMaxViews) return fail(DINO_EINVAL, "dino_augment: more than %s%lld views", "", kMaxViews);
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemcpyAsync(c->d_view_ptrs, d_views, sizeof(void*) * nv, hipMemcpyHostToDevice, s);
-  if (e != hipSuccess) return hip_fail(e, "dino_augment(view ptrs)");
-  AugmentArgs a{c->d_desc, c->last_batch, d_params, c->d_plan, c->d_ws, c->d_aws, c->aws_size, c->d_gcrop,
-                (void* const*)c->d_view_ptrs, *cfg};
-  e = launch_augment(a, s);
+  AugmentArgs a{c->d_desc, c->last_batch, d_params, c->d_plan, c->d_ws, c->d_aws, c->aws_size, c->d_gcrop, {}, *cfg};
+  for (int v = 0; v < nv; ++v) {
+    if (!d_views[v]) return fail(DINO_EINVAL, "dino_augment: null output pointer for view %s%lld", "", v);
+    a.views.p[v] = d_views[v];
+  }
+  hipError_t e = launch_augment(a, s, c->tm());
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_augment");
 }
 
@@ -190,6 +196,30 @@ int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32
                    log_aspect_max, n_masks, d_py_state, d_np_state, d_out, scratch, s);
   (void)hipFreeAsync(scratch, s);
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_masks");
+}
+
+int dino_set_timing(dino_ctx* c, int32_t enable) {
+  if (!c) return fail(DINO_EINVAL, "dino_set_timing: null ctx%s%lld");
+  if (!c->timer) c->timer = new KernelTimer();
+  c->timer->enabled = enable != 0;
+  if (c->timer->created) c->timer->reset();
+  return DINO_OK;
+}
+
+int dino_kernel_times(dino_ctx* c, double* total_ms, int64_t* counts, int32_t n) {
+  if (!c || !total_ms || !counts) return fail(DINO_EINVAL, "dino_kernel_times: null argument%s%lld");
+  for (int i = 0; i < n; ++i) {
+    total_ms[i] = 0.0;
+    counts[i] = 0;
+  }
+  if (!c->timer || !c->timer->created) return DINO_OK;
+  c->timer->collect();
+  for (int i = 0; i < n && i < kKNumKernels; ++i) {
+    total_ms[i] = c->timer->total_ms[i];
+    counts[i] = c->timer->count[i];
+  }
+  c->timer->reset();
+  return DINO_OK;
 }
 
 int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream) {

@@ -244,7 +244,16 @@ struct RangeOut {
   int32_t dcsum[kMaxComp];
 };
 
+// A state is only ever produced by the decoder itself; clamp anyway so that no
+// index derived from it can leave the MCU tables.
+DHD HState sanitize(HState st, int bpm) {
+  if (st.c < 0 || st.c >= bpm) st.c = 0;
+  if (st.z < 0 || st.z > 63) st.z = 0;
+  return st;
+}
+
 DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, uint32_t end) {
+  st = sanitize(st, im.blocks_per_mcu);
   RangeOut r;
   r.nblk = 0;
   for (int c = 0; c < kMaxComp; ++c) r.dcsum[c] = 0;
@@ -271,6 +280,7 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 template <typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
                           int32_t total_blocks, int32_t* pred, Sink& sink) {
+  st = sanitize(st, im.blocks_per_mcu);
   BitCursor cur;
   bc_init(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;

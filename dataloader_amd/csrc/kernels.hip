@@ -24,6 +24,9 @@
 #include "mask.hpp"
 #include "sampler.hpp"
 
+#include <stdio.h>
+#include <stdlib.h>
+
 namespace dino {
 
 // ---------------------------------------------------------------------------
@@ -221,6 +224,9 @@ struct HuffLds {
   int32_t bad;
 };
 
+static_assert(sizeof(HuffLds) == 58600, "HuffLds layout");
+static_assert(sizeof(ImgDesc) == 896, "ImgDesc layout");
+
 struct LdsSink {
   int16_t* blk;
   int16_t* coef;  // image coefficient area (global)
@@ -320,6 +326,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restr
     L.S[t] = s0;
     L.R[t] = decode_range(br, im, s0, my_end_range);
   }
+  __syncthreads();  // phase-1 results of lane t-1 (another wave) must be visible before round 0 reads them
   for (int round = 0; round < kHuffThreads + 1; ++round) {
     HState want;
     bool redo = false;
@@ -569,8 +576,8 @@ template <typename OutT, bool kLdsCrop>
 __global__ void __launch_bounds__(512) k_augment(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  const ViewPlan* __restrict__ plan, int nv, int v0,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws,
-                                                 uint8_t* __restrict__ gcrop, void* const* __restrict__ views,
-                                                 dino_aug_config cfg, int S) {
+                                                 uint8_t* __restrict__ gcrop, ViewPtrs views, dino_aug_config cfg,
+                                                 int S) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   AugLdsHead& H = *reinterpret_cast<AugLdsHead*>(smem);
   float* s_k1 = H.k1;
@@ -581,7 +588,7 @@ __global__ void __launch_bounds__(512) k_augment(const ImgDesc* __restrict__ des
   const dino_view_params p = prm[i];
   const ViewPlan vp = plan[i];  // vp.ok implies p.out_size == S and an in-bounds crop
   const int64_t N = (int64_t)S * S;
-  OutT* out = (OutT*)views[v] + (int64_t)b * 3 * N;
+  OutT* out = (OutT*)views.p[v] + (int64_t)b * 3 * N;
   const int t = threadIdx.x, nt = blockDim.x;
   if (!vp.ok) {  // reference cpu.py:253: undecodable -> zeros
     for (int64_t e = t; e < 3 * N; e += nt) out[e] = (OutT)0;
@@ -705,74 +712,152 @@ __global__ void k_info(const ImgDesc* __restrict__ desc, int B, int32_t* __restr
 // ===========================================================================
 namespace dino {
 
+void KernelTimer::begin(int k, hipStream_t s) {
+  if (!enabled) return;
+  if (!created) {
+    for (int i = 0; i < kMaxPending; ++i) {
+      (void)hipEventCreate(&ev[i][0]);
+      (void)hipEventCreate(&ev[i][1]);
+    }
+    created = true;
+    reset();
+  }
+  if (n >= kMaxPending) collect();
+  id[n] = k;
+  (void)hipEventRecord(ev[n][0], s);
+}
+
+void KernelTimer::end(hipStream_t s) {
+  if (!enabled || !created) return;
+  (void)hipEventRecord(ev[n][1], s);
+  ++n;
+}
+
+void KernelTimer::collect() {
+  for (int i = 0; i < n; ++i) {
+    float ms = 0.f;
+    (void)hipEventSynchronize(ev[i][1]);
+    if (hipEventElapsedTime(&ms, ev[i][0], ev[i][1]) == hipSuccess) {
+      total_ms[id[i]] += ms;
+      count[id[i]] += 1;
+    }
+  }
+  n = 0;
+}
+
+void KernelTimer::reset() {
+  n = 0;
+  for (int i = 0; i < kKNumKernels; ++i) {
+    total_ms[i] = 0.0;
+    count[i] = 0;
+  }
+}
+
+void KernelTimer::destroy() {
+  if (!created) return;
+  for (int i = 0; i < kMaxPending; ++i) {
+    (void)hipEventDestroy(ev[i][0]);
+    (void)hipEventDestroy(ev[i][1]);
+  }
+  created = false;
+}
+
+// DINO_SYNC_CHECK=1: synchronise after every kernel and report which one failed
+// (debugging aid; pinpoints a faulting kernel instead of a later sync point).
+static const bool g_sync_check = [] {
+  const char* v = getenv("DINO_SYNC_CHECK");
+  return v && v[0] == '1';
+}();
+static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct",
+                                                       "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
+                                                       "k_augment_global", "k_augment_local"};
+const char* g_failed_kernel = "";
+
+#define TIMED(tm, kid, s, launch)                          \
+  do {                                                     \
+    if (tm) (tm)->begin(kid, s);                           \
+    launch;                                                \
+    if (tm) (tm)->end(s);                                  \
+    if (g_sync_check) {                                    \
+      hipError_t se_ = hipStreamSynchronize(s);            \
+      if (se_ == hipSuccess) se_ = hipGetLastError();      \
+      if (se_ != hipSuccess) {                             \
+        g_failed_kernel = kKernelNames[kid];               \
+        fprintf(stderr, "[dino] %s failed: %s\n", kKernelNames[kid], hipGetErrorString(se_)); \
+        return se_;                                        \
+      }                                                    \
+    }                                                      \
+  } while (0)
+
 static int huff_lds_bytes() { return (int)((sizeof(HuffLds) + 15) & ~(size_t)15); }
 
-hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
   if (B <= 0) return hipSuccess;
-  k_parse<<<(B + 63) / 64, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc);
-  k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size);
-  k_destuff<<<B, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws);
+  TIMED(tm, kKParse, s, (k_parse<<<(B + 63) / 64, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc)));
+  TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
+  TIMED(tm, kKDestuff, s, (k_destuff<<<B, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huffman), hipFuncAttributeMaxDynamicSharedMemorySize,
                         huff_lds_bytes());
     attr_set = true;
   }
-  k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws);
-  k_idct<<<dim3(32, B), 256, 0, s>>>(a.desc, a.ws);
-  k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws);
+  TIMED(tm, kKHuffman, s, (k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  TIMED(tm, kKIdct, s, (k_idct<<<dim3(32, B), 256, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
   return hipGetLastError();
 }
 
 hipError_t launch_params(const ImgDesc* desc, int batch, const dino_aug_config& cfg, uint64_t seed,
-                         uint64_t batch_index, dino_view_params* out, hipStream_t s) {
+                         uint64_t batch_index, dino_view_params* out, hipStream_t s, KernelTimer* tm) {
   const int n = batch * (cfg.n_global + cfg.n_local);
   if (n <= 0) return hipSuccess;
-  k_params<<<(n + 63) / 64, 64, 0, s>>>(desc, batch, cfg, seed, batch_index, out);
+  TIMED(tm, kKParams, s, (k_params<<<(n + 63) / 64, 64, 0, s>>>(desc, batch, cfg, seed, batch_index, out)));
   return hipGetLastError();
 }
 
 template <typename OutT>
-static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, int S, hipStream_t s) {
+static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, int S, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch, nv = a.cfg.n_global + a.cfg.n_local;
   if (nvc <= 0) return hipSuccess;
-  k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws);
-  k_hresize<<<dim3(8, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws);
+  const int kaug = v0 == 0 ? kKAugmentGlobal : kKAugmentLocal;
+  TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
+  TIMED(tm, kKHresize, s, (k_hresize<<<dim3(8, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
   const int threads = S >= 128 ? 512 : 256;
   if (S <= kMaxLdsCropSize) {
     const int lds = (int)sizeof(AugLdsHead) + 3 * S * S;
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_augment<OutT, true>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    k_augment<OutT, true><<<dim3(nvc, B), threads, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.gcrop,
-                                                           a.d_views, a.cfg, S);
+    TIMED(tm, kaug, s, (k_augment<OutT, true><<<dim3(nvc, B), threads, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
+                                                                             a.aws, a.gcrop, a.views, a.cfg, S)));
   } else {
     if (!a.gcrop) return hipErrorInvalidValue;
-    k_augment<OutT, false><<<dim3(nvc, B), threads, sizeof(AugLdsHead), s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
-                                                                            a.aws, a.gcrop, a.d_views, a.cfg, S);
+    TIMED(tm, kaug, s, (k_augment<OutT, false><<<dim3(nvc, B), threads, sizeof(AugLdsHead), s>>>(
+                           a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.gcrop, a.views, a.cfg, S)));
   }
   return hipGetLastError();
 }
 
 template <typename OutT>
-static hipError_t launch_augment_t(const AugmentArgs& a, hipStream_t s) {
-  hipError_t e = launch_augment_class<OutT>(a, 0, a.cfg.n_global, a.cfg.global_size, s);
+static hipError_t launch_augment_t(const AugmentArgs& a, hipStream_t s, KernelTimer* tm) {
+  hipError_t e = launch_augment_class<OutT>(a, 0, a.cfg.n_global, a.cfg.global_size, s, tm);
   if (e != hipSuccess) return e;
-  return launch_augment_class<OutT>(a, a.cfg.n_global, a.cfg.n_local, a.cfg.local_size, s);
+  return launch_augment_class<OutT>(a, a.cfg.n_global, a.cfg.n_local, a.cfg.local_size, s, tm);
 }
 
-hipError_t launch_augment(const AugmentArgs& a, hipStream_t s) {
+hipError_t launch_augment(const AugmentArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch, nv = a.cfg.n_global + a.cfg.n_local;
   if (B <= 0 || nv <= 0) return hipSuccess;
-  k_vplan<<<1, 1024, 0, s>>>(a.desc, a.params, B, nv, a.cfg.n_global, a.cfg.global_size, a.cfg.local_size,
-                             a.aws_size, a.plan);
+  TIMED(tm, kKVplan, s, (k_vplan<<<1, 1024, 0, s>>>(a.desc, a.params, B, nv, a.cfg.n_global, a.cfg.global_size,
+                                                     a.cfg.local_size, a.aws_size, a.plan)));
   switch (a.cfg.out_dtype) {
     case DINO_OUT_FP32:
-      return launch_augment_t<float>(a, s);
+      return launch_augment_t<float>(a, s, tm);
     case DINO_OUT_FP8_E4M3:
-      return launch_augment_t<uint8_t>(a, s);
+      return launch_augment_t<uint8_t>(a, s, tm);
     default:
-      return launch_augment_t<uint16_t>(a, s);
+      return launch_augment_t<uint16_t>(a, s, tm);
   }
 }
 

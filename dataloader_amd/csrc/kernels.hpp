@@ -25,6 +25,29 @@ struct AugLdsHead {
 // Largest S whose three u8 planes fit next to the header in 160 KiB of LDS.
 constexpr int kMaxLdsCropSize = 233;
 
+// Optional per-kernel HIP-event timing (bench / profiling).  Events are recorded on
+// the launch stream around each kernel; elapsed times are summed on demand.
+enum KernelId : int {
+  kKParse = 0, kKPlan, kKDestuff, kKHuffman, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
+  kKAugmentGlobal, kKAugmentLocal, kKNumKernels
+};
+
+struct KernelTimer {
+  static constexpr int kMaxPending = 4096;
+  hipEvent_t ev[kMaxPending][2];
+  int id[kMaxPending];
+  int n = 0;
+  bool enabled = false;
+  bool created = false;
+  double total_ms[kKNumKernels];
+  int64_t count[kKNumKernels];
+  void begin(int k, hipStream_t s);
+  void end(hipStream_t s);
+  void collect();  // synchronises the recorded events, accumulates, resets the pending list
+  void reset();
+  void destroy();
+};
+
 struct DecodeArgs {
   const uint8_t* bytes;
   const int64_t* offsets;
@@ -33,6 +56,13 @@ struct DecodeArgs {
   ImgDesc* desc;
   uint8_t* ws;
   int64_t ws_size;
+};
+
+// Output pointers travel as a kernel argument (no host->device copy whose source
+// could die before an asynchronous copy reads it).
+constexpr int kMaxViews = 32;
+struct ViewPtrs {
+  void* p[kMaxViews];
 };
 
 struct AugmentArgs {
@@ -44,14 +74,14 @@ struct AugmentArgs {
   uint8_t* aws;
   int64_t aws_size;
   uint8_t* gcrop;          // global crop scratch for S > kMaxLdsCropSize (may be null otherwise)
-  void* const* d_views;    // device array of n_views output pointers
+  ViewPtrs views;          // n_views output pointers (device memory)
   dino_aug_config cfg;
 };
 
-hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm = nullptr);
 hipError_t launch_params(const ImgDesc* desc, int batch, const dino_aug_config& cfg, uint64_t seed,
-                         uint64_t batch_index, dino_view_params* out, hipStream_t s);
-hipError_t launch_augment(const AugmentArgs& a, hipStream_t s);
+                         uint64_t batch_index, dino_view_params* out, hipStream_t s, KernelTimer* tm = nullptr);
+hipError_t launch_augment(const AugmentArgs& a, hipStream_t s, KernelTimer* tm = nullptr);
 hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_t s);
 hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s);
 hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,

@@ -78,6 +78,20 @@ class IngestEngine:
                                               _stream_handle(self.device)), "dino_debug_region")
         return out
 
+    KERNEL_NAMES = ["k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct", "k_color", "k_params", "k_vplan",
+                    "k_rcoeffs", "k_hresize", "k_augment_global", "k_augment_local"]
+
+    def set_timing(self, enable: bool) -> None:
+        _lib.check(self.lib.dino_set_timing(self._ctx, int(enable)), "dino_set_timing")
+
+    def kernel_times(self) -> dict[str, tuple[float, int]]:
+        """{kernel: (total ms, launches)} since the last call (HIP events on the launch stream)."""
+        n = len(self.KERNEL_NAMES)
+        ms = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int64 * n)()
+        _lib.check(self.lib.dino_kernel_times(self._ctx, ms, cnt, n), "dino_kernel_times")
+        return {k: (ms[i], cnt[i]) for i, k in enumerate(self.KERNEL_NAMES)}
+
     # ----------------------------------------------------------------- augment
     def sample_params(self, cfg, seed: int, batch_index: int, out: torch.Tensor | None = None) -> torch.Tensor:
         n = self.last_batch * (cfg.n_global + cfg.n_local)

@@ -137,6 +137,14 @@ int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32
                int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
                uint32_t* d_py_state, uint32_t* d_np_state, uint8_t* d_out, void* stream);
 
+/* Per-kernel HIP-event timing of this ctx's launches (bench / profiling).
+ * Kernel ids: 0 parse, 1 plan, 2 destuff, 3 huffman, 4 idct, 5 color, 6 params,
+ * 7 vplan, 8 rcoeffs, 9 hresize, 10 augment(global views), 11 augment(local views).
+ * dino_kernel_times synchronises the recorded events, returns the sums since the
+ * last call (ms, launches) and resets them. */
+int dino_set_timing(dino_ctx* ctx, int32_t enable);
+int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t n);
+
 /* Debug / test introspection of the last decoded batch: copy image `index`'s
  * region (0 descriptor, 1 destuffed entropy bytes, 2 DCT coefficients,
  * 3 component planes, 4 RGB) into d_dst (<= max_bytes).  Synchronises the stream. */

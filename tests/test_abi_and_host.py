@@ -1,0 +1,116 @@
+"""C-ABI surface and host-side logic (CPU only: no compute calls)."""
+
+from __future__ import annotations
+
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def test_library_exports_every_header_symbol():
+    from dataloader_amd import _lib
+    header = (ROOT / "include" / "dino_ingest.h").read_text()
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(dino_\w+)\(", header, flags=re.M))
+    assert declared, "no declarations parsed"
+    lib = _lib.load()
+    for name in declared:
+        assert hasattr(lib, name), f"{name} declared in dino_ingest.h but not exported"
+    assert declared == set(_lib.exported_symbols())
+    assert lib.dino_abi_version() == 1
+
+
+def test_ctx_create_fails_loudly_without_gpu():
+    from dataloader_amd import _lib
+    from dataloader_amd.engine import IngestEngine
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(_lib.DinoError):
+        IngestEngine(0, max_batch=4)
+
+
+def test_bad_arguments_rejected_before_any_launch():
+    from dataloader_amd import _lib
+    from dataloader_amd.params import DinoLimits
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    assert lib.dino_ctx_create(0, ctypes.byref(DinoLimits(0, 10, 224, 4096, 0)), ctypes.byref(ctx)) == -1
+    assert b"max_batch" in lib.dino_last_error()
+    assert lib.dino_decode(None, None, None, 1, None, None) == -1
+    assert lib.dino_masks(0, 4, 2, 1, 2, 0.0, 1.0, 1, None, None, None, None) == -1
+
+
+def test_pack_jpegs_offsets():
+    from dataloader_amd.engine import pack_jpegs
+    items = [b"abc", np.frombuffer(b"\x01\x02", np.uint8), b"", b"zzzz"]
+    buf, off = pack_jpegs(items, pin=False)
+    assert off.tolist() == [0, 3, 5, 5, 9]
+    assert bytes(buf[:9].numpy()) == b"abc\x01\x02zzzz"
+
+
+def test_config_mirrors_reference_defaults():
+    from dataloader_amd.config import DINOAugConfig, DinoV2AugSpec, PipelineConfig, ResolutionSource
+    c = DINOAugConfig()
+    assert (c.global_crop_size, c.local_crop_size, c.n_views) == (224, 96, 10)
+    assert c.max_global_crop_size == 224 and c.max_local_crop_size == 96
+    assert c.crop_size_at_epoch(5) == 224
+    c2 = DINOAugConfig(resolution_schedule=[(10, 448), (0, 224)])
+    assert c2.crop_size_at_epoch(3) == 224 and c2.crop_size_at_epoch(10) == 448
+    spec = DinoV2AugSpec(aug_cfg=DINOAugConfig(n_local_crops=2))
+    assert spec.output_map == ["view_0", "view_1", "view_2", "view_3"]
+    assert spec.split_views([1, 2, 3, 4]) == ([1, 2], [3, 4]) and spec.supports_masking
+    r = ResolutionSource(32, 16)
+    r.set(64, 32)
+    g, l = r()
+    assert (int(g), int(l)) == (64, 32) and g.dtype == np.int32
+    assert PipelineConfig().output_dtype == "bf16"
+
+
+def test_backend_protocol_surface():
+    from dataloader_amd.backend import MI355XBackend
+    be = MI355XBackend()
+    assert be.name == "mi355x" and be.supports_gpu and be.supports_fp8
+    for m in ("build_shard_cache", "build_pipeline", "build_pipeline_iterator", "build_h2d_stream",
+              "build_fp8_formatter", "init_distributed"):
+        assert callable(getattr(be, m))
+    env = be.init_distributed(rank=2, world_size=8, local_rank=2, local_world_size=8)
+    assert (env.rank, env.world_size, env.topology.is_nvl72) == (2, 8, False)
+
+    class EvalAugSpec:  # unsupported spec types raise TypeError like CPUBackend (cpu.py:708-709)
+        pass
+    from dataloader_amd.config import PipelineConfig
+    with pytest.raises(TypeError):
+        be.build_pipeline(lambda: [], EvalAugSpec(), PipelineConfig())
+
+
+def test_shard_cache_lru(tmp_path):
+    from dataloader_amd.backend import MI355XBackend
+    cache = MI355XBackend().build_shard_cache(max_gb=100 / (1 << 30))
+    paths = []
+    for i in range(3):
+        p = tmp_path / f"s{i}.tar"
+        p.write_bytes(bytes([i]) * 40)
+        paths.append(str(p))
+    for p in paths:
+        assert len(cache.get(p)) == 40
+    assert cache.utilisation <= 1.0
+    with cache.get_view(paths[-1]) as mv:
+        assert bytes(mv[:1]) == b"\x02"
+
+
+def test_masking_generator_validation_matches_reference():
+    from dataloader_amd.masking import MaskingGenerator
+    with pytest.raises(ValueError):
+        MaskingGenerator(4, num_masking_patches=17)
+    with pytest.raises(ValueError):
+        MaskingGenerator(4, num_masking_patches=-1)
+    with pytest.raises(ValueError):
+        MaskingGenerator(8, num_masking_patches=30, min_num_patches=31, max_num_patches=30)
+    MaskingGenerator(8, num_masking_patches=0)  # min > max allowed when target == 0
+    g = MaskingGenerator((10, 16))
+    assert g.get_shape() == (10, 16) and g.num_masking_patches == 80 and "10x16" in repr(g)

@@ -199,3 +199,26 @@ def test_pipeline_iterator_and_close(gpu_device):
     pipe.close()
     with pytest.raises(RuntimeError, match="close"):
         pipe.run_one_batch()
+
+
+def test_bench_pattern_multi_batch(gpu_device):
+    """The benchmark's access pattern: one device-resident dataset, offset slices, reused views."""
+    from dataloader_amd.pipeline import MI355XAugPipeline
+    cfg = DINOAugConfig()
+    uniq = [make_jpeg(640, 480, s) for s in range(8)]
+    jpegs = [uniq[i % 8] for i in range(96)]
+    buf, off = pack_jpegs(jpegs, pin=True)
+    d_bytes, d_off = buf.to(gpu_device), off.to(gpu_device)
+    B = 32
+    pipe = MI355XAugPipeline(None, cfg, B, seed=3, device=0)
+    views = pipe.engine.alloc_views(pipe._cfg(224, 96), B)
+    sums = []
+    for k in range(6):
+        s = (k % 3) * B
+        pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views)
+        assert (pipe.last_status() == 0).all()
+        sums.append(float(views[0].float().abs().sum()))
+    torch.cuda.synchronize()
+    recs = pipe.last_params()
+    _check_views(jpegs[96 - B:], views, recs, cfg.n_views, torch.bfloat16, cfg.mean, cfg.std)
+    pipe.close()
