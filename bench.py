@@ -65,26 +65,40 @@ def jpeg_meta(j: bytes):
     return im.size
 
 
-def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int) -> dict:
-    """Per-image algorithmic bytes of the path and of each kernel's interface."""
+def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int, recs=None) -> dict:
+    """Per-image algorithmic bytes of the path and of each kernel's interface.
+
+    ``recs`` (the last batch's view records) sizes the resize kernels' interfaces
+    from the crops actually drawn: k_hresize reads crop_h*crop_w*3 and writes
+    crop_h*S*3; k_vert reads that and writes the 3*S^2 u8 crop; k_final reads the
+    crop and writes the normalised view.
+    """
     s_jpeg = float(np.mean([len(j) for j in jpegs]))
     dims = [jpeg_meta(j) for j in jpegs]
     px = float(np.mean([w * h for w, h in dims]))
     # 4:2:0 coefficient count: luma + 2 quarter-size chroma, padded to 16x16 MCUs
     blocks = float(np.mean([((w + 15) // 16) * ((h + 15) // 16) * 6 for w, h in dims]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
-    return {
+    ab = {
         "path": s_jpeg + out,                       # SURVEY §8d: S_jpeg + 1 044 480 B (bf16)
         "k_destuff": 2 * s_jpeg,
         "k_huffman": s_jpeg + blocks * 128,          # entropy bytes in, int16 coefficients out
         "k_idct": blocks * 128 + blocks * 64,
         "k_color": blocks * 64 + px * 3,
-        "k_hresize": None,
-        "k_augment_global": out_bytes * 3 * n_g * g * g,   # output write floor
-        "k_augment_local": out_bytes * 3 * n_l * l * l,
+        "k_final_global": (3 + out_bytes * 3) * n_g * g * g,
+        "k_final_local": (3 + out_bytes * 3) * n_l * l * l,
         "s_jpeg": s_jpeg,
         "pixels": px,
     }
+    if recs is not None and len(recs):
+        nv = n_g + n_l
+        r = recs.reshape(-1, nv)
+        hr = (r["crop_h"].astype(np.float64) * 3 * (r["crop_w"] + r["out_size"])).sum(1).mean()
+        ab["k_hresize"] = float(hr)
+        for name, sl, S in (("k_vert_global", slice(0, n_g), g), ("k_vert_local", slice(n_g, nv), l)):
+            rr = r[:, sl]
+            ab[name] = float((rr["crop_h"].astype(np.float64) * 3 * S + 3 * S * S).sum(1).mean())
+    return ab
 
 
 def cpu_baseline(jpegs, seconds: float, batch: int = 32) -> dict:
@@ -235,7 +249,7 @@ def main() -> None:
     value = world * args.steps * B / dt
     out_bytes = {"bf16": 2, "fp8": 1, "fp32": 4}[args.dtype]
     ab = algorithmic_bytes(uniq, cfg.global_crop_size, cfg.local_crop_size, cfg.n_global_crops,
-                           cfg.n_local_crops, out_bytes)
+                           cfg.n_local_crops, out_bytes, recs=pipe.last_params())
     per_kernel = {k: {"avg_ms": (ms / n if n else 0.0), "launches": n, "total_ms": ms} for k, (ms, n) in ktimes.items()}
     dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
     dom_bytes = ab.get(dom)

@@ -50,18 +50,21 @@ struct JitterPlan {
   int32_t n_pre;        // ops in stage 0
   int32_t has_contrast; // contrast op present (then it is the first op of stage 1)
   int32_t n_post;       // ops after contrast
-  uint8_t pre[4], post[4];
+  uint32_t pre, post;   // op codes, one per byte (packed so that lanes keep them in registers)
 };
 
 DHD JitterPlan make_jitter_plan(const dino_view_params& p) {
   JitterPlan j;
   j.n_pre = j.n_post = j.has_contrast = 0;
+  j.pre = j.post = 0;
   if (!p.jitter) return j;
+  const uint32_t ord = (uint32_t)p.order[0] | ((uint32_t)p.order[1] << 8) | ((uint32_t)p.order[2] << 16) |
+                       ((uint32_t)p.order[3] << 24);
   int k = 0;
-  for (; k < 4 && p.order[k] != 1; ++k) j.pre[j.n_pre++] = p.order[k];
+  for (; k < 4 && ((ord >> (8 * k)) & 0xFF) != 1; ++k) j.pre |= ((ord >> (8 * k)) & 0xFF) << (8 * j.n_pre++);
   if (k < 4) {
     j.has_contrast = 1;
-    for (++k; k < 4; ++k) j.post[j.n_post++] = p.order[k];
+    for (++k; k < 4; ++k) j.post |= ((ord >> (8 * k)) & 0xFF) << (8 * j.n_post++);
   }
   return j;
 }
@@ -95,14 +98,14 @@ DHD void jitter_op(int op, int& r, int& g, int& b, const dino_view_params& p, in
 }
 
 DHD void jitter_stage0(const JitterPlan& j, int& r, int& g, int& b, const dino_view_params& p, int hue_d) {
-  for (int k = 0; k < j.n_pre; ++k) jitter_op(j.pre[k], r, g, b, p, 0, hue_d);
+  for (int k = 0; k < j.n_pre; ++k) jitter_op((j.pre >> (8 * k)) & 0xFF, r, g, b, p, 0, hue_d);
 }
 
 // Contrast (if any), later ops, then grayscale.
 DHD void jitter_stage1(const JitterPlan& j, int& r, int& g, int& b, const dino_view_params& p, int contrast_mean,
                        int hue_d) {
   if (j.has_contrast) jitter_op(1, r, g, b, p, contrast_mean, hue_d);
-  for (int k = 0; k < j.n_post; ++k) jitter_op(j.post[k], r, g, b, p, contrast_mean, hue_d);
+  for (int k = 0; k < j.n_post; ++k) jitter_op((j.post >> (8 * k)) & 0xFF, r, g, b, p, contrast_mean, hue_d);
   if (p.gray) {
     int l = rgb_to_l(r, g, b);
     r = g = b = l;

@@ -79,7 +79,7 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
     dino_ctx_destroy(c);
     return hip_fail(e, "dino_ctx_create: hipMalloc");
   }
-  if (L.max_crop_size > kMaxLdsCropSize) {
+  {  // u8 crop planes of every view between the vertical and final passes
     int64_t gb = (int64_t)L.max_batch * L.max_views * 3 * L.max_crop_size * L.max_crop_size;
     if ((e = hipMalloc(&c->d_gcrop, gb)) != hipSuccess) {
       dino_ctx_destroy(c);

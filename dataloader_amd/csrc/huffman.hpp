@@ -171,12 +171,34 @@ struct HState {
 DHD bool hstate_eq(const HState& a, const HState& b) { return a.pos == b.pos && a.c == b.c && a.z == b.z; }
 
 // Tables of one image as the decoder sees them (pointers into LDS on the GPU).
+// Everything a lane indexes per step is a base pointer or a packed word, so that
+// no per-lane array is dynamically indexed (which would spill it to scratch).
 struct HuffImage {
-  const HuffTable* dc[kMaxComp];
-  const HuffTable* ac[kMaxComp];
-  uint8_t mcu_comp[kMaxBlocksPerMcu];
+  const HuffTable* tabs;   // [6]: DC tables of components 0..2, then AC tables 0..2
+  uint32_t mcu_comp;       // component of block b of the MCU in bits [2b, 2b+2)
   int32_t blocks_per_mcu;
 };
+
+DHD void hi_init(HuffImage& im, const HuffTable* tabs, const uint8_t* mcu_comp, int blocks_per_mcu) {
+  im.tabs = tabs;
+  im.mcu_comp = 0;
+  for (int i = 0; i < blocks_per_mcu && i < kMaxBlocksPerMcu; ++i) im.mcu_comp |= (uint32_t)(mcu_comp[i] & 3) << (2 * i);
+  im.blocks_per_mcu = blocks_per_mcu;
+}
+
+DHD int hi_comp(const HuffImage& im, int blk) { return (int)((im.mcu_comp >> (2 * blk)) & 3u); }
+
+// a[c] += v for a 3-vector kept in registers.
+DHD void add3(int32_t* a, int c, int32_t v) {
+  if (c == 0)
+    a[0] += v;
+  else if (c == 1)
+    a[1] += v;
+  else
+    a[2] += v;
+}
+
+DHD int32_t get3(const int32_t* a, int c) { return c == 0 ? a[0] : (c == 1 ? a[1] : a[2]); }
 
 // Result of one step.
 struct StepOut {
@@ -191,9 +213,9 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
   StepOut o;
   o.block_done = 0;
   bc_fill(cur, br);
-  int comp = im.mcu_comp[blk];
+  int comp = hi_comp(im, blk);
   if (z == 0) {
-    int s = huff_decode_sym(cur, im.dc[comp]);
+    int s = huff_decode_sym(cur, im.tabs + comp);
     int diff = 0;
     if (s) {  // >= 15 bits remain after a <= 17-bit code (bc_fill guaranteed >= 32)
       uint32_t r = bc_peek(cur, s);
@@ -205,7 +227,7 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
     o.zz = 0;
     z = 1;
   } else {
-    int rs = huff_decode_sym(cur, im.ac[comp]);
+    int rs = huff_decode_sym(cur, im.tabs + 3 + comp);
     int r = rs >> 4, s = rs & 15;
     if (s) {
       z += r;
@@ -256,15 +278,15 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
   st = sanitize(st, im.blocks_per_mcu);
   RangeOut r;
   r.nblk = 0;
-  for (int c = 0; c < kMaxComp; ++c) r.dcsum[c] = 0;
+  r.dcsum[0] = r.dcsum[1] = r.dcsum[2] = 0;
   BitCursor cur;
   bc_init(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;
   while (cur.pos < end) {
     if (z == 0) r.nblk++;
-    int comp = im.mcu_comp[blk];
+    int comp = hi_comp(im, blk);
     StepOut o = huff_step(cur, br, im, blk, z);
-    if (o.kind == 0) r.dcsum[comp] += o.value;
+    if (o.kind == 0) add3(r.dcsum, comp, o.value);
   }
   r.end.pos = cur.pos;
   r.end.c = blk;
@@ -290,12 +312,12 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
   int32_t b = first_block;
   while (b < total_blocks && cur.pos < end) {
     sink.zero();
-    int comp = im.mcu_comp[blk];
+    int comp = hi_comp(im, blk);
     for (;;) {
       StepOut o = huff_step(cur, br, im, blk, z);
       if (o.kind == 0) {
-        pred[comp] += o.value;
-        sink.set(0, (int16_t)pred[comp]);
+        add3(pred, comp, o.value);
+        sink.set(0, (int16_t)get3(pred, comp));
       } else if (o.kind == 1) {
         sink.set(kNaturalOrder[o.zz], (int16_t)o.value);
       }

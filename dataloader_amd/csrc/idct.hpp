@@ -122,73 +122,73 @@ DHD void idct_islow(const int16_t* coef, const uint16_t* q, OutT* out, int64_t p
 
 DHD int32_t iabs32(int32_t x) { return x < 0 ? -x : x; }
 
-// Same result as idct_islow; each pass runs in int32 when its inputs are within
-// kIslow32Bound (always, for valid 8-bit JPEG data) and in int64 otherwise.
-template <typename OutT>
-DHD void idct_islow_fast(const int16_t* coef, const uint16_t* q, OutT* out, int64_t pitch) {
-  int32_t d[64];
+DHD int32_t max_abs8(const int32_t* v) {
   int32_t m = 0;
-  for (int i = 0; i < 64; ++i) {
-    d[i] = (int32_t)coef[i] * (int32_t)(int16_t)q[i];
-    int32_t a = iabs32(d[i]);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int32_t a = iabs32(v[i]);
     m = a > m ? a : m;
   }
+  return m;
+}
+
+// 1-D passes of idct_islow, each in int32 when its own 8 inputs are within
+// kIslow32Bound (always, for valid 8-bit JPEG data) and in int64 otherwise, so
+// the result equals libjpeg's JLONG arithmetic for any input.
+// Pass 1: one column of dequantized coefficients d[0..7] (rows) -> workspace column.
+template <typename T>
+DHD void idct_pass1_t(const int32_t* d, int32_t* w) {
+  const Islow8<T> t = islow_core<T>(d[0], d[1], d[2], d[3], d[4], d[5], d[6], d[7]);
+  const int sh = kConstBits - kPass1Bits;
+  w[0] = descale(t.t10 + t.t3, sh);
+  w[7] = descale(t.t10 - t.t3, sh);
+  w[1] = descale(t.t11 + t.t2, sh);
+  w[6] = descale(t.t11 - t.t2, sh);
+  w[2] = descale(t.t12 + t.t1, sh);
+  w[5] = descale(t.t12 - t.t1, sh);
+  w[3] = descale(t.t13 + t.t0, sh);
+  w[4] = descale(t.t13 - t.t0, sh);
+}
+
+DHD void idct_pass1(const int32_t* d, int32_t* w) {
+  if (max_abs8(d) <= kIslow32Bound)
+    idct_pass1_t<int32_t>(d, w);
+  else
+    idct_pass1_t<int64_t>(d, w);
+}
+
+// Pass 2: one workspace row w[0..7] -> 8 output samples.
+template <typename T>
+DHD void idct_pass2_t(const int32_t* w, uint8_t* o) {
+  const Islow8<T> t = islow_core<T>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
+  const int sh = kConstBits + kPass1Bits + 3;
+  o[0] = range_limit_idct(descale(t.t10 + t.t3, sh));
+  o[7] = range_limit_idct(descale(t.t10 - t.t3, sh));
+  o[1] = range_limit_idct(descale(t.t11 + t.t2, sh));
+  o[6] = range_limit_idct(descale(t.t11 - t.t2, sh));
+  o[2] = range_limit_idct(descale(t.t12 + t.t1, sh));
+  o[5] = range_limit_idct(descale(t.t12 - t.t1, sh));
+  o[3] = range_limit_idct(descale(t.t13 + t.t0, sh));
+  o[4] = range_limit_idct(descale(t.t13 - t.t0, sh));
+}
+
+DHD void idct_pass2(const int32_t* w, uint8_t* o) {
+  if (max_abs8(w) <= kIslow32Bound)
+    idct_pass2_t<int32_t>(w, o);
+  else
+    idct_pass2_t<int64_t>(w, o);
+}
+
+// Whole block through the two passes (host emulator; the kernel runs one pass per lane).
+DHD void idct_islow_fast(const int16_t* coef, const uint16_t* q, uint8_t* out, int64_t pitch) {
   int32_t ws[64];
-  const int sh1 = kConstBits - kPass1Bits;
   for (int c = 0; c < 8; ++c) {
-    if (m <= kIslow32Bound) {
-      Islow8<int32_t> t = islow_core<int32_t>(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c]);
-      ws[0 * 8 + c] = descale(t.t10 + t.t3, sh1);
-      ws[7 * 8 + c] = descale(t.t10 - t.t3, sh1);
-      ws[1 * 8 + c] = descale(t.t11 + t.t2, sh1);
-      ws[6 * 8 + c] = descale(t.t11 - t.t2, sh1);
-      ws[2 * 8 + c] = descale(t.t12 + t.t1, sh1);
-      ws[5 * 8 + c] = descale(t.t12 - t.t1, sh1);
-      ws[3 * 8 + c] = descale(t.t13 + t.t0, sh1);
-      ws[4 * 8 + c] = descale(t.t13 - t.t0, sh1);
-    } else {
-      Islow8<int64_t> t = islow_core<int64_t>(d[c], d[8 + c], d[16 + c], d[24 + c], d[32 + c], d[40 + c], d[48 + c], d[56 + c]);
-      ws[0 * 8 + c] = descale(t.t10 + t.t3, sh1);
-      ws[7 * 8 + c] = descale(t.t10 - t.t3, sh1);
-      ws[1 * 8 + c] = descale(t.t11 + t.t2, sh1);
-      ws[6 * 8 + c] = descale(t.t11 - t.t2, sh1);
-      ws[2 * 8 + c] = descale(t.t12 + t.t1, sh1);
-      ws[5 * 8 + c] = descale(t.t12 - t.t1, sh1);
-      ws[3 * 8 + c] = descale(t.t13 + t.t0, sh1);
-      ws[4 * 8 + c] = descale(t.t13 - t.t0, sh1);
-    }
+    int32_t d[8], w[8];
+    for (int r = 0; r < 8; ++r) d[r] = (int32_t)coef[r * 8 + c] * (int32_t)(int16_t)q[r * 8 + c];
+    idct_pass1(d, w);
+    for (int r = 0; r < 8; ++r) ws[r * 8 + c] = w[r];
   }
-  int32_t m2 = 0;
-  for (int i = 0; i < 64; ++i) {
-    int32_t a = iabs32(ws[i]);
-    m2 = a > m2 ? a : m2;
-  }
-  const int sh2 = kConstBits + kPass1Bits + 3;
-  for (int r = 0; r < 8; ++r) {
-    const int32_t* w = ws + r * 8;
-    OutT* o = out + r * pitch;
-    if (m2 <= kIslow32Bound) {
-      Islow8<int32_t> t = islow_core<int32_t>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
-      o[0] = range_limit_idct(descale(t.t10 + t.t3, sh2));
-      o[7] = range_limit_idct(descale(t.t10 - t.t3, sh2));
-      o[1] = range_limit_idct(descale(t.t11 + t.t2, sh2));
-      o[6] = range_limit_idct(descale(t.t11 - t.t2, sh2));
-      o[2] = range_limit_idct(descale(t.t12 + t.t1, sh2));
-      o[5] = range_limit_idct(descale(t.t12 - t.t1, sh2));
-      o[3] = range_limit_idct(descale(t.t13 + t.t0, sh2));
-      o[4] = range_limit_idct(descale(t.t13 - t.t0, sh2));
-    } else {
-      Islow8<int64_t> t = islow_core<int64_t>(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]);
-      o[0] = range_limit_idct(descale(t.t10 + t.t3, sh2));
-      o[7] = range_limit_idct(descale(t.t10 - t.t3, sh2));
-      o[1] = range_limit_idct(descale(t.t11 + t.t2, sh2));
-      o[6] = range_limit_idct(descale(t.t11 - t.t2, sh2));
-      o[2] = range_limit_idct(descale(t.t12 + t.t1, sh2));
-      o[5] = range_limit_idct(descale(t.t12 - t.t1, sh2));
-      o[3] = range_limit_idct(descale(t.t13 + t.t0, sh2));
-      o[4] = range_limit_idct(descale(t.t13 - t.t0, sh2));
-    }
-  }
+  for (int r = 0; r < 8; ++r) idct_pass2(ws + r * 8, out + r * pitch);
 }
 
 }  // namespace dino

@@ -284,12 +284,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restr
   }
   __syncthreads();
   HuffImage im;
-  for (int c = 0; c < kMaxComp; ++c) {
-    im.dc[c] = &L.tab[c];
-    im.ac[c] = &L.tab[3 + c];
-  }
-  for (int i = 0; i < kMaxBlocksPerMcu; ++i) im.mcu_comp[i] = sd.mcu_comp[i];
-  im.blocks_per_mcu = sd.blocks_per_mcu;
+  hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
   const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
   LdsSink sink;
   sink.blk = L.blkbuf + t * kBlkStride;
@@ -361,75 +356,132 @@ __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restr
 // ---------------------------------------------------------------------------
 // k_idct: grid (gx, B); lanes over the 8x8 blocks of one image
 // ---------------------------------------------------------------------------
+// 8 lanes per 8x8 block: lane l loads + dequantizes coefficient row l (one 16-byte
+// load, so a wave reads 8 consecutive blocks = 1 KiB contiguously), runs pass 1
+// on column l and pass 2 on row l through an LDS transpose, and stores output row l
+// as one 8-byte word.
+constexpr int kIdctBlocksPerWg = 32;
+
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  __shared__ int32_t s_blk[kIdctBlocksPerWg][65];
   const ImgDesc& d = desc[blockIdx.y];
   if (d.status != DINO_IMG_OK) return;
-  int64_t nb[kMaxComp], tot = 0;
-  for (int c = 0; c < kMaxComp; ++c) {
-    nb[c] = c < d.ncomp ? (int64_t)d.comp[c].bw * d.comp[c].bh : 0;
-    tot += nb[c];
-  }
+  const int ncomp = d.ncomp;
+  const int64_t nb0 = (int64_t)d.comp[0].bw * d.comp[0].bh;
+  const int64_t nb1 = ncomp > 1 ? (int64_t)d.comp[1].bw * d.comp[1].bh : 0;
+  const int64_t nb2 = ncomp > 2 ? (int64_t)d.comp[2].bw * d.comp[2].bh : 0;
+  const int64_t tot = nb0 + nb1 + nb2;
   const int16_t* coef = (const int16_t*)(ws + d.coef_off);
   uint8_t* planes = ws + d.plane_off;
-  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < tot; g += (int64_t)gridDim.x * blockDim.x) {
-    int c = 0;
-    int64_t k = g;
-    while (k >= nb[c]) {
-      k -= nb[c];
-      ++c;
-    }
+  const int grp = threadIdx.x >> 3, l = threadIdx.x & 7;
+  int32_t* sb = s_blk[grp];
+  for (int64_t g0 = (int64_t)blockIdx.x * kIdctBlocksPerWg; g0 < tot; g0 += (int64_t)gridDim.x * kIdctBlocksPerWg) {
+    const int64_t g = g0 + grp;
+    const bool valid = g < tot;
+    const int c = g < nb0 ? 0 : (g < nb0 + nb1 ? 1 : 2);
+    const int64_t k = g - (c == 0 ? 0 : (c == 1 ? nb0 : nb0 + nb1));
     const CompDesc& cd = d.comp[c];
-    int by = (int)(k / cd.bw), bx = (int)(k - (int64_t)by * cd.bw);
-    const int16_t* src = coef + cd.coef_off / 2 + k * 64;
-    int16_t blk[64];
-    const int4* s4 = (const int4*)src;
+    if (valid) {
+      const int4 raw = ((const int4*)(coef + cd.coef_off / 2 + k * 64))[l];
+      const uint16_t* q = d.qt[cd.tq] + l * 8;
+      const int32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) ((int4*)blk)[i] = s4[i];
-    uint8_t out[64];
-    idct_islow_fast(blk, d.qt[cd.tq], out, 8);
-    const int pitch = cd.bw * 8;
-    uint8_t* dst = planes + cd.plane_off + (int64_t)by * 8 * pitch + bx * 8;
+      for (int j = 0; j < 4; ++j) {
+        sb[l * 8 + 2 * j] = (int32_t)(int16_t)(w4[j] & 0xFFFF) * (int32_t)(int16_t)q[2 * j];
+        sb[l * 8 + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)w4[j] >> 16) * (int32_t)(int16_t)q[2 * j + 1];
+      }
+    }
+    __syncthreads();
+    if (valid) {  // pass 1 on column l (reads and writes only this lane's column)
+      int32_t col[8], wcol[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) *(uint64_t*)(dst + (int64_t)r * pitch) = *(const uint64_t*)(out + r * 8);
+      for (int r = 0; r < 8; ++r) col[r] = sb[r * 8 + l];
+      idct_pass1(col, wcol);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sb[r * 8 + l] = wcol[r];
+    }
+    __syncthreads();
+    if (valid) {  // pass 2 on row l
+      int32_t row[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) row[j] = sb[l * 8 + j];
+      union {
+        uint8_t b[8];
+        uint64_t u;
+      } o;
+      idct_pass2(row, o.b);
+      const int by = (int)(k / cd.bw), bx = (int)(k - (int64_t)by * cd.bw);
+      const int pitch = cd.bw * 8;
+      *(uint64_t*)(planes + cd.plane_off + ((int64_t)by * 8 + l) * pitch + bx * 8) = o.u;
+    }
+    __syncthreads();
   }
 }
 
 // ---------------------------------------------------------------------------
 // k_color: grid (gx, B); lanes over output pixels
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ PlaneView make_plane_view(const ImgDesc& d, const uint8_t* ws, int c) {
+  const CompDesc& cd = d.comp[c];
+  PlaneView v;
+  v.p = ws + d.plane_off + cd.plane_off;
+  v.pitch = cd.bw * 8;
+  v.dw = cd.dw;
+  v.dh = cd.dh;
+  v.hf = d.max_h / cd.h;
+  v.vf = d.max_v / cd.v;
+  v.method = upsample_method(v.hf, v.vf, cd.dw);
+  return v;
+}
+
+// Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
+// the RGB area is padded by 16 bytes, so the last partial quad may store whole words).
 __global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const ImgDesc& d = desc[blockIdx.y];
   if (d.status != DINO_IMG_OK) return;
-  PlaneView pv[kMaxComp];
-  for (int c = 0; c < d.ncomp; ++c) {
-    const CompDesc& cd = d.comp[c];
-    pv[c].p = ws + d.plane_off + cd.plane_off;
-    pv[c].pitch = cd.bw * 8;
-    pv[c].dw = cd.dw;
-    pv[c].dh = cd.dh;
-    pv[c].hf = d.max_h / cd.h;
-    pv[c].vf = d.max_v / cd.v;
-    pv[c].method = upsample_method(pv[c].hf, pv[c].vf, cd.dw);
-  }
-  uint8_t* rgb = ws + d.rgb_off;
+  const int nc = d.ncomp;
+  const PlaneView p0 = make_plane_view(d, ws, 0);
+  const PlaneView p1 = nc > 1 ? make_plane_view(d, ws, 1) : p0;
+  const PlaneView p2 = nc > 1 ? make_plane_view(d, ws, 2) : p0;
+  const bool ycc = nc > 1 && d.color == kYCbCr;
+  uint32_t* rgb = (uint32_t*)(ws + d.rgb_off);
   const int W = d.width;
   const int64_t npx = (int64_t)W * d.height;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < npx; i += (int64_t)gridDim.x * blockDim.x) {
-    int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
-    uint8_t* o = rgb + i * 3;
-    if (d.ncomp == 1) {
-      uint8_t v = (uint8_t)upsample_at(pv[0], x, y);
-      o[0] = o[1] = o[2] = v;
-    } else {
-      int a = upsample_at(pv[0], x, y), b = upsample_at(pv[1], x, y), c = upsample_at(pv[2], x, y);
-      if (d.color == kYCbCr) {
-        ycc_to_rgb(a, b, c, o);
+  const int64_t nq = (npx + 3) >> 2;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = q * 4;
+    int y = (int)(i0 / W), x = (int)(i0 - (int64_t)y * W);
+    union {
+      uint8_t b[12];
+      uint32_t w[3];
+    } o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (i0 + j < npx) {
+        if (nc == 1) {
+          const uint8_t v = (uint8_t)upsample_at(p0, x, y);
+          o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = v;
+        } else {
+          const int a = upsample_at(p0, x, y), b = upsample_at(p1, x, y), c = upsample_at(p2, x, y);
+          if (ycc) {
+            ycc_to_rgb(a, b, c, o.b + 3 * j);
+          } else {
+            o.b[3 * j] = (uint8_t)a;
+            o.b[3 * j + 1] = (uint8_t)b;
+            o.b[3 * j + 2] = (uint8_t)c;
+          }
+        }
       } else {
-        o[0] = (uint8_t)a;
-        o[1] = (uint8_t)b;
-        o[2] = (uint8_t)c;
+        o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = 0;
+      }
+      if (++x == W) {
+        x = 0;
+        ++y;
       }
     }
+    rgb[3 * q] = o.w[0];
+    rgb[3 * q + 1] = o.w[1];
+    rgb[3 * q + 2] = o.w[2];
   }
 }
 
@@ -503,7 +555,8 @@ __global__ void __launch_bounds__(1024) k_vplan(const ImgDesc* __restrict__ desc
     int32_t kh, kv;
     view_sizes(prm[i], ok, &a, &b, &kh, &kv);
     ViewPlan vp;
-    vp.ok = ok && (base + a + b <= aws_size);
+    vp.ok = ok && (base + a + b <= aws_size) && (prm[i].crop_w * 3 + 4 <= kHresizeLds);
+    vp.lsum = 0;
     vp.kh = kh;
     vp.kv = kv;
     vp.htmp_off = base;
@@ -531,27 +584,130 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
   }
 }
 
+// Horizontal pass.  A workgroup owns bands of R source rows of one view: the
+// crop's bytes for those rows are staged in LDS with coalesced dword loads,
+// then each lane resamples (row, x) for the three channels from LDS.
 __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  const ViewPlan* __restrict__ plan, int nv, int v0,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int b = blockIdx.z;
   const int i = b * nv + v0 + blockIdx.y;
   const ViewPlan vp = plan[i];
   if (!vp.ok || !vp.kh) return;
   const dino_view_params p = prm[i];
   const ImgDesc& d = desc[b];
-  const int S = p.out_size, W = d.width;
+  const int S = p.out_size, W = d.width, cw = p.crop_w;
   const int32_t* base = (const int32_t*)(aws + vp.rcoef_off);
-  CoefView cv{base, base + 4 * S, vp.kh};
-  SrcView src{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  const int32_t* hb = base;
+  const int32_t* ht = base + 4 * S;
+  const int kh = vp.kh;
+  const int rowbytes = cw * 3;
+  const int rpitch = (rowbytes + 3) & ~3;
+  int R = kHresizeLds / rpitch;
+  R = R > 16 ? 16 : R;
+  const uint8_t* rgb = ws + d.rgb_off;
   uint8_t* tmp = aws + vp.htmp_off;
-  const int64_t total = (int64_t)p.crop_h * S;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
-    uint8_t* o = tmp + e * 3;
-    o[0] = hresize_at(src, cv, r, x, 0);
-    o[1] = hresize_at(src, cv, r, x, 1);
-    o[2] = hresize_at(src, cv, r, x, 2);
+  for (int r0 = blockIdx.x * R; r0 < p.crop_h; r0 += gridDim.x * R) {
+    const int nr = min(R, p.crop_h - r0);
+    for (int r = 0; r < nr; ++r) {
+      const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left) * 3;
+      const uintptr_t a0 = (uintptr_t)src & ~(uintptr_t)3;
+      const int lead = (int)((uintptr_t)src - a0);
+      const int nw = (lead + rowbytes + 3) >> 2;
+      uint8_t* dst = smem + r * rpitch;
+      for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+        const uint32_t v = *(const uint32_t*)(a0 + 4 * (uintptr_t)w);
+        const int o0 = 4 * w - lead;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int o = o0 + q;
+          if (o >= 0 && o < rowbytes) dst[o] = (uint8_t)(v >> (8 * q));
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
+      const int r = e / S, x = e - r * S;
+      const int xmin = hb[2 * x], xcnt = hb[2 * x + 1];
+      const int32_t* k = ht + (int64_t)x * kh;
+      const uint8_t* q = smem + r * rpitch + xmin * 3;
+      int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+      for (int t = 0; t < xcnt; ++t) {
+        const int32_t kk = k[t];
+        a0 += (int32_t)q[3 * t] * kk;
+        a1 += (int32_t)q[3 * t + 1] * kk;
+        a2 += (int32_t)q[3 * t + 2] * kk;
+      }
+      uint8_t* o = tmp + ((int64_t)(r0 + r) * S + x) * 3;
+      o[0] = clip8_acc(a0);
+      o[1] = clip8_acc(a1);
+      o[2] = clip8_acc(a2);
+    }
+    __syncthreads();
+  }
+}
+
+// Per-view slot of the u8 crop planes [3][S][S] (global views first, then local views).
+__device__ __forceinline__ int64_t crop_slot(const dino_aug_config& cfg, int B, int b, int v) {
+  const int64_t g3 = 3ll * cfg.global_size * cfg.global_size, l3 = 3ll * cfg.local_size * cfg.local_size;
+  if (v < cfg.n_global) return ((int64_t)b * cfg.n_global + v) * g3;
+  return (int64_t)B * cfg.n_global * g3 + ((int64_t)b * cfg.n_local + (v - cfg.n_global)) * l3;
+}
+
+// Vertical pass (+ flip) and the ColorJitter ops that precede contrast, over a
+// band of kVertRows output rows; adds the band's L sum to the view's counter.
+constexpr int kVertRows = 8;
+
+__global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                              ViewPlan* __restrict__ plan, int nv, int v0, int B,
+                                              const uint8_t* __restrict__ ws, const uint8_t* __restrict__ aws,
+                                              uint8_t* __restrict__ gcrop, dino_aug_config cfg, int S) {
+  __shared__ uint32_t s_part[4];
+  const int b = blockIdx.z, v = v0 + blockIdx.y;
+  const int i = b * nv + v;
+  const ViewPlan vp = plan[i];
+  if (!vp.ok) return;
+  const dino_view_params p = prm[i];
+  const ImgDesc& d = desc[b];
+  const int64_t N = (int64_t)S * S;
+  uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);
+  const int W = d.width;
+  const bool need_h = vp.kh != 0, need_v = vp.kv != 0;
+  const int32_t* cbase = (const int32_t*)(aws + vp.rcoef_off);
+  CoefView cvv{cbase + 2 * S, cbase + 4 * S + (int64_t)S * vp.kh, vp.kv};
+  SrcView src = need_h ? SrcView{aws + vp.htmp_off, (int64_t)S * 3}
+                       : SrcView{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  const JitterPlan jp = make_jitter_plan(p);
+  const int hd = hue_delta(p.hue);
+  const int y0 = blockIdx.x * kVertRows;
+  const int nr = min(kVertRows, S - y0);
+  uint32_t lsum = 0;
+  for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
+    const int y = y0 + e / S, x = e % S;
+    int r, g, bb;
+    if (need_v) {
+      r = vresize_at(src, cvv, y, x, 0);
+      g = vresize_at(src, cvv, y, x, 1);
+      bb = vresize_at(src, cvv, y, x, 2);
+    } else {
+      const uint8_t* q = src.base + (int64_t)y * src.pitch + (int64_t)x * 3;
+      r = q[0];
+      g = q[1];
+      bb = q[2];
+    }
+    jitter_stage0(jp, r, g, bb, p, hd);
+    const int64_t o = (int64_t)y * S + (p.flip ? S - 1 - x : x);
+    crop[o] = (uint8_t)r;
+    crop[N + o] = (uint8_t)g;
+    crop[2 * N + o] = (uint8_t)bb;
+    if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
+  }
+  if (jp.has_contrast) {
+    for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
+    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = lsum;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&plan[i].lsum, s_part[0] + s_part[1] + s_part[2] + s_part[3]);
   }
 }
 
@@ -570,98 +726,83 @@ __device__ __forceinline__ void store_out<uint8_t>(uint8_t* out, int64_t o, floa
   out[o] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f)));
 }
 
-// One workgroup per (view, image).  crop: 3 planes of S*S u8 (LDS when it fits,
-// otherwise a global scratch slice).
-template <typename OutT, bool kLdsCrop>
-__global__ void __launch_bounds__(512) k_augment(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
-                                                 const ViewPlan* __restrict__ plan, int nv, int v0,
-                                                 const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws,
-                                                 uint8_t* __restrict__ gcrop, ViewPtrs views, dino_aug_config cfg,
-                                                 int S) {
+// Contrast (with the view's mean) and later ColorJitter ops, grayscale, then blur
+// + solarize + normalize + cast over a band of kFinalRows output rows.  The band
+// and its reflected blur halo are staged in LDS.
+constexpr int kFinalRows = 16;
+constexpr int kMaxBlurPad = 7;
+
+struct FinalLds {
+  float k1[16];
+  float k2[256];
+};
+
+template <typename OutT>
+__global__ void __launch_bounds__(256) k_final(const dino_view_params* __restrict__ prm, const ViewPlan* __restrict__ plan,
+                                               int nv, int v0, int B, const uint8_t* __restrict__ gcrop,
+                                               ViewPtrs views, dino_aug_config cfg, int S) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  AugLdsHead& H = *reinterpret_cast<AugLdsHead*>(smem);
-  float* s_k1 = H.k1;
-  float* s_k2 = H.k2;
-  uint32_t& s_lsum = H.lsum;
-  const int b = blockIdx.y, v = v0 + blockIdx.x;
+  FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
+  uint8_t* tile = smem + sizeof(FinalLds);
+  const int b = blockIdx.z, v = v0 + blockIdx.y;
   const int i = b * nv + v;
-  const dino_view_params p = prm[i];
-  const ViewPlan vp = plan[i];  // vp.ok implies p.out_size == S and an in-bounds crop
+  const ViewPlan vp = plan[i];
   const int64_t N = (int64_t)S * S;
+  const int y0 = blockIdx.x * kFinalRows;
+  const int nr = min(kFinalRows, S - y0);
   OutT* out = (OutT*)views.p[v] + (int64_t)b * 3 * N;
-  const int t = threadIdx.x, nt = blockDim.x;
   if (!vp.ok) {  // reference cpu.py:253: undecodable -> zeros
-    for (int64_t e = t; e < 3 * N; e += nt) out[e] = (OutT)0;
+    for (int e = threadIdx.x; e < 3 * nr * S; e += blockDim.x) {
+      const int ch = e / (nr * S), rem = e - ch * nr * S;
+      out[(int64_t)ch * N + (int64_t)y0 * S + rem] = (OutT)0;
+    }
     return;
   }
-  const ImgDesc& d = desc[b];
-  uint8_t* crop = kLdsCrop ? smem + sizeof(AugLdsHead) : gcrop + ((int64_t)b * gridDim.x + blockIdx.x) * 3 * N;
-  uint8_t *R = crop, *G = crop + N, *Bp = crop + 2 * N;
+  const dino_view_params p = prm[i];
+  const uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);
+  const int ks = p.blur ? p.ksize : 1;
+  const int pad = ks >> 1;
+  const int tr = nr + 2 * pad;                 // tile rows (band + reflected halo)
+  const int64_t tplane = (int64_t)tr * S;
+  if (p.blur && threadIdx.x == 0) gaussian_kernel1d(ks, p.sigma, H.k1);
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
-  const int W = d.width;
-  const bool need_h = vp.kh != 0, need_v = vp.kv != 0;
-  const int32_t* cbase = (const int32_t*)(aws + vp.rcoef_off);
-  CoefView cvv{cbase + 2 * S, cbase + 4 * S + (int64_t)S * vp.kh, vp.kv};
-  SrcView src = need_h ? SrcView{aws + vp.htmp_off, (int64_t)S * 3}
-                       : SrcView{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
-  if (t == 0) s_lsum = 0;
-  if (p.blur && t == 0) gaussian_kernel1d(p.ksize, p.sigma, s_k1);
-  __syncthreads();
-  if (p.blur && t < p.ksize * p.ksize) s_k2[t] = s_k1[t / p.ksize] * s_k1[t % p.ksize];
-  // pass A: vertical resample (+flip), ColorJitter ops before contrast, L sum
-  uint32_t lsum = 0;
-  for (int64_t e = t; e < N; e += nt) {
-    int y = (int)(e / S), x = (int)(e - (int64_t)y * S);
-    int r, g, bb;
-    if (need_v) {
-      r = vresize_at(src, cvv, y, x, 0);
-      g = vresize_at(src, cvv, y, x, 1);
-      bb = vresize_at(src, cvv, y, x, 2);
-    } else {
-      const uint8_t* q = src.base + (int64_t)y * src.pitch + (int64_t)x * 3;
-      r = q[0];
-      g = q[1];
-      bb = q[2];
-    }
-    jitter_stage0(jp, r, g, bb, p, hd);
-    int xo = p.flip ? S - 1 - x : x;
-    int64_t o = (int64_t)y * S + xo;
-    R[o] = (uint8_t)r;
-    G[o] = (uint8_t)g;
-    Bp[o] = (uint8_t)bb;
-    if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
-  }
-  if (jp.has_contrast) {
-    for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
-    if ((t & 63) == 0) atomicAdd(&s_lsum, lsum);
+  const int cmean = contrast_mean_from_sum(vp.lsum, N);
+  for (int e = threadIdx.x; e < tr * S; e += blockDim.x) {
+    const int lr = e / S, x = e - lr * S;
+    const int sr = reflect_idx(y0 - pad + lr, S);
+    const int64_t so = (int64_t)sr * S + x;
+    int r = crop[so], g = crop[N + so], bb = crop[2 * N + so];
+    jitter_stage1(jp, r, g, bb, p, cmean, hd);
+    tile[e] = (uint8_t)r;
+    tile[tplane + e] = (uint8_t)g;
+    tile[2 * tplane + e] = (uint8_t)bb;
   }
   __syncthreads();
-  // pass B: contrast with the crop's mean, later ops, grayscale
-  if (p.jitter || p.gray) {
-    const int cmean = contrast_mean_from_sum(s_lsum, N);
-    for (int64_t e = t; e < N; e += nt) {
-      int r = R[e], g = G[e], bb = Bp[e];
-      jitter_stage1(jp, r, g, bb, p, cmean, hd);
-      R[e] = (uint8_t)r;
-      G[e] = (uint8_t)g;
-      Bp[e] = (uint8_t)bb;
-    }
-    __syncthreads();
-  }
-  // final pass: blur + solarize + normalize + cast, NCHW
+  if (p.blur && threadIdx.x < ks * ks) H.k2[threadIdx.x] = H.k1[threadIdx.x / ks] * H.k1[threadIdx.x % ks];
+  __syncthreads();
   const float m0 = cfg.mean[0], m1 = cfg.mean[1], m2 = cfg.mean[2];
   const float d0 = cfg.std[0], d1 = cfg.std[1], d2 = cfg.std[2];
-  for (int64_t e = t; e < 3 * N; e += nt) {
-    int ch = (int)(e / N);
-    int64_t pix = e - (int64_t)ch * N;
-    int y = (int)(pix / S), x = (int)(pix - (int64_t)y * S);
-    const uint8_t* pl = crop + (int64_t)ch * N;
-    int val = p.blur ? blur_at(pl, S, y, x, s_k2, p.ksize) : pl[pix];
+  for (int e = threadIdx.x; e < 3 * nr * S; e += blockDim.x) {
+    const int ch = e / (nr * S), rem = e - ch * nr * S;
+    const int y = rem / S, x = rem - y * S;
+    const uint8_t* pl = tile + ch * tplane;
+    int val;
+    if (p.blur) {
+      float acc = 0.0f;
+      for (int a = 0; a < ks; ++a) {
+        const uint8_t* row = pl + (int64_t)(y + a) * S;
+        for (int c = 0; c < ks; ++c) acc = fmaf(H.k2[a * ks + c], (float)row[reflect_idx(x + c - pad, S)], acc);
+      }
+      const float rr = rintf(acc);
+      val = rr <= 0.0f ? 0 : (rr >= 255.0f ? 255 : (int)rr);
+    } else {
+      val = pl[(int64_t)y * S + x];
+    }
     if (p.solarize) val = solarize_u8(val);
-    float mean = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
-    float sd = ch == 0 ? d0 : (ch == 1 ? d1 : d2);
-    store_out<OutT>(out, e, u8_normalize(val, mean, sd));
+    const float mean = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
+    const float sd = ch == 0 ? d0 : (ch == 1 ? d1 : d2);
+    store_out<OutT>(out, (int64_t)ch * N + (int64_t)(y0 + y) * S + x, u8_normalize(val, mean, sd));
   }
 }
 
@@ -770,7 +911,8 @@ static const bool g_sync_check = [] {
 }();
 static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct",
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
-                                                       "k_augment_global", "k_augment_local"};
+                                                       "k_final_global", "k_final_local", "k_vert_global",
+                                                       "k_vert_local"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -804,7 +946,7 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
     attr_set = true;
   }
   TIMED(tm, kKHuffman, s, (k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws)));
-  TIMED(tm, kKIdct, s, (k_idct<<<dim3(32, B), 256, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKIdct, s, (k_idct<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
   return hipGetLastError();
 }
@@ -821,21 +963,18 @@ template <typename OutT>
 static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, int S, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch, nv = a.cfg.n_global + a.cfg.n_local;
   if (nvc <= 0) return hipSuccess;
-  const int kaug = v0 == 0 ? kKAugmentGlobal : kKAugmentLocal;
+  const int kfin = v0 == 0 ? kKFinalGlobal : kKFinalLocal;
+  const int kvert = v0 == 0 ? kKVertGlobal : kKVertLocal;
   TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
-  TIMED(tm, kKHresize, s, (k_hresize<<<dim3(8, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
-  const int threads = S >= 128 ? 512 : 256;
-  if (S <= kMaxLdsCropSize) {
-    const int lds = (int)sizeof(AugLdsHead) + 3 * S * S;
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_augment<OutT, true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    TIMED(tm, kaug, s, (k_augment<OutT, true><<<dim3(nvc, B), threads, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
-                                                                             a.aws, a.gcrop, a.views, a.cfg, S)));
-  } else {
-    if (!a.gcrop) return hipErrorInvalidValue;
-    TIMED(tm, kaug, s, (k_augment<OutT, false><<<dim3(nvc, B), threads, sizeof(AugLdsHead), s>>>(
-                           a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.gcrop, a.views, a.cfg, S)));
-  }
+  TIMED(tm, kKHresize, s,
+        (k_hresize<<<dim3(8, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
+  TIMED(tm, kvert, s,
+        (k_vert<<<dim3((S + kVertRows - 1) / kVertRows, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, B,
+                                                                             a.ws, a.aws, a.gcrop, a.cfg, S)));
+  const int lds = (int)sizeof(FinalLds) + 3 * (kFinalRows + 2 * kMaxBlurPad) * S;
+  TIMED(tm, kfin, s,
+        (k_final<OutT><<<dim3((S + kFinalRows - 1) / kFinalRows, nvc, B), 256, lds, s>>>(
+            a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S)));
   return hipGetLastError();
 }
 

@@ -6,30 +6,23 @@
 namespace dino {
 
 // Per-(image, view) scratch placement, written by k_vplan.
+// LDS staging of k_hresize: source row bytes of one band (bounds crop_w to ~21.8k px).
+constexpr int kHresizeLds = 64 * 1024;
+
 struct ViewPlan {
   int64_t htmp_off;   // horizontal-pass rows (crop_h x S x 3 u8) in the augment workspace
   int64_t rcoef_off;  // resize coefficient tables
   int32_t kh, kv;     // taps per output of the horizontal / vertical pass (0 = pass skipped)
   int32_t ok;         // image decoded and scratch available
-  int32_t pad;
+  uint32_t lsum;      // sum of L over the crop before the contrast op (k_vert atomics)
 };
 
-// Dynamic-LDS header of k_augment (kept in the dynamic region so its base stays 16-B aligned).
-struct AugLdsHead {
-  float k1[16];
-  float k2[256];
-  uint32_t lsum;
-  uint32_t pad[3];
-};
-
-// Largest S whose three u8 planes fit next to the header in 160 KiB of LDS.
-constexpr int kMaxLdsCropSize = 233;
 
 // Optional per-kernel HIP-event timing (bench / profiling).  Events are recorded on
 // the launch stream around each kernel; elapsed times are summed on demand.
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuffman, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
-  kKAugmentGlobal, kKAugmentLocal, kKNumKernels
+  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKNumKernels
 };
 
 struct KernelTimer {
@@ -73,7 +66,7 @@ struct AugmentArgs {
   const uint8_t* ws;
   uint8_t* aws;
   int64_t aws_size;
-  uint8_t* gcrop;          // global crop scratch for S > kMaxLdsCropSize (may be null otherwise)
+  uint8_t* gcrop;          // u8 crop planes of every view (k_vert -> k_final)
   ViewPtrs views;          // n_views output pointers (device memory)
   dino_aug_config cfg;
 };

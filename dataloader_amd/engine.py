@@ -79,7 +79,7 @@ class IngestEngine:
         return out
 
     KERNEL_NAMES = ["k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct", "k_color", "k_params", "k_vplan",
-                    "k_rcoeffs", "k_hresize", "k_augment_global", "k_augment_local"]
+                    "k_rcoeffs", "k_hresize", "k_final_global", "k_final_local", "k_vert_global", "k_vert_local"]
 
     def set_timing(self, enable: bool) -> None:
         _lib.check(self.lib.dino_set_timing(self._ctx, int(enable)), "dino_set_timing")

@@ -139,7 +139,8 @@ int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32
 
 /* Per-kernel HIP-event timing of this ctx's launches (bench / profiling).
  * Kernel ids: 0 parse, 1 plan, 2 destuff, 3 huffman, 4 idct, 5 color, 6 params,
- * 7 vplan, 8 rcoeffs, 9 hresize, 10 augment(global views), 11 augment(local views).
+ * 7 vplan, 8 rcoeffs, 9 hresize, 10 final(global views), 11 final(local views),
+ * 12 vert(global views), 13 vert(local views).
  * dino_kernel_times synchronises the recorded events, returns the sums since the
  * last call (ms, launches) and resets them. */
 int dino_set_timing(dino_ctx* ctx, int32_t enable);
@@ -151,7 +152,10 @@ int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t 
 int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream);
 
 /* Stage-5 cast (reference FP8Formatter.quantise, memory.py:193-214, scale 1):
- * bf16 -> OCP float8_e4m3fn, round-to-nearest-even, saturating. */
+ * bf16 -> OCP float8_e4m3fn, round-to-nearest-even, bit-identical to torch's
+ * .to(torch.float8_e4m3fn) (c10 fp8e4m3fn_from_fp32_value: |x| >= 480 -> NaN).
+ * The reference's TE cast_to_fp8 saturates to +-448 instead; the two agree on
+ * every normalised pixel value (|x| < 3), which is all this path produces. */
 int dino_bf16_to_fp8(const uint16_t* d_in, uint8_t* d_out, int64_t n, void* stream);
 
 #ifdef __cplusplus

@@ -77,11 +77,8 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* 
       tabs[c].look[i] = huff_look_entry(&tabs[c], i);
       tabs[3 + c].look[i] = huff_look_entry(&tabs[3 + c], i);
     }
-    im.dc[c] = &tabs[c];
-    im.ac[c] = &tabs[3 + c];
   }
-  for (int i = 0; i < kMaxBlocksPerMcu; ++i) im.mcu_comp[i] = d.mcu_comp[i];
-  im.blocks_per_mcu = d.blocks_per_mcu;
+  hi_init(im, tabs, d.mcu_comp, d.blocks_per_mcu);
   return true;
 }
 
