@@ -12,11 +12,14 @@
 
 namespace dino {
 
-// Accessor for a u8 HWC source region (the horizontally-resampled temp rows, or
-// the decoded RGB image itself offset to the crop origin).
+// Accessor for a u8 source region: the decoded RGB image (HWC, offset to the crop
+// origin: px = 3, cs = 1) or the horizontally-resampled rows (planar: px = 1,
+// cs = rows * S).
 struct SrcView {
   const uint8_t* base;
   int64_t pitch;  // bytes per row
+  int32_t px;     // bytes per pixel step
+  int64_t cs;     // bytes per channel step
 };
 
 struct CoefView {
@@ -28,16 +31,16 @@ struct CoefView {
 DHD uint8_t hresize_at(const SrcView& s, const CoefView& cv, int row, int x, int ch) {
   int xmin = cv.bounds[2 * x], xcnt = cv.bounds[2 * x + 1];
   const int32_t* k = cv.taps + (int64_t)x * cv.ksize;
-  const uint8_t* p = s.base + (int64_t)row * s.pitch + (int64_t)xmin * 3 + ch;
+  const uint8_t* p = s.base + (int64_t)row * s.pitch + (int64_t)xmin * s.px + ch * s.cs;
   int32_t acc = 1 << (kPrecisionBits - 1);
-  for (int t = 0; t < xcnt; ++t) acc += (int32_t)p[3 * t] * k[t];
+  for (int t = 0; t < xcnt; ++t) acc += (int32_t)p[t * s.px] * k[t];
   return clip8_acc(acc);
 }
 
 DHD uint8_t vresize_at(const SrcView& s, const CoefView& cv, int y, int x, int ch) {
   int ymin = cv.bounds[2 * y], ycnt = cv.bounds[2 * y + 1];
   const int32_t* k = cv.taps + (int64_t)y * cv.ksize;
-  const uint8_t* p = s.base + (int64_t)ymin * s.pitch + (int64_t)x * 3 + ch;
+  const uint8_t* p = s.base + (int64_t)ymin * s.pitch + (int64_t)x * s.px + ch * s.cs;
   int32_t acc = 1 << (kPrecisionBits - 1);
   for (int t = 0; t < ycnt; ++t) acc += (int32_t)p[(int64_t)t * s.pitch] * k[t];
   return clip8_acc(acc);

@@ -123,11 +123,37 @@ __device__ __forceinline__ int classify_ff(const uint8_t* r, int n, int k) {
   return 3;
 }
 
+// One pass over the scan in tiles of 256 lanes x 16 bytes: each lane loads one
+// aligned 16-byte chunk (plus the bytes either side for the 0xFF rules),
+// classifies it, and the workgroup scans (kept bytes, RST markers) packed in one
+// word to place the lane's output.  The first terminating marker ends the scan.
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wave[w] = x;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < kDestuffThreads / 64; ++k) {
+    const uint32_t t = s_wave[k];
+    before += k < w ? t : 0u;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
 __global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __restrict__ bytes,
                                                              const int64_t* __restrict__ offsets,
                                                              ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  __shared__ int s_end, s_term;
-  __shared__ int s_cnt[kDestuffThreads], s_rcnt[kDestuffThreads];
+  __shared__ uint32_t s_wave[kDestuffThreads / 64];
+  __shared__ int s_end;
   const int img = blockIdx.x, t = threadIdx.x;
   ImgDesc* d = &desc[img];
   if (d->status != DINO_IMG_OK) return;
@@ -135,73 +161,96 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __re
   const int n = d->scan_len;
   uint8_t* out = ws + d->ent_off;
   int32_t* rst = (int32_t*)(ws + d->rst_off);
-  const int chunk = (n + kDestuffThreads - 1) / kDestuffThreads;
-  const int k0 = t * chunk, k1 = min(n, k0 + chunk);
-  if (t == 0) {
-    s_end = n;
-    s_term = 0;
-  }
-  __syncthreads();
-  // pass 1: first terminating marker
-  for (int k = k0; k < k1; ++k) {
-    if (r[k] == 0xFF) {
-      int c = classify_ff(r, n, k);
-      if (c >= 3) {
-        atomicMin(&s_end, k);
-        break;
+  const int nrst_cap = d->n_rst_max + 1;
+  const int lead = (int)((uintptr_t)r & 15);
+  const uint4* base = (const uint4*)(r - lead);  // aligned; chunk c covers scan bytes [16c - lead, 16c - lead + 16)
+  const int nchunks = (lead + n + 15) >> 4;
+  const uint8_t* buf_end = bytes + offsets[gridDim.x];  // a whole-chunk load must not pass the caller's buffer
+  uint32_t o_run = 0, rc_run = 0;
+  int E = n;
+  for (int c0 = 0; c0 < nchunks; c0 += kDestuffThreads) {
+    if (t == 0) s_end = n;
+    __syncthreads();
+    const int c = c0 + t;
+    const int k0 = 16 * c - lead;  // scan index of byte 0 of this chunk
+    uint32_t wv[4] = {0u, 0u, 0u, 0u};
+    int prevb = -1, nextb = -1;
+    if (c < nchunks) {
+      if ((const uint8_t*)(base + c + 1) <= buf_end) {
+        const uint4 u = base[c];
+        wv[0] = u.x;
+        wv[1] = u.y;
+        wv[2] = u.z;
+        wv[3] = u.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (k0 + j >= 0 && k0 + j < n) wv[j >> 2] |= (uint32_t)r[k0 + j] << (8 * (j & 3));
+      }
+      if (k0 - 1 >= 0 && k0 - 1 < n) prevb = r[k0 - 1];
+      if (k0 + 16 >= 0 && k0 + 16 < n) nextb = r[k0 + 16];
+    }
+    // classify: bit j of keep / rstm / term
+    uint32_t keep = 0, rstm = 0;
+    int my_term = n;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = k0 + j;
+      if (k < 0 || k >= n) continue;
+      const int v = (wv[j >> 2] >> (8 * (j & 3))) & 255;
+      const int pv = j > 0 ? (int)((wv[(j - 1) >> 2] >> (8 * ((j - 1) & 3))) & 255) : prevb;
+      const int nx = j < 15 ? (k + 1 < n ? (int)((wv[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255) : -1) : nextb;
+      if (v == 0xFF) {
+        // 0 keep (FF00), 1 RST, 2 fill (FFFF), 3 terminating marker, 4 truncated (last byte)
+        const int cls = nx < 0 ? 4 : (nx == 0x00 ? 0 : ((nx >= 0xD0 && nx <= 0xD7) ? 1 : (nx == 0xFF ? 2 : 3)));
+        if (cls >= 3) {
+          my_term = min(my_term, k);
+          break;
+        }
+        if (cls == 0) keep |= 1u << j;
+        if (cls == 1) rstm |= 1u << j;
+      } else if (!(k > 0 && pv == 0xFF)) {
+        keep |= 1u << j;
       }
     }
-  }
-  __syncthreads();
-  const int E = s_end;
-  if (t == 0) s_term = (E < n) && classify_ff(r, n, E) == 3;
-  // pass 2: counts
-  int cnt = 0, rc = 0;
-  const int e1 = min(k1, E);
-  for (int k = k0; k < e1; ++k) {
-    int v = r[k];
-    if (v == 0xFF) {
-      int c = classify_ff(r, n, k);
-      cnt += (c == 0);
-      rc += (c == 1);
-    } else if (!(k > 0 && r[k - 1] == 0xFF)) {
-      ++cnt;
+    if (my_term < n) atomicMin(&s_end, my_term);
+    __syncthreads();
+    const int Et = s_end;
+    if (Et < n) {  // drop everything at or after the terminator
+      const int lim = Et - k0;
+      const uint32_t mask = lim <= 0 ? 0u : (lim >= 16 ? 0xFFFFu : ((1u << lim) - 1u));
+      keep &= mask;
+      rstm &= mask;
     }
-  }
-  s_cnt[t] = cnt;
-  s_rcnt[t] = rc;
-  __syncthreads();
-  for (int s = 1; s < kDestuffThreads; s <<= 1) {
-    int a = t >= s ? s_cnt[t - s] : 0, b = t >= s ? s_rcnt[t - s] : 0;
-    __syncthreads();
-    s_cnt[t] += a;
-    s_rcnt[t] += b;
-    __syncthreads();
-  }
-  int o = s_cnt[t] - cnt, ro = s_rcnt[t] - rc;
-  const int nrst_cap = d->n_rst_max + 1;
-  for (int k = k0; k < e1; ++k) {
-    int v = r[k];
-    if (v == 0xFF) {
-      int c = classify_ff(r, n, k);
-      if (c == 0) out[o++] = 0xFF;
-      else if (c == 1) {
-        if (ro < nrst_cap) rst[ro] = o;
+    const uint32_t packed = (uint32_t)__popc(keep) | ((uint32_t)__popc(rstm) << 16);
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan(packed, s_wave, &tot);
+    uint32_t o = o_run + (ex & 0xFFFFu), ro = rc_run + (ex >> 16);
+    for (uint32_t m = keep | rstm; m; m &= m - 1) {
+      const int j = __ffs(m) - 1;
+      if (keep & (1u << j)) {
+        out[o++] = (uint8_t)((wv[j >> 2] >> (8 * (j & 3))) & 255);
+      } else {
+        if ((int)ro < nrst_cap) rst[ro] = (int32_t)o;
         ++ro;
       }
-    } else if (!(k > 0 && r[k - 1] == 0xFF)) {
-      out[o++] = (uint8_t)v;
+    }
+    o_run += tot & 0xFFFFu;
+    rc_run += tot >> 16;
+    if (Et < n) {
+      E = Et;
+      break;
     }
   }
-  __syncthreads();
-  const int total = s_cnt[kDestuffThreads - 1];
+  const int total = (int)o_run;
   // zero padding for word reads past the end
   for (int k = total + t; k < total + 64 && k < n + 64; k += kDestuffThreads) out[k] = 0;
   if (t == 0) {
+    const int term = (E < n) && (E + 1 < n);  // a marker (not a trailing lone 0xFF) ended the scan
     d->ent_len = total;
-    d->n_rst = s_rcnt[kDestuffThreads - 1];
-    d->terminated = s_term;
-    if (!s_term) d->status = DINO_IMG_TRUNCATED;
+    d->n_rst = (int32_t)rc_run;
+    d->terminated = term;
+    if (!term) d->status = DINO_IMG_TRUNCATED;
     else if (d->restart_interval > 0 && d->n_rst < d->n_rst_max - 1) d->status = DINO_IMG_BADDATA;
   }
 }
@@ -512,7 +561,8 @@ __device__ bool params_valid(const dino_view_params& p, const ImgDesc& d, int S)
   if (p.out_size != S) return false;
   if (p.crop_top < 0 || p.crop_left < 0 || p.crop_h < 1 || p.crop_w < 1) return false;
   if ((int64_t)p.crop_top + p.crop_h > d.height || (int64_t)p.crop_left + p.crop_w > d.width) return false;
-  if (p.blur && (p.ksize < 1 || p.ksize > 15 || (p.ksize & 1) == 0 || !(p.sigma > 0.0))) return false;
+  if (p.blur && (p.ksize < 1 || p.ksize > 15 || (p.ksize & 1) == 0 || !(p.sigma > 0.0) || p.ksize / 2 >= S))
+    return false;  // torch reflect padding needs pad < S
   for (int k = 0; k < 4; ++k)
     if (p.order[k] > 3) return false;
   return true;
@@ -555,7 +605,7 @@ __global__ void __launch_bounds__(1024) k_vplan(const ImgDesc* __restrict__ desc
     int32_t kh, kv;
     view_sizes(prm[i], ok, &a, &b, &kh, &kv);
     ViewPlan vp;
-    vp.ok = ok && (base + a + b <= aws_size) && (prm[i].crop_w * 3 + 4 <= kHresizeLds);
+    vp.ok = ok && (base + a + b <= aws_size);
     vp.lsum = 0;
     vp.kh = kh;
     vp.kv = kv;
@@ -584,9 +634,38 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
   }
 }
 
-// Horizontal pass.  A workgroup owns bands of R source rows of one view: the
-// crop's bytes for those rows are staged in LDS with coalesced dword loads,
-// then each lane resamples (row, x) for the three channels from LDS.
+// Horizontal pass.  A workgroup owns bands of R source rows of one view.  The
+// crop's pixels for those rows are staged in LDS as RGBX words (each lane turns
+// 12 source bytes = 4 pixels into one 16-byte LDS store); the view's taps are
+// staged in LDS too when they fit.  Each lane then resamples one (row, x) with
+// one LDS word per tap and writes the three channels to planar temp rows
+// [3][crop_h][S].  Crops too wide for LDS take a direct (global) path.
+constexpr int kHresizeTapLds = 16 * 1024;
+
+template <bool kLdsTaps>
+__device__ __forceinline__ void hresize_band(const uint32_t* __restrict__ rows, int rpw, int nr, int r0, int S,
+                                             const int32_t* __restrict__ hb, const int32_t* __restrict__ ht, int kh,
+                                             uint8_t* __restrict__ tmp, int64_t cpl) {
+  for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
+    const int r = e / S, x = e - r * S;
+    const int xmin = hb[2 * x], xcnt = hb[2 * x + 1];
+    const int32_t* k = ht + x * kh;
+    const uint32_t* q = rows + r * rpw + xmin;
+    int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
+    for (int t = 0; t < xcnt; ++t) {
+      const uint32_t v = q[t];
+      const int32_t kk = k[t];
+      a0 += (int32_t)(v & 255u) * kk;
+      a1 += (int32_t)((v >> 8) & 255u) * kk;
+      a2 += (int32_t)((v >> 16) & 255u) * kk;
+    }
+    const int64_t o = (int64_t)(r0 + r) * S + x;
+    tmp[o] = clip8_acc(a0);
+    tmp[cpl + o] = clip8_acc(a1);
+    tmp[2 * cpl + o] = clip8_acc(a2);
+  }
+}
+
 __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  const ViewPlan* __restrict__ plan, int nv, int v0,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
@@ -597,53 +676,57 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   if (!vp.ok || !vp.kh) return;
   const dino_view_params p = prm[i];
   const ImgDesc& d = desc[b];
-  const int S = p.out_size, W = d.width, cw = p.crop_w;
-  const int32_t* base = (const int32_t*)(aws + vp.rcoef_off);
-  const int32_t* hb = base;
-  const int32_t* ht = base + 4 * S;
-  const int kh = vp.kh;
-  const int rowbytes = cw * 3;
-  const int rpitch = (rowbytes + 3) & ~3;
-  int R = kHresizeLds / rpitch;
-  R = R > 16 ? 16 : R;
+  const int S = p.out_size, W = d.width, cw = p.crop_w, kh = vp.kh;
+  const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);
+  const int32_t* gt = gb + 4 * S;
   const uint8_t* rgb = ws + d.rgb_off;
   uint8_t* tmp = aws + vp.htmp_off;
+  const int64_t cpl = (int64_t)p.crop_h * S;
+  const int tap_words = 2 * S + S * kh;
+  const bool lds_taps = tap_words * 4 <= kHresizeTapLds;
+  const int rbase = lds_taps ? ((tap_words * 4 + 15) & ~15) : 0;
+  const int ngroups = (cw + 3) >> 2;
+  const int rpw = ngroups * 4;  // LDS words per staged row
+  int R = (kHresizeLds - rbase) / (rpw * 4);
+  R = R > 16 ? 16 : R;
+  if (R < 1) {  // direct path: taps and pixels from global memory
+    const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
+    const CoefView cv{gb, gt, kh};
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cpl; e += (int64_t)gridDim.x * blockDim.x) {
+      const int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
+      for (int c = 0; c < 3; ++c) tmp[c * cpl + e] = hresize_at(src, cv, r, x, c);
+    }
+    return;
+  }
+  int32_t* lt = (int32_t*)smem;
+  if (lds_taps) {
+    for (int k = threadIdx.x; k < 2 * S; k += blockDim.x) lt[k] = gb[k];
+    for (int k = threadIdx.x; k < S * kh; k += blockDim.x) lt[2 * S + k] = gt[k];
+  }
+  uint32_t* rows = (uint32_t*)(smem + rbase);
   for (int r0 = blockIdx.x * R; r0 < p.crop_h; r0 += gridDim.x * R) {
     const int nr = min(R, p.crop_h - r0);
-    for (int r = 0; r < nr; ++r) {
-      const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left) * 3;
-      const uintptr_t a0 = (uintptr_t)src & ~(uintptr_t)3;
-      const int lead = (int)((uintptr_t)src - a0);
-      const int nw = (lead + rowbytes + 3) >> 2;
-      uint8_t* dst = smem + r * rpitch;
-      for (int w = threadIdx.x; w < nw; w += blockDim.x) {
-        const uint32_t v = *(const uint32_t*)(a0 + 4 * (uintptr_t)w);
-        const int o0 = 4 * w - lead;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int o = o0 + q;
-          if (o >= 0 && o < rowbytes) dst[o] = (uint8_t)(v >> (8 * q));
-        }
-      }
+    for (int e = threadIdx.x; e < nr * ngroups; e += blockDim.x) {
+      const int r = e / ngroups, g = e - r * ngroups;
+      const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left) * 3 + 12 * g;
+      const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
+      const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
+      const uint32_t w0 = a0[0], w1 = a0[1], w2 = a0[2], w3 = a0[3];
+      const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
+      const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
+      const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);
+      uint4 px;
+      px.x = b0 & 0xFFFFFFu;
+      px.y = (b0 >> 24) | ((b1 & 0xFFFFu) << 8);
+      px.z = (b1 >> 16) | ((b2 & 0xFFu) << 16);
+      px.w = b2 >> 8;
+      *(uint4*)(rows + r * rpw + 4 * g) = px;
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
-      const int r = e / S, x = e - r * S;
-      const int xmin = hb[2 * x], xcnt = hb[2 * x + 1];
-      const int32_t* k = ht + (int64_t)x * kh;
-      const uint8_t* q = smem + r * rpitch + xmin * 3;
-      int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
-      for (int t = 0; t < xcnt; ++t) {
-        const int32_t kk = k[t];
-        a0 += (int32_t)q[3 * t] * kk;
-        a1 += (int32_t)q[3 * t + 1] * kk;
-        a2 += (int32_t)q[3 * t + 2] * kk;
-      }
-      uint8_t* o = tmp + ((int64_t)(r0 + r) * S + x) * 3;
-      o[0] = clip8_acc(a0);
-      o[1] = clip8_acc(a1);
-      o[2] = clip8_acc(a2);
-    }
+    if (lds_taps)
+      hresize_band<true>(rows, rpw, nr, r0, S, lt, lt + 2 * S, kh, tmp, cpl);
+    else
+      hresize_band<false>(rows, rpw, nr, r0, S, gb, gt, kh, tmp, cpl);
     __syncthreads();
   }
 }
@@ -657,6 +740,8 @@ __device__ __forceinline__ int64_t crop_slot(const dino_aug_config& cfg, int B, 
 
 // Vertical pass (+ flip) and the ColorJitter ops that precede contrast, over a
 // band of kVertRows output rows; adds the band's L sum to the view's counter.
+// Fast path (planar temp rows, S % 4 == 0): a lane produces 4 adjacent pixels
+// from one 4-byte load per channel and tap and stores one word per plane.
 constexpr int kVertRows = 8;
 
 __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
@@ -675,33 +760,79 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   const int W = d.width;
   const bool need_h = vp.kh != 0, need_v = vp.kv != 0;
   const int32_t* cbase = (const int32_t*)(aws + vp.rcoef_off);
-  CoefView cvv{cbase + 2 * S, cbase + 4 * S + (int64_t)S * vp.kh, vp.kv};
-  SrcView src = need_h ? SrcView{aws + vp.htmp_off, (int64_t)S * 3}
-                       : SrcView{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  const CoefView cvv{cbase + 2 * S, cbase + 4 * S + (int64_t)S * vp.kh, vp.kv};
+  const int64_t cpl = (int64_t)p.crop_h * S;
+  const uint8_t* htmp = aws + vp.htmp_off;
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
   const int y0 = blockIdx.x * kVertRows;
   const int nr = min(kVertRows, S - y0);
   uint32_t lsum = 0;
-  for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
-    const int y = y0 + e / S, x = e % S;
-    int r, g, bb;
-    if (need_v) {
-      r = vresize_at(src, cvv, y, x, 0);
-      g = vresize_at(src, cvv, y, x, 1);
-      bb = vresize_at(src, cvv, y, x, 2);
-    } else {
-      const uint8_t* q = src.base + (int64_t)y * src.pitch + (int64_t)x * 3;
-      r = q[0];
-      g = q[1];
-      bb = q[2];
+  if (need_h && (S & 3) == 0) {
+    const int nq = S >> 2;
+    for (int e = threadIdx.x; e < nr * nq; e += blockDim.x) {
+      const int y = y0 + e / nq, xq = e % nq;
+      uint32_t w[3];
+      if (need_v) {
+        const int ymin = cvv.bounds[2 * y], ycnt = cvv.bounds[2 * y + 1];
+        const int32_t* k = cvv.taps + (int64_t)y * cvv.ksize;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const uint8_t* q = htmp + c * cpl + (int64_t)ymin * S + 4 * xq;
+          int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0, a3 = a0;
+          for (int t = 0; t < ycnt; ++t) {
+            const uint32_t u = *(const uint32_t*)(q + (int64_t)t * S);
+            const int32_t kk = k[t];
+            a0 += (int32_t)(u & 255u) * kk;
+            a1 += (int32_t)((u >> 8) & 255u) * kk;
+            a2 += (int32_t)((u >> 16) & 255u) * kk;
+            a3 += (int32_t)(u >> 24) * kk;
+          }
+          w[c] = (uint32_t)clip8_acc(a0) | ((uint32_t)clip8_acc(a1) << 8) | ((uint32_t)clip8_acc(a2) << 16) |
+                 ((uint32_t)clip8_acc(a3) << 24);
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) w[c] = *(const uint32_t*)(htmp + c * cpl + (int64_t)y * S + 4 * xq);
+      }
+      uint32_t o[3] = {0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int r = (w[0] >> (8 * j)) & 255, g = (w[1] >> (8 * j)) & 255, bb = (w[2] >> (8 * j)) & 255;
+        jitter_stage0(jp, r, g, bb, p, hd);
+        if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
+        o[0] |= (uint32_t)r << (8 * j);
+        o[1] |= (uint32_t)g << (8 * j);
+        o[2] |= (uint32_t)bb << (8 * j);
+      }
+      const int64_t off = (int64_t)y * S + (p.flip ? S - 4 - 4 * xq : 4 * xq);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) *(uint32_t*)(crop + c * N + off) = p.flip ? __builtin_bswap32(o[c]) : o[c];
     }
-    jitter_stage0(jp, r, g, bb, p, hd);
-    const int64_t o = (int64_t)y * S + (p.flip ? S - 1 - x : x);
-    crop[o] = (uint8_t)r;
-    crop[N + o] = (uint8_t)g;
-    crop[2 * N + o] = (uint8_t)bb;
-    if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
+  } else {
+    const SrcView src = need_h ? SrcView{htmp, (int64_t)S, 1, cpl}
+                               : SrcView{ws + d.rgb_off + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3,
+                                         3, 1};
+    for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
+      const int y = y0 + e / S, x = e % S;
+      int r, g, bb;
+      if (need_v) {
+        r = vresize_at(src, cvv, y, x, 0);
+        g = vresize_at(src, cvv, y, x, 1);
+        bb = vresize_at(src, cvv, y, x, 2);
+      } else {
+        const uint8_t* q = src.base + (int64_t)y * src.pitch + (int64_t)x * src.px;
+        r = q[0];
+        g = q[src.cs];
+        bb = q[2 * src.cs];
+      }
+      jitter_stage0(jp, r, g, bb, p, hd);
+      const int64_t o = (int64_t)y * S + (p.flip ? S - 1 - x : x);
+      crop[o] = (uint8_t)r;
+      crop[N + o] = (uint8_t)g;
+      crop[2 * N + o] = (uint8_t)bb;
+      if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
+    }
   }
   if (jp.has_contrast) {
     for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
@@ -726,16 +857,116 @@ __device__ __forceinline__ void store_out<uint8_t>(uint8_t* out, int64_t o, floa
   out[o] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f)));
 }
 
+// Four adjacent outputs; one vector store when all four are in the row and aligned.
+template <typename OutT>
+__device__ __forceinline__ void store_out4(OutT* out, int64_t o, const float* f, int n, bool vec);
+template <>
+__device__ __forceinline__ void store_out4<uint16_t>(uint16_t* out, int64_t o, const float* f, int n, bool vec) {
+  if (vec) {
+    uint2 u;
+    u.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
+    u.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
+    *(uint2*)(out + o) = u;
+  } else {
+    for (int j = 0; j < n; ++j) out[o + j] = f32_to_bf16(f[j]);
+  }
+}
+template <>
+__device__ __forceinline__ void store_out4<float>(float* out, int64_t o, const float* f, int n, bool vec) {
+  if (vec) {
+    *(float4*)(out + o) = make_float4(f[0], f[1], f[2], f[3]);
+  } else {
+    for (int j = 0; j < n; ++j) out[o + j] = f[j];
+  }
+}
+template <>
+__device__ __forceinline__ void store_out4<uint8_t>(uint8_t* out, int64_t o, const float* f, int n, bool vec) {
+  uint8_t q[4];
+  for (int j = 0; j < 4; ++j) q[j] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f[j])));
+  if (vec) {
+    *(uint32_t*)(out + o) = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+  } else {
+    for (int j = 0; j < n; ++j) out[o + j] = q[j];
+  }
+}
+
 // Contrast (with the view's mean) and later ColorJitter ops, grayscale, then blur
 // + solarize + normalize + cast over a band of kFinalRows output rows.  The band
-// and its reflected blur halo are staged in LDS.
-constexpr int kFinalRows = 16;
+// and its blur halo (rows and columns, reflected as torch's reflect padding) are
+// staged in LDS after the stage-1 jitter, so the blur reads a plain window.  A
+// lane produces 4 adjacent outputs of one channel; the kernel size is a template
+// parameter for the sizes the DINO sigma range yields (3..9).
+constexpr int kFinalRows = 32;
 constexpr int kMaxBlurPad = 7;
 
 struct FinalLds {
   float k1[16];
   float k2[256];
 };
+
+__host__ __device__ __forceinline__ int final_tile_pitch(int S, int pad) { return (((S + 3) & ~3) + 2 * pad + 3) & ~3; }
+
+template <int KS, typename OutT>
+__device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, int tp, int64_t tplane, int nr, int y0,
+                                              int S, int ks_rt, const float* __restrict__ k2, bool solarize,
+                                              const dino_aug_config& cfg, OutT* __restrict__ out) {
+  const int ks = KS > 0 ? KS : ks_rt;
+  const int nq = (S + 3) >> 2;
+  const int64_t N = (int64_t)S * S;
+  const bool vec_ok = (S & 3) == 0;
+  for (int e = threadIdx.x; e < 3 * nr * nq; e += blockDim.x) {
+    const int ch = e / (nr * nq), rem = e - ch * nr * nq;
+    const int y = rem / nq, x0 = 4 * (rem - (rem / nq) * nq);
+    const uint8_t* pl = tile + ch * tplane;
+    int val[4];
+    if (KS == 1) {
+      const uint32_t u = *(const uint32_t*)(pl + y * tp + x0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) val[j] = (u >> (8 * j)) & 255;
+    } else {
+      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (KS > 0) {
+        constexpr int NW = (KS + 3 + 3) / 4;
+#pragma unroll 1
+        for (int a = 0; a < KS; ++a) {
+          const uint32_t* row = (const uint32_t*)(pl + (y + a) * tp + x0);
+          uint32_t wv[NW];
+#pragma unroll
+          for (int q = 0; q < NW; ++q) wv[q] = row[q];
+#pragma unroll
+          for (int c = 0; c < KS; ++c) {
+            const float kk = k2[a * KS + c];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int bi = c + j;
+              acc[j] = fmaf(kk, (float)((wv[bi >> 2] >> (8 * (bi & 3))) & 255u), acc[j]);
+            }
+          }
+        }
+      } else {
+        for (int a = 0; a < ks; ++a) {
+          const uint8_t* row = pl + (y + a) * tp + x0;
+          for (int c = 0; c < ks; ++c) {
+            const float kk = k2[a * ks + c];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = fmaf(kk, (float)row[c + j], acc[j]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float rr = rintf(acc[j]);
+        val[j] = rr <= 0.0f ? 0 : (rr >= 255.0f ? 255 : (int)rr);
+      }
+    }
+    const float mean = cfg.mean[ch], sd = cfg.std[ch];
+    float f[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f[j] = u8_normalize(solarize ? solarize_u8(val[j]) : val[j], mean, sd);
+    const int n = min(4, S - x0);
+    store_out4<OutT>(out, ch * N + (int64_t)(y0 + y) * S + x0, f, n, vec_ok);
+  }
+}
 
 template <typename OutT>
 __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restrict__ prm, const ViewPlan* __restrict__ plan,
@@ -763,46 +994,35 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   const int ks = p.blur ? p.ksize : 1;
   const int pad = ks >> 1;
   const int tr = nr + 2 * pad;                 // tile rows (band + reflected halo)
-  const int64_t tplane = (int64_t)tr * S;
+  const int tw = S + 2 * pad;                  // tile columns (row + reflected halo)
+  const int tp = final_tile_pitch(S, pad);
+  const int64_t tplane = (int64_t)tr * tp;
   if (p.blur && threadIdx.x == 0) gaussian_kernel1d(ks, p.sigma, H.k1);
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
   const int cmean = contrast_mean_from_sum(vp.lsum, N);
-  for (int e = threadIdx.x; e < tr * S; e += blockDim.x) {
-    const int lr = e / S, x = e - lr * S;
-    const int sr = reflect_idx(y0 - pad + lr, S);
-    const int64_t so = (int64_t)sr * S + x;
+  for (int e = threadIdx.x; e < tr * tw; e += blockDim.x) {
+    const int lr = e / tw, tc = e - lr * tw;
+    const int sr = reflect_idx(y0 - pad + lr, S), sc = reflect_idx(tc - pad, S);
+    const int64_t so = (int64_t)sr * S + sc;
     int r = crop[so], g = crop[N + so], bb = crop[2 * N + so];
     jitter_stage1(jp, r, g, bb, p, cmean, hd);
-    tile[e] = (uint8_t)r;
-    tile[tplane + e] = (uint8_t)g;
-    tile[2 * tplane + e] = (uint8_t)bb;
+    const int to = lr * tp + tc;
+    tile[to] = (uint8_t)r;
+    tile[tplane + to] = (uint8_t)g;
+    tile[2 * tplane + to] = (uint8_t)bb;
   }
   __syncthreads();
   if (p.blur && threadIdx.x < ks * ks) H.k2[threadIdx.x] = H.k1[threadIdx.x / ks] * H.k1[threadIdx.x % ks];
   __syncthreads();
-  const float m0 = cfg.mean[0], m1 = cfg.mean[1], m2 = cfg.mean[2];
-  const float d0 = cfg.std[0], d1 = cfg.std[1], d2 = cfg.std[2];
-  for (int e = threadIdx.x; e < 3 * nr * S; e += blockDim.x) {
-    const int ch = e / (nr * S), rem = e - ch * nr * S;
-    const int y = rem / S, x = rem - y * S;
-    const uint8_t* pl = tile + ch * tplane;
-    int val;
-    if (p.blur) {
-      float acc = 0.0f;
-      for (int a = 0; a < ks; ++a) {
-        const uint8_t* row = pl + (int64_t)(y + a) * S;
-        for (int c = 0; c < ks; ++c) acc = fmaf(H.k2[a * ks + c], (float)row[reflect_idx(x + c - pad, S)], acc);
-      }
-      const float rr = rintf(acc);
-      val = rr <= 0.0f ? 0 : (rr >= 255.0f ? 255 : (int)rr);
-    } else {
-      val = pl[(int64_t)y * S + x];
-    }
-    if (p.solarize) val = solarize_u8(val);
-    const float mean = ch == 0 ? m0 : (ch == 1 ? m1 : m2);
-    const float sd = ch == 0 ? d0 : (ch == 1 ? d1 : d2);
-    store_out<OutT>(out, (int64_t)ch * N + (int64_t)(y0 + y) * S + x, u8_normalize(val, mean, sd));
+  const bool sol = p.solarize != 0;
+  switch (ks) {
+    case 1: final_compute<1, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
+    case 3: final_compute<3, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
+    case 5: final_compute<5, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
+    case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
+    case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
+    default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
   }
 }
 
@@ -967,11 +1187,11 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   const int kvert = v0 == 0 ? kKVertGlobal : kKVertLocal;
   TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
   TIMED(tm, kKHresize, s,
-        (k_hresize<<<dim3(8, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
+        (k_hresize<<<dim3(16, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
   TIMED(tm, kvert, s,
         (k_vert<<<dim3((S + kVertRows - 1) / kVertRows, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, B,
                                                                              a.ws, a.aws, a.gcrop, a.cfg, S)));
-  const int lds = (int)sizeof(FinalLds) + 3 * (kFinalRows + 2 * kMaxBlurPad) * S;
+  const int lds = (int)sizeof(FinalLds) + 3 * (kFinalRows + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
   TIMED(tm, kfin, s,
         (k_final<OutT><<<dim3((S + kFinalRows - 1) / kFinalRows, nvc, B), 256, lds, s>>>(
             a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S)));

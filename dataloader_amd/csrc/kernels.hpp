@@ -6,8 +6,8 @@
 namespace dino {
 
 // Per-(image, view) scratch placement, written by k_vplan.
-// LDS staging of k_hresize: source row bytes of one band (bounds crop_w to ~21.8k px).
-constexpr int kHresizeLds = 64 * 1024;
+// LDS of k_hresize: taps (when they fit in 16 KiB) + RGBX rows of one band.
+constexpr int kHresizeLds = 40 * 1024;
 
 struct ViewPlan {
   int64_t htmp_off;   // horizontal-pass rows (crop_h x S x 3 u8) in the augment workspace

@@ -232,7 +232,7 @@ inline void model_coeffs(int in_size, int S, std::vector<int32_t>& b, std::vecto
 inline void model_resize_planar(const uint8_t* rgb, int W, int H, const dino_view_params& p, uint8_t* planes) {
   const int S = p.out_size;
   const bool need_h = p.crop_w != S, need_v = p.crop_h != S;
-  SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3};
+  SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
   ViewModel vm;
   if (need_h) {
     model_coeffs(p.crop_w, S, vm.hb, vm.ht, vm.kh);
@@ -240,8 +240,9 @@ inline void model_resize_planar(const uint8_t* rgb, int W, int H, const dino_vie
     vm.tmp.assign((size_t)p.crop_h * S * 3, 0);
     for (int r = 0; r < p.crop_h; ++r)
       for (int x = 0; x < S; ++x)
-        for (int ch = 0; ch < 3; ++ch) vm.tmp[((size_t)r * S + x) * 3 + ch] = hresize_at(src, cv, r, x, ch);
-    src = SrcView{vm.tmp.data(), (int64_t)S * 3};
+        for (int ch = 0; ch < 3; ++ch)
+          vm.tmp[(size_t)ch * p.crop_h * S + (size_t)r * S + x] = hresize_at(src, cv, r, x, ch);
+    src = SrcView{vm.tmp.data(), (int64_t)S, 1, (int64_t)p.crop_h * S};  // planar, as k_hresize writes it
   }
   if (need_v) model_coeffs(p.crop_h, S, vm.vb, vm.vt, vm.kv);
   CoefView cvv{vm.vb.data(), vm.vt.data(), vm.kv};
@@ -249,7 +250,8 @@ inline void model_resize_planar(const uint8_t* rgb, int W, int H, const dino_vie
     for (int x = 0; x < S; ++x) {
       int xo = p.flip ? S - 1 - x : x;
       for (int ch = 0; ch < 3; ++ch) {
-        uint8_t v = need_v ? vresize_at(src, cvv, y, x, ch) : src.base[(int64_t)y * src.pitch + (int64_t)x * 3 + ch];
+        uint8_t v = need_v ? vresize_at(src, cvv, y, x, ch)
+                           : src.base[(int64_t)y * src.pitch + (int64_t)x * src.px + ch * src.cs];
         planes[(size_t)ch * S * S + (size_t)y * S + xo] = v;
       }
     }

@@ -222,3 +222,85 @@ def test_bench_pattern_multi_batch(gpu_device):
     recs = pipe.last_params()
     _check_views(jpegs[96 - B:], views, recs, cfg.n_views, torch.bfloat16, cfg.mean, cfg.std)
     pipe.close()
+
+
+def _edge_records(dims, gsize, lsize):
+    """Hand-made records that reach every branch of the resize / blur kernels:
+    crop == S on one or both axes (no resample pass), S % 4 != 0 (scalar paths),
+    crops too wide for LDS staging (direct path), blur kernel sizes 3..13
+    (templated and generic), every jitter op order, flip, gray, solarize."""
+    P = cpu_ref.ViewParams
+    recs = []
+    from tests.helpers import params_to_record
+    orders = [(3, 2, 1, 0), (1, 0, 2, 3), (0, 1, 2, 3), (2, 3, 0, 1)]
+    for k, (w, h) in enumerate(dims):
+        views = []
+        for v, S in enumerate((gsize, gsize, lsize, lsize)):
+            cw = [w, min(S, w), min(w, S if v == 3 else w // 2 + 1), S if S <= w else w][v]
+            ch = [h, min(S, h), min(h, S), min(h, h // 2 + 1)][v]
+            if v == 1 and (w < S or h < S):
+                cw, ch = w, h
+            top, left = (h - ch) // 3, (w - cw) // 2
+            ks = [9, 13, 11, 3, 5, 7][(k + v) % 6]
+            while ks // 2 >= S:
+                ks -= 2
+            views.append(P(out_size=S, crop_top=top, crop_left=left, crop_h=ch, crop_w=cw, flip=bool((k + v) & 1),
+                           jitter=v != 2, order=orders[(k + v) % 4], brightness=1.25, contrast=0.7, saturation=1.3,
+                           hue=[0.1, -0.07, 0.03, -0.2][v], gray=(k + v) % 3 == 0, blur=v != 1,
+                           sigma=[1.9, 2.6, 2.4, 0.5, 1.1, 1.6][(k + v) % 6] * ks / 9 + 0.1, ksize=ks,
+                           solarize=v == 1))
+        recs += [params_to_record(p) for p in views]
+    return np.stack(recs)
+
+
+@pytest.mark.parametrize("gsize,lsize", [(30, 18), (32, 16)])
+def test_augment_edge_paths(gpu_device, gsize, lsize):
+    rng = np.random.default_rng(9)
+    dims = [(12000, 24), (7000, 40), (300, 200), (gsize, gsize), (lsize, 50), (41, lsize)]
+    jpegs = [encode_jpeg(textured_rgb(w, h, rng), quality=90) for w, h in dims]
+    cfg = DINOAugConfig(global_crop_size=gsize, local_crop_size=lsize, n_local_crops=2)
+    recs = _edge_records(dims, gsize, lsize)
+    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=4, max_crop_size=32, max_image_dim=16384)
+    d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    assert (info[:, 0] == 0).all(), info
+    for out_code, tdtype in [(OUT_BF16, torch.bfloat16), (OUT_FP32, torch.float32)]:
+        views = eng.augment(make_aug_config(cfg, gsize, lsize, out_code), params_to_device(recs, gpu_device))
+        torch.cuda.synchronize()
+        _check_views(jpegs, views, recs, 4, tdtype, cfg.mean, cfg.std)
+    eng.close()
+
+
+def test_decode_marker_edge_cases(gpu_device):
+    """Entropy-segment edge cases of the destuffing pass, at every byte alignment
+    of the packed buffer: 0xFF fill bytes before EOI (legal, B.1.1.2), junk after
+    EOI, a scan cut before EOI (Pillow raises -> TRUNCATED), a lone trailing 0xFF,
+    restart markers, and the last image ending exactly at the end of the buffer."""
+    rng = np.random.default_rng(77)
+    base = encode_jpeg(textured_rgb(120, 90, rng), quality=90)
+    dri = encode_jpeg(textured_rgb(160, 64, rng), restart_mcus=2)
+    assert base[-2:] == b"\xff\xd9"
+    cases = [
+        (base, 0),
+        (base[:-2] + b"\xff\xff\xff\xd9", 0),
+        (base + b"trailing junk \xff\x00\xff", 0),
+        (base[: len(base) * 3 // 4], -2),
+        (base[:-2] + b"\xff", -2),
+        (dri, 0),
+        (dri[:-2] + b"\xff\xff\xd9", 0),
+    ]
+    for pad in range(16):
+        jpegs = [b"\0" * pad] + [c for c, _ in cases] + [base]
+        eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
+        d_bytes, d_off = _to_dev(jpegs, gpu_device)
+        d_bytes = d_bytes[: int(d_off[-1])].clone()  # exact-size buffer: no slack after the last image
+        info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+        assert info[0, 0] < 0
+        for i, (data, want) in enumerate(cases + [(base, 0)], start=1):
+            ref = cpu_ref.decode_rgb(data)
+            assert (ref is None) == (want != 0), i
+            assert info[i, 0] == want, f"pad {pad} case {i}: status {info[i, 0]} want {want}"
+            if want == 0:
+                got = eng.copy_rgb(i, int(info[i, 1]), int(info[i, 2])).cpu().numpy()
+                np.testing.assert_array_equal(got, np.asarray(ref), err_msg=f"pad {pad} case {i}")
+        eng.close()
