@@ -53,8 +53,14 @@ def _gen_one(args):
 def make_unique(n: int, w: int, h: int, base_seed: int, mixed: bool, procs: int) -> list[bytes]:
     # 'spawn': never fork a process that may already hold a HIP context
     jobs = [(w, h, base_seed * 100003 + k, mixed) for k in range(n)]
-    with get_context("spawn").Pool(max(1, procs)) as pool:
+    if procs <= 1:  # in-process (profiler runs: no worker processes to tear down)
+        return [_gen_one(j) for j in jobs]
+    pool = get_context("spawn").Pool(procs)
+    try:
         return pool.map(_gen_one, jobs, chunksize=4)
+    finally:
+        pool.close()  # let workers exit on their own (no SIGTERM under rocprofv3)
+        pool.join()
 
 
 def jpeg_meta(j: bytes):
@@ -159,6 +165,8 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--images", type=int, default=50000)
     ap.add_argument("--unique", type=int, default=256)
+    ap.add_argument("--procs", type=int, default=-1, help="JPEG encoder processes (0: in-process)")
+    ap.add_argument("--depth", type=int, default=2, help="batches in flight (slots with their own ctx + stream)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600}")
@@ -173,7 +181,7 @@ def main() -> None:
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     # synthetic data first, before anything initialises the GPU in this process
-    procs = min(16, os.cpu_count() or 4)
+    procs = args.procs if args.procs >= 0 else min(16, os.cpu_count() or 4)
     uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs)
 
     import torch
@@ -199,13 +207,14 @@ def main() -> None:
     cfg = DINOAugConfig()
     B = args.batch
     pipe = MI355XAugPipeline(None, cfg, B, seed=rank_seed(1234, rank), out_dtype=args.dtype, device=local_rank,
-                             max_image_dim=4096 if args.mixed else 2048)
-    views = pipe.engine.alloc_views(pipe._cfg(cfg.global_crop_size, cfg.local_crop_size), B)
+                             max_image_dim=4096 if args.mixed else 2048, depth=args.depth)
+    ccfg = pipe._cfg(cfg.global_crop_size, cfg.local_crop_size)
+    views = [sl.engine.alloc_views(ccfg, B) for sl in pipe._slots]  # one output set per in-flight slot
     n_batches = n_img // B
 
     def step(k: int):
         s = (k % n_batches) * B
-        pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views)
+        pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views[k % pipe.depth])
 
     for k in range(args.warmup):
         step(k)
@@ -213,8 +222,6 @@ def main() -> None:
     st = pipe.last_status()
     if (st != 0).any():
         raise RuntimeError(f"decode failures in warmup batch: {np.unique(st, return_counts=True)}")
-    pipe.engine.set_timing(True)
-    pipe.engine.kernel_times()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -225,8 +232,17 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    ktimes = pipe.engine.kernel_times()
-    pipe.engine.set_timing(False)
+    # per-kernel HIP-event times: a separate pass with the batches serialised, so that a
+    # kernel's events do not also span the other slot's concurrently running kernels
+    pipe.set_timing(True)
+    pipe.kernel_times()
+    t_ser = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + args.steps + k)
+        torch.cuda.synchronize()
+    t_ser = time.perf_counter() - t_ser
+    ktimes = pipe.kernel_times()
+    pipe.set_timing(False)
     if world > 1:
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -242,7 +258,7 @@ def main() -> None:
             nbytes = int(offsets[s + B]) - base
             hb = host_buf[base:base + nbytes].to(dev, non_blocking=True)
             ho = (offsets[s:s + B + 1] - base).to(dev, non_blocking=True)
-            pipe.run_device_batch(hb, ho, B, views=views)
+            pipe.run_device_batch(hb, ho, B, views=views[k % pipe.depth])
         torch.cuda.synchronize()
         h2d_rate = args.steps * B / (time.perf_counter() - t1)
 
@@ -276,11 +292,13 @@ def main() -> None:
                                     f"C2 {args.images} synthetic {args.width}x{args.height} q85 4:2:0 JPEGs "
                                     "resident in HBM") + f", 2x224^2+8x96^2 views, {args.dtype} out",
                        "global_batch": B * world, "batch_per_gpu": B, "parallelism": f"dp{world}",
+                       "batches_in_flight": pipe.depth,
                        "mean_jpeg_bytes": round(ab["s_jpeg"]), "out_dtype": args.dtype},
             "roofline": roof,
             "path_roofline": {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
                               "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5)},
             "kernels_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in per_kernel.items()},
+            "serialized_ms_per_step": round(t_ser / args.steps * 1e3, 3),
             "cpu_baseline": cpu,
         }
         if h2d_rate is not None:

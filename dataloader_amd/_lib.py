@@ -31,10 +31,11 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
-    if not LIB_PATH.exists():
-        raise DinoError(f"{LIB_PATH} not found: run `python -c 'import __graft_entry__ as g; g.build()'` "
+    path = Path(os.environ.get("DINO_INGEST_LIB", LIB_PATH))  # experiments may point at a variant build
+    if not path.exists():
+        raise DinoError(f"{path} not found: run `python -c 'import __graft_entry__ as g; g.build()'` "
                         "(hipcc --offload-arch=gfx950). There is no CPU fallback.")
-    lib = ctypes.CDLL(str(LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    lib = ctypes.CDLL(str(path), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
     vp, i32, i64, u64, dbl = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_double
     sig = {
         "dino_abi_version": (i32, []),

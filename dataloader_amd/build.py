@@ -22,14 +22,14 @@ def needs_build() -> bool:
     return any(d.stat().st_mtime > mt for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> Path:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = True, out: Path = OUT, defines: tuple = ()) -> Path:
+    if out == OUT and not force and not needs_build():
         return OUT
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = OUT.with_suffix(".so.tmp")
-    cmd = [hipcc, *FLAGS, "-o", str(tmp), *map(str, SOURCES)]
+    tmp = out.with_suffix(".so.tmp")
+    cmd = [hipcc, *FLAGS, *[f"-D{d}" for d in defines], "-o", str(tmp), *map(str, SOURCES)]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out

@@ -18,7 +18,7 @@ namespace dino {
 
 constexpr int kMaxComp = 3;
 constexpr int kMaxBlocksPerMcu = 10;   // libjpeg D_MAX_BLOCKS_IN_MCU
-constexpr int kLookBits = 9;           // Huffman lookahead table bits
+constexpr int kLookBits = 10;          // Huffman lookahead table bits
 
 enum ColorSpace : int32_t { kGray = 0, kYCbCr = 1, kRGB = 2 };
 
@@ -50,7 +50,9 @@ struct ImgDesc {
   int32_t total_blocks;    // MCUs * blocks_per_mcu
   // filled by k_plan (byte offsets into the ctx workspace)
   int64_t base;            // start of this image's chunk
-  int64_t ent_off, rst_off, coef_off, plane_off, rgb_off, htmp_off, rcoef_off;
+  int64_t ent_off, rst_off, coef_off, plane_off, rgb_off;
+  int64_t cps_off;         // k_huffman checkpoints (speculative decode), kHuffThreads x kHuffCheckpoints
+  int64_t dcd_off;         // int32 DC differences per block (decode order), summed by k_dcscan
   int64_t coef_bytes;
   // filled by k_destuff
   int32_t ent_len;         // destuffed entropy bytes

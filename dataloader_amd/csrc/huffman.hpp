@@ -19,11 +19,16 @@
 namespace dino {
 
 // Derived decoding table for one Huffman table (jpeg_make_d_derived_tbl).
+// Lookahead entry for each kLookBits-bit prefix, two 16-bit halves:
+//   low  = (symbol << 8) | code length, 0 when the code is longer than kLookBits;
+//   high = the whole step when the code *and* its extra bits fit the prefix:
+//          (value << 8) | (run << 4) | bits consumed, as int16 (0 = not resolvable).
+//          AC: value 0 marks the s == 0 symbols (EOB, ZRL); DC: run 0, value = diff.
 struct HuffTable {
   int32_t maxcode[18];     // maxcode[l], -1 if no codes of length l; [17] sentinel
   int32_t valoffset[18];
   uint8_t huffval[256];
-  uint16_t look[1 << kLookBits];  // (len << 8) | symbol for codes <= kLookBits bits, 0 = slow path
+  uint32_t look[1 << kLookBits];
 };
 
 // Build maxcode/valoffset/huffval (not the lookahead) from BITS[16] + HUFFVAL.
@@ -64,13 +69,22 @@ DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTable* t) {
   return true;
 }
 
+DHD int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(((unsigned)-1) << s) + 1 : x; }
+
 // Lookahead entry for the kLookBits-bit prefix `idx` (computable independently per entry).
-DHD uint16_t huff_look_entry(const HuffTable* t, int idx) {
+DHD uint32_t huff_look_entry(const HuffTable* t, int idx, bool is_dc) {
   for (int l = 1; l <= kLookBits; ++l) {
-    int code = idx >> (kLookBits - l);
+    const int code = idx >> (kLookBits - l);
     if (code <= t->maxcode[l]) {  // canonical code: first length whose maxcode covers the prefix
-      int sym = t->huffval[(code + t->valoffset[l]) & 255];
-      return (uint16_t)((l << 8) | sym);
+      const int sym = t->huffval[(code + t->valoffset[l]) & 255];
+      const uint32_t lo = (uint32_t)((sym << 8) | l);
+      const int r = is_dc ? 0 : sym >> 4, s = is_dc ? sym : sym & 15;
+      int hi = 0;
+      if (l + s <= kLookBits) {
+        const int v = s ? huff_extend((idx >> (kLookBits - l - s)) & ((1 << s) - 1), s) : 0;
+        if (v >= -128 && v <= 127) hi = v * 256 + ((r << 4) | (l + s));
+      }
+      return ((uint32_t)(uint16_t)(int16_t)hi << 16) | lo;
     }
   }
   return 0;
@@ -101,29 +115,52 @@ DHD uint32_t br_peek32(const BitReader& br, uint32_t pos) {
   return (uint32_t)(v >> (32 - sh));
 }
 
-// A lane's cached view of the stream: 64-bit window, left aligned.
+// A lane's cached view of the stream: 64-bit window, left aligned, plus the
+// next stream word already in flight (its load is issued one refill ahead, so
+// the lane does not wait on memory latency at each refill).
 struct BitCursor {
   uint64_t buf;   // next bits, MSB first
   int32_t nbits;  // valid bits in buf
   uint32_t pos;   // absolute bit position of the next unread bit
-  uint32_t next_word;
+  uint32_t next_word;  // index of the word held in pf
+  uint32_t pf;         // prefetched stream word
 };
 
-DHD void bc_init(BitCursor& c, const BitReader& br, uint32_t pos) {
-  c.pos = pos;
-  uint32_t w = pos >> 5, sh = pos & 31;
-  c.buf = (((uint64_t)br_word(br, w) << 32) | br_word(br, w + 1)) << sh;
-  c.nbits = 64 - (int)sh;
-  c.next_word = w + 2;
+// Two stream sources: kWin = false reads the destuffed bytes from global memory;
+// kWin = true reads a copy staged in LDS as big-endian-swapped words (br.words,
+// br.nbytes = bytes valid, zero beyond).  Either way 32 bits are refilled at a
+// time from a word fetched one refill ahead.
+DHD uint32_t win_word(const BitReader& br, uint32_t i) {
+  const uint32_t b = i * 4;
+  if (b + 4 <= br.nbytes) return br.words[i];
+  if (b >= br.nbytes) return 0u;
+  return br.words[i] & (0xFFFFFFFFu << (8 * (b + 4 - br.nbytes)));  // keep the first (nbytes-b) bytes
+}
+
+template <bool kWin>
+DHD uint32_t src_word(const BitReader& br, uint32_t i) {
+  return kWin ? win_word(br, i) : br_word(br, i);
 }
 
 // Ensure >= 32 valid bits.
+template <bool kWin>
 DHD void bc_fill(BitCursor& c, const BitReader& br) {
   if (c.nbits < 32) {
-    c.buf |= (uint64_t)br_word(br, c.next_word) << (32 - c.nbits);
+    c.buf |= (uint64_t)c.pf << (32 - c.nbits);
     c.nbits += 32;
     c.next_word++;
+    c.pf = src_word<kWin>(br, c.next_word);
   }
+}
+
+template <bool kWin>
+DHD void bc_init(BitCursor& c, const BitReader& br, uint32_t pos) {
+  c.pos = pos;
+  uint32_t w = pos >> 5, sh = pos & 31;
+  c.buf = (((uint64_t)src_word<kWin>(br, w) << 32) | src_word<kWin>(br, w + 1)) << sh;
+  c.nbits = 64 - (int)sh;
+  c.next_word = w + 2;
+  c.pf = src_word<kWin>(br, w + 2);
 }
 
 DHD uint32_t bc_peek(const BitCursor& c, int n) { return (uint32_t)(c.buf >> (64 - n)); }
@@ -134,32 +171,34 @@ DHD void bc_skip(BitCursor& c, int n) {
   c.pos += n;
 }
 
-// Decode one Huffman symbol (jpeg_huff_decode semantics incl. the l=17 "fake zero").
-// Requires >= 17 valid bits in the cursor.
-DHD int huff_decode_sym(BitCursor& c, const HuffTable* t) {
-  uint32_t look = bc_peek(c, kLookBits);
-  uint16_t e = t->look[look];
-  if (e) {
-    bc_skip(c, e >> 8);
-    return e & 0xFF;
+// Symbol whose code is longer than kLookBits (jpeg_huff_decode's bit-serial loop,
+// incl. the l = 17 "fake zero").  The maxcode values are read up front and the
+// length found by comparisons, so the lane waits on LDS once, not per bit.
+DHD void huff_slow(const BitCursor& c, const HuffTable* t, int* sym, int* len) {
+  const uint32_t p17 = bc_peek(c, 17);  // code of up to 16 bits + sentinel
+  int32_t mc[17 - kLookBits], vo[17 - kLookBits];
+#pragma unroll
+  for (int k = 0; k < 17 - kLookBits; ++k) {
+    mc[k] = t->maxcode[kLookBits + 1 + k];
+    vo[k] = t->valoffset[kLookBits + 1 + k];
   }
-  uint32_t p16 = bc_peek(c, 17);  // 17 bits: code of up to 16 bits + sentinel
-  int l = kLookBits + 1;
-  int code = (int)(p16 >> (17 - l));
-  while (code > t->maxcode[l]) {
-    ++l;
-    code = (int)(p16 >> (17 - l));
-    if (l == 17) break;
+  int l = 17, off = 0;
+#pragma unroll
+  for (int k = 16 - kLookBits; k >= 0; --k) {
+    if ((int32_t)(p17 >> (16 - kLookBits - k)) <= mc[k]) {
+      l = kLookBits + 1 + k;
+      off = vo[k];
+    }
   }
-  if (l > 16) {
-    bc_skip(c, 17);
-    return 0;  // JWRN_HUFF_BAD_CODE: libjpeg fakes a zero
+  if (l > 16) {  // JWRN_HUFF_BAD_CODE: libjpeg fakes a zero after 17 bits
+    *sym = 0;
+    *len = 17;
+    return;
   }
-  bc_skip(c, l);
-  return t->huffval[(code + t->valoffset[l]) & 255];
+  const int code = (int)(p17 >> (17 - l));
+  *sym = t->huffval[(code + off) & 255];
+  *len = l;
 }
-
-DHD int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(((unsigned)-1) << s) + 1 : x; }
 
 // Decoder state between steps.
 struct HState {
@@ -208,44 +247,61 @@ struct StepOut {
   int32_t block_done;
 };
 
-// Execute one step from cursor c / state (c, z).  Updates state.
+// Execute one step from cursor c / state (c, z).  Updates state.  One lookahead
+// read resolves the common case (code + extra bits inside kLookBits) for DC and
+// AC alike, so the lanes of a wave rarely diverge into separate table reads.
+template <bool kWin>
 DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
   StepOut o;
   o.block_done = 0;
-  bc_fill(cur, br);
-  int comp = hi_comp(im, blk);
-  if (z == 0) {
-    int s = huff_decode_sym(cur, im.tabs + comp);
-    int diff = 0;
-    if (s) {  // >= 15 bits remain after a <= 17-bit code (bc_fill guaranteed >= 32)
-      uint32_t r = bc_peek(cur, s);
-      bc_skip(cur, s);
-      diff = huff_extend((int)r, s);
+  bc_fill<kWin>(cur, br);
+  const int comp = hi_comp(im, blk);
+  const bool dc = z == 0;
+  const HuffTable* t = im.tabs + (dc ? comp : 3 + comp);
+  const uint32_t e = t->look[bc_peek(cur, kLookBits)];
+  const int f = (int)(int16_t)(e >> 16);
+  int r, v;
+  if (f) {
+    bc_skip(cur, f & 15);
+    r = (f >> 4) & 15;
+    v = f >> 8;
+  } else {
+    int sym, len;
+    if (e & 0xFFFFu) {
+      sym = (int)((e >> 8) & 255u);
+      len = (int)(e & 255u);
+    } else {
+      huff_slow(cur, t, &sym, &len);
     }
+    bc_skip(cur, len);  // >= 15 bits remain after a <= 17-bit code (bc_fill guaranteed >= 32)
+    const int s = dc ? sym : sym & 15;
+    r = dc ? 0 : sym >> 4;
+    v = 0;
+    if (s) {
+      const uint32_t x = bc_peek(cur, s);
+      bc_skip(cur, s);
+      v = huff_extend((int)x, s);
+    }
+  }
+  if (dc) {
     o.kind = 0;
-    o.value = diff;
+    o.value = v;
     o.zz = 0;
     z = 1;
+  } else if (v) {
+    z += r;
+    o.kind = 1;
+    o.value = v;
+    o.zz = z > 79 ? 79 : z;
+    z += 1;
   } else {
-    int rs = huff_decode_sym(cur, im.tabs + 3 + comp);
-    int r = rs >> 4, s = rs & 15;
-    if (s) {
-      z += r;
-      uint32_t v = bc_peek(cur, s);
-      bc_skip(cur, s);
-      o.kind = 1;
-      o.value = huff_extend((int)v, s);
-      o.zz = z > 79 ? 79 : z;
-      z += 1;
-    } else {
-      o.kind = 2;
-      o.value = 0;
-      o.zz = 0;
-      if (r == 15)
-        z += 16;
-      else
-        z = 64;  // EOB
-    }
+    o.kind = 2;
+    o.value = 0;
+    o.zz = 0;
+    if (r == 15)
+      z += 16;
+    else
+      z = 64;  // EOB
   }
   if (z >= 64) {
     z = 0;
@@ -261,9 +317,17 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
 
 // What a lane learns by decoding the steps that start in [st.pos, end).
 struct RangeOut {
-  HState end;          // state at the first step boundary >= end
-  int32_t nblk;        // blocks whose DC step starts in the range
-  int32_t dcsum[kMaxComp];
+  HState end;      // state at the first step boundary >= end
+  int32_t nblk;    // blocks whose DC step starts in the range
+};
+
+constexpr int kHuffCheckpoints = 32;  // block boundaries recorded per lane by the first decode
+
+// A block boundary (state before a DC step) seen by a lane's first decode:
+// bit position, block-in-MCU index c and the blocks started before it.
+struct Checkpoint {
+  uint32_t pos;
+  uint32_t cn;  // (blocks before << 4) | c
 };
 
 // A state is only ever produced by the decoder itself; clamp anyway so that no
@@ -274,59 +338,114 @@ DHD HState sanitize(HState st, int bpm) {
   return st;
 }
 
-DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, uint32_t end) {
+// First (speculative) decode of a range; records up to kmax block boundaries.
+template <bool kWin>
+DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, uint32_t end, Checkpoint* cps,
+                          int kmax, int32_t* ncp) {
   st = sanitize(st, im.blocks_per_mcu);
   RangeOut r;
   r.nblk = 0;
-  r.dcsum[0] = r.dcsum[1] = r.dcsum[2] = 0;
+  int n = 0;
   BitCursor cur;
-  bc_init(cur, br, st.pos);
+  bc_init<kWin>(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;
   while (cur.pos < end) {
-    if (z == 0) r.nblk++;
-    int comp = hi_comp(im, blk);
-    StepOut o = huff_step(cur, br, im, blk, z);
-    if (o.kind == 0) add3(r.dcsum, comp, o.value);
+    if (z == 0) {
+      if (n < kmax) cps[n++] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
+      r.nblk++;
+    }
+    huff_step<kWin>(cur, br, im, blk, z);
   }
   r.end.pos = cur.pos;
   r.end.c = blk;
   r.end.z = z;
+  *ncp = n;
   return r;
 }
 
-// Block sink interface (duck-typed): zero(), set(natural_index, int16), flush(absolute_block).
-// Decode from `st` (a true state, with DC predictors `pred`) and emit every block whose DC
-// step starts before `end`, finishing the last one past `end`; the leading partial block
-// (st.z != 0) belongs to the previous lane and is decoded without being emitted.  Stops at
-// `total_blocks`.  Returns the bit position reached.
-template <typename Sink>
+// Re-decode of a range from a corrected start state.  As soon as the decode
+// reaches a block boundary the first decode also passed through (same bit
+// position, same block-in-MCU index), everything after it is what the first
+// decode already found: its end state and remaining block count are reused.
+template <bool kWin>
+DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
+                               const Checkpoint* cps, int ncp, RangeOut first) {
+  st = sanitize(st, im.blocks_per_mcu);
+  int32_t nblk = 0;
+  int j = 0;
+  BitCursor cur;
+  bc_init<kWin>(cur, br, st.pos);
+  int32_t blk = st.c, z = st.z;
+  while (cur.pos < end) {
+    if (z == 0) {
+      while (j < ncp && cps[j].pos < cur.pos) ++j;
+      if (j < ncp && cps[j].pos == cur.pos && (int32_t)(cps[j].cn & 15u) == blk) {
+        RangeOut r = first;
+        r.nblk = nblk + first.nblk - (int32_t)(cps[j].cn >> 4);
+        return r;
+      }
+      nblk++;
+    }
+    huff_step<kWin>(cur, br, im, blk, z);
+  }
+  RangeOut r;
+  r.end.pos = cur.pos;
+  r.end.c = blk;
+  r.end.z = z;
+  r.nblk = nblk;
+  return r;
+}
+
+// Block sink interface (duck-typed): begin(absolute_block) zero-fills the block,
+// set(natural_index, int16) stores one coefficient.
+// Decode from `st` (a true state) and emit every block whose DC step starts before
+// `end`, finishing the last one past `end`; the leading partial block (st.z != 0)
+// belongs to the previous lane and is decoded without being emitted.  Stops at
+// `total_blocks`.  DC: with `pred` the absolute value is stored (DC predictors
+// carried by the caller); without, the difference goes to dcd[block] and the
+// coefficient is left 0 for the DC prefix pass (k_dcscan).  Returns the bit position.
+template <bool kWin, typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
-                          int32_t total_blocks, int32_t* pred, Sink& sink) {
+                          int32_t total_blocks, int32_t* pred, int32_t* dcd, Sink& sink) {
   st = sanitize(st, im.blocks_per_mcu);
   BitCursor cur;
-  bc_init(cur, br, st.pos);
+  bc_init<kWin>(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;
   while (z != 0) {  // skip the tail of the previous lane's block
-    huff_step(cur, br, im, blk, z);
+    huff_step<kWin>(cur, br, im, blk, z);
   }
   int32_t b = first_block;
   while (b < total_blocks && cur.pos < end) {
-    sink.zero();
+    sink.begin(b);
     int comp = hi_comp(im, blk);
     for (;;) {
-      StepOut o = huff_step(cur, br, im, blk, z);
+      StepOut o = huff_step<kWin>(cur, br, im, blk, z);
       if (o.kind == 0) {
-        add3(pred, comp, o.value);
-        sink.set(0, (int16_t)get3(pred, comp));
+        if (pred) {
+          add3(pred, comp, o.value);
+          sink.set(0, (int16_t)get3(pred, comp));
+        } else {
+          dcd[b] = o.value;
+        }
       } else if (o.kind == 1) {
         sink.set(kNaturalOrder[o.zz], (int16_t)o.value);
       }
       if (o.block_done) break;
     }
-    sink.flush(b);
     ++b;
   }
   return cur.pos;
+}
+
+// Element offset (int16 units) of absolute block b inside the image's coefficient area.
+DHD int64_t coef_block_offset(const ImgDesc& d, int32_t b) {
+  const int bpm = d.blocks_per_mcu;
+  const int m = b / bpm, c = b - m * bpm;
+  const CompDesc& cd = d.comp[d.mcu_comp[c]];
+  const int one = d.ncomp == 1;
+  const int bx = (m % d.mcus_x) * (one ? 1 : cd.h) + d.mcu_bx[c];
+  const int by = (m / d.mcus_x) * (one ? 1 : cd.v) + d.mcu_by[c];
+  return cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64;
 }
 
 }  // namespace dino

@@ -50,6 +50,14 @@ __global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __rest
 // ---------------------------------------------------------------------------
 // k_plan: exclusive scan of per-image chunk sizes (single workgroup of 1024)
 // ---------------------------------------------------------------------------
+// Checkpoints + DC differences of the speculative Huffman decode (no restart intervals).
+__device__ int64_t spec_cps_bytes(const ImgDesc& d) {
+  return d.restart_interval > 0 ? 0 : (int64_t)kHuffThreads * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
+}
+__device__ int64_t spec_bytes(const ImgDesc& d) {
+  return d.restart_interval > 0 ? 0 : spec_cps_bytes(d) + align16(4 * (int64_t)d.total_blocks);
+}
+
 __device__ int64_t image_chunk_bytes(const ImgDesc& d, int64_t* ent, int64_t* rst, int64_t* coef, int64_t* plane,
                                      int64_t* rgb) {
   if (d.status != DINO_IMG_OK) {
@@ -63,7 +71,7 @@ __device__ int64_t image_chunk_bytes(const ImgDesc& d, int64_t* ent, int64_t* rs
   for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
   *plane = align16(p);
   *rgb = align16((int64_t)d.width * d.height * 3 + 16);
-  return *ent + *rst + *coef + *plane + *rgb;
+  return *ent + *rst + *coef + *plane + *rgb + spec_bytes(d);
 }
 
 __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size) {
@@ -103,6 +111,8 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
       d.coef_off = d.rst_off + rst;
       d.plane_off = d.coef_off + coef;
       d.rgb_off = d.plane_off + plane;
+      d.cps_off = d.rgb_off + rgb;
+      d.dcd_off = d.cps_off + spec_cps_bytes(d);
     }
     base += sz;
   }
@@ -127,6 +137,7 @@ __device__ __forceinline__ int classify_ff(const uint8_t* r, int n, int k) {
 // aligned 16-byte chunk (plus the bytes either side for the 0xFF rules),
 // classifies it, and the workgroup scans (kept bytes, RST markers) packed in one
 // word to place the lane's output.  The first terminating marker ends the scan.
+template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave, uint32_t* total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t x = v;
@@ -139,7 +150,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   __syncthreads();
   uint32_t before = 0, all = 0;
 #pragma unroll
-  for (int k = 0; k < kDestuffThreads / 64; ++k) {
+  for (int k = 0; k < NT / 64; ++k) {
     const uint32_t t = s_wave[k];
     before += k < w ? t : 0u;
     all += t;
@@ -224,7 +235,7 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __re
     }
     const uint32_t packed = (uint32_t)__popc(keep) | ((uint32_t)__popc(rstm) << 16);
     uint32_t tot;
-    const uint32_t ex = block_excl_scan(packed, s_wave, &tot);
+    const uint32_t ex = block_excl_scan<kDestuffThreads>(packed, s_wave, &tot);
     uint32_t o = o_run + (ex & 0xFFFFu), ro = rc_run + (ex >> 16);
     for (uint32_t m = keep | rstm; m; m &= m - 1) {
       const int j = __ffs(m) - 1;
@@ -256,63 +267,141 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// k_huffman: one workgroup (256 lanes) per image
+// k_huffman: one workgroup (kHuffThreads lanes) per image
 // ---------------------------------------------------------------------------
-constexpr int kHuffThreads = 256;
-constexpr int kMinSubBits = 2048;
-constexpr int kBlkStride = 68;  // int16 per lane block buffer (136 B: 8-byte aligned, 2-way banks)
+constexpr int kMinSubBits = 1024;
+
 
 struct HuffLds {
   ImgDesc sd;
   HuffTable tab[6];
   HState S[kHuffThreads];
   RangeOut R[kHuffThreads];
-  int32_t blk0[kHuffThreads];
-  int32_t pred[kHuffThreads][kMaxComp];
-  int16_t blkbuf[kHuffThreads * kBlkStride];
+  RangeOut R1[kHuffThreads];
+  uint32_t wsum[kHuffThreads / 64];
   int32_t bad;
 };
 
-static_assert(sizeof(HuffLds) == 58600, "HuffLds layout");
 static_assert(sizeof(ImgDesc) == 896, "ImgDesc layout");
+constexpr int kHuffWinOff = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
+// Dynamic LDS of k_huffman: tables + lane state, plus (DINO_HUFF_LDS_KB builds) a window
+// holding the whole destuffed stream when it fits.  Measured on MI355X (640x480 q85,
+// batch 512): the window halves the per-step time but, at 156 KiB, allows one workgroup
+// per CU; without it four fit, which wins both alone and overlapped with other kernels.
+#ifdef DINO_HUFF_LDS_KB
+constexpr int kHuffLdsBytes = DINO_HUFF_LDS_KB * 1024;
+#else
+constexpr int kHuffLdsBytes = kHuffWinOff;
+#endif
+static_assert(kHuffWinOff <= kHuffLdsBytes, "HuffLds does not fit the LDS budget");
 
-struct LdsSink {
-  int16_t* blk;
-  int16_t* coef;  // image coefficient area (global)
+// Blocks go straight to the image's coefficient area: zero-filled, then the
+// non-zero coefficients stored.
+struct GlobalSink {
   const ImgDesc* d;
-  __device__ void zero() {
-    uint64_t* p = (uint64_t*)blk;
+  int16_t* coef;
+  int16_t* blk;
+  __device__ void begin(int32_t b) {
+    blk = coef + coef_block_offset(*d, b);
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) p[i] = 0;
+    for (int i = 0; i < 8; ++i) ((uint4*)blk)[i] = z;
   }
   __device__ void set(int i, int16_t v) { blk[i] = v; }
-  __device__ void flush(int32_t b) {
-    int bpm = d->blocks_per_mcu;
-    int m = b / bpm, c = b - m * bpm;
-    int ci = d->mcu_comp[c];
-    const CompDesc& cd = d->comp[ci];
-    int one = d->ncomp == 1;
-    int bx = (m % d->mcus_x) * (one ? 1 : cd.h) + d->mcu_bx[c];
-    int by = (m / d->mcus_x) * (one ? 1 : cd.v) + d->mcu_by[c];
-    uint64_t* dst = (uint64_t*)(coef + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64);
-    const uint64_t* src = (const uint64_t*)blk;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) dst[i] = src[i];
-  }
 };
+
+// prof (nullable, DINO_HUFF_PROFILE=1): per image int64[8] = wall-clock stamps
+// (100 MHz) at start / tables / phase 1 / sync / write end, sync rounds, lanes.
+__device__ __forceinline__ void huff_stamp(int64_t* prof, int img, int k) {
+  if (prof && threadIdx.x == 0) prof[img * 8 + k] = (int64_t)wall_clock64();
+}
+
+template <bool kWin>
+__device__ void huff_restart(HuffLds& L, const HuffImage& im, const uint32_t* words, const int32_t* rst,
+                             GlobalSink& sink, int t) {
+  const ImgDesc& sd = L.sd;
+  const int nseg = sd.n_rst_max;
+  const int per = sd.restart_interval * sd.blocks_per_mcu;
+  for (int k = t; k < nseg; k += kHuffThreads) {
+    uint32_t start = k == 0 ? 0u : (uint32_t)rst[k - 1] * 8u;
+    BitReader sb{words, k + 1 < nseg ? (uint32_t)rst[k] : (uint32_t)sd.ent_len};
+    int32_t pred[kMaxComp] = {0, 0, 0};
+    int first = k * per, last = min(first + per, sd.total_blocks);
+    decode_write<kWin>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+  }
+}
+
+// Speculative self-synchronising decode of one image's entropy stream.
+template <bool kWin>
+__device__ void huff_spec(HuffLds& L, const HuffImage& im, const BitReader br, const uint32_t nbits, uint8_t* ws,
+                          GlobalSink& sink, int64_t* prof, int img, int t) {
+  const ImgDesc& sd = L.sd;
+  int n = (int)((nbits + kMinSubBits - 1) / kMinSubBits);
+  n = n < 1 ? 1 : (n > kHuffThreads ? kHuffThreads : n);
+  uint32_t sub = (nbits + n - 1) / n;
+  sub = (sub + 31) & ~31u;
+  if (sub == 0) sub = 32;
+  const bool active = t < n;
+  const uint32_t my_end_range = (t == n - 1) ? nbits : (uint32_t)(t + 1) * sub;
+  const uint32_t my_end_write = (t == n - 1) ? 0xFFFFFFFFu : (uint32_t)(t + 1) * sub;
+  Checkpoint* cps = (Checkpoint*)(ws + sd.cps_off) + (int64_t)t * kHuffCheckpoints;
+  int32_t ncp = 0;
+  if (active) {
+    HState s0{(uint32_t)t * sub, 0, 0};
+    L.S[t] = s0;
+    const RangeOut r = decode_range<kWin>(br, im, s0, my_end_range, cps, kHuffCheckpoints, &ncp);
+    L.R[t] = r;
+    L.R1[t] = r;
+  }
+  __syncthreads();  // phase-1 results of lane t-1 (another wave) must be visible before round 0 reads them
+  huff_stamp(prof, img, 2);
+  int round = 0;
+  for (; round < kHuffThreads + 1; ++round) {
+    HState want;
+    bool redo = false;
+    if (active && t >= 1) {
+      want = L.R[t - 1].end;
+      redo = !hstate_eq(want, L.S[t]);
+    }
+    __syncthreads();
+    if (redo) {
+      L.S[t] = want;
+      L.R[t] = decode_range_sync<kWin>(br, im, want, my_end_range, cps, ncp, L.R1[t]);
+    }
+    if (!__syncthreads_or(redo ? 1 : 0)) break;
+  }
+  huff_stamp(prof, img, 3);
+  // first block of each lane: exclusive prefix sum of block counts
+  uint32_t tot;
+  const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)L.R[t].nblk : 0u, L.wsum, &tot);
+  if (active)
+    decode_write<kWin>(br, im, L.S[t], my_end_write, (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
+                       (int32_t*)(ws + sd.dcd_off), sink);
+  if (prof) {
+    __syncthreads();
+    huff_stamp(prof, img, 4);
+    if (t == 0) {
+      prof[img * 8 + 5] = round;
+      prof[img * 8 + 6] = n;
+      prof[img * 8 + 7] = kWin;
+    }
+  }
+}
 
 __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restrict__ bytes,
                                                           const int64_t* __restrict__ offsets,
-                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
+                                                          int64_t* __restrict__ prof) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   ImgDesc& sd = L.sd;
   const int img = blockIdx.x, t = threadIdx.x;
+  huff_stamp(prof, img, 0);
   if (t == 0) sd = desc[img];
   __syncthreads();
   if (sd.status != DINO_IMG_OK) return;
   const uint8_t* p = bytes + offsets[img];
-  // ---- tables: derived (6 lanes), then lookahead (all lanes)
+  // ---- tables: derived (6 lanes), then lookahead, then the AC fast tables (all lanes)
   if (t == 0) L.bad = 0;
   __syncthreads();
   if (t < 2 * sd.ncomp) {
@@ -329,76 +418,72 @@ __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restr
   for (int e = t; e < 6 * (1 << kLookBits); e += kHuffThreads) {
     int slot = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
     int c = slot % 3;
-    if (c < sd.ncomp) L.tab[slot].look[idx] = huff_look_entry(&L.tab[slot], idx);
+    if (c < sd.ncomp) L.tab[slot].look[idx] = huff_look_entry(&L.tab[slot], idx, slot < 3);
   }
   __syncthreads();
   HuffImage im;
   hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
   const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
-  LdsSink sink;
-  sink.blk = L.blkbuf + t * kBlkStride;
+  GlobalSink sink;
   sink.coef = (int16_t*)(ws + sd.coef_off);
   sink.d = &sd;
+  // ---- stage the destuffed stream (+ its 64 zero bytes) in LDS as swapped words when it fits
+  uint32_t* lwin = (uint32_t*)(smem + kHuffWinOff);
+  const uint32_t need = ((uint32_t)sd.ent_len + 64u + 3u) / 4u;
+  const uint32_t nwin = kHuffLdsBytes - kHuffWinOff >= 4096 && need * 4u <= (uint32_t)(kHuffLdsBytes - kHuffWinOff)
+                            ? need
+                            : 0u;
+  for (uint32_t i = t; i < nwin; i += kHuffThreads) lwin[i] = bswap32(words[i]);
+  __syncthreads();
+  huff_stamp(prof, img, 1);
 
   if (sd.restart_interval > 0) {
-    // ---- restart intervals are independent: one lane per segment
+    // ---- restart intervals are independent: one lane per segment, absolute DC
     const int32_t* rst = (const int32_t*)(ws + sd.rst_off);
-    const int nseg = sd.n_rst_max;
-    const int per = sd.restart_interval * sd.blocks_per_mcu;
-    for (int k = t; k < nseg; k += kHuffThreads) {
-      uint32_t start = k == 0 ? 0u : (uint32_t)rst[k - 1] * 8u;
-      BitReader sb{words, k + 1 < nseg ? (uint32_t)rst[k] : (uint32_t)sd.ent_len};
-      int32_t pred[kMaxComp] = {0, 0, 0};
-      int first = k * per, last = min(first + per, sd.total_blocks);
-      decode_write(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+    if (nwin) {
+      huff_restart<true>(L, im, lwin, rst, sink, t);
+    } else {
+      huff_restart<false>(L, im, words, rst, sink, t);
     }
     return;
   }
-  // ---- speculative self-synchronising decode
-  const BitReader br{words, (uint32_t)sd.ent_len};
-  const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
-  int n = (int)((nbits + kMinSubBits - 1) / kMinSubBits);
-  n = n < 1 ? 1 : (n > kHuffThreads ? kHuffThreads : n);
-  uint32_t sub = (nbits + n - 1) / n;
-  sub = (sub + 31) & ~31u;
-  if (sub == 0) sub = 32;
-  const bool active = t < n;
-  const uint32_t my_end_range = (t == n - 1) ? nbits : (uint32_t)(t + 1) * sub;
-  const uint32_t my_end_write = (t == n - 1) ? 0xFFFFFFFFu : (uint32_t)(t + 1) * sub;
-  if (active) {
-    HState s0{(uint32_t)t * sub, 0, 0};
-    L.S[t] = s0;
-    L.R[t] = decode_range(br, im, s0, my_end_range);
-  }
-  __syncthreads();  // phase-1 results of lane t-1 (another wave) must be visible before round 0 reads them
-  for (int round = 0; round < kHuffThreads + 1; ++round) {
-    HState want;
-    bool redo = false;
-    if (active && t >= 1) {
-      want = L.R[t - 1].end;
-      redo = !hstate_eq(want, L.S[t]);
-    }
-    __syncthreads();
-    if (redo) {
-      L.S[t] = want;
-      L.R[t] = decode_range(br, im, want, my_end_range);
-    }
-    if (!__syncthreads_or(redo ? 1 : 0)) break;
-  }
-  // prefix sums of blocks and DC differences (serial over <= 256 lanes)
-  if (t == 0) {
-    int32_t b = 0, pr[kMaxComp] = {0, 0, 0};
-    for (int i = 0; i < n; ++i) {
-      L.blk0[i] = b;
-      for (int c = 0; c < kMaxComp; ++c) L.pred[i][c] = pr[c];
-      b += L.R[i].nblk;
-      for (int c = 0; c < kMaxComp; ++c) pr[c] += L.R[i].dcsum[c];
-    }
-  }
-  __syncthreads();
-  if (active) {
-    int32_t pred[kMaxComp] = {L.pred[t][0], L.pred[t][1], L.pred[t][2]};
-    decode_write(br, im, L.S[t], my_end_write, L.blk0[t], sd.total_blocks, pred, sink);
+  if (nwin)
+    huff_spec<true>(L, im, BitReader{lwin, nwin * 4u}, (uint32_t)sd.ent_len * 8u, ws, sink, prof, img, t);
+  else
+    huff_spec<false>(L, im, BitReader{words, (uint32_t)sd.ent_len}, (uint32_t)sd.ent_len * 8u, ws, sink, prof, img,
+                     t);
+}
+
+// ---------------------------------------------------------------------------
+// k_dcscan: DC predictors of a speculatively decoded image (no restart
+// intervals): per-component running sums of the DC differences k_huffman left
+// in decode order, written into the blocks' DC coefficients.  One workgroup per
+// image, a contiguous run of blocks per lane.
+// ---------------------------------------------------------------------------
+constexpr int kDcScanThreads = 256;
+
+__global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  __shared__ uint32_t s_wave[kDcScanThreads / 64];
+  const ImgDesc& d = desc[blockIdx.x];
+  if (d.status != DINO_IMG_OK || d.restart_interval > 0) return;
+  const int T = d.total_blocks, bpm = d.blocks_per_mcu;
+  uint32_t mc = 0;
+  for (int i = 0; i < bpm && i < kMaxBlocksPerMcu; ++i) mc |= (uint32_t)(d.mcu_comp[i] & 3) << (2 * i);
+  const int32_t* dcd = (const int32_t*)(ws + d.dcd_off);
+  int16_t* coef = (int16_t*)(ws + d.coef_off);
+  const int per = (T + kDcScanThreads - 1) / kDcScanThreads;
+  const int b0 = min(T, threadIdx.x * per), b1 = min(T, b0 + per);
+  int32_t s[kMaxComp] = {0, 0, 0};
+  for (int b = b0; b < b1; ++b) add3(s, (int)((mc >> (2 * (b % bpm))) & 3u), dcd[b]);
+  uint32_t tot;
+  int32_t pfx[kMaxComp];
+  pfx[0] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[0], s_wave, &tot);
+  pfx[1] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[1], s_wave, &tot);
+  pfx[2] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[2], s_wave, &tot);
+  for (int b = b0; b < b1; ++b) {
+    const int c = (int)((mc >> (2 * (b % bpm))) & 3u);
+    add3(pfx, c, dcd[b]);
+    coef[coef_block_offset(d, b)] = (int16_t)get3(pfx, c);
   }
 }
 
@@ -1132,7 +1217,7 @@ static const bool g_sync_check = [] {
 static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct",
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
-                                                       "k_vert_local"};
+                                                       "k_vert_local", "k_dcscan"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -1151,7 +1236,7 @@ const char* g_failed_kernel = "";
     }                                                      \
   } while (0)
 
-static int huff_lds_bytes() { return (int)((sizeof(HuffLds) + 15) & ~(size_t)15); }
+static int huff_lds_bytes() { return kHuffLdsBytes; }
 
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
@@ -1165,7 +1250,8 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
                         huff_lds_bytes());
     attr_set = true;
   }
-  TIMED(tm, kKHuffman, s, (k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  TIMED(tm, kKHuffman, s, (k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws, a.prof)));
+  TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKIdct, s, (k_idct<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
   return hipGetLastError();

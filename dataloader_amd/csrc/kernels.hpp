@@ -6,6 +6,12 @@
 namespace dino {
 
 // Per-(image, view) scratch placement, written by k_vplan.
+// Lanes of k_huffman (one workgroup per image).
+#ifndef DINO_HUFF_THREADS
+#define DINO_HUFF_THREADS 256
+#endif
+constexpr int kHuffThreads = DINO_HUFF_THREADS;
+
 // LDS of k_hresize: taps (when they fit in 16 KiB) + RGBX rows of one band.
 constexpr int kHresizeLds = 40 * 1024;
 
@@ -22,7 +28,7 @@ struct ViewPlan {
 // the launch stream around each kernel; elapsed times are summed on demand.
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuffman, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
-  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKNumKernels
+  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKNumKernels
 };
 
 struct KernelTimer {
@@ -49,6 +55,7 @@ struct DecodeArgs {
   ImgDesc* desc;
   uint8_t* ws;
   int64_t ws_size;
+  int64_t* prof;  // k_huffman phase stamps (nullable)
 };
 
 // Output pointers travel as a kernel argument (no host->device copy whose source

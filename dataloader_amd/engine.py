@@ -7,6 +7,7 @@ HIP kernels of ``libdino_ingest.so``.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import numpy as np
@@ -22,8 +23,9 @@ def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _stream_handle(device: torch.device) -> ctypes.c_void_p:
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+def _stream_handle(device: torch.device, stream: torch.cuda.Stream | None = None) -> ctypes.c_void_p:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
 
 
 def pack_jpegs(jpegs, pin: bool = True) -> tuple[torch.Tensor, torch.Tensor]:
@@ -43,7 +45,8 @@ class IngestEngine:
     """Owns a ``dino_ctx`` (decode + augment workspaces sized from the limits)."""
 
     def __init__(self, device: int | torch.device = 0, max_batch: int = 512, max_views: int = 10,
-                 max_crop_size: int = 224, max_image_dim: int = 8192, workspace_bytes: int = 0):
+                 max_crop_size: int = 224, max_image_dim: int = 8192, workspace_bytes: int = 0,
+                 stream: torch.cuda.Stream | None = None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
             raise _lib.DinoError("IngestEngine needs a ROCm GPU (torch.cuda.is_available() is False); "
@@ -55,31 +58,42 @@ class IngestEngine:
             _lib.check(self.lib.dino_ctx_create(self.device.index or 0, ctypes.byref(self.limits),
                                                 ctypes.byref(self._ctx)), "dino_ctx_create")
         self.last_batch = 0
+        self.stream = stream  # None: launch on torch's current stream
+
+    def _s(self) -> ctypes.c_void_p:
+        return _stream_handle(self.device, self.stream)
+
+    def on_stream(self):
+        """Context in which torch allocations/ops are ordered with this engine's launches."""
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
     # ------------------------------------------------------------------ decode
     def decode(self, d_bytes: torch.Tensor, d_offsets: torch.Tensor, batch: int,
                info: torch.Tensor | None = None) -> torch.Tensor:
         if info is None:
-            info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
+            with self.on_stream():
+                info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
         _lib.check(self.lib.dino_decode(self._ctx, _ptr(d_bytes), _ptr(d_offsets), batch, _ptr(info),
-                                        _stream_handle(self.device)), "dino_decode")
+                                        self._s()), "dino_decode")
         self.last_batch = batch
         return info
 
     def copy_rgb(self, index: int, width: int, height: int) -> torch.Tensor:
-        out = torch.zeros(height, width, 3, dtype=torch.uint8, device=self.device)
-        _lib.check(self.lib.dino_copy_rgb(self._ctx, index, _ptr(out), _stream_handle(self.device)),
+        with self.on_stream():
+            out = torch.zeros(height, width, 3, dtype=torch.uint8, device=self.device)
+        _lib.check(self.lib.dino_copy_rgb(self._ctx, index, _ptr(out), self._s()),
                    "dino_copy_rgb")
         return out
 
     def debug_region(self, index: int, region: int, nbytes: int) -> torch.Tensor:
-        out = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
+        with self.on_stream():
+            out = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
         _lib.check(self.lib.dino_debug_region(self._ctx, index, region, _ptr(out), nbytes,
-                                              _stream_handle(self.device)), "dino_debug_region")
+                                              self._s()), "dino_debug_region")
         return out
 
     KERNEL_NAMES = ["k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct", "k_color", "k_params", "k_vplan",
-                    "k_rcoeffs", "k_hresize", "k_final_global", "k_final_local", "k_vert_global", "k_vert_local"]
+                    "k_rcoeffs", "k_hresize", "k_final_global", "k_final_local", "k_vert_global", "k_vert_local", "k_dcscan"]
 
     def set_timing(self, enable: bool) -> None:
         _lib.check(self.lib.dino_set_timing(self._ctx, int(enable)), "dino_set_timing")
@@ -96,22 +110,24 @@ class IngestEngine:
     def sample_params(self, cfg, seed: int, batch_index: int, out: torch.Tensor | None = None) -> torch.Tensor:
         n = self.last_batch * (cfg.n_global + cfg.n_local)
         if out is None:
-            out = torch.empty(n * VIEW_PARAMS_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
+            with self.on_stream():
+                out = torch.empty(n * VIEW_PARAMS_DTYPE.itemsize, dtype=torch.uint8, device=self.device)
         _lib.check(self.lib.dino_sample_params(self._ctx, ctypes.byref(cfg), seed & (2**64 - 1), batch_index,
-                                               _ptr(out), _stream_handle(self.device)), "dino_sample_params")
+                                               _ptr(out), self._s()), "dino_sample_params")
         return out
 
     def alloc_views(self, cfg, batch: int) -> list[torch.Tensor]:
         dt = _TORCH_OUT[cfg.out_dtype]
         sizes = [cfg.global_size] * cfg.n_global + [cfg.local_size] * cfg.n_local
-        return [torch.empty(batch, 3, s, s, dtype=dt, device=self.device) for s in sizes]
+        with self.on_stream():
+            return [torch.empty(batch, 3, s, s, dtype=dt, device=self.device) for s in sizes]
 
     def augment(self, cfg, params: torch.Tensor, views: list[torch.Tensor] | None = None) -> list[torch.Tensor]:
         if views is None:
             views = self.alloc_views(cfg, self.last_batch)
         ptrs = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
         _lib.check(self.lib.dino_augment(self._ctx, ctypes.byref(cfg), _ptr(params), ptrs,
-                                         _stream_handle(self.device)), "dino_augment")
+                                         self._s()), "dino_augment")
         return views
 
     def run_batch(self, d_bytes, d_offsets, batch: int, cfg, seed: int, batch_index: int,
@@ -120,12 +136,13 @@ class IngestEngine:
         if views is None:
             views = self.alloc_views(cfg, batch)
         if info is None:
-            info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
+            with self.on_stream():
+                info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
         ptrs = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
         pp = _ptr(params_out) if params_out is not None else ctypes.c_void_p(0)
         _lib.check(self.lib.dino_run_batch(self._ctx, _ptr(d_bytes), _ptr(d_offsets), batch, ctypes.byref(cfg),
                                            seed & (2**64 - 1), batch_index, pp, ptrs, _ptr(info),
-                                           _stream_handle(self.device)), "dino_run_batch")
+                                           self._s()), "dino_run_batch")
         self.last_batch = batch
         return views, info
 

@@ -18,6 +18,7 @@ records so the CPU oracle can replay a batch exactly.
 
 from __future__ import annotations
 
+from collections import deque
 from typing import Any
 
 import numpy as np
@@ -37,10 +38,26 @@ def _out_code(out_dtype) -> int:
     return _DTYPES.get(out_dtype, OUT_BF16)
 
 
+class _Slot:
+    """One in-flight batch: an engine (ctx + stream) and the batch's small buffers."""
+
+    def __init__(self, engine: IngestEngine):
+        self.engine = engine
+        self.params: torch.Tensor | None = None
+        self.info: torch.Tensor | None = None
+        self.event: torch.cuda.Event | None = None
+        self.inflight = None
+        self.outputs: dict[str, torch.Tensor] | None = None
+
+
 class MI355XAugPipeline:
+    """``depth`` > 1 keeps that many batches in flight: each slot owns a ctx and a
+    HIP stream, consecutive batches alternate slots, so one batch's entropy
+    decode (latency bound) overlaps another's resize/jitter kernels."""
+
     def __init__(self, source: Any, aug_cfg, batch_size: int, resolution_src=None, seed: int = 0,
                  out_dtype="bf16", device: int = 0, max_image_dim: int = 8192, workspace_bytes: int = 0,
-                 engine: IngestEngine | None = None):
+                 engine: IngestEngine | None = None, depth: int = 1):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -48,19 +65,43 @@ class MI355XAugPipeline:
         self._out = _out_code(out_dtype)
         self._seed = int(seed)
         self._batch_index = 0
+        self.depth = max(1, int(depth))
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
-        self.engine = engine or IngestEngine(device, max_batch=self._batch_size, max_views=aug_cfg.n_views,
-                                             max_crop_size=max_crop, max_image_dim=max_image_dim,
-                                             workspace_bytes=workspace_bytes)
+        self._slots: list[_Slot] = []
+        for k in range(self.depth):
+            if k == 0 and engine is not None:
+                eng = engine
+            else:
+                stream = torch.cuda.Stream(device=device) if self.depth > 1 else None
+                eng = IngestEngine(device, max_batch=self._batch_size, max_views=aug_cfg.n_views,
+                                   max_crop_size=max_crop, max_image_dim=max_image_dim,
+                                   workspace_bytes=workspace_bytes, stream=stream)
+            self._slots.append(_Slot(eng))
+        self._last: _Slot = self._slots[0]
         self._closed = False
-        self._last_params: torch.Tensor | None = None
-        self._last_info: torch.Tensor | None = None
+
+    @property
+    def engine(self) -> IngestEngine:
+        return self._slots[0].engine
 
     @property
     def device(self) -> torch.device:
         return self.engine.device
+
+    def set_timing(self, enable: bool) -> None:
+        for sl in self._slots:
+            sl.engine.set_timing(enable)
+
+    def kernel_times(self) -> dict[str, tuple[float, int]]:
+        """Per-kernel (ms, launches) summed over the slots (HIP events on each slot's stream)."""
+        tot: dict[str, tuple[float, int]] = {}
+        for sl in self._slots:
+            for k, (ms, n) in sl.engine.kernel_times().items():
+                a, b = tot.get(k, (0.0, 0))
+                tot[k] = (a + ms, b + n)
+        return tot
 
     def _sizes(self) -> tuple[int, int]:
         if self._resolution_src is None:
@@ -71,49 +112,94 @@ class MI355XAugPipeline:
     def _cfg(self, g: int, l: int):
         return make_aug_config(self._aug_cfg, g, l, self._out)
 
+    def _next_slot(self) -> _Slot:
+        return self._slots[self._batch_index % self.depth]
+
     def run_device_batch(self, d_bytes: torch.Tensor, d_offsets: torch.Tensor, batch: int | None = None,
                          views: list[torch.Tensor] | None = None) -> dict[str, torch.Tensor]:
-        """Stage 3 on JPEG bytes already resident in HBM (the benchmark's device-resident path)."""
+        """Stage 3 on JPEG bytes already resident in HBM (the benchmark's device-resident path).
+
+        With depth > 1 the work is enqueued on the slot's stream after the caller's
+        stream (which produced d_bytes); the caller's stream is NOT made to wait for
+        the outputs — call ``wait()`` (or synchronise) before reading them."""
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
+        sl = self._next_slot()
+        if sl.engine.stream is not None:
+            sl.engine.stream.wait_stream(torch.cuda.current_stream(self.device))
+        return self._launch(sl, d_bytes, d_offsets, batch, views)
+
+    def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views):
         batch = self._batch_size if batch is None else int(batch)
         g, l = self._sizes()
         cfg = self._cfg(g, l)
-        if self._last_params is None or self._last_params.numel() < batch * self._aug_cfg.n_views * 64:
-            self._last_params = torch.empty(batch * self._aug_cfg.n_views * 64, dtype=torch.uint8,
-                                            device=self.device)
-        views, info = self.engine.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
-                                            views=views, params_out=self._last_params)
-        self._last_info = info
+        eng = sl.engine
+        if sl.params is None or sl.params.numel() < batch * self._aug_cfg.n_views * 64:
+            with eng.on_stream():
+                sl.params = torch.empty(batch * self._aug_cfg.n_views * 64, dtype=torch.uint8, device=self.device)
+        views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
+                                    views=views, params_out=sl.params)
+        sl.info = info
+        sl.outputs = {f"view_{i}": v for i, v in enumerate(views)}
+        if eng.stream is not None:
+            sl.event = torch.cuda.Event()
+            sl.event.record(eng.stream)
+        self._last = sl
         self._batch_index += 1
-        return {f"view_{i}": v for i, v in enumerate(views)}
+        return sl.outputs
 
-    def run_one_batch(self) -> dict[str, torch.Tensor]:
+    def _enqueue_one(self) -> _Slot:
+        """Pull one batch from the source and enqueue it on the next slot (H2D on that slot's stream)."""
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
         jpeg_batch = self._source()  # may raise StopIteration (end of epoch)
         if len(jpeg_batch) != self._batch_size:
             raise ValueError(f"source returned {len(jpeg_batch)} samples, expected {self._batch_size}")
+        sl = self._next_slot()
         host_buf, offsets = pack_jpegs(jpeg_batch, pin=True)
-        d_bytes = host_buf.to(self.device, non_blocking=True)
-        d_offsets = offsets.to(self.device, non_blocking=True)
-        out = self.run_device_batch(d_bytes, d_offsets, len(jpeg_batch))
+        with sl.engine.on_stream():
+            d_bytes = host_buf.to(self.device, non_blocking=True)
+            d_offsets = offsets.to(self.device, non_blocking=True)
+        self._launch(sl, d_bytes, d_offsets, len(jpeg_batch), None)
         # torch's caching host allocator keeps the pinned staging block until the copy retires
-        self._inflight = (host_buf, d_bytes, d_offsets)
-        return out
+        sl.inflight = (host_buf, d_bytes, d_offsets)
+        return sl
+
+    def _hand_over(self, sl: _Slot) -> dict[str, torch.Tensor]:
+        """Order the caller's stream after the slot's work and tie the outputs to it."""
+        if sl.event is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(sl.event)
+            for t in sl.outputs.values():
+                t.record_stream(cur)
+        return sl.outputs
+
+    def wait(self) -> None:
+        """Make the caller's stream wait for the last enqueued batch."""
+        self._hand_over(self._last)
+
+    def run_one_batch(self) -> dict[str, torch.Tensor]:
+        return self._hand_over(self._enqueue_one())
 
     def last_params(self) -> np.ndarray:
         """Records of the last batch, sample-major (``[b * n_views + v]``)."""
-        n = self.engine.last_batch * self._aug_cfg.n_views
-        return params_from_device(self._last_params[: n * 64])
+        sl = self._last
+        if sl.event is not None:
+            sl.event.synchronize()
+        n = sl.engine.last_batch * self._aug_cfg.n_views
+        return params_from_device(sl.params[: n * 64])
 
     def last_status(self) -> np.ndarray:
-        return self._last_info[:, 0].cpu().numpy() if self._last_info is not None else np.zeros(0, np.int32)
+        sl = self._last
+        if sl.event is not None:
+            sl.event.synchronize()
+        return sl.info[:, 0].cpu().numpy() if sl.info is not None else np.zeros(0, np.int32)
 
     def close(self) -> None:
         if not self._closed:
             self._closed = True
-            self.engine.close()
+            for sl in self._slots:
+                sl.engine.close()
 
     def __del__(self):
         try:
@@ -123,12 +209,17 @@ class MI355XAugPipeline:
 
 
 class MI355XPipelineIterator:
-    """DALIGenericIterator-shaped wrapper: ``next()`` -> ``[ {view_name: Tensor} ]``."""
+    """DALIGenericIterator-shaped wrapper: ``next()`` -> ``[ {view_name: Tensor} ]``.
+
+    Keeps ``pipeline.depth`` batches in flight (DALI's prefetch queue): each
+    ``next()`` tops the queue up, then hands over the oldest batch."""
 
     def __init__(self, pipeline: MI355XAugPipeline, output_map: list[str], batch_size: int) -> None:
         self._pipe = pipeline
         self._output_map = list(output_map)
         self._exhausted = False
+        self._queue: deque = deque()
+        self._source_done = False
 
     def __iter__(self):
         return self
@@ -136,11 +227,17 @@ class MI355XPipelineIterator:
     def __next__(self) -> list[dict[str, torch.Tensor]]:
         if self._exhausted:
             raise StopIteration
-        try:
-            return [self._pipe.run_one_batch()]
-        except StopIteration:
+        while not self._source_done and len(self._queue) < self._pipe.depth:
+            try:
+                self._queue.append(self._pipe._enqueue_one())
+            except StopIteration:
+                self._source_done = True
+        if not self._queue:
             self._exhausted = True
-            raise
+            raise StopIteration
+        return [self._pipe._hand_over(self._queue.popleft())]
 
     def reset(self) -> None:
         self._exhausted = False
+        self._source_done = False
+        self._queue.clear()

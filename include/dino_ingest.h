@@ -140,7 +140,7 @@ int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32
 /* Per-kernel HIP-event timing of this ctx's launches (bench / profiling).
  * Kernel ids: 0 parse, 1 plan, 2 destuff, 3 huffman, 4 idct, 5 color, 6 params,
  * 7 vplan, 8 rcoeffs, 9 hresize, 10 final(global views), 11 final(local views),
- * 12 vert(global views), 13 vert(local views).
+ * 12 vert(global views), 13 vert(local views), 14 dcscan.
  * dino_kernel_times synchronises the recorded events, returns the sums since the
  * last call (ms, launches) and resets them. */
 int dino_set_timing(dino_ctx* ctx, int32_t enable);
@@ -148,7 +148,9 @@ int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t 
 
 /* Debug / test introspection of the last decoded batch: copy image `index`'s
  * region (0 descriptor, 1 destuffed entropy bytes, 2 DCT coefficients,
- * 3 component planes, 4 RGB) into d_dst (<= max_bytes).  Synchronises the stream. */
+ * 3 component planes, 4 RGB, 5 Huffman phase stamps: int64[8] = wall clock (100 MHz) at
+ * start / tables / first decode / sync / write end, sync rounds, lanes; needs the env
+ * DINO_HUFF_PROFILE=1 at ctx creation) into d_dst (<= max_bytes).  Synchronises the stream. */
 int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream);
 
 /* Stage-5 cast (reference FP8Formatter.quantise, memory.py:193-214, scale 1):

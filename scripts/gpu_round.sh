@@ -5,4 +5,4 @@ cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp && \
 DINO_SYNC_CHECK=1 scripts/gpu_step.sh 300 gpurun_out/${TAG}_e4.log -- python scripts/exp_batches.py 512 full 0,0,512 && \
 scripts/gpu_step.sh 600 gpurun_out/${TAG}_tests.log -- python -m pytest tests/test_gpu_parity.py -q -m gpu && \
 scripts/gpu_step.sh 900 gpurun_out/${TAG}_bench.log -- python bench.py --steps 20 --warmup 3 --h2d --kernel-json gpurun_out/${TAG}_kernels.json && \
-scripts/gpu_step.sh 900 gpurun_out/${TAG}_prof.log -- rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --images 8192
+scripts/gpu_step.sh 900 gpurun_out/${TAG}_prof.log -- rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --images 8192 --procs 0 --depth 1

@@ -54,28 +54,33 @@ inline Destuffed model_destuff(const uint8_t* r, int n) {
 }
 
 struct CoefSink {
-  int16_t blk[64];
   const ImgDesc* d;
   int16_t* coef;  // image coefficient area
-  void zero() { memset(blk, 0, sizeof(blk)); }
-  void set(int i, int16_t v) { blk[i] = v; }
-  void flush(int32_t b) {
-    int m = b / d->blocks_per_mcu, c = b % d->blocks_per_mcu;
-    int ci = d->mcu_comp[c];
-    const CompDesc& cd = d->comp[ci];
-    int bx = (m % d->mcus_x) * (d->ncomp == 1 ? 1 : cd.h) + d->mcu_bx[c];
-    int by = (m / d->mcus_x) * (d->ncomp == 1 ? 1 : cd.v) + d->mcu_by[c];
-    memcpy(coef + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64, blk, 128);
+  int16_t* blk = nullptr;
+  void begin(int32_t b) {
+    blk = coef + coef_block_offset(*d, b);
+    memset(blk, 0, 128);
   }
+  void set(int i, int16_t v) { blk[i] = v; }
 };
+
+// k_dcscan: running DC sums per component over the blocks in decode order.
+inline void model_dcscan(const ImgDesc& d, const HuffImage& im, const int32_t* dcd, int16_t* coef) {
+  int32_t p[kMaxComp] = {0, 0, 0};
+  for (int32_t b = 0; b < d.total_blocks; ++b) {
+    const int c = hi_comp(im, b % d.blocks_per_mcu);
+    add3(p, c, dcd[b]);
+    coef[coef_block_offset(d, b)] = (int16_t)get3(p, c);
+  }
+}
 
 inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* [6] */, HuffImage& im) {
   for (int c = 0; c < d.ncomp; ++c) {
     if (!huff_build_derived(p + d.huff_off[d.comp[c].td], true, &tabs[c])) return false;
     if (!huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &tabs[3 + c])) return false;
     for (int i = 0; i < (1 << kLookBits); ++i) {
-      tabs[c].look[i] = huff_look_entry(&tabs[c], i);
-      tabs[3 + c].look[i] = huff_look_entry(&tabs[3 + c], i);
+      tabs[c].look[i] = huff_look_entry(&tabs[c], i, true);
+      tabs[3 + c].look[i] = huff_look_entry(&tabs[3 + c], i, false);
     }
   }
   hi_init(im, tabs, d.mcu_comp, d.blocks_per_mcu);
@@ -83,18 +88,26 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* 
 }
 
 // ---- k_huffman, speculative mode: phases 1..4 over `lanes` lanes ------------
-inline void model_huffman_spec(const BitReader& br, const HuffImage& im, uint32_t nbits, int total_blocks, int lanes,
-                               CoefSink& sink, int32_t* stats) {
+// Phase 1 decodes every range from a guessed state recording checkpoints; each
+// round re-decodes the ranges whose start state changed (stopping at the first
+// checkpoint match); phase 4 writes blocks (DC as differences); then k_dcscan.
+template <bool kWin>
+inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
+                               CoefSink& sink, int32_t* dcd, int32_t* stats) {
+  const int total_blocks = d.total_blocks;
   int n = lanes;
   uint32_t sub = (nbits + n - 1) / n;
   sub = (sub + 31) & ~31u;
   if (sub == 0) sub = 32;
   std::vector<HState> S(n);
-  std::vector<RangeOut> R(n);
-  auto endof = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
+  std::vector<RangeOut> R(n), R1(n);
+  std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
+  std::vector<int32_t> ncp(n);
+  auto rend = [&](int i) -> uint32_t { return i == n - 1 ? nbits : (uint32_t)(i + 1) * sub; };
+  auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
   for (int i = 0; i < n; ++i) {
     S[i] = HState{(uint32_t)i * sub, 0, 0};
-    R[i] = decode_range(br, im, S[i], i == n - 1 ? nbits : endof(i));
+    R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], kHuffCheckpoints, &ncp[i]);
   }
   int rounds = 0, redone = 0;
   for (;;) {
@@ -104,7 +117,7 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, uint32_
     for (int i = 1; i < n; ++i) {
       if (!hstate_eq(want[i], S[i])) {
         S[i] = want[i];
-        R[i] = decode_range(br, im, S[i], i == n - 1 ? nbits : endof(i));
+        R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], ncp[i], R1[i]);
         any = true;
         ++redone;
       }
@@ -112,13 +125,12 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, uint32_
     ++rounds;
     if (!any) break;
   }
-  int32_t blk0 = 0, pred[kMaxComp] = {0, 0, 0};
+  int32_t blk0 = 0;
   for (int i = 0; i < n; ++i) {
-    int32_t p[kMaxComp] = {pred[0], pred[1], pred[2]};
-    decode_write(br, im, S[i], endof(i), blk0, total_blocks, p, sink);
+    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, dcd, sink);
     blk0 += R[i].nblk;
-    for (int c = 0; c < kMaxComp; ++c) pred[c] += R[i].dcsum[c];
   }
+  model_dcscan(d, im, dcd, sink.coef);
   if (stats) {
     stats[0] = rounds;
     stats[1] = redone;
@@ -151,6 +163,9 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
   sink.d = &d;
   sink.coef = coef.data();
   BitReader br{(const uint32_t*)ds.bytes.data(), (uint32_t)ds.len};
+  // mode 2: the stream as k_huffman stages it in LDS (big-endian-swapped words + zero pad)
+  std::vector<uint32_t> win((ds.len + 64 + 3) / 4, 0u);
+  for (size_t i = 0; i < win.size(); ++i) win[i] = br_word(br, (uint32_t)i);
   if (d.restart_interval > 0) {
     int nseg = d.n_rst_max;
     if ((int)ds.rst.size() < nseg - 1) return DINO_IMG_BADDATA;
@@ -160,13 +175,24 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
       BitReader sb{br.words, k + 1 < nseg ? (uint32_t)ds.rst[k] : (uint32_t)ds.len};
       int32_t pred[kMaxComp] = {0, 0, 0};
       int first = k * per, last = std::min(first + per, d.total_blocks);
-      decode_write(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+      if (mode == 2) {  // segments read from the staged (swapped) words, as k_huffman's LDS window
+        BitReader sw{win.data(), k + 1 < nseg ? (uint32_t)ds.rst[k] : (uint32_t)ds.len};
+        decode_write<true>(sw, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+      } else {
+        decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+      }
     }
   } else if (mode == 0) {
     int32_t pred[kMaxComp] = {0, 0, 0};
-    decode_write(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, sink);
+    decode_write<false>(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, (int32_t*)nullptr, sink);
   } else {
-    model_huffman_spec(br, im, (uint32_t)ds.len * 8, d.total_blocks, lanes, sink, stats);
+    std::vector<int32_t> dcd(d.total_blocks, 0);
+    if (mode == 2) {
+      BitReader bw{win.data(), (uint32_t)win.size() * 4};
+      model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, sink, dcd.data(), stats);
+    } else {
+      model_huffman_spec<false>(br, im, d, (uint32_t)ds.len * 8, lanes, sink, dcd.data(), stats);
+    }
   }
   if (cap) cap->coef = coef;
   // k_idct

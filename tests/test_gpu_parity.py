@@ -304,3 +304,29 @@ def test_decode_marker_edge_cases(gpu_device):
                 got = eng.copy_rgb(i, int(info[i, 1]), int(info[i, 2])).cpu().numpy()
                 np.testing.assert_array_equal(got, np.asarray(ref), err_msg=f"pad {pad} case {i}")
         eng.close()
+
+
+def test_depth2_overlap_matches_serial(gpu_device):
+    """Two batches in flight (two ctx + streams) give bit-identical views to the
+    serial pipeline for the same (seed, batch index); the prefetching iterator
+    hands batches over in order."""
+    from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
+    cfg = DINOAugConfig()
+    uniq = [make_jpeg(320 + 16 * s, 240 + 8 * s, s) for s in range(8)]
+    B = 16
+    batches = [[uniq[(k * 3 + i) % 8] for i in range(B)] for k in range(5)]
+
+    def run(depth):
+        src = iter(batches)
+        pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=11, device=0, depth=depth)
+        it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
+        outs = [{k: v.clone() for k, v in out[0].items()} for out in it]
+        torch.cuda.synchronize()
+        pipe.close()
+        return outs
+
+    serial, overlapped = run(1), run(2)
+    assert len(serial) == len(overlapped) == len(batches)
+    for a, b in zip(serial, overlapped):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
