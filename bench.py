@@ -166,7 +166,7 @@ def main() -> None:
     ap.add_argument("--images", type=int, default=50000)
     ap.add_argument("--unique", type=int, default=256)
     ap.add_argument("--procs", type=int, default=-1, help="JPEG encoder processes (0: in-process)")
-    ap.add_argument("--depth", type=int, default=2, help="batches in flight (slots with their own ctx + stream)")
+    ap.add_argument("--depth", type=int, default=3, help="batches in flight (slots with their own ctx + stream)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600}")

@@ -242,7 +242,7 @@ int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, i
   switch (region) {
     case 0: src = c->d_desc + index; n = sizeof(ImgDesc); break;
     case 1: src = c->d_ws + d.ent_off; n = d.ent_len; break;
-    case 2: src = c->d_ws + d.coef_off; n = d.coef_bytes; break;
+    case 2: src = c->d_ws + d.coef_off; n = d.plane_off - d.coef_off; break;  // sparse entries + block info
     case 3: src = c->d_ws + d.plane_off; n = d.rgb_off - d.plane_off; break;
     case 4: src = c->d_ws + d.rgb_off; n = (int64_t)d.width * d.height * 3; break;
     case 5:  // k_huffman phase stamps (DINO_HUFF_PROFILE=1)

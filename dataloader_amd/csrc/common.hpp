@@ -50,10 +50,12 @@ struct ImgDesc {
   int32_t total_blocks;    // MCUs * blocks_per_mcu
   // filled by k_plan (byte offsets into the ctx workspace)
   int64_t base;            // start of this image's chunk
-  int64_t ent_off, rst_off, coef_off, plane_off, rgb_off;
+  int64_t ent_off, rst_off, plane_off, rgb_off;
+  int64_t coef_off;        // sparse AC entries (u32, 64 per block of capacity; k_huffman SparseSink)
   int64_t cps_off;         // k_huffman checkpoints (speculative decode), kHuffThreads x kHuffCheckpoints
-  int64_t dcd_off;         // int32 DC differences per block (decode order), summed by k_dcscan
-  int64_t coef_bytes;
+  int64_t dcd_off;         // int32 DC value per block (decode order): differences until k_dcscan sums them
+  int64_t binfo_off;       // uint2 per block (decode order): first sparse entry, entry count
+  int64_t coef_bytes;      // dense int16 coefficient bytes (host emulator layout)
   // filled by k_destuff
   int32_t ent_len;         // destuffed entropy bytes
   int32_t n_rst;           // RST markers found

@@ -396,14 +396,18 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
   return r;
 }
 
-// Block sink interface (duck-typed): begin(absolute_block) zero-fills the block,
-// set(natural_index, int16) stores one coefficient.
+// Block sink interface (duck-typed): begin(absolute_block) opens a block,
+// ac(zigzag_index, int16) receives one non-zero AC coefficient (zigzag indices are
+// strictly increasing within a block; an index > 63 only comes from a corrupt
+// stream and is the block's last, mapped to natural position 63 as libjpeg's
+// jpeg_natural_order does), dc(int16) the absolute DC value (only with `pred`),
+// end() closes the block.
 // Decode from `st` (a true state) and emit every block whose DC step starts before
 // `end`, finishing the last one past `end`; the leading partial block (st.z != 0)
 // belongs to the previous lane and is decoded without being emitted.  Stops at
-// `total_blocks`.  DC: with `pred` the absolute value is stored (DC predictors
-// carried by the caller); without, the difference goes to dcd[block] and the
-// coefficient is left 0 for the DC prefix pass (k_dcscan).  Returns the bit position.
+// `total_blocks`.  DC: with `pred` the absolute value goes to the sink (DC
+// predictors carried by the caller); without, the difference goes to dcd[block]
+// for the DC prefix pass (k_dcscan).  Returns the bit position.
 template <bool kWin, typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
                           int32_t total_blocks, int32_t* pred, int32_t* dcd, Sink& sink) {
@@ -423,15 +427,16 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
       if (o.kind == 0) {
         if (pred) {
           add3(pred, comp, o.value);
-          sink.set(0, (int16_t)get3(pred, comp));
+          sink.dc((int16_t)get3(pred, comp));
         } else {
           dcd[b] = o.value;
         }
       } else if (o.kind == 1) {
-        sink.set(kNaturalOrder[o.zz], (int16_t)o.value);
+        sink.ac(o.zz, (int16_t)o.value);
       }
       if (o.block_done) break;
     }
+    sink.end();
     ++b;
   }
   return cur.pos;

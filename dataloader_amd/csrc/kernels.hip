@@ -54,24 +54,30 @@ __global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __rest
 __device__ int64_t spec_cps_bytes(const ImgDesc& d) {
   return d.restart_interval > 0 ? 0 : (int64_t)kHuffThreads * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
 }
-__device__ int64_t spec_bytes(const ImgDesc& d) {
-  return d.restart_interval > 0 ? 0 : spec_cps_bytes(d) + align16(4 * (int64_t)d.total_blocks);
-}
 
-__device__ int64_t image_chunk_bytes(const ImgDesc& d, int64_t* ent, int64_t* rst, int64_t* coef, int64_t* plane,
-                                     int64_t* rgb) {
-  if (d.status != DINO_IMG_OK) {
-    *ent = *rst = *coef = *plane = *rgb = 0;
-    return 0;
-  }
-  *ent = align16((int64_t)d.scan_len + 64);
-  *rst = align16(4 * ((int64_t)d.n_rst_max + 1));
-  *coef = align16(d.coef_bytes);
+// Byte sizes of an image's workspace regions, in chunk order: destuffed entropy
+// bytes, restart offsets, sparse coefficient entries (64 u32 per block, see
+// SparseSink), block info (uint2 per block), component planes, RGB, speculative
+// checkpoints, DC values (int32 per block).
+struct ChunkSizes {
+  int64_t ent, rst, coef, binfo, plane, rgb, cps, dcd;
+  __device__ int64_t total() const { return ent + rst + coef + binfo + plane + rgb + cps + dcd; }
+};
+
+__device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
+  ChunkSizes z{};
+  if (d.status != DINO_IMG_OK) return z;
+  z.ent = align16((int64_t)d.scan_len + 64);
+  z.rst = align16(4 * ((int64_t)d.n_rst_max + 1));
+  z.coef = (int64_t)d.total_blocks * 256;
+  z.binfo = align16((int64_t)d.total_blocks * 8);
   int64_t p = 0;
   for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
-  *plane = align16(p);
-  *rgb = align16((int64_t)d.width * d.height * 3 + 16);
-  return *ent + *rst + *coef + *plane + *rgb + spec_bytes(d);
+  z.plane = align16(p);
+  z.rgb = align16((int64_t)d.width * d.height * 3 + 16);
+  z.cps = spec_cps_bytes(d);
+  z.dcd = align16(4 * (int64_t)d.total_blocks);
+  return z;
 }
 
 __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size) {
@@ -81,10 +87,7 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
   int64_t local = 0;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
-    if (i < B) {
-      int64_t a, b, c, d2, e;
-      local += image_chunk_bytes(desc[i], &a, &b, &c, &d2, &e);
-    }
+    if (i < B) local += image_chunk_bytes(desc[i]).total();
   }
   part[t] = local;
   __syncthreads();
@@ -99,20 +102,21 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
     int i = t * per + k;
     if (i >= B) continue;
     ImgDesc& d = desc[i];
-    int64_t ent, rst, coef, plane, rgb;
-    int64_t sz = image_chunk_bytes(d, &ent, &rst, &coef, &plane, &rgb);
+    const ChunkSizes z = image_chunk_bytes(d);
+    const int64_t sz = z.total();
     if (sz == 0) continue;
     if (base + sz > ws_size) {
       d.status = DINO_IMG_TOO_LARGE;
     } else {
       d.base = base;
       d.ent_off = base;
-      d.rst_off = d.ent_off + ent;
-      d.coef_off = d.rst_off + rst;
-      d.plane_off = d.coef_off + coef;
-      d.rgb_off = d.plane_off + plane;
-      d.cps_off = d.rgb_off + rgb;
-      d.dcd_off = d.cps_off + spec_cps_bytes(d);
+      d.rst_off = d.ent_off + z.ent;
+      d.coef_off = d.rst_off + z.rst;
+      d.binfo_off = d.coef_off + z.coef;
+      d.plane_off = d.binfo_off + z.binfo;
+      d.rgb_off = d.plane_off + z.plane;
+      d.cps_off = d.rgb_off + z.rgb;
+      d.dcd_off = d.cps_off + z.cps;
     }
     base += sz;
   }
@@ -282,7 +286,7 @@ struct HuffLds {
   int32_t bad;
 };
 
-static_assert(sizeof(ImgDesc) == 896, "ImgDesc layout");
+static_assert(sizeof(ImgDesc) == 904, "ImgDesc layout");
 constexpr int kHuffWinOff = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
 // Dynamic LDS of k_huffman: tables + lane state, plus (DINO_HUFF_LDS_KB builds) a window
 // holding the whole destuffed stream when it fits.  Measured on MI355X (640x480 q85,
@@ -295,19 +299,49 @@ constexpr int kHuffLdsBytes = kHuffWinOff;
 #endif
 static_assert(kHuffWinOff <= kHuffLdsBytes, "HuffLds does not fit the LDS budget");
 
-// Blocks go straight to the image's coefficient area: zero-filled, then the
-// non-zero coefficients stored.
-struct GlobalSink {
-  const ImgDesc* d;
-  int16_t* coef;
-  int16_t* blk;
-  __device__ void begin(int32_t b) {
-    blk = coef + coef_block_offset(*d, b);
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ((uint4*)blk)[i] = z;
+// Sparse coefficient output.  A lane appends its blocks' non-zero AC coefficients
+// as u32 entries ((int16 value << 16) | zigzag index) to a private region of the
+// image's entry area that starts at 64 entries per block before its first block
+// (a block has at most 63 AC entries, so regions never overlap), buffered four at
+// a time into 16-byte stores so that each lane writes whole contiguous lines
+// instead of scattered 2-byte coefficients into a dense block.  binfo[b] =
+// {first entry, entry count}; the DC value lives in dcd[b] (absolute after
+// k_dcscan, or written here with restart intervals).  k_idct scatters the entries
+// into its LDS block.
+struct SparseSink {
+  uint32_t* ent;   // image entry area
+  uint2* binfo;    // image block info
+  int32_t* dcd;    // image DC values
+  uint32_t n;      // entries written (relative to the image entry area), multiple of 4
+  uint32_t k;      // entries buffered in e0..e3
+  uint32_t e0, e1, e2, e3;
+  uint32_t bstart;
+  int32_t b;
+  __device__ void open(int32_t first_block) {
+    n = (uint32_t)first_block * 64u;
+    k = 0;
   }
-  __device__ void set(int i, int16_t v) { blk[i] = v; }
+  __device__ void begin(int32_t blk) {
+    b = blk;
+    bstart = n + k;
+  }
+  __device__ void push(uint32_t e) {
+    e0 = k == 0 ? e : e0;
+    e1 = k == 1 ? e : e1;
+    e2 = k == 2 ? e : e2;
+    e3 = k == 3 ? e : e3;
+    if (++k == 4) {
+      *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
+      n += 4;
+      k = 0;
+    }
+  }
+  __device__ void ac(int zz, int16_t v) { push(((uint32_t)(uint16_t)v << 16) | (uint32_t)zz); }
+  __device__ void dc(int16_t v) { dcd[b] = (int32_t)v; }
+  __device__ void end() { binfo[b] = make_uint2(bstart, n + k - bstart); }
+  __device__ void close() {  // the region is a multiple of 4 entries: a whole-word tail store stays inside it
+    if (k) *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
+  }
 };
 
 // prof (nullable, DINO_HUFF_PROFILE=1): per image int64[8] = wall-clock stamps
@@ -318,7 +352,7 @@ __device__ __forceinline__ void huff_stamp(int64_t* prof, int img, int k) {
 
 template <bool kWin>
 __device__ void huff_restart(HuffLds& L, const HuffImage& im, const uint32_t* words, const int32_t* rst,
-                             GlobalSink& sink, int t) {
+                             SparseSink& sink, int t) {
   const ImgDesc& sd = L.sd;
   const int nseg = sd.n_rst_max;
   const int per = sd.restart_interval * sd.blocks_per_mcu;
@@ -327,14 +361,16 @@ __device__ void huff_restart(HuffLds& L, const HuffImage& im, const uint32_t* wo
     BitReader sb{words, k + 1 < nseg ? (uint32_t)rst[k] : (uint32_t)sd.ent_len};
     int32_t pred[kMaxComp] = {0, 0, 0};
     int first = k * per, last = min(first + per, sd.total_blocks);
+    sink.open(first);
     decode_write<kWin>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+    sink.close();
   }
 }
 
 // Speculative self-synchronising decode of one image's entropy stream.
 template <bool kWin>
 __device__ void huff_spec(HuffLds& L, const HuffImage& im, const BitReader br, const uint32_t nbits, uint8_t* ws,
-                          GlobalSink& sink, int64_t* prof, int img, int t) {
+                          SparseSink& sink, int64_t* prof, int img, int t) {
   const ImgDesc& sd = L.sd;
   int n = (int)((nbits + kMinSubBits - 1) / kMinSubBits);
   n = n < 1 ? 1 : (n > kHuffThreads ? kHuffThreads : n);
@@ -374,9 +410,12 @@ __device__ void huff_spec(HuffLds& L, const HuffImage& im, const BitReader br, c
   // first block of each lane: exclusive prefix sum of block counts
   uint32_t tot;
   const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)L.R[t].nblk : 0u, L.wsum, &tot);
-  if (active)
+  if (active) {
+    sink.open((int32_t)blk0);
     decode_write<kWin>(br, im, L.S[t], my_end_write, (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
                        (int32_t*)(ws + sd.dcd_off), sink);
+    sink.close();
+  }
   if (prof) {
     __syncthreads();
     huff_stamp(prof, img, 4);
@@ -424,9 +463,10 @@ __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restr
   HuffImage im;
   hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
   const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
-  GlobalSink sink;
-  sink.coef = (int16_t*)(ws + sd.coef_off);
-  sink.d = &sd;
+  SparseSink sink;
+  sink.ent = (uint32_t*)(ws + sd.coef_off);
+  sink.binfo = (uint2*)(ws + sd.binfo_off);
+  sink.dcd = (int32_t*)(ws + sd.dcd_off);
   // ---- stage the destuffed stream (+ its 64 zero bytes) in LDS as swapped words when it fits
   uint32_t* lwin = (uint32_t*)(smem + kHuffWinOff);
   const uint32_t need = ((uint32_t)sd.ent_len + 64u + 3u) / 4u;
@@ -457,7 +497,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restr
 // ---------------------------------------------------------------------------
 // k_dcscan: DC predictors of a speculatively decoded image (no restart
 // intervals): per-component running sums of the DC differences k_huffman left
-// in decode order, written into the blocks' DC coefficients.  One workgroup per
+// in decode order, replaced in place by the absolute (int16) DC values.  One workgroup per
 // image, a contiguous run of blocks per lane.
 // ---------------------------------------------------------------------------
 constexpr int kDcScanThreads = 256;
@@ -469,8 +509,7 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
   const int T = d.total_blocks, bpm = d.blocks_per_mcu;
   uint32_t mc = 0;
   for (int i = 0; i < bpm && i < kMaxBlocksPerMcu; ++i) mc |= (uint32_t)(d.mcu_comp[i] & 3) << (2 * i);
-  const int32_t* dcd = (const int32_t*)(ws + d.dcd_off);
-  int16_t* coef = (int16_t*)(ws + d.coef_off);
+  int32_t* dcd = (int32_t*)(ws + d.dcd_off);
   const int per = (T + kDcScanThreads - 1) / kDcScanThreads;
   const int b0 = min(T, threadIdx.x * per), b1 = min(T, b0 + per);
   int32_t s[kMaxComp] = {0, 0, 0};
@@ -483,53 +522,84 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
   for (int b = b0; b < b1; ++b) {
     const int c = (int)((mc >> (2 * (b % bpm))) & 3u);
     add3(pfx, c, dcd[b]);
-    coef[coef_block_offset(d, b)] = (int16_t)get3(pfx, c);
+    dcd[b] = (int32_t)(int16_t)get3(pfx, c);  // in place: JCOEF (int16) DC, as libjpeg stores it
   }
 }
 
 // ---------------------------------------------------------------------------
 // k_idct: grid (gx, B); lanes over the 8x8 blocks of one image
 // ---------------------------------------------------------------------------
-// 8 lanes per 8x8 block: lane l loads + dequantizes coefficient row l (one 16-byte
-// load, so a wave reads 8 consecutive blocks = 1 KiB contiguously), runs pass 1
-// on column l and pass 2 on row l through an LDS transpose, and stores output row l
-// as one 8-byte word.
+// 8 lanes per 8x8 block, blocks in component-plane raster order (so that a wave's
+// output rows are 8 blocks = 64 contiguous bytes of a plane row).  The group reads
+// the block's decode-order index, its sparse entries (binfo, see SparseSink) and
+// DC, zeroes the LDS block and scatters the entries (lane l takes entries l, l+8,
+// ...), then lane l dequantizes + runs pass 1 on column l and pass 2 on row l, and
+// stores output row l as one 8-byte word.
 constexpr int kIdctBlocksPerWg = 32;
 
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   __shared__ int32_t s_blk[kIdctBlocksPerWg][65];
+  __shared__ uint8_t s_nat[80];
   const ImgDesc& d = desc[blockIdx.y];
   if (d.status != DINO_IMG_OK) return;
+  if (threadIdx.x < 80) s_nat[threadIdx.x] = kNaturalOrder[threadIdx.x];
   const int ncomp = d.ncomp;
   const int64_t nb0 = (int64_t)d.comp[0].bw * d.comp[0].bh;
   const int64_t nb1 = ncomp > 1 ? (int64_t)d.comp[1].bw * d.comp[1].bh : 0;
   const int64_t nb2 = ncomp > 2 ? (int64_t)d.comp[2].bw * d.comp[2].bh : 0;
   const int64_t tot = nb0 + nb1 + nb2;
-  const int16_t* coef = (const int16_t*)(ws + d.coef_off);
+  const uint32_t* ent = (const uint32_t*)(ws + d.coef_off);
+  const uint2* binfo = (const uint2*)(ws + d.binfo_off);
+  const int32_t* dcv = (const int32_t*)(ws + d.dcd_off);
   uint8_t* planes = ws + d.plane_off;
+  // first position of each component inside the MCU (interleaved scans)
+  int moff[kMaxComp] = {0, 0, 0};
+  for (int i = d.blocks_per_mcu - 1; i >= 0; --i) {
+    const int c = d.mcu_comp[i];
+    if (c == 0) moff[0] = i;
+    else if (c == 1) moff[1] = i;
+    else moff[2] = i;
+  }
   const int grp = threadIdx.x >> 3, l = threadIdx.x & 7;
   int32_t* sb = s_blk[grp];
   for (int64_t g0 = (int64_t)blockIdx.x * kIdctBlocksPerWg; g0 < tot; g0 += (int64_t)gridDim.x * kIdctBlocksPerWg) {
     const int64_t g = g0 + grp;
     const bool valid = g < tot;
-    const int c = g < nb0 ? 0 : (g < nb0 + nb1 ? 1 : 2);
-    const int64_t k = g - (c == 0 ? 0 : (c == 1 ? nb0 : nb0 + nb1));
+    const int64_t gg = valid ? g : 0;
+    const int c = gg < nb0 ? 0 : (gg < nb0 + nb1 ? 1 : 2);
+    const int64_t k = gg - (c == 0 ? 0 : (c == 1 ? nb0 : nb0 + nb1));
     const CompDesc& cd = d.comp[c];
-    if (valid) {
-      const int4 raw = ((const int4*)(coef + cd.coef_off / 2 + k * 64))[l];
-      const uint16_t* q = d.qt[cd.tq] + l * 8;
-      const int32_t w4[4] = {raw.x, raw.y, raw.z, raw.w};
+    const int by = (int)(k / cd.bw), bx = (int)(k - (int64_t)by * cd.bw);
+    // decode-order index of plane block (bx, by); a plane block no MCU covers stays all zero
+    int64_t b;
+    if (ncomp == 1) {
+      b = bx < d.mcus_x ? (int64_t)by * d.mcus_x + bx : -1;
+    } else {
+      const int mo = c == 0 ? moff[0] : (c == 1 ? moff[1] : moff[2]);
+      b = ((int64_t)(by / cd.v) * d.mcus_x + bx / cd.h) * d.blocks_per_mcu + mo + (by % cd.v) * cd.h + bx % cd.h;
+    }
+    uint2 bi = make_uint2(0u, 0u);
+    int32_t dc = 0;
+    if (valid && b >= 0 && b < d.total_blocks) {
+      bi = binfo[b];
+      dc = dcv[b];
+    }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sb[l * 8 + 2 * j] = (int32_t)(int16_t)(w4[j] & 0xFFFF) * (int32_t)(int16_t)q[2 * j];
-        sb[l * 8 + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)w4[j] >> 16) * (int32_t)(int16_t)q[2 * j + 1];
+    for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
+    __syncthreads();
+    if (valid) {
+      if (l == 0) sb[0] = dc;
+      for (uint32_t j = l; j < bi.y; j += 8) {
+        const uint32_t e = ent[bi.x + j];
+        sb[s_nat[e & 0x7Fu]] = (int32_t)(int16_t)(e >> 16);
       }
     }
     __syncthreads();
-    if (valid) {  // pass 1 on column l (reads and writes only this lane's column)
+    if (valid) {  // dequantize + pass 1 on column l (reads and writes only this lane's column)
+      const uint16_t* q = d.qt[cd.tq];
       int32_t col[8], wcol[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) col[r] = sb[r * 8 + l];
+      for (int r = 0; r < 8; ++r) col[r] = sb[r * 8 + l] * (int32_t)(int16_t)q[r * 8 + l];
       idct_pass1(col, wcol);
 #pragma unroll
       for (int r = 0; r < 8; ++r) sb[r * 8 + l] = wcol[r];
@@ -544,7 +614,6 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
         uint64_t u;
       } o;
       idct_pass2(row, o.b);
-      const int by = (int)(k / cd.bw), bx = (int)(k - (int64_t)by * cd.bw);
       const int pitch = cd.bw * 8;
       *(uint64_t*)(planes + cd.plane_off + ((int64_t)by * 8 + l) * pitch + bx * 8) = o.u;
     }

@@ -147,7 +147,7 @@ int dino_set_timing(dino_ctx* ctx, int32_t enable);
 int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t n);
 
 /* Debug / test introspection of the last decoded batch: copy image `index`'s
- * region (0 descriptor, 1 destuffed entropy bytes, 2 DCT coefficients,
+ * region (0 descriptor, 1 destuffed entropy bytes, 2 sparse DCT coefficient entries + block info,
  * 3 component planes, 4 RGB, 5 Huffman phase stamps: int64[8] = wall clock (100 MHz) at
  * start / tables / first decode / sync / write end, sync rounds, lanes; needs the env
  * DINO_HUFF_PROFILE=1 at ctx creation) into d_dst (<= max_bytes).  Synchronises the stream. */

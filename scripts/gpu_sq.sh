@@ -1,0 +1,12 @@
+# SQ counter passes for instruction-mix / stall analysis of the decode kernels.
+# usage: scripts/gpu_sq.sh TAG
+TAG=${1:-sq}
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp && \
+BENCH="python bench.py --steps 2 --warmup 1 --no-cpu-baseline --images 2048 --unique 64 --procs 0 --depth 1" && \
+(timeout -s KILL 60 rocprofv3 -L > gpurun_out/${TAG}_counters.txt 2>&1 || true) && \
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d gpurun_out/${TAG}_a -o run --output-format csv -- $BENCH > gpurun_out/${TAG}_a.log 2>&1 && \
+timeout -s KILL 240 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH -d gpurun_out/${TAG}_b -o run --output-format csv -- $BENCH > gpurun_out/${TAG}_b.log 2>&1 ; \
+python scripts/pmc_counters.py gpurun_out/${TAG}_a gpurun_out/${TAG}_b > gpurun_out/${TAG}_table.txt 2>&1; \
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/${TAG}_fetch -o run --output-format csv -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --images 8192 --procs 0 --depth 1 > gpurun_out/${TAG}_fetch.log 2>&1 && \
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/${TAG}_write -o run --output-format csv -- python bench.py --steps 4 --warmup 2 --no-cpu-baseline --images 8192 --procs 0 --depth 1 > gpurun_out/${TAG}_write.log 2>&1 && \
+python scripts/pmc_traffic.py gpurun_out/${TAG}_fetch gpurun_out/${TAG}_write gpurun_out/${TAG}_traffic.json

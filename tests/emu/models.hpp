@@ -61,7 +61,9 @@ struct CoefSink {
     blk = coef + coef_block_offset(*d, b);
     memset(blk, 0, 128);
   }
-  void set(int i, int16_t v) { blk[i] = v; }
+  void ac(int zz, int16_t v) { blk[kNaturalOrder[zz]] = v; }
+  void dc(int16_t v) { blk[0] = v; }
+  void end() {}
 };
 
 // k_dcscan: running DC sums per component over the blocks in decode order.
