@@ -146,6 +146,82 @@ def cpu_baseline(jpegs, seconds: float, batch: int = 32) -> dict:
                       f"(PIL+torch), decode per view, ThreadPoolExecutor({workers}), {dt:.1f}s"}
 
 
+def make_shards(jpegs, shard_size: int) -> list[bytes]:
+    """WebDataset tar shards shaped like the reference fixtures (sample_%06d.jpg + .json)."""
+    import io
+    import tarfile
+    shards = []
+    for s0 in range(0, len(jpegs), shard_size):
+        buf = io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w") as tf:
+            for i in range(s0, min(len(jpegs), s0 + shard_size)):
+                for name, data in ((f"sample_{i:06d}.jpg", jpegs[i]),
+                                   (f"sample_{i:06d}.json", json.dumps({"quality_score": 1.0}).encode())):
+                    ti = tarfile.TarInfo(name)
+                    ti.size = len(data)
+                    tf.addfile(ti, io.BytesIO(data))
+        shards.append(buf.getvalue())
+    return shards
+
+
+def run_e2e(args, uniq, rank: int, world: int, dev, cfg, B: int) -> dict:
+    """C5 end-to-end: shards in /dev/shm (reference cache file format) -> dino_tar_index ->
+    dino_gather into pinned staging -> H2D -> Stage 3, batches in flight as the main run."""
+    import torch
+    import torch.distributed as dist
+
+    from dataloader_amd.pipeline import MI355XAugPipeline
+    from dataloader_amd.sharding import rank_seed
+    from dataloader_amd.tario import ShardBatchFeeder, ShmShardCache
+
+    n = (args.warmup + args.steps + 1) * B
+    jpegs = [uniq[i % len(uniq)] for i in range(n)]
+    shards = make_shards(jpegs, args.shard_size)
+    cache = ShmShardCache(job_id=f"dino_bench_{os.getpid()}", base_dir="/dev/shm", max_gb=64.0)
+    try:
+        paths = [f"/synthetic/rank{rank}/shard-{k:05d}.tar" for k in range(len(shards))]
+        for p, t in zip(paths, shards):
+            cache.put(p, t)  # Stage 1 (filesystem -> /dev/shm) is outside the timed region
+        del shards
+        feeder = ShardBatchFeeder(cache, paths, B, nthreads=args.gather_threads)
+        pipe = MI355XAugPipeline(feeder, cfg, B, seed=rank_seed(1234, rank), out_dtype=args.dtype,
+                                 device=dev.index, max_image_dim=4096 if args.mixed else 2048, depth=args.depth)
+        for _ in range(args.warmup):
+            pipe._enqueue_one()
+        pipe.wait()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        feeder.index_seconds = 0.0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            pipe._enqueue_one()
+        pipe.wait()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        st = pipe.last_status()
+        if (st != 0).any():
+            raise RuntimeError(f"e2e decode failures: {np.unique(st, return_counts=True)}")
+        shards_opened = feeder._shard
+        feeder.close()
+        pipe.close()
+        if world > 1:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
+                "e2e_ms_per_step": round(dt / args.steps * 1e3, 3),
+                "e2e_shard_prepare_ms_total": round(feeder.index_seconds * 1e3, 3),
+                "e2e_shard_wait_ms_total": round(feeder.wait_seconds * 1e3, 3),
+                "e2e_shards": shards_opened, "e2e_gather_threads": args.gather_threads,
+                "e2e_path": "/dev/shm tar shards (shard_cache file format) -> dino_tar_index -> dino_gather "
+                            "(pinned) -> H2D -> Stage 3"}
+    finally:
+        cache.close(remove=True)
+
+
 def load_traffic(kernel: str):
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
@@ -175,6 +251,10 @@ def main() -> None:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--h2d", action="store_true", help="also time the H2D-inclusive rate (pinned host bytes)")
     ap.add_argument("--kernel-json", default="", help="write per-kernel times here (rank 0)")
+    ap.add_argument("--e2e", action="store_true",
+                    help="C5: also time tar shards in /dev/shm -> native index -> pinned gather -> H2D -> kernels")
+    ap.add_argument("--shard-size", type=int, default=1000, help="samples per synthetic tar shard (--e2e)")
+    ap.add_argument("--gather-threads", type=int, default=8, help="dino_gather copier threads (--e2e)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -262,6 +342,8 @@ def main() -> None:
         torch.cuda.synchronize()
         h2d_rate = args.steps * B / (time.perf_counter() - t1)
 
+    e2e = run_e2e(args, uniq, rank, world, dev, cfg, B) if args.e2e else None
+
     value = world * args.steps * B / dt
     out_bytes = {"bf16": 2, "fp8": 1, "fp32": 4}[args.dtype]
     ab = algorithmic_bytes(uniq, cfg.global_crop_size, cfg.local_crop_size, cfg.n_global_crops,
@@ -303,6 +385,8 @@ def main() -> None:
         }
         if h2d_rate is not None:
             line["h2d_inclusive_images_per_s"] = round(h2d_rate, 1)
+        if e2e is not None:
+            line["e2e"] = e2e
         print(json.dumps(line), flush=True)
         if args.kernel_json:
             Path(args.kernel_json).write_text(json.dumps(per_kernel, indent=1))

@@ -48,6 +48,8 @@ class _Slot:
         self.event: torch.cuda.Event | None = None
         self.inflight = None
         self.outputs: dict[str, torch.Tensor] | None = None
+        self.staging: torch.Tensor | None = None      # pinned JPEG bytes of a packed (native) source
+        self.staging_off: torch.Tensor | None = None  # pinned int64 offsets[B+1]
 
 
 class MI355XAugPipeline:
@@ -148,10 +150,40 @@ class MI355XAugPipeline:
         self._batch_index += 1
         return sl.outputs
 
+    def _enqueue_packed(self) -> _Slot:
+        """Native feed (``source.next_spans()``, e.g. :class:`~dataloader_amd.tario.ShardBatchFeeder`):
+        the batch's JPEG byte ranges are gathered by ``dino_gather`` straight into the
+        slot's pinned staging buffer, then one H2D copy on the slot's stream."""
+        from .tario import gather
+
+        spans = self._source.next_spans()  # may raise StopIteration (end of epoch)
+        if len(spans) != self._batch_size:
+            raise ValueError(f"source returned {len(spans)} samples, expected {self._batch_size}")
+        sl = self._next_slot()
+        if sl.event is not None:
+            sl.event.synchronize()  # the slot's previous batch (and its H2D copy) retired: staging is free
+        need = sum(n for _, n in spans)
+        if sl.staging is None or sl.staging.numel() < need:
+            sl.staging = torch.empty(max(need, 1) * 5 // 4, dtype=torch.uint8, pin_memory=True)
+        if sl.staging_off is None or sl.staging_off.numel() < len(spans) + 1:
+            sl.staging_off = torch.empty(len(spans) + 1, dtype=torch.int64, pin_memory=True)
+        off = gather(spans, sl.staging, getattr(self._source, "nthreads", 8))
+        sl.staging_off.numpy()[: len(off)] = off
+        with sl.engine.on_stream():
+            d_bytes = sl.staging[:need].to(self.device, non_blocking=True)
+            d_offsets = sl.staging_off[: len(off)].to(self.device, non_blocking=True)
+        self._launch(sl, d_bytes, d_offsets, len(spans), None)
+        sl.inflight = (d_bytes, d_offsets)
+        if sl.event is None:  # depth 1 (no side stream): the staging buffer is reused next batch
+            torch.cuda.current_stream(self.device).synchronize()
+        return sl
+
     def _enqueue_one(self) -> _Slot:
         """Pull one batch from the source and enqueue it on the next slot (H2D on that slot's stream)."""
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
+        if hasattr(self._source, "next_spans"):
+            return self._enqueue_packed()
         jpeg_batch = self._source()  # may raise StopIteration (end of epoch)
         if len(jpeg_batch) != self._batch_size:
             raise ValueError(f"source returned {len(jpeg_batch)} samples, expected {self._batch_size}")

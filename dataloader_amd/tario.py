@@ -1,0 +1,466 @@
+"""Host-side shard ingest: /dev/shm shard cache → native tar index → pinned batch.
+
+This is the feed of the Stage-3 device path:
+
+* :class:`ShmShardCache` — the read path of the reference's node-local
+  ``NodeSharedShardCache`` (``shard_cache.py:476-712``): one file per shard in
+  ``/dev/shm/<job_id>/<sha1(path)[:16]>`` laid out as ``[data_len:u64][magic:u64]``
+  + tar bytes, magic ``0xDEADBEEFCAFEF00D`` written last (``:83-85, :689-703``),
+  mmapped zero-copy (``get_view``, ``:584-609``).  The node master loads missing
+  shards synchronously and evicts LRU files over budget; the asyncio prefetch,
+  inotify waits and heartbeat of the reference are control plane (out of scope).
+* :func:`index_tar` — ``dino_tar_index`` (C++, ``csrc/tario.cpp``) over a mapped
+  shard: WebDataset samples (key, .jpg range, .json range) without Python
+  per-member work.
+* :func:`extract_jpegs_with_meta` — the reference's extraction call
+  (``hpc_source.py:461-467`` → the absent ``dino_datasets`` helper
+  ``_extract_jpegs_with_meta``) restated on the native index: ``SampleRecord``s with
+  JSON metadata, optional quality filter and shuffle buffer.  The helper itself is
+  not in ``/root/reference``; its semantics here are restated from its call site
+  (parity unpinned beyond the reference's fixture tars).
+* :class:`ShardBatchFeeder` — B JPEGs per batch from mapped shards packed by
+  ``dino_gather`` (threaded memcpy) into a pinned buffer + int64 offsets, the
+  layout ``dino_run_batch`` reads after one H2D copy.
+"""
+
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import hashlib
+import json
+import mmap
+import os
+import struct
+import threading
+from collections import OrderedDict
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Any, Iterator, Sequence
+
+import numpy as np
+
+from . import _lib
+
+HDR_FMT = "QQ"
+HDR_SIZE = struct.calcsize(HDR_FMT)
+READY_MAGIC = 0xDEAD_BEEF_CAFE_F00D
+TAR_TRUNCATED, TAR_BAD_HEADER = 1, 2
+
+
+class DinoTarSample(ctypes.Structure):
+    _fields_ = [("img_off", ctypes.c_int64), ("img_len", ctypes.c_int64), ("meta_off", ctypes.c_int64),
+                ("meta_len", ctypes.c_int64), ("key_off", ctypes.c_int64), ("key_len", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+SAMPLE_DTYPE = np.dtype([("img_off", "<i8"), ("img_len", "<i8"), ("meta_off", "<i8"), ("meta_len", "<i8"),
+                         ("key_off", "<i8"), ("key_len", "<i4"), ("reserved", "<i4")])
+assert SAMPLE_DTYPE.itemsize == ctypes.sizeof(DinoTarSample)
+
+
+class SampleRecord:
+    """Same contract as reference ``augmentation.SampleRecord`` (augmentation.py:67-90)."""
+
+    __slots__ = ("jpeg", "key", "metadata")
+
+    def __init__(self, jpeg, metadata: dict | None = None, key: str = "") -> None:
+        self.jpeg = jpeg
+        self.metadata = metadata
+        self.key = key
+
+
+def _addr(buf) -> tuple[int, int, Any]:
+    """(address, length, keep-alive) of a bytes-like object without copying it."""
+    if isinstance(buf, np.ndarray):
+        a = np.ascontiguousarray(buf).view(np.uint8).reshape(-1)
+        return a.ctypes.data, a.size, a
+    if isinstance(buf, (bytes, bytearray, memoryview, mmap.mmap)):
+        a = np.frombuffer(buf, dtype=np.uint8)
+        return (a.ctypes.data if a.size else 0), a.size, a
+    raise TypeError(f"unsupported buffer type {type(buf).__name__}")
+
+
+@dataclass
+class TarIndex:
+    """Samples of one shard: byte ranges into the indexed buffer, keys, status."""
+
+    samples: np.ndarray   # SAMPLE_DTYPE[n]
+    keys: list[str]
+    n_members: int
+    status: int           # 0 ok, 1 truncated member, 2 bad header after offset 0
+
+    def __len__(self) -> int:
+        return len(self.samples)
+
+
+def index_tar(buf) -> TarIndex:
+    """Index a WebDataset tar held in memory (``dino_tar_index``)."""
+    lib = _lib.load()
+    addr, n, keep = _addr(buf)
+    cap = max(16, n // 1024 + 16)           # a member takes >= 1024 bytes (header + data block)
+    out = np.zeros(cap, SAMPLE_DTYPE)
+    keys = np.zeros(max(256, cap * 64), np.uint8)
+    ns, nm = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib.dino_tar_index(ctypes.c_void_p(addr), n, ctypes.c_void_p(out.ctypes.data), cap,
+                            ctypes.c_void_p(keys.ctypes.data), keys.size, ctypes.byref(ns), ctypes.byref(nm))
+    del keep
+    if rc < 0:
+        raise _lib.DinoError(f"dino_tar_index failed ({rc}): {lib.dino_tar_last_error().decode(errors='replace')}")
+    s = out[:ns.value].copy()
+    kb = keys.tobytes()
+    names = [kb[o:o + ln].decode("utf-8", errors="surrogateescape") if o >= 0 else "" for o, ln in
+             zip(s["key_off"].tolist(), s["key_len"].tolist())]
+    return TarIndex(s, names, int(nm.value), int(rc))
+
+
+def extract_jpegs_with_meta(data, metadata_key: str | None = None, min_quality: float | None = None,
+                            shuffle_buffer: int = 0, rng: np.random.Generator | None = None,
+                            copy: bool = False) -> list[SampleRecord]:
+    """Samples of one shard as ``SampleRecord`` (reference call site hpc_source.py:461-467).
+
+    ``jpeg`` is a zero-copy ``memoryview`` into ``data`` unless ``copy``;
+    ``metadata`` the parsed JSON sidecar (``metadata[metadata_key]`` when a key is
+    given and present); samples whose ``quality_score`` is below ``min_quality``
+    are dropped; ``shuffle_buffer > 1`` permutes the shard's samples with ``rng``.
+    """
+    idx = index_tar(data)
+    mv = memoryview(data) if not isinstance(data, np.ndarray) else memoryview(np.ascontiguousarray(data))
+    mv = mv.cast("B") if mv.format != "B" else mv
+    recs: list[SampleRecord] = []
+    for row, key in zip(idx.samples, idx.keys):
+        meta = None
+        if row["meta_off"] >= 0:
+            try:
+                meta = json.loads(bytes(mv[row["meta_off"]:row["meta_off"] + row["meta_len"]]))
+            except (ValueError, UnicodeDecodeError):
+                meta = None
+        if metadata_key is not None and isinstance(meta, dict) and metadata_key in meta:
+            meta = meta[metadata_key]
+        if min_quality is not None and isinstance(meta, dict):
+            q = meta.get("quality_score")
+            if q is not None and q < min_quality:
+                continue
+        j = mv[row["img_off"]:row["img_off"] + row["img_len"]]
+        recs.append(SampleRecord(bytes(j) if copy else j, meta, key))
+    if shuffle_buffer > 1 and len(recs) > 1:
+        rng = rng if rng is not None else np.random.default_rng()
+        recs = [recs[i] for i in rng.permutation(len(recs))]
+    return recs
+
+
+def gather(srcs: Sequence, dst: "Any", nthreads: int = 8) -> np.ndarray:
+    """Pack byte ranges back to back into ``dst`` (pinned torch uint8 tensor or ndarray).
+
+    ``srcs``: sequence of (address, length) pairs or bytes-like objects.
+    Returns int64 offsets[n+1] (``dino_gather``)."""
+    lib = _lib.load()
+    keep = []
+    ptrs = np.empty(len(srcs), np.uint64)
+    lens = np.empty(len(srcs), np.int64)
+    for i, s in enumerate(srcs):
+        if isinstance(s, tuple):
+            ptrs[i], lens[i] = s
+        else:
+            a, n, k = _addr(s)
+            keep.append(k)
+            ptrs[i], lens[i] = a, n
+    off = np.empty(len(srcs) + 1, np.int64)
+    if hasattr(dst, "data_ptr"):
+        daddr, dcap = dst.data_ptr(), dst.numel() * dst.element_size()
+    else:
+        daddr, dcap, _ = _addr(dst)
+    rc = lib.dino_gather(ctypes.c_void_p(ptrs.ctypes.data), ctypes.c_void_p(lens.ctypes.data), len(srcs),
+                         ctypes.c_void_p(daddr), dcap, ctypes.c_void_p(off.ctypes.data), nthreads)
+    if rc != 0:
+        raise _lib.DinoError(f"dino_gather failed ({rc}): {lib.dino_tar_last_error().decode(errors='replace')}")
+    return off
+
+
+# ---------------------------------------------------------------------------
+# /dev/shm shard cache (read path of reference NodeSharedShardCache)
+# ---------------------------------------------------------------------------
+class _Mapped:
+    __slots__ = ("fd", "mm", "data_len", "refs", "arr")
+
+    def __init__(self, path: Path) -> None:
+        self.fd = os.open(str(path), os.O_RDONLY)
+        try:
+            self.mm = mmap.mmap(self.fd, 0, access=mmap.ACCESS_READ)
+        except Exception:
+            os.close(self.fd)
+            raise
+        data_len, magic = struct.unpack_from(HDR_FMT, self.mm, 0)
+        if magic != READY_MAGIC:
+            self.close()
+            raise RuntimeError(f"Shard {path} has corrupt header (magic={magic:#x})")
+        self.data_len = int(data_len)
+        self.refs = 0
+        self.arr = np.frombuffer(self.mm, np.uint8, count=self.data_len, offset=HDR_SIZE)
+
+    def close(self) -> None:
+        self.arr = None
+        with contextlib.suppress(Exception):
+            self.mm.close()
+        with contextlib.suppress(Exception):
+            os.close(self.fd)
+
+
+def shm_path(base: Path, shard_path: str) -> Path:
+    """``/dev/shm/<job>/<sha1(shard_path)[:16]>`` (reference shard_cache.py:619-622)."""
+    return base / hashlib.sha1(shard_path.encode()).hexdigest()[:16]
+
+
+def write_shm_shard(shm: Path, data) -> None:
+    """Atomic shard write: header with magic 0, data, then the ready magic, rename
+    (reference shard_cache.py:689-703)."""
+    tmp = shm.with_suffix(".tmp")
+    try:
+        with open(tmp, "wb") as f:
+            n = len(data) if not isinstance(data, np.ndarray) else data.nbytes
+            f.write(struct.pack(HDR_FMT, n, 0))
+            f.write(data)
+            f.seek(0)
+            f.write(struct.pack(HDR_FMT, n, READY_MAGIC))
+        tmp.rename(shm)
+    except Exception:
+        with contextlib.suppress(Exception):
+            tmp.unlink()
+        raise
+
+
+def is_ready(shm: Path) -> bool:
+    try:
+        with open(shm, "rb") as f:
+            hdr = f.read(HDR_SIZE)
+        return len(hdr) == HDR_SIZE and struct.unpack(HDR_FMT, hdr)[1] == READY_MAGIC
+    except OSError:
+        return False
+
+
+class ShmShardCache:
+    """Node-local ``/dev/shm`` shard cache with zero-copy mapped reads.
+
+    Same public surface as the reference cache (``prefetch``, ``get``, ``get_view``,
+    ``utilisation``) plus ``get_array`` (a uint8 ndarray over the mapping, what
+    :func:`index_tar` and :class:`ShardBatchFeeder` consume) and ``close``.
+    """
+
+    def __init__(self, job_id: str = "dino", node_master: bool = True, max_gb: float = 128.0,
+                 base_dir: str | os.PathLike = "/dev/shm", max_mapped: int = 256) -> None:
+        self._base = Path(base_dir) / job_id
+        self._base.mkdir(parents=True, exist_ok=True)
+        self._node_master = node_master
+        self._max_bytes = int(max_gb * (1 << 30))
+        self._lru: OrderedDict[str, int] = OrderedDict()
+        self._total = 0
+        self._lock = threading.Lock()
+        self._maps: OrderedDict[str, _Mapped] = OrderedDict()
+        self._max_mapped = max_mapped
+
+    @property
+    def base(self) -> Path:
+        return self._base
+
+    def _path(self, shard_path: str) -> Path:
+        return shm_path(self._base, shard_path)
+
+    def _ensure(self, shard_path: str) -> Path:
+        shm = self._path(shard_path)
+        if is_ready(shm):
+            return shm
+        if not self._node_master:
+            raise FileNotFoundError(f"shard {shard_path} not in the node cache ({shm})")
+        with open(shard_path, "rb") as f:
+            data = f.read()
+        self.put(shard_path, data)
+        return shm
+
+    def put(self, shard_path: str, data) -> Path:
+        """Write shard bytes into the cache (node master), evicting LRU shards over budget."""
+        n = len(data) if not isinstance(data, np.ndarray) else data.nbytes
+        shm = self._path(shard_path)
+        with self._lock:
+            while self._lru and self._total + n > self._max_bytes:
+                old, sz = self._lru.popitem(last=False)
+                self._total -= sz
+                self._drop(old)
+        write_shm_shard(shm, data)
+        with self._lock:
+            self._lru[shard_path] = n
+            self._total += n
+        return shm
+
+    def _drop(self, shard_path: str) -> None:
+        m = self._maps.get(shard_path)
+        if m is not None and m.refs == 0:
+            self._maps.pop(shard_path).close()
+        with contextlib.suppress(OSError):
+            self._path(shard_path).unlink()
+
+    def prefetch(self, shard_path: str) -> None:
+        if self._node_master:
+            self._ensure(shard_path)
+
+    def _acquire(self, shard_path: str) -> _Mapped:
+        shm = self._ensure(shard_path)
+        with self._lock:
+            m = self._maps.get(shard_path)
+            if m is None:
+                idle = [k for k, v in self._maps.items() if v.refs == 0]
+                while idle and len(self._maps) >= self._max_mapped:
+                    self._maps.pop(idle.pop(0)).close()
+                m = _Mapped(shm)
+                self._maps[shard_path] = m
+            self._maps.move_to_end(shard_path)
+            m.refs += 1
+            if shard_path in self._lru:
+                self._lru.move_to_end(shard_path)
+            return m
+
+    def _release(self, shard_path: str) -> None:
+        with self._lock:
+            m = self._maps.get(shard_path)
+            if m is not None:
+                m.refs = max(0, m.refs - 1)
+
+    @contextlib.contextmanager
+    def get_view(self, shard_path: str) -> Iterator[memoryview]:
+        """Zero-copy view of the shard's tar bytes (reference shard_cache.py:584-609)."""
+        m = self._acquire(shard_path)
+        try:
+            yield memoryview(m.mm)[HDR_SIZE:HDR_SIZE + m.data_len]
+        finally:
+            self._release(shard_path)
+
+    def get_array(self, shard_path: str) -> np.ndarray:
+        """uint8 array over the mapped tar bytes; the mapping stays open until close()."""
+        m = self._acquire(shard_path)
+        return m.arr
+
+    def get(self, shard_path: str) -> bytes:
+        with self.get_view(shard_path) as v:
+            return bytes(v)
+
+    @property
+    def utilisation(self) -> float:
+        if self._max_bytes == 0:
+            return 0.0
+        with self._lock:
+            return self._total / self._max_bytes
+
+    def close(self, remove: bool = False) -> None:
+        with self._lock:
+            for m in self._maps.values():
+                m.close()
+            self._maps.clear()
+            if remove and self._node_master:
+                for k in list(self._lru):
+                    with contextlib.suppress(OSError):
+                        self._path(k).unlink()
+                self._lru.clear()
+                self._total = 0
+                with contextlib.suppress(OSError):
+                    self._base.rmdir()
+
+
+class ShardBatchFeeder:
+    """Batches of B JPEGs from mapped shards, packed into pinned host buffers.
+
+    Shard i of the list belongs to this rank when ``i % world == rank``
+    (reference hpc_source.py:154-156).  Each shard is indexed natively once when
+    first reached; batches never straddle an epoch and the last partial batch is
+    dropped (dali_backend.py:187).  ``next_into(dst)`` packs the next batch into a
+    pinned tensor and returns the int64 offsets; ``MI355XAugPipeline`` consumes
+    ``next_spans()`` directly (gathering into its per-slot pinned staging)."""
+
+    def __init__(self, cache: ShmShardCache, shard_paths: Sequence[str], batch_size: int, rank: int = 0,
+                 world: int = 1, nthreads: int = 8, lookahead: int = 2) -> None:
+        from concurrent.futures import ThreadPoolExecutor
+        self._cache = cache
+        self._paths = [p for i, p in enumerate(shard_paths) if i % world == rank]
+        self._B = batch_size
+        self.nthreads = nthreads
+        self._shard = 0
+        self._row = 0
+        self._cur: tuple[np.ndarray, TarIndex] | None = None
+        self.index_seconds = 0.0   # time spent preparing shards (map + pre-fault + index), off the caller's thread
+        self.wait_seconds = 0.0    # time the caller waited for a shard to be ready
+        self._lookahead = max(0, int(lookahead))
+        self._pool = ThreadPoolExecutor(max_workers=max(1, self._lookahead), thread_name_prefix="shard-index") \
+            if self._lookahead else None
+        self._futs: dict[int, Any] = {}
+
+    def _prepare(self, k: int) -> tuple[np.ndarray, TarIndex]:
+        """Map shard k, fault its pages in and index it (a worker thread; ctypes drops the GIL)."""
+        import time
+        t0 = time.perf_counter()
+        arr = self._cache.get_array(self._paths[k])
+        prefault(arr)
+        idx = index_tar(arr)
+        self.index_seconds += time.perf_counter() - t0
+        return arr, idx
+
+    def _open(self, k: int) -> tuple[np.ndarray, TarIndex]:
+        import time
+        if self._pool is None:
+            return self._prepare(k)
+        for j in range(k, min(len(self._paths), k + 1 + self._lookahead)):
+            if j not in self._futs:
+                self._futs[j] = self._pool.submit(self._prepare, j)
+        t0 = time.perf_counter()
+        res = self._futs.pop(k).result()
+        self.wait_seconds += time.perf_counter() - t0
+        return res
+
+    def next_spans(self) -> list[tuple[int, int]]:
+        """(address, length) of the next batch's JPEGs; StopIteration at the epoch end."""
+        spans: list[tuple[int, int]] = []
+        while len(spans) < self._B:
+            if self._cur is None:
+                if self._shard >= len(self._paths):
+                    raise StopIteration
+                self._cur = self._open(self._shard)
+                self._row = 0
+            arr, idx = self._cur
+            base = arr.ctypes.data
+            take = min(self._B - len(spans), len(idx) - self._row)
+            rows = idx.samples[self._row:self._row + take]
+            spans.extend(zip((base + rows["img_off"]).tolist(), rows["img_len"].tolist()))
+            self._row += take
+            if self._row >= len(idx):
+                self._cur = None
+                self._shard += 1
+        return spans
+
+    def next_into(self, dst) -> np.ndarray:
+        return gather(self.next_spans(), dst, self.nthreads)
+
+    def reset(self) -> None:
+        self._shard, self._row, self._cur = 0, 0, None
+
+    def close(self) -> None:
+        if self._pool is not None:
+            self._pool.shutdown(wait=True, cancel_futures=True)
+            self._pool = None
+        self._futs.clear()
+
+
+_MADV_POPULATE_READ = 22  # Linux >= 5.14
+
+
+def prefault(arr: np.ndarray) -> None:
+    """Populate the page tables of a mapped shard before the gather reads it
+    (madvise(MADV_POPULATE_READ) on the mapping, else a one-byte-per-page read)."""
+    base = getattr(arr, "base", None)
+    if isinstance(base, memoryview):
+        base = base.obj
+    mm = base if isinstance(base, mmap.mmap) else None
+    if mm is not None and hasattr(mm, "madvise"):
+        try:
+            mm.madvise(_MADV_POPULATE_READ)
+            return
+        except OSError:
+            pass
+    if arr.size:
+        int(arr[::4096].sum())

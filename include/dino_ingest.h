@@ -40,6 +40,11 @@ extern "C" {
 #define DINO_ENOMEM (-2)
 #define DINO_EHIP (-3)
 #define DINO_ECAPACITY (-4)
+#define DINO_EFORMAT (-5)            /* input is not in the expected format (e.g. not a tar) */
+#define DINO_ERANGE (-6)             /* caller-provided output capacity too small */
+/* positive warnings of dino_tar_index (the samples before the fault are reported) */
+#define DINO_TAR_TRUNCATED 1         /* a member's data runs past the buffer (tarfile ReadError) */
+#define DINO_TAR_BAD_HEADER 2        /* invalid header after offset 0 (tarfile stops iterating) */
 
 /* per-image status codes */
 #define DINO_IMG_OK 0
@@ -159,6 +164,37 @@ int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst,
  * The reference's TE cast_to_fp8 saturates to +-448 instead; the two agree on
  * every normalised pixel value (|x| < 3), which is all this path produces. */
 int dino_bf16_to_fp8(const uint16_t* d_in, uint8_t* d_out, int64_t n, void* stream);
+
+/* ---- Host-side shard ingest (tario.cpp) ---------------- */
+
+/* One WebDataset sample of a tar shard: byte ranges inside the tar buffer (-1 when
+ * the member is absent) and its key (into the caller's key buffer, -1 if it did
+ * not fit; key_len is always the full length). */
+typedef struct dino_tar_sample {
+  int64_t img_off, img_len;    /* .jpg / .jpeg member */
+  int64_t meta_off, meta_len;  /* .json sidecar */
+  int64_t key_off;
+  int32_t key_len;
+  int32_t reserved;
+} dino_tar_sample;
+
+/* Index a tar shard held in memory (e.g. the mmap of a /dev/shm shard-cache file
+ * past its 16-byte header, reference shard_cache.py:83-85, 584-609): members are
+ * grouped into samples by WebDataset key; samples without an image are skipped.
+ * Replaces the tar walk of dino_loader.datasets.utils._extract_jpegs_with_meta
+ * (absent dependency; called at reference hpc_source.py:461-467).  Returns DINO_OK,
+ * a positive DINO_TAR_* warning (samples before the fault are valid), or < 0. */
+int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_t cap, char* keys, int64_t keys_cap,
+                   int64_t* n_samples, int64_t* n_members);
+const char* dino_tar_last_error(void);
+
+/* Pack n byte ranges (absolute host addresses, e.g. JPEG members of mapped shards)
+ * into dst (pinned host memory) back to back; dst_offsets[n+1] receives the int64
+ * offsets dino_run_batch reads.  nthreads copier threads (1 below 1 MiB).  Replaces
+ * the per-sample bytes(mv) copies of reference hpc_source.py:360 and the batch
+ * assembly of shard_reader.py:346-376. */
+int dino_gather(const uint64_t* src_ptrs, const int64_t* lens, int64_t n, uint8_t* dst, int64_t dst_cap,
+                int64_t* dst_offsets, int32_t nthreads);
 
 #ifdef __cplusplus
 }

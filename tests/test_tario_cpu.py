@@ -1,0 +1,212 @@
+"""Host-side shard ingest (native tar index, gather, /dev/shm cache, batch feeder) on CPU.
+
+The oracle for the tar walk is Python's ``tarfile`` plus WebDataset's key rule
+(``base_plus_ext``), applied to shards built like the reference's fixtures
+(``tests/fixtures/__init__.py:80-139``: ``sample_%06d.jpg`` + ``.json`` sidecars).
+"""
+
+from __future__ import annotations
+
+import hashlib
+import io
+import json
+import re
+import struct
+import tarfile
+
+import numpy as np
+import pytest
+import torch
+
+from dataloader_amd import tario
+
+
+def _add(tf: tarfile.TarFile, name: str, data: bytes) -> None:
+    ti = tarfile.TarInfo(name)
+    ti.size = len(data)
+    tf.addfile(ti, io.BytesIO(data))
+
+
+def make_shard(n: int, with_meta: bool = True, fmt=tarfile.GNU_FORMAT, seed: int = 0, prefix: str = "") -> bytes:
+    """Reference-fixture-shaped shard: JPEG-like payloads of varied length + JSON sidecars."""
+    rng = np.random.default_rng(seed)
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w", format=fmt) as tf:
+        for i in range(n):
+            key = f"{prefix}sample_{i:06d}"
+            body = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+            _add(tf, f"{key}.jpg", b"\xff\xd8" + body + b"\xff\xd9")
+            if with_meta:
+                _add(tf, f"{key}.json", json.dumps({"quality_score": float(i % 5) / 4,
+                                                    "caption": f"A test image number {i}"}).encode())
+    return buf.getvalue()
+
+
+_KEY_RE = re.compile(r"^((?:.*/|)[^.]+)[.]([^/]*)$")  # webdataset base_plus_ext
+
+
+def oracle_samples(tar: bytes) -> list[tuple[str, bytes, bytes | None]]:
+    """tarfile walk + WebDataset grouping: (key, jpeg bytes, json bytes or None)."""
+    out: list[tuple[str, dict]] = []
+    with tarfile.open(fileobj=io.BytesIO(tar), mode="r") as tf:
+        for m in tf:
+            if not m.isfile():
+                continue
+            mt = _KEY_RE.match(m.name)
+            if not mt:
+                continue
+            key, ext = mt.group(1), mt.group(2).lower()
+            if not out or out[-1][0] != key:
+                out.append((key, {}))
+            out[-1][1][ext] = tf.extractfile(m).read()
+    res = []
+    for key, d in out:
+        img = d.get("jpg", d.get("jpeg"))
+        if img is not None:
+            res.append((key, img, d.get("json")))
+    return res
+
+
+@pytest.mark.parametrize("fmt", [tarfile.GNU_FORMAT, tarfile.PAX_FORMAT, tarfile.USTAR_FORMAT])
+@pytest.mark.parametrize("prefix", ["", "d" * 140 + "/"])
+def test_tar_index_matches_tarfile(fmt, prefix):
+    tar = make_shard(37, fmt=fmt, seed=3, prefix=prefix)
+    idx = tario.index_tar(tar)
+    ref = oracle_samples(tar)
+    assert idx.status == 0 and len(idx) == len(ref) == 37
+    assert idx.n_members == 74
+    for row, key, (rk, rimg, rjson) in zip(idx.samples, idx.keys, ref):
+        assert key == rk
+        assert tar[row["img_off"]:row["img_off"] + row["img_len"]] == rimg
+        assert tar[row["meta_off"]:row["meta_off"] + row["meta_len"]] == rjson
+
+
+def test_tar_index_grouping_edge_cases():
+    buf = io.BytesIO()
+    with tarfile.open(fileobj=buf, mode="w") as tf:
+        _add(tf, "a.json", b"{}")                # sample without an image: skipped
+        _add(tf, "b.JPEG", b"B")                 # extension lower-cased
+        _add(tf, "noext", b"?")                  # no dot: not a sample member
+        _add(tf, "dir/c.seg.jpg", b"C")          # key up to the first dot of the basename
+        _add(tf, "dir/c.jpg", b"C2")             # same key, other extension
+        _add(tf, ".hidden.jpg", b"H")            # basename starting with '.': no key
+        ti = tarfile.TarInfo("somedir")
+        ti.type = tarfile.DIRTYPE
+        tf.addfile(ti)
+        _add(tf, "e.jpg", b"")                   # empty image member
+    tar = buf.getvalue()
+    idx = tario.index_tar(tar)
+    assert idx.keys == ["b", "dir/c", "e"]
+    got = [tar[r["img_off"]:r["img_off"] + r["img_len"]] for r in idx.samples]
+    assert got == [b"B", b"C2", b""]
+    assert [(k, i) for k, i, _ in oracle_samples(tar)] == list(zip(idx.keys, got))
+
+
+def test_tar_index_truncation_and_bad_headers():
+    tar = make_shard(6, seed=1)
+    full = tario.index_tar(tar)
+    # truncated inside the 4th jpg's data: 3 samples, truncation status
+    cut = int(full.samples[3]["img_off"]) + 5
+    t = tario.index_tar(tar[:cut])
+    assert t.status == tario.TAR_TRUNCATED and len(t) == 3
+    # corrupt checksum of a later header: iteration stops there (tarfile semantics)
+    bad = bytearray(tar)
+    h = int(full.samples[2]["img_off"]) - 512
+    bad[h + 148:h + 156] = b"0000000\x00"
+    t = tario.index_tar(bytes(bad))
+    assert t.status == tario.TAR_BAD_HEADER and len(t) == 2
+    # corrupt first header: error, like tarfile.ReadError
+    with pytest.raises(tario._lib.DinoError):
+        tario.index_tar(b"\x01" * 2048)
+    assert len(tario.index_tar(b"")) == 0
+    assert len(tario.index_tar(b"\x00" * 1024)) == 0
+
+
+def test_extract_jpegs_with_meta_records():
+    tar = make_shard(10, seed=2)
+    recs = tario.extract_jpegs_with_meta(tar)
+    ref = oracle_samples(tar)
+    assert [r.key for r in recs] == [k for k, _, _ in ref]
+    assert all(bytes(r.jpeg) == img for r, (_, img, _) in zip(recs, ref))
+    assert recs[3].metadata == json.loads(ref[3][2])
+    kept = tario.extract_jpegs_with_meta(tar, min_quality=0.5)
+    assert [r.key for r in kept] == [r.key for r in recs if r.metadata["quality_score"] >= 0.5]
+    sh = tario.extract_jpegs_with_meta(tar, shuffle_buffer=8, rng=np.random.default_rng(0), copy=True)
+    assert sorted(r.key for r in sh) == [r.key for r in recs] and isinstance(sh[0].jpeg, bytes)
+    assert tario.extract_jpegs_with_meta(make_shard(3, with_meta=False))[0].metadata is None
+
+
+@pytest.mark.parametrize("nthreads", [1, 3, 8])
+def test_gather_packs_ranges(nthreads):
+    rng = np.random.default_rng(nthreads)
+    items = [rng.integers(0, 256, int(rng.integers(0, 400_000)), dtype=np.uint8) for _ in range(40)]
+    items[5] = items[5][:0]
+    dst = torch.empty(sum(i.size for i in items) + 7, dtype=torch.uint8)
+    off = tario.gather(items, dst, nthreads)
+    assert off[0] == 0 and (np.diff(off) == [i.size for i in items]).all()
+    flat = dst.numpy()
+    for i, it in enumerate(items):
+        assert np.array_equal(flat[off[i]:off[i + 1]], it)
+    with pytest.raises(tario._lib.DinoError):
+        tario.gather(items, torch.empty(10, dtype=torch.uint8))
+
+
+def test_shm_cache_format_and_views(tmp_path):
+    cache = tario.ShmShardCache(job_id="job", base_dir=tmp_path, max_gb=1.0)
+    tar = make_shard(5, seed=4)
+    src = tmp_path / "shard-000.tar"
+    src.write_bytes(tar)
+    cache.prefetch(str(src))                                   # node master loads it
+    shm = tmp_path / "job" / hashlib.sha1(str(src).encode()).hexdigest()[:16]
+    raw = shm.read_bytes()
+    assert struct.unpack_from("QQ", raw) == (len(tar), 0xDEADBEEFCAFEF00D) and raw[16:] == tar
+    with cache.get_view(str(src)) as v:
+        assert bytes(v) == tar
+    arr = cache.get_array(str(src))
+    assert arr.tobytes() == tar and len(tario.index_tar(arr)) == 5
+    assert cache.get(str(src)) == tar and 0 < cache.utilisation < 1
+    # a reader that is not the node master fails on a missing shard; a corrupt magic is refused
+    other = tario.ShmShardCache(job_id="job", base_dir=tmp_path, node_master=False)
+    with pytest.raises(FileNotFoundError):
+        other.get(str(tmp_path / "missing.tar"))
+    bad = tmp_path / "job" / hashlib.sha1(b"bad").hexdigest()[:16]
+    bad.write_bytes(struct.pack("QQ", 3, 0xDEADBEEFCAFEF00D - 1) + b"abc")
+    with pytest.raises(FileNotFoundError):
+        other.get("bad")                                        # not ready: the magic is the ready flag
+    cache.close(remove=True)
+    assert not shm.exists()
+
+
+def test_shm_cache_evicts_lru_over_budget(tmp_path):
+    tar = make_shard(4, seed=5)
+    cache = tario.ShmShardCache(job_id="j2", base_dir=tmp_path, max_gb=2.5 * len(tar) / (1 << 30))
+    for k in range(4):
+        cache.put(f"s{k}", tar)
+    alive = [tario.is_ready(tario.shm_path(cache.base, f"s{k}")) for k in range(4)]
+    assert alive == [False, False, True, True]
+    cache.close(remove=True)
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_batch_feeder_partitions_and_drops_last(tmp_path, world):
+    shards = [make_shard(n, seed=10 + k) for k, n in enumerate([7, 5, 9, 4])]
+    cache = tario.ShmShardCache(job_id=f"feed{world}", base_dir=tmp_path)
+    paths = []
+    for k, t in enumerate(shards):
+        paths.append(f"/data/shard-{k:03d}.tar")
+        cache.put(paths[-1], t)
+    for rank in range(world):
+        mine = [k for k in range(4) if k % world == rank]              # hpc_source.py:154-156
+        expect = [img for k in mine for _, img, _ in oracle_samples(shards[k])]
+        feeder = tario.ShardBatchFeeder(cache, paths, batch_size=3, rank=rank, world=world, nthreads=2)
+        dst = torch.empty(1 << 16, dtype=torch.uint8)
+        got = []
+        while True:
+            try:
+                off = feeder.next_into(dst)
+            except StopIteration:
+                break
+            assert len(off) == 4
+            got += [dst.numpy()[off[i]:off[i + 1]].tobytes() for i in range(3)]
+        assert got == expect[:len(expect) // 3 * 3]
+    cache.close(remove=True)
