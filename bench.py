@@ -245,7 +245,8 @@ def main() -> None:
     ap.add_argument("--depth", type=int, default=3, help="batches in flight (slots with their own ctx + stream)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600}")
+    ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600} (+ iBOT masks)")
+    ap.add_argument("--masks", action="store_true", help="iBOT masks per batch (default with --mixed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -287,14 +288,24 @@ def main() -> None:
     cfg = DINOAugConfig()
     B = args.batch
     pipe = MI355XAugPipeline(None, cfg, B, seed=rank_seed(1234, rank), out_dtype=args.dtype, device=local_rank,
-                             max_image_dim=4096 if args.mixed else 2048, depth=args.depth)
+                             max_image_dim=4096 if args.mixed else 2048, depth=args.depth,
+                             workspace_bytes=B * (40 << 20) if args.mixed else 0)
     ccfg = pipe._cfg(cfg.global_crop_size, cfg.local_crop_size)
     views = [sl.engine.alloc_views(ccfg, B) for sl in pipe._slots]  # one output set per in-flight slot
     n_batches = n_img // B
+    masks_on = args.masks or args.mixed
+    maskgen = None
+    if masks_on:
+        from dataloader_amd.masking import MaskingGenerator
+        grid = cfg.global_crop_size // 14                     # patch 14: 16x16 at 224
+        maskgen = MaskingGenerator((grid, grid), num_masking_patches=grid * grid // 2, device=dev)
+        maskgen.seed(rank_seed(1234, rank))
 
     def step(k: int):
         s = (k % n_batches) * B
         pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views[k % pipe.depth])
+        if maskgen is not None:  # one mask per batch, broadcast to [B, H*W] (loader.py:585-590)
+            maskgen.generate(1).expand(B, -1)
 
     for k in range(args.warmup):
         step(k)
@@ -370,11 +381,11 @@ def main() -> None:
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
-            "config": {"workload": ("C3 mixed short side 224-1600" if args.mixed else
+            "config": {"workload": ("C3 mixed short side 224-1600, iBOT masks 16x16" if args.mixed else
                                     f"C2 {args.images} synthetic {args.width}x{args.height} q85 4:2:0 JPEGs "
                                     "resident in HBM") + f", 2x224^2+8x96^2 views, {args.dtype} out",
                        "global_batch": B * world, "batch_per_gpu": B, "parallelism": f"dp{world}",
-                       "batches_in_flight": pipe.depth,
+                       "batches_in_flight": pipe.depth, "masks": masks_on,
                        "mean_jpeg_bytes": round(ab["s_jpeg"]), "out_dtype": args.dtype},
             "roofline": roof,
             "path_roofline": {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
