@@ -47,7 +47,6 @@ struct dino_ctx {
   uint8_t* d_gcrop = nullptr;
   int32_t last_batch = -1;
   KernelTimer* timer = nullptr;
-  int64_t* d_prof = nullptr;  // k_huffman phase stamps when DINO_HUFF_PROFILE=1
   KernelTimer* tm() { return timer && timer->enabled ? timer : nullptr; }
 };
 
@@ -88,11 +87,6 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
       return hip_fail(e, "dino_ctx_create: hipMalloc(gcrop)");
     }
   }
-  const char* hp = getenv("DINO_HUFF_PROFILE");
-  if (hp && hp[0] == '1' && (e = hipMalloc(&c->d_prof, sizeof(int64_t) * 8 * L.max_batch)) != hipSuccess) {
-    dino_ctx_destroy(c);
-    return hip_fail(e, "dino_ctx_create: hipMalloc(prof)");
-  }
   *out = c;
   return DINO_OK;
 }
@@ -105,7 +99,6 @@ int dino_ctx_destroy(dino_ctx* c) {
   (void)hipFree(c->d_plan);
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_gcrop);
-  (void)hipFree(c->d_prof);
   if (c->timer) {
     c->timer->destroy();
     delete c->timer;
@@ -120,7 +113,7 @@ int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, i
   if (batch < 0 || batch > c->lim.max_batch)
     return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
   hipStream_t s = (hipStream_t)stream;
-  DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size, c->d_prof};
+  DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size};
   hipError_t e = launch_decode(a, s, c->tm());
   if (e != hipSuccess) return hip_fail(e, "dino_decode");
   if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
@@ -245,10 +238,9 @@ int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, i
     case 2: src = c->d_ws + d.coef_off; n = d.plane_off - d.coef_off; break;  // sparse entries + block info
     case 3: src = c->d_ws + d.plane_off; n = d.rgb_off - d.plane_off; break;
     case 4: src = c->d_ws + d.rgb_off; n = (int64_t)d.width * d.height * 3; break;
-    case 5:  // k_huffman phase stamps (DINO_HUFF_PROFILE=1)
-      if (!c->d_prof) return fail(DINO_EINVAL, "dino_debug_region: DINO_HUFF_PROFILE is not set%s%lld");
-      src = c->d_prof + 8 * index;
-      n = 8 * sizeof(int64_t);
+    case 5:  // speculative-decode lane records (68 bytes each, restart images: none)
+      src = c->d_ws + d.hlane_off;
+      n = d.restart_interval > 0 ? 0 : (int64_t)d.h_lanes * 68;
       break;
     default: return fail(DINO_EINVAL, "dino_debug_region: region %s%lld", "", region);
   }

@@ -56,6 +56,14 @@ struct ImgDesc {
   int64_t dcd_off;         // int32 DC value per block (decode order): differences until k_dcscan sums them
   int64_t binfo_off;       // uint2 per block (decode order): first sparse entry, entry count
   int64_t coef_bytes;      // dense int16 coefficient bytes (host emulator layout)
+  int64_t htab_off;        // Huffman decoder tables (6 x HuffTable), built once per image by k_htab
+  int64_t hlane_off;       // per-lane records of the speculative decode (LaneRec x h_lanes_cap)
+  int32_t h_lanes_cap;     // lanes reserved by k_plan (from the raw scan length)
+  int32_t h_lanes;         // active lanes (restart images: restart intervals)
+  int32_t h_sub;           // bits per lane range
+  int32_t h_items;         // Huffman work items (kHuffThreads lanes each)
+  int32_t h_item_base;     // first work item of the image in the batch (k_hseg)
+  int32_t pad2;
   // filled by k_destuff
   int32_t ent_len;         // destuffed entropy bytes
   int32_t n_rst;           // RST markers found

@@ -115,41 +115,53 @@ DHD uint32_t br_peek32(const BitReader& br, uint32_t pos) {
   return (uint32_t)(v >> (32 - sh));
 }
 
-// A lane's cached view of the stream: 64-bit window, left aligned, plus the
-// next stream word already in flight (its load is issued one refill ahead, so
-// the lane does not wait on memory latency at each refill).
+// A lane's cached view of the stream: 64-bit window, left aligned, plus the next
+// stream word in flight.  The word is kept raw (as loaded) and only byte-swapped /
+// end-masked when it enters the window, so its load is waited on at the next
+// refill (~32 bits later) rather than right after it is issued.
 struct BitCursor {
-  uint64_t buf;   // next bits, MSB first
-  int32_t nbits;  // valid bits in buf
-  uint32_t pos;   // absolute bit position of the next unread bit
-  uint32_t next_word;  // index of the word held in pf
-  uint32_t pf;         // prefetched stream word
+  uint64_t buf;        // next bits, MSB first
+  int32_t nbits;       // valid bits in buf
+  uint32_t pos;        // absolute bit position of the next unread bit
+  uint32_t next_word;  // index of the word held (raw) in pf
+  uint32_t pf;
 };
 
 // Two stream sources: kWin = false reads the destuffed bytes from global memory;
 // kWin = true reads a copy staged in LDS as big-endian-swapped words (br.words,
-// br.nbytes = bytes valid, zero beyond).  Either way 32 bits are refilled at a
-// time from a word fetched one refill ahead.
-DHD uint32_t win_word(const BitReader& br, uint32_t i) {
+// br.nbytes = bytes valid, zero beyond).  A load past the end is clamped to the
+// last word holding data (never out of bounds, no branch around the load) and
+// src_cook turns whatever it returned into the zero fill.
+template <bool kWin>
+DHD uint32_t src_raw(const BitReader& br, uint32_t i) {
+  const uint32_t last = br.nbytes > 0 ? (br.nbytes - 1) >> 2 : 0u;
+  return br.words[i < last ? i : last];
+}
+
+template <bool kWin>
+DHD uint32_t src_cook(const BitReader& br, uint32_t raw, uint32_t i) {
+  const uint32_t w = kWin ? raw : bswap32(raw);
   const uint32_t b = i * 4;
-  if (b + 4 <= br.nbytes) return br.words[i];
+  if (b + 4 <= br.nbytes) return w;
   if (b >= br.nbytes) return 0u;
-  return br.words[i] & (0xFFFFFFFFu << (8 * (b + 4 - br.nbytes)));  // keep the first (nbytes-b) bytes
+  return w & (0xFFFFFFFFu << (8 * (b + 4 - br.nbytes)));  // keep the first (nbytes-b) bytes
 }
 
 template <bool kWin>
 DHD uint32_t src_word(const BitReader& br, uint32_t i) {
-  return kWin ? win_word(br, i) : br_word(br, i);
+  return src_cook<kWin>(br, src_raw<kWin>(br, i), i);
 }
+
+DHD uint32_t win_word(const BitReader& br, uint32_t i) { return src_word<true>(br, i); }
 
 // Ensure >= 32 valid bits.
 template <bool kWin>
 DHD void bc_fill(BitCursor& c, const BitReader& br) {
   if (c.nbits < 32) {
-    c.buf |= (uint64_t)c.pf << (32 - c.nbits);
+    c.buf |= (uint64_t)src_cook<kWin>(br, c.pf, c.next_word) << (32 - c.nbits);
     c.nbits += 32;
     c.next_word++;
-    c.pf = src_word<kWin>(br, c.next_word);
+    c.pf = src_raw<kWin>(br, c.next_word);
   }
 }
 
@@ -160,7 +172,7 @@ DHD void bc_init(BitCursor& c, const BitReader& br, uint32_t pos) {
   c.buf = (((uint64_t)src_word<kWin>(br, w) << 32) | src_word<kWin>(br, w + 1)) << sh;
   c.nbits = 64 - (int)sh;
   c.next_word = w + 2;
-  c.pf = src_word<kWin>(br, w + 2);
+  c.pf = src_raw<kWin>(br, w + 2);
 }
 
 DHD uint32_t bc_peek(const BitCursor& c, int n) { return (uint32_t)(c.buf >> (64 - n)); }

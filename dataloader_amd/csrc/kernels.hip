@@ -4,7 +4,8 @@
 //   k_parse     1 lane / image      marker parse -> ImgDesc
 //   k_plan      1 workgroup         per-image workspace offsets (prefix sum), capacity check
 //   k_destuff   256 lanes / image   0xFF00 unstuffing + RSTn removal (block compaction)
-//   k_huffman   256 lanes / image   self-synchronising speculative Huffman decode
+//   k_htab .. k_huff3                self-synchronising speculative Huffman decode in
+//                                   work items of 256 lanes (see the Huffman section)
 //   k_idct      lanes over blocks   islow IDCT (int32 fast path, int64 exact fallback)
 //   k_color     lanes over pixels   fancy upsampling + YCbCr->RGB
 // Augment half (per view):
@@ -51,8 +52,24 @@ __global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __rest
 // k_plan: exclusive scan of per-image chunk sizes (single workgroup of 1024)
 // ---------------------------------------------------------------------------
 // Checkpoints + DC differences of the speculative Huffman decode (no restart intervals).
-__device__ int64_t spec_cps_bytes(const ImgDesc& d) {
-  return d.restart_interval > 0 ? 0 : (int64_t)kHuffThreads * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
+// Per-lane state of the speculative decode (global, k_huff1 -> k_huff2 -> k_huff3).
+struct LaneRec {
+  HState S;       // start state used by the lane's current decode
+  RangeOut R;     // its result
+  RangeOut R1;    // result of the first (guessed-state) decode, for checkpoint syncs
+  int32_t ncp;    // checkpoints recorded by the first decode
+  int32_t blk0;   // first block the lane emits (k_huff2 scan)
+  HState W;       // k_huff2 scratch: wanted start state
+  int32_t pad;
+};
+static_assert(sizeof(LaneRec) == 68, "LaneRec layout");
+
+// Lanes reserved for the speculative Huffman decode (restart images decode per interval).
+__device__ int32_t huff_lanes_cap(const ImgDesc& d) {
+  if (d.restart_interval > 0) return 0;
+  const int64_t nbits = ((int64_t)d.scan_len + 64) * 8;  // >= the destuffed stream
+  const int64_t seg = nbits <= kHuffSegBits ? 1 : (nbits + kHuffSegBits - 1) / kHuffSegBits;
+  return (int32_t)(seg * kHuffThreads);
 }
 
 // Byte sizes of an image's workspace regions, in chunk order: destuffed entropy
@@ -60,8 +77,8 @@ __device__ int64_t spec_cps_bytes(const ImgDesc& d) {
 // SparseSink), block info (uint2 per block), component planes, RGB, speculative
 // checkpoints, DC values (int32 per block).
 struct ChunkSizes {
-  int64_t ent, rst, coef, binfo, plane, rgb, cps, dcd;
-  __device__ int64_t total() const { return ent + rst + coef + binfo + plane + rgb + cps + dcd; }
+  int64_t ent, rst, coef, binfo, plane, rgb, cps, dcd, htab, hlane;
+  __device__ int64_t total() const { return ent + rst + coef + binfo + plane + rgb + cps + dcd + htab + hlane; }
 };
 
 __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
@@ -75,8 +92,11 @@ __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
   z.plane = align16(p);
   z.rgb = align16((int64_t)d.width * d.height * 3 + 16);
-  z.cps = spec_cps_bytes(d);
+  const int64_t lanes = huff_lanes_cap(d);
+  z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
   z.dcd = align16(4 * (int64_t)d.total_blocks);
+  z.htab = align16(6 * (int64_t)sizeof(HuffTable));
+  z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
   return z;
 }
 
@@ -117,6 +137,9 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
       d.rgb_off = d.plane_off + z.plane;
       d.cps_off = d.rgb_off + z.rgb;
       d.dcd_off = d.cps_off + z.cps;
+      d.htab_off = d.dcd_off + z.dcd;
+      d.hlane_off = d.htab_off + z.htab;
+      d.h_lanes_cap = huff_lanes_cap(d);
     }
     base += sz;
   }
@@ -271,10 +294,34 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// k_huffman: one workgroup (kHuffThreads lanes) per image
+// Huffman stage: self-synchronising speculative decode, split in work items of
+// kHuffThreads lanes so that a large image spreads over many workgroups.
+//
+// An image's destuffed stream (nbits) is cut into lane ranges of `h_sub` bits;
+// kHuffThreads consecutive ranges form one work item (a "segment").  Segments
+// target kHuffSegBits bits, so work per workgroup is about the same for a
+// 640x480 and a 1600x2133 image, and a batch of mixed sizes balances over the
+// chip instead of waiting on its largest image.
+//   k_htab   1 WG / image   decoder tables -> global (once per image), segment plan
+//   k_hseg   1 WG           exclusive scan of work items over the batch
+//   k_huff1  persistent     per segment: first decode of every range from a guessed
+//                           state (block-in-MCU 0, zigzag 0) recording checkpoints,
+//                           then sync rounds inside the segment (lane 0's guess kept)
+//   k_huff2  1 WG / image   sync rounds across the whole image (fixes each segment's
+//                           first lane and anything it cascades into), then the
+//                           exclusive scan of block counts -> each lane's first block
+//   k_huff3  persistent     per segment: each lane re-decodes its range from its true
+//                           state and appends its blocks (SparseSink); images with
+//                           restart intervals decode one interval per lane here
 // ---------------------------------------------------------------------------
-constexpr int kMinSubBits = 1024;
+constexpr int kMinSubBits = 1024;  // shortest lane range of a one-segment image
 
+
+// Work items (segments) an image needs for a stream of `nbits` bits, and the
+// lanes reserved for it at plan time (from the raw scan length, >= the destuffed one).
+__device__ __forceinline__ int huff_segments(int64_t nbits) {
+  return nbits <= kHuffSegBits ? 1 : (int)((nbits + kHuffSegBits - 1) / kHuffSegBits);
+}
 
 struct HuffLds {
   ImgDesc sd;
@@ -284,20 +331,11 @@ struct HuffLds {
   RangeOut R1[kHuffThreads];
   uint32_t wsum[kHuffThreads / 64];
   int32_t bad;
+  int32_t img, item;
 };
 
-static_assert(sizeof(ImgDesc) == 904, "ImgDesc layout");
-constexpr int kHuffWinOff = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
-// Dynamic LDS of k_huffman: tables + lane state, plus (DINO_HUFF_LDS_KB builds) a window
-// holding the whole destuffed stream when it fits.  Measured on MI355X (640x480 q85,
-// batch 512): the window halves the per-step time but, at 156 KiB, allows one workgroup
-// per CU; without it four fit, which wins both alone and overlapped with other kernels.
-#ifdef DINO_HUFF_LDS_KB
-constexpr int kHuffLdsBytes = DINO_HUFF_LDS_KB * 1024;
-#else
-constexpr int kHuffLdsBytes = kHuffWinOff;
-#endif
-static_assert(kHuffWinOff <= kHuffLdsBytes, "HuffLds does not fit the LDS budget");
+static_assert(sizeof(ImgDesc) == 944, "ImgDesc layout");
+constexpr int kHuffLdsBytes = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
 
 // Sparse coefficient output.  A lane appends its blocks' non-zero AC coefficients
 // as u32 entries ((int16 value << 16) | zigzag index) to a private region of the
@@ -344,154 +382,282 @@ struct SparseSink {
   }
 };
 
-// prof (nullable, DINO_HUFF_PROFILE=1): per image int64[8] = wall-clock stamps
-// (100 MHz) at start / tables / phase 1 / sync / write end, sync rounds, lanes.
-__device__ __forceinline__ void huff_stamp(int64_t* prof, int img, int k) {
-  if (prof && threadIdx.x == 0) prof[img * 8 + k] = (int64_t)wall_clock64();
+// Lane geometry of a non-restart image: range [i*sub, end) of every active lane.
+__device__ __forceinline__ uint32_t lane_range_end(const ImgDesc& d, int i, uint32_t nbits) {
+  return i == d.h_lanes - 1 ? nbits : (uint32_t)(i + 1) * (uint32_t)d.h_sub;
+}
+__device__ __forceinline__ uint32_t lane_write_end(const ImgDesc& d, int i) {
+  return i == d.h_lanes - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * (uint32_t)d.h_sub;
 }
 
-template <bool kWin>
-__device__ void huff_restart(HuffLds& L, const HuffImage& im, const uint32_t* words, const int32_t* rst,
-                             SparseSink& sink, int t) {
-  const ImgDesc& sd = L.sd;
-  const int nseg = sd.n_rst_max;
-  const int per = sd.restart_interval * sd.blocks_per_mcu;
-  for (int k = t; k < nseg; k += kHuffThreads) {
-    uint32_t start = k == 0 ? 0u : (uint32_t)rst[k - 1] * 8u;
-    BitReader sb{words, k + 1 < nseg ? (uint32_t)rst[k] : (uint32_t)sd.ent_len};
-    int32_t pred[kMaxComp] = {0, 0, 0};
-    int first = k * per, last = min(first + per, sd.total_blocks);
-    sink.open(first);
-    decode_write<kWin>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
-    sink.close();
-  }
-}
-
-// Speculative self-synchronising decode of one image's entropy stream.
-template <bool kWin>
-__device__ void huff_spec(HuffLds& L, const HuffImage& im, const BitReader br, const uint32_t nbits, uint8_t* ws,
-                          SparseSink& sink, int64_t* prof, int img, int t) {
-  const ImgDesc& sd = L.sd;
-  int n = (int)((nbits + kMinSubBits - 1) / kMinSubBits);
-  n = n < 1 ? 1 : (n > kHuffThreads ? kHuffThreads : n);
-  uint32_t sub = (nbits + n - 1) / n;
-  sub = (sub + 31) & ~31u;
-  if (sub == 0) sub = 32;
-  const bool active = t < n;
-  const uint32_t my_end_range = (t == n - 1) ? nbits : (uint32_t)(t + 1) * sub;
-  const uint32_t my_end_write = (t == n - 1) ? 0xFFFFFFFFu : (uint32_t)(t + 1) * sub;
-  Checkpoint* cps = (Checkpoint*)(ws + sd.cps_off) + (int64_t)t * kHuffCheckpoints;
-  int32_t ncp = 0;
-  if (active) {
-    HState s0{(uint32_t)t * sub, 0, 0};
-    L.S[t] = s0;
-    const RangeOut r = decode_range<kWin>(br, im, s0, my_end_range, cps, kHuffCheckpoints, &ncp);
-    L.R[t] = r;
-    L.R1[t] = r;
-  }
-  __syncthreads();  // phase-1 results of lane t-1 (another wave) must be visible before round 0 reads them
-  huff_stamp(prof, img, 2);
-  int round = 0;
-  for (; round < kHuffThreads + 1; ++round) {
-    HState want;
-    bool redo = false;
-    if (active && t >= 1) {
-      want = L.R[t - 1].end;
-      redo = !hstate_eq(want, L.S[t]);
-    }
-    __syncthreads();
-    if (redo) {
-      L.S[t] = want;
-      L.R[t] = decode_range_sync<kWin>(br, im, want, my_end_range, cps, ncp, L.R1[t]);
-    }
-    if (!__syncthreads_or(redo ? 1 : 0)) break;
-  }
-  huff_stamp(prof, img, 3);
-  // first block of each lane: exclusive prefix sum of block counts
-  uint32_t tot;
-  const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)L.R[t].nblk : 0u, L.wsum, &tot);
-  if (active) {
-    sink.open((int32_t)blk0);
-    decode_write<kWin>(br, im, L.S[t], my_end_write, (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
-                       (int32_t*)(ws + sd.dcd_off), sink);
-    sink.close();
-  }
-  if (prof) {
-    __syncthreads();
-    huff_stamp(prof, img, 4);
-    if (t == 0) {
-      prof[img * 8 + 5] = round;
-      prof[img * 8 + 6] = n;
-      prof[img * 8 + 7] = kWin;
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kHuffThreads) k_huffman(const uint8_t* __restrict__ bytes,
-                                                          const int64_t* __restrict__ offsets,
-                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
-                                                          int64_t* __restrict__ prof) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
-  ImgDesc& sd = L.sd;
-  const int img = blockIdx.x, t = threadIdx.x;
-  huff_stamp(prof, img, 0);
-  if (t == 0) sd = desc[img];
+// ---------------------------------------------------------------------------
+// k_htab: one workgroup per image.  Builds the decoder tables (derived tables of the
+// DC/AC table of every component, then the kLookBits lookahead) in LDS and copies
+// them to the image's table area; plans the image's segments.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict__ bytes,
+                                                       const int64_t* __restrict__ offsets,
+                                                       ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  __shared__ HuffTable s_tab[6];
+  __shared__ int32_t s_bad;
+  ImgDesc& d = desc[blockIdx.x];
+  const int t = threadIdx.x;
+  if (d.status != DINO_IMG_OK) return;
+  const uint8_t* p = bytes + offsets[blockIdx.x];
+  if (t == 0) s_bad = 0;
   __syncthreads();
-  if (sd.status != DINO_IMG_OK) return;
-  const uint8_t* p = bytes + offsets[img];
-  // ---- tables: derived (6 lanes), then lookahead, then the AC fast tables (all lanes)
-  if (t == 0) L.bad = 0;
-  __syncthreads();
-  if (t < 2 * sd.ncomp) {
-    int c = t >> 1, ac = t & 1;
-    int slot = ac ? 3 + c : c;
-    int off = ac ? sd.huff_off[4 + sd.comp[c].ta] : sd.huff_off[sd.comp[c].td];
-    if (!huff_build_derived(p + off, !ac, &L.tab[slot])) atomicOr(&L.bad, 1);
+  if (t < 2 * d.ncomp) {
+    const int c = t >> 1, ac = t & 1;
+    const int slot = ac ? 3 + c : c;
+    const int off = ac ? d.huff_off[4 + d.comp[c].ta] : d.huff_off[d.comp[c].td];
+    if (!huff_build_derived(p + off, !ac, &s_tab[slot])) atomicOr(&s_bad, 1);
   }
   __syncthreads();
-  if (L.bad) {
-    if (t == 0) desc[img].status = DINO_IMG_CORRUPT;
+  if (s_bad) {
+    if (t == 0) d.status = DINO_IMG_CORRUPT;
     return;
   }
   for (int e = t; e < 6 * (1 << kLookBits); e += kHuffThreads) {
-    int slot = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
-    int c = slot % 3;
-    if (c < sd.ncomp) L.tab[slot].look[idx] = huff_look_entry(&L.tab[slot], idx, slot < 3);
+    const int slot = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
+    if (slot % 3 < d.ncomp) s_tab[slot].look[idx] = huff_look_entry(&s_tab[slot], idx, slot < 3);
   }
   __syncthreads();
-  HuffImage im;
-  hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
-  const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
-  SparseSink sink;
-  sink.ent = (uint32_t*)(ws + sd.coef_off);
-  sink.binfo = (uint2*)(ws + sd.binfo_off);
-  sink.dcd = (int32_t*)(ws + sd.dcd_off);
-  // ---- stage the destuffed stream (+ its 64 zero bytes) in LDS as swapped words when it fits
-  uint32_t* lwin = (uint32_t*)(smem + kHuffWinOff);
-  const uint32_t need = ((uint32_t)sd.ent_len + 64u + 3u) / 4u;
-  const uint32_t nwin = kHuffLdsBytes - kHuffWinOff >= 4096 && need * 4u <= (uint32_t)(kHuffLdsBytes - kHuffWinOff)
-                            ? need
-                            : 0u;
-  for (uint32_t i = t; i < nwin; i += kHuffThreads) lwin[i] = bswap32(words[i]);
-  __syncthreads();
-  huff_stamp(prof, img, 1);
-
-  if (sd.restart_interval > 0) {
-    // ---- restart intervals are independent: one lane per segment, absolute DC
-    const int32_t* rst = (const int32_t*)(ws + sd.rst_off);
-    if (nwin) {
-      huff_restart<true>(L, im, lwin, rst, sink, t);
+  uint4* dst = (uint4*)(ws + d.htab_off);
+  const uint4* src = (const uint4*)s_tab;
+  for (int k = t; k < (int)(sizeof(HuffTable) * 6 / 16); k += kHuffThreads) dst[k] = src[k];
+  if (t == 0) {
+    const int64_t nbits = (int64_t)d.ent_len * 8;
+    if (d.restart_interval > 0) {
+      d.h_items = (d.n_rst_max + kHuffThreads - 1) / kHuffThreads;
+      d.h_sub = 0;
+      d.h_lanes = d.n_rst_max;
     } else {
-      huff_restart<false>(L, im, words, rst, sink, t);
+      const int nseg = min(huff_segments(nbits), d.h_lanes_cap / kHuffThreads);
+      int n = nseg * kHuffThreads;
+      if (nseg == 1) n = (int)max((int64_t)1, min((int64_t)kHuffThreads, (nbits + kMinSubBits - 1) / kMinSubBits));
+      uint32_t sub = (uint32_t)((nbits + n - 1) / n);
+      sub = max(32u, (sub + 31u) & ~31u);
+      d.h_sub = (int32_t)sub;
+      d.h_lanes = (int32_t)max((int64_t)1, (nbits + sub - 1) / sub);
+      d.h_items = (d.h_lanes + kHuffThreads - 1) / kHuffThreads;
     }
-    return;
   }
-  if (nwin)
-    huff_spec<true>(L, im, BitReader{lwin, nwin * 4u}, (uint32_t)sd.ent_len * 8u, ws, sink, prof, img, t);
-  else
-    huff_spec<false>(L, im, BitReader{words, (uint32_t)sd.ent_len}, (uint32_t)sd.ent_len * 8u, ws, sink, prof, img,
-                     t);
+}
+
+// k_hseg: first work item of every image (exclusive scan over the batch, one WG of 1024).
+__global__ void __launch_bounds__(1024) k_hseg(ImgDesc* __restrict__ desc, int B) {
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (B + 1023) / 1024;
+  int32_t local = 0;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i < B && desc[i].status == DINO_IMG_OK) local += desc[i].h_items;
+  }
+  part[t] = local;
+  __syncthreads();
+  for (int s = 1; s < 1024; s <<= 1) {
+    const int32_t v = t >= s ? part[t - s] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int32_t base = part[t] - local;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i >= B) continue;
+    ImgDesc& d = desc[i];
+    d.h_item_base = base;
+    if (d.status == DINO_IMG_OK) base += d.h_items;
+    else d.h_items = 0;
+  }
+}
+
+// Image owning work item `item` (binary search over h_item_base); -1 past the end.
+__device__ int huff_item_image(const ImgDesc* desc, int B, int item) {
+  const ImgDesc& last = desc[B - 1];
+  if (item >= last.h_item_base + last.h_items) return -1;
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {  // last image with h_item_base <= item and h_items > 0
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid].h_item_base <= item) lo = mid;
+    else hi = mid - 1;
+  }
+  while (lo > 0 && desc[lo].h_items == 0) --lo;
+  return lo;
+}
+
+// Loads work item `item`'s image descriptor and tables into LDS; false past the end.
+__device__ bool huff_load_item(HuffLds& L, const ImgDesc* desc, int B, const uint8_t* ws, int item) {
+  if (threadIdx.x == 0) {
+    L.img = huff_item_image(desc, B, item);
+    if (L.img >= 0) L.sd = desc[L.img];
+  }
+  __syncthreads();
+  if (L.img < 0) return false;
+  const uint4* src = (const uint4*)(ws + L.sd.htab_off);
+  uint4* dst = (uint4*)L.tab;
+  for (int k = threadIdx.x; k < (int)(sizeof(HuffTable) * 6 / 16); k += kHuffThreads) dst[k] = src[k];
+  __syncthreads();
+  return true;
+}
+
+__global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
+                                                        uint8_t* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
+  const int t = threadIdx.x;
+  for (int item = blockIdx.x;; item += gridDim.x) {
+    if (!huff_load_item(L, desc, B, ws, item)) return;
+    const ImgDesc& sd = L.sd;
+    if (sd.restart_interval > 0) {
+      __syncthreads();
+      continue;
+    }
+    HuffImage im;
+    hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
+    const BitReader br{(const uint32_t*)(ws + sd.ent_off), (uint32_t)sd.ent_len};
+    const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
+    const int i = (item - sd.h_item_base) * kHuffThreads + t;  // lane index within the image
+    const bool active = i < sd.h_lanes;
+    const uint32_t rend = lane_range_end(sd, i, nbits);
+    LaneRec* lr = (LaneRec*)(ws + sd.hlane_off);
+    Checkpoint* cps = (Checkpoint*)(ws + sd.cps_off) + (int64_t)i * kHuffCheckpoints;
+    int32_t ncp = 0;
+    if (active) {
+      const HState s0{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};
+      L.S[t] = s0;
+      const RangeOut r = decode_range<false>(br, im, s0, rend, cps, kHuffCheckpoints, &ncp);
+      L.R[t] = r;
+      L.R1[t] = r;
+    }
+    __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
+    for (int round = 0; round < kHuffThreads + 1; ++round) {
+      HState want;
+      bool redo = false;
+      if (active && t >= 1) {
+        want = L.R[t - 1].end;
+        redo = !hstate_eq(want, L.S[t]);
+      }
+      __syncthreads();
+      if (redo) {
+        L.S[t] = want;
+        L.R[t] = decode_range_sync<false>(br, im, want, rend, cps, ncp, L.R1[t]);
+      }
+      if (!__syncthreads_or(redo ? 1 : 0)) break;
+    }
+    if (active) {
+      LaneRec& o = lr[i];
+      o.S = L.S[t];
+      o.R = L.R[t];
+      o.R1 = L.R1[t];
+      o.ncp = ncp;
+    }
+    __syncthreads();
+  }
+}
+
+// k_huff2: one workgroup per image.  Rounds over all the image's lanes: a lane whose
+// start state differs from its predecessor's end re-decodes (stopping at the first
+// checkpoint the first decode also passed).  Then blk0 = exclusive scan of nblk.
+constexpr int kHuff2Threads = 256;
+
+__global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  __shared__ HuffTable s_tab[6];
+  __shared__ uint32_t s_wave[kHuff2Threads / 64];
+  const ImgDesc& d = desc[blockIdx.x];
+  const int t = threadIdx.x;
+  if (d.status != DINO_IMG_OK || d.restart_interval > 0) return;
+  const int n = d.h_lanes;
+  LaneRec* lr = (LaneRec*)(ws + d.hlane_off);
+  if (n > kHuffThreads) {  // several segments: their first lanes started from guesses
+    {
+      const uint4* src = (const uint4*)(ws + d.htab_off);
+      uint4* dst = (uint4*)s_tab;
+      for (int k = t; k < (int)(sizeof(HuffTable) * 6 / 16); k += kHuff2Threads) dst[k] = src[k];
+    }
+    __syncthreads();
+    HuffImage im;
+    hi_init(im, s_tab, d.mcu_comp, d.blocks_per_mcu);
+    const BitReader br{(const uint32_t*)(ws + d.ent_off), (uint32_t)d.ent_len};
+    const uint32_t nbits = (uint32_t)d.ent_len * 8u;
+    const Checkpoint* cps = (const Checkpoint*)(ws + d.cps_off);
+    for (int round = 0; round <= n; ++round) {
+      int any = 0;
+      for (int i = 1 + t; i < n; i += kHuff2Threads) {
+        const HState want = lr[i - 1].R.end;
+        const bool redo = !hstate_eq(want, lr[i].S);
+        lr[i].W = want;
+        lr[i].pad = redo;
+        any |= redo;
+      }
+      if (!__syncthreads_or(any)) break;
+      for (int i = 1 + t; i < n; i += kHuff2Threads) {
+        if (lr[i].pad) {
+          const HState want = lr[i].W;
+          lr[i].S = want;
+          lr[i].R = decode_range_sync<false>(br, im, want, lane_range_end(d, i, nbits),
+                                             cps + (int64_t)i * kHuffCheckpoints, lr[i].ncp, lr[i].R1);
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // blk0: contiguous chunk of lanes per thread, block scan of the chunk sums
+  const int per = (n + kHuff2Threads - 1) / kHuff2Threads;
+  const int i0 = min(n, t * per), i1 = min(n, i0 + per);
+  uint32_t sum = 0;
+  for (int i = i0; i < i1; ++i) sum += (uint32_t)lr[i].R.nblk;
+  uint32_t tot;
+  uint32_t run = block_excl_scan<kHuff2Threads>(sum, s_wave, &tot);
+  for (int i = i0; i < i1; ++i) {
+    lr[i].blk0 = (int32_t)run;
+    run += (uint32_t)lr[i].R.nblk;
+  }
+}
+
+__global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restrict__ desc, int B,
+                                                        uint8_t* __restrict__ ws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
+  const int t = threadIdx.x;
+  for (int item = blockIdx.x;; item += gridDim.x) {
+    if (!huff_load_item(L, desc, B, ws, item)) return;
+    const ImgDesc& sd = L.sd;
+    HuffImage im;
+    hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
+    const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
+    SparseSink sink;
+    sink.ent = (uint32_t*)(ws + sd.coef_off);
+    sink.binfo = (uint2*)(ws + sd.binfo_off);
+    sink.dcd = (int32_t*)(ws + sd.dcd_off);
+    const int i = (item - sd.h_item_base) * kHuffThreads + t;
+    if (sd.restart_interval > 0) {
+      // restart intervals are independent: one lane per interval, absolute DC
+      const int nseg = sd.n_rst_max;
+      if (i < nseg) {
+        const int32_t* rst = (const int32_t*)(ws + sd.rst_off);
+        const int per = sd.restart_interval * sd.blocks_per_mcu;
+        const uint32_t start = i == 0 ? 0u : (uint32_t)rst[i - 1] * 8u;
+        const BitReader sb{words, i + 1 < nseg ? (uint32_t)rst[i] : (uint32_t)sd.ent_len};
+        int32_t pred[kMaxComp] = {0, 0, 0};
+        const int first = i * per, last = min(first + per, sd.total_blocks);
+        if (first < last) {
+          sink.open(first);
+          decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+          sink.close();
+        }
+      }
+    } else if (i < sd.h_lanes) {
+      const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
+      const BitReader br{words, (uint32_t)sd.ent_len};
+      sink.open(r.blk0);
+      decode_write<false>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr, sink.dcd,
+                          sink);
+      sink.close();
+    }
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1283,10 +1449,11 @@ static const bool g_sync_check = [] {
   const char* v = getenv("DINO_SYNC_CHECK");
   return v && v[0] == '1';
 }();
-static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_destuff", "k_huffman", "k_idct",
+static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_destuff", "k_huff1", "k_idct",
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
-                                                       "k_vert_local", "k_dcscan"};
+                                                       "k_vert_local", "k_dcscan", "k_htab", "k_hseg", "k_huff2",
+                                                       "k_huff3"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -1305,7 +1472,9 @@ const char* g_failed_kernel = "";
     }                                                      \
   } while (0)
 
-static int huff_lds_bytes() { return kHuffLdsBytes; }
+// Persistent grid of the segment kernels: enough resident workgroups to fill the chip
+// (4 per CU at ~40 KiB of LDS each); items beyond the grid are taken in later turns.
+constexpr int kHuffGrid = 1024;
 
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
@@ -1315,11 +1484,17 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKDestuff, s, (k_destuff<<<B, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huffman), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        huff_lds_bytes());
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kHuffLdsBytes);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              kHuffLdsBytes);
     attr_set = true;
   }
-  TIMED(tm, kKHuffman, s, (k_huffman<<<B, kHuffThreads, huff_lds_bytes(), s>>>(a.bytes, a.offsets, a.desc, a.ws, a.prof)));
+  TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
+  TIMED(tm, kKHuff1, s, (k_huff1<<<kHuffGrid, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
+  TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKHuff3, s, (k_huff3<<<kHuffGrid, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKIdct, s, (k_idct<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));

@@ -11,6 +11,12 @@ namespace dino {
 #define DINO_HUFF_THREADS 256
 #endif
 constexpr int kHuffThreads = DINO_HUFF_THREADS;
+// Bits of entropy-coded stream per Huffman work item (kHuffThreads lanes); an image
+// larger than this is decoded by several workgroups (k_huff1 / k_huff3).
+#ifndef DINO_HUFF_SEG_KBITS
+#define DINO_HUFF_SEG_KBITS 2048
+#endif
+constexpr int64_t kHuffSegBits = (int64_t)DINO_HUFF_SEG_KBITS * 1024;
 
 // LDS of k_hresize: taps (when they fit in 16 KiB) + RGBX rows of one band.
 constexpr int kHresizeLds = 40 * 1024;
@@ -27,8 +33,8 @@ struct ViewPlan {
 // Optional per-kernel HIP-event timing (bench / profiling).  Events are recorded on
 // the launch stream around each kernel; elapsed times are summed on demand.
 enum KernelId : int {
-  kKParse = 0, kKPlan, kKDestuff, kKHuffman, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
-  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKNumKernels
+  kKParse = 0, kKPlan, kKDestuff, kKHuff1, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
+  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKNumKernels
 };
 
 struct KernelTimer {
@@ -55,7 +61,6 @@ struct DecodeArgs {
   ImgDesc* desc;
   uint8_t* ws;
   int64_t ws_size;
-  int64_t* prof;  // k_huffman phase stamps (nullable)
 };
 
 // Output pointers travel as a kernel argument (no host->device copy whose source

@@ -153,9 +153,9 @@ int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t 
 
 /* Debug / test introspection of the last decoded batch: copy image `index`'s
  * region (0 descriptor, 1 destuffed entropy bytes, 2 sparse DCT coefficient entries + block info,
- * 3 component planes, 4 RGB, 5 Huffman phase stamps: int64[8] = wall clock (100 MHz) at
- * start / tables / first decode / sync / write end, sync rounds, lanes; needs the env
- * DINO_HUFF_PROFILE=1 at ctx creation) into d_dst (<= max_bytes).  Synchronises the stream. */
+ * 3 component planes, 4 RGB, 5 speculative Huffman lane records: 68 bytes per lane =
+ * start state, range result, first-decode result, checkpoints, first block) into d_dst
+ * (<= max_bytes).  Synchronises the stream. */
 int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream);
 
 /* Stage-5 cast (reference FP8Formatter.quantise, memory.py:193-214, scale 1):

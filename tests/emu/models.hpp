@@ -89,18 +89,21 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* 
   return true;
 }
 
-// ---- k_huffman, speculative mode: phases 1..4 over `lanes` lanes ------------
-// Phase 1 decodes every range from a guessed state recording checkpoints; each
-// round re-decodes the ranges whose start state changed (stopping at the first
-// checkpoint match); phase 4 writes blocks (DC as differences); then k_dcscan.
+// ---- k_huffman, speculative mode over `lanes` lanes in segments of `seg` lanes ----
+// k_huff1: every range decoded from a guessed state recording checkpoints, then
+// rounds inside each segment re-decode the ranges whose start state changed
+// (stopping at the first checkpoint match; a segment's first lane keeps its
+// guess).  k_huff2: the same rounds across the whole image, then the block scan.
+// k_huff3: blocks written (DC as differences); then k_dcscan.
 template <bool kWin>
 inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
-                               CoefSink& sink, int32_t* dcd, int32_t* stats) {
+                               int seg, CoefSink& sink, int32_t* dcd, int32_t* stats) {
   const int total_blocks = d.total_blocks;
   int n = lanes;
   uint32_t sub = (nbits + n - 1) / n;
   sub = (sub + 31) & ~31u;
   if (sub == 0) sub = 32;
+  if (seg <= 0) seg = n;
   std::vector<HState> S(n);
   std::vector<RangeOut> R(n), R1(n);
   std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
@@ -112,20 +115,26 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
     R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], kHuffCheckpoints, &ncp[i]);
   }
   int rounds = 0, redone = 0;
-  for (;;) {
-    std::vector<HState> want(n);
-    for (int i = 1; i < n; ++i) want[i] = R[i - 1].end;
-    bool any = false;
-    for (int i = 1; i < n; ++i) {
-      if (!hstate_eq(want[i], S[i])) {
+  for (int pass = 0; pass < 2; ++pass) {  // 0: inside segments (k_huff1), 1: whole image (k_huff2)
+    for (;;) {
+      std::vector<HState> want(n);
+      std::vector<char> redo(n, 0);
+      for (int i = 1; i < n; ++i) {
+        if (pass == 0 && i % seg == 0) continue;
+        want[i] = R[i - 1].end;
+        redo[i] = !hstate_eq(want[i], S[i]);
+      }
+      bool any = false;
+      for (int i = 1; i < n; ++i) {
+        if (!redo[i]) continue;
         S[i] = want[i];
         R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], ncp[i], R1[i]);
         any = true;
         ++redone;
       }
+      ++rounds;
+      if (!any) break;
     }
-    ++rounds;
-    if (!any) break;
   }
   int32_t blk0 = 0;
   for (int i = 0; i < n; ++i) {
@@ -191,9 +200,10 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     std::vector<int32_t> dcd(d.total_blocks, 0);
     if (mode == 2) {
       BitReader bw{win.data(), (uint32_t)win.size() * 4};
-      model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, sink, dcd.data(), stats);
+      model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, 0, sink, dcd.data(), stats);
     } else {
-      model_huffman_spec<false>(br, im, d, (uint32_t)ds.len * 8, lanes, sink, dcd.data(), stats);
+      model_huffman_spec<false>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
+                                stats);
     }
   }
   if (cap) cap->coef = coef;

@@ -93,7 +93,7 @@ def _zoo():
     return out
 
 
-@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512)])
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024)])
 def test_decode_bit_exact_vs_pillow(emu, mode, lanes):
     for j in _zoo():
         r, out, _ = emu_decode(emu, j, mode, lanes)
