@@ -868,12 +868,19 @@ __global__ void k_params(const ImgDesc* __restrict__ desc, int B, dino_aug_confi
   sample_view(cfg, seed, batch_index, b, v, ok ? d.width : 1, ok ? d.height : 1, ok, &out[i]);
 }
 
+// Horizontal taps in the signed-dot4 layout (k_hresize): per output x an int4
+// {xmin, groups, corr, 0}, then groups of 4 taps as signed base-256 digit planes
+// uint4 {D0, D1, D2, 0} stored [group][x] (lanes of a wave read consecutive x).
+__device__ __forceinline__ int64_t hdot_table_bytes(int S, int kh) {
+  return kh ? (int64_t)S * 16 * (1 + (kh + 3) / 4) : 0;
+}
+
 __device__ void view_sizes(const dino_view_params& p, int ok, int64_t* htmp, int64_t* rcoef, int32_t* kh, int32_t* kv) {
   const int S = p.out_size;
   *kh = ok && p.crop_w != S ? resample_ksize(p.crop_w, S) : 0;
   *kv = ok && p.crop_h != S ? resample_ksize(p.crop_h, S) : 0;
   *htmp = (*kh) ? align16((int64_t)p.crop_h * S * 3) : 0;
-  *rcoef = ok ? align16((int64_t)S * (4 + *kh + *kv) * 4) : 0;
+  *rcoef = ok ? align16((int64_t)S * (4 + *kh + *kv) * 4) + hdot_table_bytes(S, *kh) : 0;
 }
 
 // Host-supplied records are validated before any kernel indexes memory with them.
@@ -948,8 +955,35 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
   int32_t* vb = base + 2 * S;         // [S][2]
   int32_t* ht = base + 4 * S;         // [S][kh]
   int32_t* vt = ht + (int64_t)S * vp.kh;
+  int4* hx = (int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
+  uint4* hg = (uint4*)(hx + S);
   for (int x = threadIdx.x; x < S; x += blockDim.x) {
-    if (vp.kh) resample_coeffs_one(p.crop_w, S, x, vp.kh, &hb[2 * x], &hb[2 * x + 1], ht + (int64_t)x * vp.kh);
+    if (vp.kh) {
+      int32_t* k = ht + (int64_t)x * vp.kh;
+      resample_coeffs_one(p.crop_w, S, x, vp.kh, &hb[2 * x], &hb[2 * x + 1], k);
+      // sum_t p_t k_t = sum_t (p_t - 128) k_t + 128 sum_t k_t, and k_t = D0 + 256 D1 + 65536 D2
+      // with signed digits D in [-128, 127] (exact for |k| < 2^23 - 2^15; normalised bicubic
+      // taps stay below 1.1 x 2^22): three v_dot4 products per 4 taps
+      const int cnt = hb[2 * x + 1], ng = (cnt + 3) / 4;
+      int32_t ksum = 0;
+      for (int g = 0; g < ng; ++g) {
+        uint32_t dp[3] = {0u, 0u, 0u};
+        for (int j = 0; j < 4; ++j) {
+          const int t = 4 * g + j;
+          const int32_t kt = t < cnt ? k[t] : 0;
+          ksum += kt;
+          const int32_t d0 = (int32_t)(int8_t)(uint8_t)(kt & 0xFF);
+          const int32_t r1 = (kt - d0) >> 8;
+          const int32_t d1 = (int32_t)(int8_t)(uint8_t)(r1 & 0xFF);
+          const int32_t d2 = (r1 - d1) >> 8;
+          dp[0] |= (uint32_t)(uint8_t)d0 << (8 * j);
+          dp[1] |= (uint32_t)(uint8_t)d1 << (8 * j);
+          dp[2] |= (uint32_t)(uint8_t)d2 << (8 * j);
+        }
+        hg[(int64_t)g * S + x] = make_uint4(dp[0], dp[1], dp[2], 0u);
+      }
+      hx[x] = make_int4(hb[2 * x], ng, 128 * ksum + (1 << (kPrecisionBits - 1)), 0);
+    }
     if (vp.kv) resample_coeffs_one(p.crop_h, S, x, vp.kv, &vb[2 * x], &vb[2 * x + 1], vt + (int64_t)x * vp.kv);
   }
 }
@@ -962,27 +996,51 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
 // [3][crop_h][S].  Crops too wide for LDS take a direct (global) path.
 constexpr int kHresizeTapLds = 16 * 1024;
 
+// One band of nr staged rows: lane (r, x) accumulates three signed-dot4 digit
+// products per channel and group of 4 taps.  Rows are staged planar with the
+// sign bit flipped (p - 128 as int8); the taps' pixels start at xmin, so each
+// group's 4 pixels are one v_alignbyte of two consecutive LDS words (the upper
+// word carried to the next group).  Exact: the int32 sum equals Pillow's.
 template <bool kLdsTaps>
-__device__ __forceinline__ void hresize_band(const uint32_t* __restrict__ rows, int rpw, int nr, int r0, int S,
-                                             const int32_t* __restrict__ hb, const int32_t* __restrict__ ht, int kh,
-                                             uint8_t* __restrict__ tmp, int64_t cpl) {
+__device__ __forceinline__ void hresize_band_dot(const uint8_t* __restrict__ rows, int pitch, int nr, int r0, int S,
+                                                 const int4* __restrict__ hx, const uint4* __restrict__ hg,
+                                                 uint8_t* __restrict__ tmp, int64_t cpl, int plane_bytes) {
   for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
     const int r = e / S, x = e - r * S;
-    const int xmin = hb[2 * x], xcnt = hb[2 * x + 1];
-    const int32_t* k = ht + x * kh;
-    const uint32_t* q = rows + r * rpw + xmin;
-    int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0;
-    for (int t = 0; t < xcnt; ++t) {
-      const uint32_t v = q[t];
-      const int32_t kk = k[t];
-      a0 += (int32_t)(v & 255u) * kk;
-      a1 += (int32_t)((v >> 8) & 255u) * kk;
-      a2 += (int32_t)((v >> 16) & 255u) * kk;
+    const int4 h = hx[x];
+    const int xmin = h.x, ng = h.y;
+    const uint32_t sh = (uint32_t)(xmin & 3);
+    const uint32_t* q0 = (const uint32_t*)(rows + r * pitch) + (xmin >> 2);
+    const uint32_t* q1 = (const uint32_t*)((const uint8_t*)q0 + plane_bytes);
+    const uint32_t* q2 = (const uint32_t*)((const uint8_t*)q1 + plane_bytes);
+    int32_t a00 = 0, a01 = 0, a02 = 0, a10 = 0, a11 = 0, a12 = 0, a20 = 0, a21 = 0, a22 = 0;
+    uint32_t l0 = q0[0], l1 = q1[0], l2 = q2[0];
+#pragma unroll 2
+    for (int g = 0; g < ng; ++g) {
+      const uint4 dg = hg[g * S + x];
+      const uint32_t u0 = q0[g + 1], u1 = q1[g + 1], u2 = q2[g + 1];
+      const int32_t p0 = (int32_t)__builtin_amdgcn_alignbyte(u0, l0, sh);
+      const int32_t p1 = (int32_t)__builtin_amdgcn_alignbyte(u1, l1, sh);
+      const int32_t p2 = (int32_t)__builtin_amdgcn_alignbyte(u2, l2, sh);
+      a00 = __builtin_amdgcn_sdot4(p0, (int32_t)dg.x, a00, false);
+      a01 = __builtin_amdgcn_sdot4(p0, (int32_t)dg.y, a01, false);
+      a02 = __builtin_amdgcn_sdot4(p0, (int32_t)dg.z, a02, false);
+      a10 = __builtin_amdgcn_sdot4(p1, (int32_t)dg.x, a10, false);
+      a11 = __builtin_amdgcn_sdot4(p1, (int32_t)dg.y, a11, false);
+      a12 = __builtin_amdgcn_sdot4(p1, (int32_t)dg.z, a12, false);
+      a20 = __builtin_amdgcn_sdot4(p2, (int32_t)dg.x, a20, false);
+      a21 = __builtin_amdgcn_sdot4(p2, (int32_t)dg.y, a21, false);
+      a22 = __builtin_amdgcn_sdot4(p2, (int32_t)dg.z, a22, false);
+      l0 = u0;
+      l1 = u1;
+      l2 = u2;
     }
     const int64_t o = (int64_t)(r0 + r) * S + x;
-    tmp[o] = clip8_acc(a0);
-    tmp[cpl + o] = clip8_acc(a1);
-    tmp[2 * cpl + o] = clip8_acc(a2);
+    // int32 wrap-around is harmless: the true sum (Pillow's int32 ss) fits in int32
+    tmp[o] = clip8_acc((int32_t)((uint32_t)a00 + ((uint32_t)a01 << 8) + ((uint32_t)a02 << 16) + (uint32_t)h.z));
+    tmp[cpl + o] = clip8_acc((int32_t)((uint32_t)a10 + ((uint32_t)a11 << 8) + ((uint32_t)a12 << 16) + (uint32_t)h.z));
+    tmp[2 * cpl + o] =
+        clip8_acc((int32_t)((uint32_t)a20 + ((uint32_t)a21 << 8) + ((uint32_t)a22 << 16) + (uint32_t)h.z));
   }
 }
 
@@ -999,15 +1057,19 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   const int S = p.out_size, W = d.width, cw = p.crop_w, kh = vp.kh;
   const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);
   const int32_t* gt = gb + 4 * S;
+  const int4* ghx = (const int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
+  const uint4* ghg = (const uint4*)(ghx + S);
   const uint8_t* rgb = ws + d.rgb_off;
   uint8_t* tmp = aws + vp.htmp_off;
   const int64_t cpl = (int64_t)p.crop_h * S;
-  const int tap_words = 2 * S + S * kh;
-  const bool lds_taps = tap_words * 4 <= kHresizeTapLds;
-  const int rbase = lds_taps ? ((tap_words * 4 + 15) & ~15) : 0;
+  const int ng_max = (kh + 3) / 4;
+  const int tab_bytes = S * 16 * (1 + ng_max);
+  const bool lds_taps = tab_bytes <= kHresizeTapLds;
+  const int rbase = lds_taps ? tab_bytes : 0;
   const int ngroups = (cw + 3) >> 2;
-  const int rpw = ngroups * 4;  // LDS words per staged row
-  int R = (kHresizeLds - rbase) / (rpw * 4);
+  // planar rows: [3][R][pitch] with 8 bytes of slack for the last group's upper word
+  const int pitch = ngroups * 4 + 8;
+  int R = (kHresizeLds - rbase) / (3 * pitch);
   R = R > 16 ? 16 : R;
   if (R < 1) {  // direct path: taps and pixels from global memory
     const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
@@ -1018,12 +1080,14 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
     }
     return;
   }
-  int32_t* lt = (int32_t*)smem;
+  int4* lx = (int4*)smem;
+  uint4* lg = (uint4*)(lx + S);
   if (lds_taps) {
-    for (int k = threadIdx.x; k < 2 * S; k += blockDim.x) lt[k] = gb[k];
-    for (int k = threadIdx.x; k < S * kh; k += blockDim.x) lt[2 * S + k] = gt[k];
+    for (int k = threadIdx.x; k < S; k += blockDim.x) lx[k] = ghx[k];
+    for (int k = threadIdx.x; k < S * ng_max; k += blockDim.x) lg[k] = ghg[k];
   }
-  uint32_t* rows = (uint32_t*)(smem + rbase);
+  uint8_t* rows = smem + rbase;
+  const int plane_bytes = R * pitch;
   for (int r0 = blockIdx.x * R; r0 < p.crop_h; r0 += gridDim.x * R) {
     const int nr = min(R, p.crop_h - r0);
     for (int e = threadIdx.x; e < nr * ngroups; e += blockDim.x) {
@@ -1032,21 +1096,23 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
       const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
       const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
       const uint32_t w0 = a0[0], w1 = a0[1], w2 = a0[2], w3 = a0[3];
-      const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
-      const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
-      const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);
-      uint4 px;
-      px.x = b0 & 0xFFFFFFu;
-      px.y = (b0 >> 24) | ((b1 & 0xFFFFu) << 8);
-      px.z = (b1 >> 16) | ((b2 & 0xFFu) << 16);
-      px.w = b2 >> 8;
-      *(uint4*)(rows + r * rpw + 4 * g) = px;
+      const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);  // R0 G0 B0 R1
+      const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);  // G1 B1 R2 G2
+      const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);  // B2 R3 G3 B3
+      // de-interleave 4 pixels into one word per channel (v_perm byte selects), sign bit flipped
+      const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
+      const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
+      const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
+      uint8_t* dst = rows + r * pitch + 4 * g;
+      *(uint32_t*)dst = cr ^ 0x80808080u;
+      *(uint32_t*)(dst + plane_bytes) = cg ^ 0x80808080u;
+      *(uint32_t*)(dst + 2 * plane_bytes) = cb ^ 0x80808080u;
     }
     __syncthreads();
     if (lds_taps)
-      hresize_band<true>(rows, rpw, nr, r0, S, lt, lt + 2 * S, kh, tmp, cpl);
+      hresize_band_dot<true>(rows, pitch, nr, r0, S, lx, lg, tmp, cpl, plane_bytes);
     else
-      hresize_band<false>(rows, rpw, nr, r0, S, gb, gt, kh, tmp, cpl);
+      hresize_band_dot<false>(rows, pitch, nr, r0, S, ghx, ghg, tmp, cpl, plane_bytes);
     __syncthreads();
   }
 }
