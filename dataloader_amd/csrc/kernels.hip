@@ -803,8 +803,35 @@ __device__ __forceinline__ PlaneView make_plane_view(const ImgDesc& d, const uin
   return v;
 }
 
+// 4 bytes at row[s] as one word from two aligned loads + v_alignbyte (the second
+// word may lie past the row: planes are followed by more workspace, never unmapped).
+__device__ __forceinline__ uint32_t load4(const uint8_t* row, int s) {
+  const uint32_t* w = (const uint32_t*)(row + (s & ~3));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(s & 3));
+}
+
+// 4 chroma samples [c-1, c+2] of a row.
+__device__ __forceinline__ uint32_t chroma_quad(const uint8_t* row, int c) { return load4(row, c - 1); }
+
+// h2v2 fancy upsampling of one chroma plane for the 4 pixels x0..x0+3 of row y,
+// given the samples [c0-1, c0+2] of the nearer row (n) and the farther row (f).
+__device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, int* out) {
+  int cs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cs[j] = 3 * (int)((n >> (8 * j)) & 255u) + (int)((f >> (8 * j)) & 255u);
+  const int c0 = x0 >> 1;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int x = x0 + j, c = (x >> 1) - c0 + 1;  // index of column x>>1 in cs
+    out[j] = (x & 1) ? (cs[c] * 3 + cs[c + 1] + 7) >> 4 : (cs[c] * 3 + cs[c - 1] + 8) >> 4;
+  }
+}
+
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
 // the RGB area is padded by 16 bytes, so the last partial quad may store whole words).
+// 4:2:0 interior quads (the common case) take a vectorised path: one word of Y and
+// two words per chroma row instead of per-pixel byte loads; edges, quads that wrap
+// a row and other samplings use the per-pixel path (same arithmetic).
 __global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const ImgDesc& d = desc[blockIdx.y];
   if (d.status != DINO_IMG_OK) return;
@@ -813,6 +840,8 @@ __global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc,
   const PlaneView p1 = nc > 1 ? make_plane_view(d, ws, 1) : p0;
   const PlaneView p2 = nc > 1 ? make_plane_view(d, ws, 2) : p0;
   const bool ycc = nc > 1 && d.color == kYCbCr;
+  const bool fast420 = ycc && p0.method == kUpFull && p1.method == kUpH2V2Fancy && p2.method == kUpH2V2Fancy &&
+                       p1.dw == p2.dw && p1.dh == p2.dh;
   uint32_t* rgb = (uint32_t*)(ws + d.rgb_off);
   const int W = d.width;
   const int64_t npx = (int64_t)W * d.height;
@@ -824,28 +853,40 @@ __global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc,
       uint8_t b[12];
       uint32_t w[3];
     } o;
+    if (fast420 && x >= 2 && x + 3 < W && ((x + 3) >> 1) + 1 < p1.dw) {
+      const int r = y >> 1;
+      const int rf = (y & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
+      const int c0 = x >> 1;
+      const uint32_t yw = load4(p0.p + (int64_t)y * p0.pitch, x);
+      int cb[4], cr[4];
+      h2v2_quad(chroma_quad(p1.p + (int64_t)r * p1.pitch, c0), chroma_quad(p1.p + (int64_t)rf * p1.pitch, c0), x, cb);
+      h2v2_quad(chroma_quad(p2.p + (int64_t)r * p2.pitch, c0), chroma_quad(p2.p + (int64_t)rf * p2.pitch, c0), x, cr);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (i0 + j < npx) {
-        if (nc == 1) {
-          const uint8_t v = (uint8_t)upsample_at(p0, x, y);
-          o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = v;
-        } else {
-          const int a = upsample_at(p0, x, y), b = upsample_at(p1, x, y), c = upsample_at(p2, x, y);
-          if (ycc) {
-            ycc_to_rgb(a, b, c, o.b + 3 * j);
+      for (int j = 0; j < 4; ++j) ycc_to_rgb((int)((yw >> (8 * j)) & 255u), cb[j], cr[j], o.b + 3 * j);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (i0 + j < npx) {
+          if (nc == 1) {
+            const uint8_t v = (uint8_t)upsample_at(p0, x, y);
+            o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = v;
           } else {
-            o.b[3 * j] = (uint8_t)a;
-            o.b[3 * j + 1] = (uint8_t)b;
-            o.b[3 * j + 2] = (uint8_t)c;
+            const int a = upsample_at(p0, x, y), b = upsample_at(p1, x, y), c = upsample_at(p2, x, y);
+            if (ycc) {
+              ycc_to_rgb(a, b, c, o.b + 3 * j);
+            } else {
+              o.b[3 * j] = (uint8_t)a;
+              o.b[3 * j + 1] = (uint8_t)b;
+              o.b[3 * j + 2] = (uint8_t)c;
+            }
           }
+        } else {
+          o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = 0;
         }
-      } else {
-        o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = 0;
-      }
-      if (++x == W) {
-        x = 0;
-        ++y;
+        if (++x == W) {
+          x = 0;
+          ++y;
+        }
       }
     }
     rgb[3 * q] = o.w[0];
