@@ -18,7 +18,7 @@ namespace dino {
 
 constexpr int kMaxComp = 3;
 constexpr int kMaxBlocksPerMcu = 10;   // libjpeg D_MAX_BLOCKS_IN_MCU
-constexpr int kLookBits = 10;          // Huffman lookahead table bits
+constexpr int kLookBits = 11;          // Huffman lookahead table bits
 
 enum ColorSpace : int32_t { kGray = 0, kYCbCr = 1, kRGB = 2 };
 

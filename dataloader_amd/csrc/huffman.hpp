@@ -19,16 +19,13 @@
 namespace dino {
 
 // Derived decoding table for one Huffman table (jpeg_make_d_derived_tbl).
-// Lookahead entry for each kLookBits-bit prefix, two 16-bit halves:
-//   low  = (symbol << 8) | code length, 0 when the code is longer than kLookBits;
-//   high = the whole step when the code *and* its extra bits fit the prefix:
-//          (value << 8) | (run << 4) | bits consumed, as int16 (0 = not resolvable).
-//          AC: value 0 marks the s == 0 symbols (EOB, ZRL); DC: run 0, value = diff.
+// Lookahead entry for each kLookBits-bit prefix: (symbol << 5) | code length, 0
+// when the code is longer than kLookBits (16 bits: six tables take 14.7 KiB of LDS).
 struct HuffTable {
   int32_t maxcode[18];     // maxcode[l], -1 if no codes of length l; [17] sentinel
   int32_t valoffset[18];
   uint8_t huffval[256];
-  uint32_t look[1 << kLookBits];
+  uint16_t look[1 << kLookBits];
 };
 
 // Build maxcode/valoffset/huffval (not the lookahead) from BITS[16] + HUFFVAL.
@@ -72,19 +69,13 @@ DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTable* t) {
 DHD int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(((unsigned)-1) << s) + 1 : x; }
 
 // Lookahead entry for the kLookBits-bit prefix `idx` (computable independently per entry).
-DHD uint32_t huff_look_entry(const HuffTable* t, int idx, bool is_dc) {
+DHD uint16_t huff_look_entry(const HuffTable* t, int idx, bool is_dc) {
+  (void)is_dc;
   for (int l = 1; l <= kLookBits; ++l) {
     const int code = idx >> (kLookBits - l);
     if (code <= t->maxcode[l]) {  // canonical code: first length whose maxcode covers the prefix
       const int sym = t->huffval[(code + t->valoffset[l]) & 255];
-      const uint32_t lo = (uint32_t)((sym << 8) | l);
-      const int r = is_dc ? 0 : sym >> 4, s = is_dc ? sym : sym & 15;
-      int hi = 0;
-      if (l + s <= kLookBits) {
-        const int v = s ? huff_extend((idx >> (kLookBits - l - s)) & ((1 << s) - 1), s) : 0;
-        if (v >= -128 && v <= 127) hi = v * 256 + ((r << 4) | (l + s));
-      }
-      return ((uint32_t)(uint16_t)(int16_t)hi << 16) | lo;
+      return (uint16_t)((sym << 5) | l);
     }
   }
   return 0;
@@ -127,35 +118,46 @@ struct BitCursor {
   uint32_t pf;
 };
 
-// Two stream sources: kWin = false reads the destuffed bytes from global memory;
-// kWin = true reads a copy staged in LDS as big-endian-swapped words (br.words,
-// br.nbytes = bytes valid, zero beyond).  A load past the end is clamped to the
-// last word holding data (never out of bounds, no branch around the load) and
-// src_cook turns whatever it returned into the zero fill.
-template <bool kWin>
+// Stream sources (template argument kWin of the routines below):
+//   kSrcGlobal (false)  destuffed bytes in global memory, exact end: the word holding
+//                       br.nbytes keeps only its first bytes, later words read as 0
+//                       (restart intervals, whose data is followed by the next one);
+//   kSrcWin (true)      a copy staged as big-endian-swapped words, zero beyond nbytes;
+//   kSrcPadded          destuffed bytes in global memory followed by >= 8 zero bytes
+//                       (k_destuff's pad): a read past the end is clamped to the first
+//                       all-zero word, so no masking is needed on the hot path.
+// A load past the end is clamped (never out of bounds, no branch around the load).
+enum : int { kSrcGlobal = 0, kSrcWin = 1, kSrcPadded = 2 };
+
+template <int kWin>
 DHD uint32_t src_raw(const BitReader& br, uint32_t i) {
+  if (kWin == kSrcPadded) {
+    const uint32_t zw = (br.nbytes + 3) >> 2;  // first word wholly inside the zero pad
+    return br.words[i < zw ? i : zw];
+  }
   const uint32_t last = br.nbytes > 0 ? (br.nbytes - 1) >> 2 : 0u;
   return br.words[i < last ? i : last];
 }
 
-template <bool kWin>
+template <int kWin>
 DHD uint32_t src_cook(const BitReader& br, uint32_t raw, uint32_t i) {
-  const uint32_t w = kWin ? raw : bswap32(raw);
+  const uint32_t w = kWin == kSrcWin ? raw : bswap32(raw);
+  if (kWin == kSrcPadded) return w;
   const uint32_t b = i * 4;
   if (b + 4 <= br.nbytes) return w;
   if (b >= br.nbytes) return 0u;
   return w & (0xFFFFFFFFu << (8 * (b + 4 - br.nbytes)));  // keep the first (nbytes-b) bytes
 }
 
-template <bool kWin>
+template <int kWin>
 DHD uint32_t src_word(const BitReader& br, uint32_t i) {
   return src_cook<kWin>(br, src_raw<kWin>(br, i), i);
 }
 
-DHD uint32_t win_word(const BitReader& br, uint32_t i) { return src_word<true>(br, i); }
+DHD uint32_t win_word(const BitReader& br, uint32_t i) { return src_word<kSrcWin>(br, i); }
 
 // Ensure >= 32 valid bits.
-template <bool kWin>
+template <int kWin>
 DHD void bc_fill(BitCursor& c, const BitReader& br) {
   if (c.nbits < 32) {
     c.buf |= (uint64_t)src_cook<kWin>(br, c.pf, c.next_word) << (32 - c.nbits);
@@ -165,7 +167,7 @@ DHD void bc_fill(BitCursor& c, const BitReader& br) {
   }
 }
 
-template <bool kWin>
+template <int kWin>
 DHD void bc_init(BitCursor& c, const BitReader& br, uint32_t pos) {
   c.pos = pos;
   uint32_t w = pos >> 5, sh = pos & 31;
@@ -259,10 +261,21 @@ struct StepOut {
   int32_t block_done;
 };
 
+// Bits [off, off + width) (LSB = bit 0) of x; width 0 gives 0.
+DHD uint32_t ubfe(uint32_t x, uint32_t off, uint32_t width) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ubfe(x, off, width);
+#else
+  return width ? (x >> off) & (0xFFFFFFFFu >> (32 - width)) : 0u;
+#endif
+}
+
 // Execute one step from cursor c / state (c, z).  Updates state.  One lookahead
-// read resolves the common case (code + extra bits inside kLookBits) for DC and
-// AC alike, so the lanes of a wave rarely diverge into separate table reads.
-template <bool kWin>
+// read gives the symbol and code length of every code of <= kLookBits bits; the
+// extra bits are then extracted from the same 32-bit view of the window, so
+// short and long (code + extra) steps take one branch-free path and the lanes of
+// a wave only diverge for codes longer than kLookBits.
+template <int kWin>
 DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
   StepOut o;
   o.block_done = 0;
@@ -270,31 +283,20 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
   const int comp = hi_comp(im, blk);
   const bool dc = z == 0;
   const HuffTable* t = im.tabs + (dc ? comp : 3 + comp);
-  const uint32_t e = t->look[bc_peek(cur, kLookBits)];
-  const int f = (int)(int16_t)(e >> 16);
-  int r, v;
-  if (f) {
-    bc_skip(cur, f & 15);
-    r = (f >> 4) & 15;
-    v = f >> 8;
+  const uint32_t hi32 = (uint32_t)(cur.buf >> 32);  // >= 32 valid bits after bc_fill
+  const uint32_t e = t->look[hi32 >> (32 - kLookBits)];
+  int sym, len;
+  if (e) {
+    sym = (int)(e >> 5);
+    len = (int)(e & 31u);
   } else {
-    int sym, len;
-    if (e & 0xFFFFu) {
-      sym = (int)((e >> 8) & 255u);
-      len = (int)(e & 255u);
-    } else {
-      huff_slow(cur, t, &sym, &len);
-    }
-    bc_skip(cur, len);  // >= 15 bits remain after a <= 17-bit code (bc_fill guaranteed >= 32)
-    const int s = dc ? sym : sym & 15;
-    r = dc ? 0 : sym >> 4;
-    v = 0;
-    if (s) {
-      const uint32_t x = bc_peek(cur, s);
-      bc_skip(cur, s);
-      v = huff_extend((int)x, s);
-    }
+    huff_slow(cur, t, &sym, &len);
   }
+  const int s = dc ? sym : sym & 15;  // s <= 15 (DC tables are validated), len <= 17: len + s < 32
+  const int r = dc ? 0 : sym >> 4;
+  const uint32_t x = ubfe(hi32, (uint32_t)(32 - len - s), (uint32_t)s);
+  const int v = s ? huff_extend((int)x, s) : 0;
+  bc_skip(cur, len + s);
   if (dc) {
     o.kind = 0;
     o.value = v;
@@ -351,7 +353,7 @@ DHD HState sanitize(HState st, int bpm) {
 }
 
 // First (speculative) decode of a range; records up to kmax block boundaries.
-template <bool kWin>
+template <int kWin>
 DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, uint32_t end, Checkpoint* cps,
                           int kmax, int32_t* ncp) {
   st = sanitize(st, im.blocks_per_mcu);
@@ -379,7 +381,7 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 // reaches a block boundary the first decode also passed through (same bit
 // position, same block-in-MCU index), everything after it is what the first
 // decode already found: its end state and remaining block count are reused.
-template <bool kWin>
+template <int kWin>
 DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
                                const Checkpoint* cps, int ncp, RangeOut first) {
   st = sanitize(st, im.blocks_per_mcu);
@@ -420,7 +422,7 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
 // `total_blocks`.  DC: with `pred` the absolute value goes to the sink (DC
 // predictors carried by the caller); without, the difference goes to dcd[block]
 // for the DC prefix pass (k_dcscan).  Returns the bit position.
-template <bool kWin, typename Sink>
+template <int kWin, typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
                           int32_t total_blocks, int32_t* pred, int32_t* dcd, Sink& sink) {
   st = sanitize(st, im.blocks_per_mcu);
@@ -441,7 +443,11 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
           add3(pred, comp, o.value);
           sink.dc((int16_t)get3(pred, comp));
         } else {
+#ifdef DINO_EXP_NOSTORE
+          sink.dc((int16_t)o.value);
+#else
           dcd[b] = o.value;
+#endif
         }
       } else if (o.kind == 1) {
         sink.ac(o.zz, (int16_t)o.value);

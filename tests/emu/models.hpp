@@ -95,7 +95,7 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* 
 // (stopping at the first checkpoint match; a segment's first lane keeps its
 // guess).  k_huff2: the same rounds across the whole image, then the block scan.
 // k_huff3: blocks written (DC as differences); then k_dcscan.
-template <bool kWin>
+template <int kWin>
 inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
                                int seg, CoefSink& sink, int32_t* dcd, int32_t* stats) {
   const int total_blocks = d.total_blocks;
@@ -202,7 +202,7 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
       BitReader bw{win.data(), (uint32_t)win.size() * 4};
       model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, 0, sink, dcd.data(), stats);
     } else {
-      model_huffman_spec<false>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
+      model_huffman_spec<kSrcPadded>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
                                 stats);
     }
   }
