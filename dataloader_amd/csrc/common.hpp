@@ -63,7 +63,10 @@ struct ImgDesc {
   int32_t h_sub;           // bits per lane range
   int32_t h_items;         // Huffman work items (kHuffThreads lanes each)
   int32_t h_item_base;     // first work item of the image in the batch (k_hseg)
+  int32_t ds_items;        // destuff work items (32 KiB parts of the scan, k_plan)
+  int32_t ds_item_base;    // first destuff work item of the image in the batch (k_plan)
   int32_t pad2;
+  int64_t dspart_off;      // per-part counts of k_destuff_count (16 bytes per part)
   // filled by k_destuff
   int32_t ent_len;         // destuffed entropy bytes
   int32_t n_rst;           // RST markers found

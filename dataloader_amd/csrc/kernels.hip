@@ -77,9 +77,18 @@ __device__ int32_t huff_lanes_cap(const ImgDesc& d) {
 // SparseSink), block info (uint2 per block), component planes, RGB, speculative
 // checkpoints, DC values (int32 per block).
 struct ChunkSizes {
-  int64_t ent, rst, coef, binfo, plane, rgb, cps, dcd, htab, hlane;
-  __device__ int64_t total() const { return ent + rst + coef + binfo + plane + rgb + cps + dcd + htab + hlane; }
+  int64_t ent, rst, coef, binfo, plane, rgb, cps, dcd, htab, hlane, dspart;
+  __device__ int64_t total() const {
+    return ent + rst + coef + binfo + plane + rgb + cps + dcd + htab + hlane + dspart;
+  }
 };
+
+// Destuff work items of an image: 32 KiB parts of its scan (>= 1, so that the
+// descriptor is always completed by k_destuff_write).
+constexpr int kDsPartBytes = 32 * 1024;
+__device__ __forceinline__ int ds_parts(const ImgDesc& d) {
+  return d.status != DINO_IMG_OK ? 0 : max(1, (d.scan_len + 16 + kDsPartBytes - 1) / kDsPartBytes);
+}
 
 __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   ChunkSizes z{};
@@ -97,33 +106,46 @@ __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   z.dcd = align16(4 * (int64_t)d.total_blocks);
   z.htab = align16(6 * (int64_t)sizeof(HuffTable));
   z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
+  z.dspart = 16 * (int64_t)ds_parts(d);
   return z;
 }
 
 __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size) {
   __shared__ int64_t part[1024];
+  __shared__ int32_t dpart[1024];
   const int t = threadIdx.x;
   const int per = (B + 1023) / 1024;
   int64_t local = 0;
+  int32_t dlocal = 0;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
-    if (i < B) local += image_chunk_bytes(desc[i]).total();
+    if (i < B) {
+      local += image_chunk_bytes(desc[i]).total();
+      dlocal += ds_parts(desc[i]);
+    }
   }
   part[t] = local;
+  dpart[t] = dlocal;
   __syncthreads();
-  for (int s = 1; s < 1024; s <<= 1) {  // Hillis-Steele inclusive scan
+  for (int s = 1; s < 1024; s <<= 1) {  // Hillis-Steele inclusive scans
     int64_t v = t >= s ? part[t - s] : 0;
+    int32_t dv = t >= s ? dpart[t - s] : 0;
     __syncthreads();
     part[t] += v;
+    dpart[t] += dv;
     __syncthreads();
   }
   int64_t base = part[t] - local;
+  int32_t dbase = dpart[t] - dlocal;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
     if (i >= B) continue;
     ImgDesc& d = desc[i];
     const ChunkSizes z = image_chunk_bytes(d);
     const int64_t sz = z.total();
+    d.ds_item_base = dbase;
+    d.ds_items = ds_parts(d);  // as counted by the scan above (the kernels skip images not OK)
+    dbase += d.ds_items;
     if (sz == 0) continue;
     if (base + sz > ws_size) {
       d.status = DINO_IMG_TOO_LARGE;
@@ -139,6 +161,7 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
       d.dcd_off = d.cps_off + z.cps;
       d.htab_off = d.dcd_off + z.dcd;
       d.hlane_off = d.htab_off + z.htab;
+      d.dspart_off = d.hlane_off + z.hlane;
       d.h_lanes_cap = huff_lanes_cap(d);
     }
     base += sz;
@@ -187,109 +210,257 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_wave
   return before + x - v;
 }
 
-__global__ void __launch_bounds__(kDestuffThreads) k_destuff(const uint8_t* __restrict__ bytes,
-                                                             const int64_t* __restrict__ offsets,
-                                                             ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+// A lane's 16-byte chunk c of the scan, classified: bit j of keep = byte kept,
+// of rstm = an RSTn marker starts there; term = scan index of the first
+// terminating marker in the chunk (n if none).
+struct DsChunk {
+  uint32_t wv[4];
+  uint32_t keep, rstm;
+  int term;
+};
+
+__device__ __forceinline__ DsChunk ds_classify(const uint8_t* r, int n, const uint4* base, int lead, int nchunks,
+                                               const uint8_t* buf_end, int c) {
+  DsChunk o;
+  o.wv[0] = o.wv[1] = o.wv[2] = o.wv[3] = 0u;
+  o.keep = o.rstm = 0u;
+  o.term = n;
+  const int k0 = 16 * c - lead;  // scan index of byte 0 of this chunk
+  int prevb = -1, nextb = -1;
+  if (c >= nchunks) return o;
+  if ((const uint8_t*)(base + c + 1) <= buf_end) {
+    const uint4 u = base[c];
+    o.wv[0] = u.x;
+    o.wv[1] = u.y;
+    o.wv[2] = u.z;
+    o.wv[3] = u.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (k0 + j >= 0 && k0 + j < n) o.wv[j >> 2] |= (uint32_t)r[k0 + j] << (8 * (j & 3));
+  }
+  if (k0 - 1 >= 0 && k0 - 1 < n) prevb = r[k0 - 1];
+  if (k0 + 16 >= 0 && k0 + 16 < n) nextb = r[k0 + 16];
+  // branch-free per byte; the first terminating marker clips the chunk afterwards
+  uint32_t termm = 0u;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = k0 + j;
+    const bool valid = k >= 0 && k < n;
+    const int v = (o.wv[j >> 2] >> (8 * (j & 3))) & 255;
+    const int pv = j > 0 ? (int)((o.wv[(j - 1) >> 2] >> (8 * ((j - 1) & 3))) & 255) : prevb;
+    const int nx = j < 15 ? (k + 1 < n ? (int)((o.wv[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255) : -1) : nextb;
+    // for 0xFF: 0 keep (FF00), 1 RST, 2 fill (FFFF), 3 terminating marker, 4 truncated (last byte)
+    const int cls = nx < 0 ? 4 : (nx == 0x00 ? 0 : ((nx >= 0xD0 && nx <= 0xD7) ? 1 : (nx == 0xFF ? 2 : 3)));
+    const bool ff = v == 0xFF;
+    const bool kept = ff ? cls == 0 : !(k > 0 && pv == 0xFF);
+    o.keep |= (uint32_t)(valid && kept) << j;
+    o.rstm |= (uint32_t)(valid && ff && cls == 1) << j;
+    termm |= (uint32_t)(valid && ff && cls >= 3) << j;
+  }
+  if (termm) {
+    const int f = __ffs(termm) - 1;
+    const uint32_t low = (1u << f) - 1u;
+    o.keep &= low;
+    o.rstm &= low;
+    o.term = k0 + f;
+  }
+  return o;
+}
+
+// Drop a chunk's bytes at or after scan index E.
+__device__ __forceinline__ void ds_clip(DsChunk& ch, int k0, int E) {
+  const int lim = E - k0;
+  const uint32_t mask = lim <= 0 ? 0u : (lim >= 16 ? 0xFFFFu : ((1u << lim) - 1u));
+  ch.keep &= mask;
+  ch.rstm &= mask;
+}
+
+// Geometry of an image's scan in 16-byte chunks (aligned loads; chunk c covers
+// scan bytes [16c - lead, 16c - lead + 16)) and parts of kDsPartChunks chunks.
+constexpr int kDsTiles = 8;
+constexpr int kDsPartChunks = kDestuffThreads * kDsTiles;  // 32 KiB of scan per work item
+struct DsGeom {
+  const uint8_t* r;
+  int n, lead, nchunks;
+  const uint4* base;
+  const uint8_t* buf_end;
+};
+
+__device__ __forceinline__ DsGeom ds_geom(const uint8_t* bytes, const int64_t* offsets, int B, const ImgDesc& d,
+                                          int img) {
+  DsGeom g;
+  g.r = bytes + offsets[img] + d.scan_off;
+  g.n = d.scan_len;
+  g.lead = (int)((uintptr_t)g.r & 15);
+  g.base = (const uint4*)(g.r - g.lead);
+  g.nchunks = (g.lead + g.n + 15) >> 4;
+  g.buf_end = bytes + offsets[B];  // a whole-chunk load must not pass the caller's buffer
+  return g;
+}
+
+// Work item -> (image, part) over desc[].ds_item_base (k_plan); -1 past the end.
+__device__ int ds_item_image(const ImgDesc* desc, int B, int item) {
+  const ImgDesc& last = desc[B - 1];
+  if (item >= last.ds_item_base + last.ds_items) return -1;
+  int lo = 0, hi = B - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (desc[mid].ds_item_base <= item) lo = mid;
+    else hi = mid - 1;
+  }
+  while (lo > 0 && desc[lo].ds_items == 0) --lo;
+  return lo;
+}
+
+// Per-part results of k_destuff_count: kept bytes, RST markers, first terminator.
+struct DsPart {
+  int32_t kept, nrst, term, pad;
+};
+
+// k_destuff_count: persistent over (image, part) items; counts the part's kept
+// bytes and RST markers and finds its first terminating marker.
+__global__ void __launch_bounds__(kDestuffThreads) k_destuff_count(const uint8_t* __restrict__ bytes,
+                                                                   const int64_t* __restrict__ offsets, int B,
+                                                                   const ImgDesc* __restrict__ desc,
+                                                                   uint8_t* __restrict__ ws) {
   __shared__ uint32_t s_wave[kDestuffThreads / 64];
-  __shared__ int s_end;
-  const int img = blockIdx.x, t = threadIdx.x;
-  ImgDesc* d = &desc[img];
-  if (d->status != DINO_IMG_OK) return;
-  const uint8_t* r = bytes + offsets[img] + d->scan_off;
-  const int n = d->scan_len;
-  uint8_t* out = ws + d->ent_off;
-  int32_t* rst = (int32_t*)(ws + d->rst_off);
-  const int nrst_cap = d->n_rst_max + 1;
-  const int lead = (int)((uintptr_t)r & 15);
-  const uint4* base = (const uint4*)(r - lead);  // aligned; chunk c covers scan bytes [16c - lead, 16c - lead + 16)
-  const int nchunks = (lead + n + 15) >> 4;
-  const uint8_t* buf_end = bytes + offsets[gridDim.x];  // a whole-chunk load must not pass the caller's buffer
-  uint32_t o_run = 0, rc_run = 0;
-  int E = n;
-  for (int c0 = 0; c0 < nchunks; c0 += kDestuffThreads) {
-    if (t == 0) s_end = n;
-    __syncthreads();
-    const int c = c0 + t;
-    const int k0 = 16 * c - lead;  // scan index of byte 0 of this chunk
-    uint32_t wv[4] = {0u, 0u, 0u, 0u};
-    int prevb = -1, nextb = -1;
-    if (c < nchunks) {
-      if ((const uint8_t*)(base + c + 1) <= buf_end) {
-        const uint4 u = base[c];
-        wv[0] = u.x;
-        wv[1] = u.y;
-        wv[2] = u.z;
-        wv[3] = u.w;
-      } else {
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if (k0 + j >= 0 && k0 + j < n) wv[j >> 2] |= (uint32_t)r[k0 + j] << (8 * (j & 3));
-      }
-      if (k0 - 1 >= 0 && k0 - 1 < n) prevb = r[k0 - 1];
-      if (k0 + 16 >= 0 && k0 + 16 < n) nextb = r[k0 + 16];
+  __shared__ int s_img;
+  __shared__ int s_term;
+  const int t = threadIdx.x;
+  for (int item = blockIdx.x;; item += gridDim.x) {
+    if (t == 0) {
+      s_img = ds_item_image(desc, B, item);
+      s_term = 0x7FFFFFFF;
     }
-    // classify: bit j of keep / rstm / term
-    uint32_t keep = 0, rstm = 0;
-    int my_term = n;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = k0 + j;
-      if (k < 0 || k >= n) continue;
-      const int v = (wv[j >> 2] >> (8 * (j & 3))) & 255;
-      const int pv = j > 0 ? (int)((wv[(j - 1) >> 2] >> (8 * ((j - 1) & 3))) & 255) : prevb;
-      const int nx = j < 15 ? (k + 1 < n ? (int)((wv[(j + 1) >> 2] >> (8 * ((j + 1) & 3))) & 255) : -1) : nextb;
-      if (v == 0xFF) {
-        // 0 keep (FF00), 1 RST, 2 fill (FFFF), 3 terminating marker, 4 truncated (last byte)
-        const int cls = nx < 0 ? 4 : (nx == 0x00 ? 0 : ((nx >= 0xD0 && nx <= 0xD7) ? 1 : (nx == 0xFF ? 2 : 3)));
-        if (cls >= 3) {
-          my_term = min(my_term, k);
+    __syncthreads();
+    const int img = s_img;
+    if (img < 0) return;
+    const ImgDesc& d = desc[img];
+    if (d.status != DINO_IMG_OK) {
+      __syncthreads();
+      continue;
+    }
+    const DsGeom g = ds_geom(bytes, offsets, B, d, img);
+    const int part = item - d.ds_item_base;
+    uint32_t kept = 0, nrst = 0;
+    int term = g.n;
+#pragma unroll 1
+    for (int tile = 0; tile < kDsTiles; ++tile) {
+      const int c = part * kDsPartChunks + tile * kDestuffThreads + t;
+      DsChunk ch = ds_classify(g.r, g.n, g.base, g.lead, g.nchunks, g.buf_end, c);
+      if (ch.term < g.n) ds_clip(ch, 16 * c - g.lead, ch.term);
+      term = min(term, ch.term);
+      kept += __popc(ch.keep);
+      nrst += __popc(ch.rstm);
+    }
+    if (term < g.n) atomicMin(&s_term, term);
+    uint32_t tot;
+    (void)block_excl_scan<kDestuffThreads>(kept | (nrst << 16), s_wave, &tot);  // nrst per part < 65536
+    if (t == 0) {
+      // bytes after the part's own first terminator were not counted past it in each
+      // lane, but a later lane of the same part may have counted bytes after an earlier
+      // lane's terminator: k_destuff_write recounts exactly; here only the totals of parts
+      // wholly before the image's first terminator are used
+      DsPart* dp = (DsPart*)(ws + d.dspart_off) + part;
+      dp->kept = (int32_t)(tot & 0xFFFFu) + (int32_t)0;
+      dp->nrst = (int32_t)(tot >> 16);
+      dp->term = s_term == 0x7FFFFFFF ? g.n : s_term;
+      dp->pad = 0;
+    }
+    __syncthreads();
+  }
+}
+
+// k_destuff_write: persistent over the same items.  The part's output offset is
+// the kept bytes of the image's earlier parts (all before the first terminator E);
+// bytes at or after E are dropped; the part holding E (or the image's last part)
+// zero-pads the stream and fills the descriptor.
+__global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t* __restrict__ bytes,
+                                                                   const int64_t* __restrict__ offsets, int B,
+                                                                   ImgDesc* __restrict__ desc,
+                                                                   uint8_t* __restrict__ ws) {
+  __shared__ uint32_t s_wave[kDestuffThreads / 64];
+  __shared__ int s_img;
+  __shared__ int s_E;
+  __shared__ uint32_t s_o0, s_r0;
+  const int t = threadIdx.x;
+  for (int item = blockIdx.x;; item += gridDim.x) {
+    if (t == 0) s_img = ds_item_image(desc, B, item);
+    __syncthreads();
+    const int img = s_img;
+    if (img < 0) return;
+    ImgDesc* d = &desc[img];
+    if (d->status != DINO_IMG_OK) {
+      __syncthreads();
+      continue;
+    }
+    const DsGeom g = ds_geom(bytes, offsets, B, *d, img);
+    const int part = item - d->ds_item_base;
+    const DsPart* dp = (const DsPart*)(ws + d->dspart_off);
+    if (t == 0) {  // first terminator of the image, output offset of this part
+      int E = g.n;
+      uint32_t o0 = 0, r0 = 0;
+      for (int p = 0; p < d->ds_items; ++p) {
+        if (p < part && E == g.n) {
+          o0 += (uint32_t)dp[p].kept;
+          r0 += (uint32_t)dp[p].nrst;
+        }
+        if (dp[p].term < g.n) {
+          E = dp[p].term;
           break;
         }
-        if (cls == 0) keep |= 1u << j;
-        if (cls == 1) rstm |= 1u << j;
-      } else if (!(k > 0 && pv == 0xFF)) {
-        keep |= 1u << j;
       }
+      s_E = E;
+      s_o0 = o0;
+      s_r0 = r0;
     }
-    if (my_term < n) atomicMin(&s_end, my_term);
     __syncthreads();
-    const int Et = s_end;
-    if (Et < n) {  // drop everything at or after the terminator
-      const int lim = Et - k0;
-      const uint32_t mask = lim <= 0 ? 0u : (lim >= 16 ? 0xFFFFu : ((1u << lim) - 1u));
-      keep &= mask;
-      rstm &= mask;
-    }
-    const uint32_t packed = (uint32_t)__popc(keep) | ((uint32_t)__popc(rstm) << 16);
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan<kDestuffThreads>(packed, s_wave, &tot);
-    uint32_t o = o_run + (ex & 0xFFFFu), ro = rc_run + (ex >> 16);
-    for (uint32_t m = keep | rstm; m; m &= m - 1) {
-      const int j = __ffs(m) - 1;
-      if (keep & (1u << j)) {
-        out[o++] = (uint8_t)((wv[j >> 2] >> (8 * (j & 3))) & 255);
-      } else {
-        if ((int)ro < nrst_cap) rst[ro] = (int32_t)o;
-        ++ro;
+    const int E = s_E;
+    const int part_k0 = part * kDsPartChunks * 16 - g.lead;
+    if (part_k0 < E || (part == 0)) {
+      uint8_t* out = ws + d->ent_off;
+      int32_t* rst = (int32_t*)(ws + d->rst_off);
+      const int nrst_cap = d->n_rst_max + 1;
+      uint32_t o_run = s_o0, rc_run = s_r0;
+#pragma unroll 1
+      for (int tile = 0; tile < kDsTiles; ++tile) {
+        const int c = part * kDsPartChunks + tile * kDestuffThreads + t;
+        DsChunk ch = ds_classify(g.r, g.n, g.base, g.lead, g.nchunks, g.buf_end, c);
+        if (E < g.n) ds_clip(ch, 16 * c - g.lead, E);
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<kDestuffThreads>((uint32_t)__popc(ch.keep) | ((uint32_t)__popc(ch.rstm) << 16),
+                                                             s_wave, &tot);
+        uint32_t o = o_run + (ex & 0xFFFFu), ro = rc_run + (ex >> 16);
+        for (uint32_t m = ch.keep | ch.rstm; m; m &= m - 1) {
+          const int j = __ffs(m) - 1;
+          if (ch.keep & (1u << j)) {
+            out[o++] = (uint8_t)((ch.wv[j >> 2] >> (8 * (j & 3))) & 255);
+          } else {
+            if ((int)ro < nrst_cap) rst[ro] = (int32_t)o;
+            ++ro;
+          }
+        }
+        o_run += tot & 0xFFFFu;
+        rc_run += tot >> 16;
+      }
+      // the part that ends the stream: holds E, or is the image's last part
+      const int part_k1 = part_k0 + kDsPartChunks * 16;
+      const bool last = (E < g.n) ? (E >= part_k0 && E < part_k1) : (part == d->ds_items - 1);
+      if (last) {
+        const int total = (int)o_run;
+        for (int k = total + t; k < total + 64 && k < g.n + 64; k += kDestuffThreads) out[k] = 0;
+        if (t == 0) {
+          const int term = (E < g.n) && (E + 1 < g.n);  // a marker (not a trailing lone 0xFF) ended the scan
+          d->ent_len = total;
+          d->n_rst = (int32_t)rc_run;
+          d->terminated = term;
+          if (!term) d->status = DINO_IMG_TRUNCATED;
+          else if (d->restart_interval > 0 && d->n_rst < d->n_rst_max - 1) d->status = DINO_IMG_BADDATA;
+        }
       }
     }
-    o_run += tot & 0xFFFFu;
-    rc_run += tot >> 16;
-    if (Et < n) {
-      E = Et;
-      break;
-    }
-  }
-  const int total = (int)o_run;
-  // zero padding for word reads past the end
-  for (int k = total + t; k < total + 64 && k < n + 64; k += kDestuffThreads) out[k] = 0;
-  if (t == 0) {
-    const int term = (E < n) && (E + 1 < n);  // a marker (not a trailing lone 0xFF) ended the scan
-    d->ent_len = total;
-    d->n_rst = (int32_t)rc_run;
-    d->terminated = term;
-    if (!term) d->status = DINO_IMG_TRUNCATED;
-    else if (d->restart_interval > 0 && d->n_rst < d->n_rst_max - 1) d->status = DINO_IMG_BADDATA;
+    __syncthreads();
   }
 }
 
@@ -335,7 +506,7 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
   int32_t img, item;
 };
 
-static_assert(sizeof(ImgDesc) == 944, "ImgDesc layout");
+static_assert(sizeof(ImgDesc) == 960, "ImgDesc layout");
 constexpr int kHuffLdsBytes = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
 constexpr int kHuff3LdsBytes = (int)((sizeof(HuffLds3) + 15) & ~(size_t)15);
 
@@ -1610,7 +1781,15 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   if (B <= 0) return hipSuccess;
   TIMED(tm, kKParse, s, (k_parse<<<(B + 63) / 64, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc)));
   TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
-  TIMED(tm, kKDestuff, s, (k_destuff<<<B, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  static int grid_ds = 0;
+  if (!grid_ds) {
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid_ds = 4 * cus;
+  }
+  TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
+  TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   static int grid1 = 0, grid3 = 0;
   if (!grid1) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff1), hipFuncAttributeMaxDynamicSharedMemorySize,
