@@ -443,11 +443,7 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
           add3(pred, comp, o.value);
           sink.dc((int16_t)get3(pred, comp));
         } else {
-#ifdef DINO_EXP_NOSTORE
-          sink.dc((int16_t)o.value);
-#else
           dcd[b] = o.value;
-#endif
         }
       } else if (o.kind == 1) {
         sink.ac(o.zz, (int16_t)o.value);

@@ -528,14 +528,6 @@ struct SparseSink {
   uint32_t e0, e1, e2, e3;
   uint32_t bstart;
   int32_t b;
-#ifdef DINO_EXP_NOSTORE
-  uint32_t acc = 0;
-  __device__ void dc(int16_t v) { acc += (uint32_t)v; }
-  __device__ void end() { acc += bstart; }
-  __device__ void close() {
-    if (acc == 0x12345678u) ent[0] = acc;
-  }
-#endif
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * 64u;
     k = 0;
@@ -550,23 +542,17 @@ struct SparseSink {
     e2 = k == 2 ? e : e2;
     e3 = k == 3 ? e : e3;
     if (++k == 4) {
-#ifdef DINO_EXP_NOSTORE
-      acc ^= e0 ^ e1 ^ e2 ^ e3;
-#else
       *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
-#endif
       n += 4;
       k = 0;
     }
   }
   __device__ void ac(int zz, int16_t v) { push(((uint32_t)(uint16_t)v << 16) | (uint32_t)zz); }
-#ifndef DINO_EXP_NOSTORE
   __device__ void dc(int16_t v) { dcd[b] = (int32_t)v; }
   __device__ void end() { binfo[b] = make_uint2(bstart, n + k - bstart); }
   __device__ void close() {  // the region is a multiple of 4 entries: a whole-word tail store stays inside it
     if (k) *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
   }
-#endif
 };
 
 // Lane geometry of a non-restart image: range [i*sub, end) of every active lane.
@@ -1222,30 +1208,30 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
 // staged in LDS too when they fit.  Each lane then resamples one (row, x) with
 // one LDS word per tap and writes the three channels to planar temp rows
 // [3][crop_h][S].  Crops too wide for LDS take a direct (global) path.
-constexpr int kHresizeTapLds = 16 * 1024;
+constexpr int kHresizeTapLds = 16 * 1024;  // taps of one slice; the rest of kHresizeLds stages rows
 
-// One band of nr staged rows: lane (r, x) accumulates three signed-dot4 digit
-// products per channel and group of 4 taps.  Rows are staged planar with the
-// sign bit flipped (p - 128 as int8); the taps' pixels start at xmin, so each
-// group's 4 pixels are one v_alignbyte of two consecutive LDS words (the upper
-// word carried to the next group).  Exact: the int32 sum equals Pillow's.
-template <bool kLdsTaps>
-__device__ __forceinline__ void hresize_band_dot(const uint8_t* __restrict__ rows, int pitch, int nr, int r0, int S,
-                                                 const int4* __restrict__ hx, const uint4* __restrict__ hg,
-                                                 uint8_t* __restrict__ tmp, int64_t cpl, int plane_bytes) {
-  for (int e = threadIdx.x; e < nr * S; e += blockDim.x) {
-    const int r = e / S, x = e - r * S;
-    const int4 h = hx[x];
-    const int xmin = h.x, ng = h.y;
-    const uint32_t sh = (uint32_t)(xmin & 3);
-    const uint32_t* q0 = (const uint32_t*)(rows + r * pitch) + (xmin >> 2);
+// One tile: nr staged rows x the outputs [x0, x0 + sw) of a slice.  Lane (r, x)
+// accumulates three signed-dot4 digit products per channel and group of 4 taps.
+// Rows are staged planar with the sign bit flipped (p - 128 as int8), starting at
+// source column c0; the taps' pixels start at xmin, so each group's 4 pixels are one
+// v_alignbyte of two consecutive LDS words (the upper word carried to the next
+// group).  Exact: the int32 sum equals Pillow's.
+__device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ rows, int pitch, int plane_bytes, int nr,
+                                                 int r0, int x0, int sw, int c0, int S, const int4* __restrict__ hx,
+                                                 const uint4* __restrict__ hg, uint8_t* __restrict__ tmp, int64_t cpl) {
+  for (int e = threadIdx.x; e < nr * sw; e += blockDim.x) {
+    const int r = e / sw, xl = e - r * sw;
+    const int4 h = hx[xl];
+    const int lo = h.x - c0, ng = h.y;
+    const uint32_t sh = (uint32_t)(lo & 3);
+    const uint32_t* q0 = (const uint32_t*)(rows + r * pitch) + (lo >> 2);
     const uint32_t* q1 = (const uint32_t*)((const uint8_t*)q0 + plane_bytes);
     const uint32_t* q2 = (const uint32_t*)((const uint8_t*)q1 + plane_bytes);
     int32_t a00 = 0, a01 = 0, a02 = 0, a10 = 0, a11 = 0, a12 = 0, a20 = 0, a21 = 0, a22 = 0;
     uint32_t l0 = q0[0], l1 = q1[0], l2 = q2[0];
 #pragma unroll 2
     for (int g = 0; g < ng; ++g) {
-      const uint4 dg = hg[g * S + x];
+      const uint4 dg = hg[g * sw + xl];
       const uint32_t u0 = q0[g + 1], u1 = q1[g + 1], u2 = q2[g + 1];
       const int32_t p0 = (int32_t)__builtin_amdgcn_alignbyte(u0, l0, sh);
       const int32_t p1 = (int32_t)__builtin_amdgcn_alignbyte(u1, l1, sh);
@@ -1263,7 +1249,7 @@ __device__ __forceinline__ void hresize_band_dot(const uint8_t* __restrict__ row
       l1 = u1;
       l2 = u2;
     }
-    const int64_t o = (int64_t)(r0 + r) * S + x;
+    const int64_t o = (int64_t)(r0 + r) * S + x0 + xl;
     // int32 wrap-around is harmless: the true sum (Pillow's int32 ss) fits in int32
     tmp[o] = clip8_acc((int32_t)((uint32_t)a00 + ((uint32_t)a01 << 8) + ((uint32_t)a02 << 16) + (uint32_t)h.z));
     tmp[cpl + o] = clip8_acc((int32_t)((uint32_t)a10 + ((uint32_t)a11 << 8) + ((uint32_t)a12 << 16) + (uint32_t)h.z));
@@ -1272,6 +1258,10 @@ __device__ __forceinline__ void hresize_band_dot(const uint8_t* __restrict__ row
   }
 }
 
+// Horizontal pass in tiles of (slice of outputs) x (band of rows).  A slice is as
+// many outputs as fit their taps in kHresizeTapLds, so the taps always come from
+// LDS; the band stages only the source columns the slice reads
+// [xmin(x0), xmin(x1-1) + xcnt(x1-1)), so narrower slices also mean more rows per band.
 __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  const ViewPlan* __restrict__ plan, int nv, int v0,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
@@ -1291,15 +1281,15 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   uint8_t* tmp = aws + vp.htmp_off;
   const int64_t cpl = (int64_t)p.crop_h * S;
   const int ng_max = (kh + 3) / 4;
-  const int tab_bytes = S * 16 * (1 + ng_max);
-  const bool lds_taps = tab_bytes <= kHresizeTapLds;
-  const int rbase = lds_taps ? tab_bytes : 0;
-  const int ngroups = (cw + 3) >> 2;
-  // planar rows: [3][R][pitch] with 8 bytes of slack for the last group's upper word
-  const int pitch = ngroups * 4 + 8;
-  int R = (kHresizeLds - rbase) / (3 * pitch);
+  int sw = kHresizeTapLds / (16 * (1 + ng_max));
+  sw = sw >= S ? S : (sw & ~7);
+  const int nsl = sw > 0 ? (S + sw - 1) / sw : 0;
+  // widest source span of a slice (+ 4 for the word alignment of its first column)
+  const int span = min(cw, (int)(((int64_t)sw * cw + S - 1) / S) + kh + 2) + 4;
+  const int pitch = ((span + 3) & ~3) + 8;  // + slack for the last group's upper word
+  int R = sw > 0 ? (kHresizeLds - kHresizeTapLds) / (3 * pitch) : 0;
   R = R > 16 ? 16 : R;
-  if (R < 1) {  // direct path: taps and pixels from global memory
+  if (R < 1) {  // direct path: taps and pixels from global memory (crops too wide for LDS)
     const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
     const CoefView cv{gb, gt, kh};
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cpl; e += (int64_t)gridDim.x * blockDim.x) {
@@ -1309,18 +1299,30 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
     return;
   }
   int4* lx = (int4*)smem;
-  uint4* lg = (uint4*)(lx + S);
-  if (lds_taps) {
-    for (int k = threadIdx.x; k < S; k += blockDim.x) lx[k] = ghx[k];
-    for (int k = threadIdx.x; k < S * ng_max; k += blockDim.x) lg[k] = ghg[k];
-  }
-  uint8_t* rows = smem + rbase;
+  uint4* lg = (uint4*)(lx + sw);
+  uint8_t* rows = smem + kHresizeTapLds;
   const int plane_bytes = R * pitch;
-  for (int r0 = blockIdx.x * R; r0 < p.crop_h; r0 += gridDim.x * R) {
-    const int nr = min(R, p.crop_h - r0);
+  const int nbands = (p.crop_h + R - 1) / R;
+  int cur = -1;
+  for (int u = blockIdx.x; u < nsl * nbands; u += gridDim.x) {
+    const int sl = u / nbands, band = u - sl * nbands;
+    const int x0 = sl * sw, swn = min(sw, S - x0);
+    const int r0 = band * R, nr = min(R, p.crop_h - r0);
+    if (sl != cur) {  // taps of the slice -> LDS
+      __syncthreads();
+      for (int k = threadIdx.x; k < swn; k += blockDim.x) lx[k] = ghx[x0 + k];
+      for (int k = threadIdx.x; k < swn * ng_max; k += blockDim.x) {
+        const int g = k / swn, xl = k - g * swn;
+        lg[g * swn + xl] = ghg[(int64_t)g * S + x0 + xl];
+      }
+      cur = sl;
+    }
+    const int c0 = ghx[x0].x & ~3;  // first source column staged (4-aligned within the crop)
+    const int c1 = min(cw, ghx[x0 + swn - 1].x + gb[2 * (x0 + swn - 1) + 1]);
+    const int ngroups = (c1 - c0 + 3) >> 2;
     for (int e = threadIdx.x; e < nr * ngroups; e += blockDim.x) {
       const int r = e / ngroups, g = e - r * ngroups;
-      const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left) * 3 + 12 * g;
+      const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left + c0) * 3 + 12 * g;
       const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
       const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
       const uint32_t w0 = a0[0], w1 = a0[1], w2 = a0[2], w3 = a0[3];
@@ -1337,10 +1339,7 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
       *(uint32_t*)(dst + 2 * plane_bytes) = cb ^ 0x80808080u;
     }
     __syncthreads();
-    if (lds_taps)
-      hresize_band_dot<true>(rows, pitch, nr, r0, S, lx, lg, tmp, cpl, plane_bytes);
-    else
-      hresize_band_dot<false>(rows, pitch, nr, r0, S, ghx, ghg, tmp, cpl, plane_bytes);
+    hresize_tile_dot(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
     __syncthreads();
   }
 }
