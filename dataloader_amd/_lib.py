@@ -56,6 +56,7 @@ def load() -> ctypes.CDLL:
         "dino_tar_index": (i32, [vp, i64, vp, i64, vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "dino_tar_last_error": (ctypes.c_char_p, []),
         "dino_gather": (i32, [vp, vp, i64, vp, i64, vp, i32]),
+        "dino_set_norm": (i32, [vp, vp, i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -75,4 +76,4 @@ def exported_symbols() -> list[str]:
     return ["dino_abi_version", "dino_last_error", "dino_ctx_create", "dino_ctx_destroy", "dino_decode",
             "dino_copy_rgb", "dino_sample_params", "dino_augment", "dino_run_batch", "dino_masks",
             "dino_bf16_to_fp8", "dino_debug_region", "dino_set_timing", "dino_kernel_times",
-            "dino_tar_index", "dino_tar_last_error", "dino_gather"]
+            "dino_tar_index", "dino_tar_last_error", "dino_gather", "dino_set_norm"]

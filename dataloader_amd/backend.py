@@ -167,6 +167,13 @@ class MI355XBackend:
         out = pipeline_cfg.output_dtype
         if getattr(pipeline_cfg, "dali_fp8_output", False) or getattr(aug_spec, "fp8_output", False):
             out = "fp8"
+        norm = None
+        if getattr(pipeline_cfg, "fuse_normalization", False) and specs is not None:
+            # per-dataset mean/std as DALIBackend wires NormSource (dali_backend.py:142-153)
+            from .norm import NormTable
+            norm = NormTable(aug_spec.aug_cfg, specs)
+            if hasattr(source, "register_dataset_index_callback"):
+                source.register_dataset_index_callback(norm.set_dataset_indices)
         return MI355XAugPipeline(
             source=source,
             aug_cfg=aug_spec.aug_cfg,
@@ -177,6 +184,7 @@ class MI355XBackend:
             device=pipeline_cfg.device_id,
             max_image_dim=self._max_image_dim,
             workspace_bytes=self._workspace_bytes,
+            norm=norm,
         )
 
     def build_pipeline_iterator(self, pipeline: Any, aug_spec: Any, output_map: list[str],

@@ -45,6 +45,8 @@ struct dino_ctx {
   ViewPlan* d_plan = nullptr;
   dino_view_params* d_params = nullptr;
   uint8_t* d_gcrop = nullptr;
+  const float* d_norm = nullptr;  // per-image normalisation (dino_set_norm), nullable
+  int32_t norm_n = 0;
   int32_t last_batch = -1;
   KernelTimer* timer = nullptr;
   KernelTimer* tm() { return timer && timer->enabled ? timer : nullptr; }
@@ -159,14 +161,25 @@ int dino_augment(dino_ctx* c, const dino_aug_config* cfg, const dino_view_params
   if (r) return r;
   const int nv = cfg->n_global + cfg->n_local;
   if (nv > kMaxViews) return fail(DINO_EINVAL, "dino_augment: more than %s%lld views", "", kMaxViews);
+  if (c->d_norm && c->norm_n < c->last_batch)
+    return fail(DINO_EINVAL, "dino_augment: dino_set_norm covers %s%lld images, fewer than the batch", "", c->norm_n);
   hipStream_t s = (hipStream_t)stream;
-  AugmentArgs a{c->d_desc, c->last_batch, d_params, c->d_plan, c->d_ws, c->d_aws, c->aws_size, c->d_gcrop, {}, *cfg};
+  AugmentArgs a{c->d_desc, c->last_batch, d_params, c->d_plan, c->d_ws, c->d_aws, c->aws_size, c->d_gcrop, {}, *cfg,
+                c->d_norm};
   for (int v = 0; v < nv; ++v) {
     if (!d_views[v]) return fail(DINO_EINVAL, "dino_augment: null output pointer for view %s%lld", "", v);
     a.views.p[v] = d_views[v];
   }
   hipError_t e = launch_augment(a, s, c->tm());
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_augment");
+}
+
+int dino_set_norm(dino_ctx* c, const float* d_norm, int32_t n) {
+  if (!c) return fail(DINO_EINVAL, "dino_set_norm: null ctx%s%lld");
+  if (d_norm && n < 1) return fail(DINO_EINVAL, "dino_set_norm: %s%lld entries", "", n);
+  c->d_norm = d_norm;
+  c->norm_n = d_norm ? n : 0;
+  return DINO_OK;
 }
 
 int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,

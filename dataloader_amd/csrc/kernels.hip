@@ -1522,7 +1522,8 @@ __host__ __device__ __forceinline__ int final_tile_pitch(int S, int pad) { retur
 template <int KS, typename OutT>
 __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, int tp, int64_t tplane, int nr, int y0,
                                               int S, int ks_rt, const float* __restrict__ k2, bool solarize,
-                                              const dino_aug_config& cfg, OutT* __restrict__ out) {
+                                              const dino_aug_config& cfg, const float* __restrict__ nb,
+                                              OutT* __restrict__ out) {
   const int ks = KS > 0 ? KS : ks_rt;
   const int nq = (S + 3) >> 2;
   const int64_t N = (int64_t)S * S;
@@ -1572,7 +1573,7 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
         val[j] = rr <= 0.0f ? 0 : (rr >= 255.0f ? 255 : (int)rr);
       }
     }
-    const float mean = cfg.mean[ch], sd = cfg.std[ch];
+    const float mean = nb ? nb[ch] : cfg.mean[ch], sd = nb ? nb[3 + ch] : cfg.std[ch];
     float f[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) f[j] = u8_normalize(solarize ? solarize_u8(val[j]) : val[j], mean, sd);
@@ -1584,7 +1585,8 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
 template <typename OutT>
 __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restrict__ prm, const ViewPlan* __restrict__ plan,
                                                int nv, int v0, int B, const uint8_t* __restrict__ gcrop,
-                                               ViewPtrs views, dino_aug_config cfg, int S) {
+                                               ViewPtrs views, dino_aug_config cfg, int S,
+                                               const float* __restrict__ norm) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
   uint8_t* tile = smem + sizeof(FinalLds);
@@ -1629,13 +1631,14 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   if (p.blur && threadIdx.x < ks * ks) H.k2[threadIdx.x] = H.k1[threadIdx.x / ks] * H.k1[threadIdx.x % ks];
   __syncthreads();
   const bool sol = p.solarize != 0;
+  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
   switch (ks) {
-    case 1: final_compute<1, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
-    case 3: final_compute<3, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
-    case 5: final_compute<5, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
-    case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
-    case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
-    default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, out); break;
+    case 1: final_compute<1, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
+    case 3: final_compute<3, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
+    case 5: final_compute<5, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
+    case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
+    case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
+    default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
   }
 }
 
@@ -1832,7 +1835,7 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   const int lds = (int)sizeof(FinalLds) + 3 * (kFinalRows + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
   TIMED(tm, kfin, s,
         (k_final<OutT><<<dim3((S + kFinalRows - 1) / kFinalRows, nvc, B), 256, lds, s>>>(
-            a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S)));
+            a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S, a.norm)));
   return hipGetLastError();
 }
 

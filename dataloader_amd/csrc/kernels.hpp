@@ -81,6 +81,7 @@ struct AugmentArgs {
   uint8_t* gcrop;          // u8 crop planes of every view (k_vert -> k_final)
   ViewPtrs views;          // n_views output pointers (device memory)
   dino_aug_config cfg;
+  const float* norm;       // per-image {mean[3], std[3]} ([0, 1] scale), nullable -> cfg.mean / cfg.std
 };
 
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm = nullptr);

@@ -147,6 +147,15 @@ class IngestEngine:
         self.last_batch = batch
         return views, info
 
+    def set_norm(self, d_norm: torch.Tensor | None) -> None:
+        """Per-image {mean[3], std[3]} ([0, 1] scale) for the next batches (``dino_set_norm``);
+        None restores the global statistics.  The tensor must outlive the batches using it."""
+        if d_norm is None:
+            _lib.check(self.lib.dino_set_norm(self._ctx, ctypes.c_void_p(0), 0), "dino_set_norm")
+            return
+        assert d_norm.dtype == torch.float32 and d_norm.is_contiguous() and d_norm.shape[-1] == 6
+        _lib.check(self.lib.dino_set_norm(self._ctx, _ptr(d_norm), int(d_norm.shape[0])), "dino_set_norm")
+
     def close(self) -> None:
         if self._ctx:
             torch.cuda.synchronize(self.device)

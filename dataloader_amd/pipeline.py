@@ -48,6 +48,7 @@ class _Slot:
         self.event: torch.cuda.Event | None = None
         self.inflight = None
         self.outputs: dict[str, torch.Tensor] | None = None
+        self.norm: torch.Tensor | None = None         # per-image normalisation records of the batch
         self.staging: torch.Tensor | None = None      # pinned JPEG bytes of a packed (native) source
         self.staging_off: torch.Tensor | None = None  # pinned int64 offsets[B+1]
 
@@ -59,13 +60,14 @@ class MI355XAugPipeline:
 
     def __init__(self, source: Any, aug_cfg, batch_size: int, resolution_src=None, seed: int = 0,
                  out_dtype="bf16", device: int = 0, max_image_dim: int = 8192, workspace_bytes: int = 0,
-                 engine: IngestEngine | None = None, depth: int = 1):
+                 engine: IngestEngine | None = None, depth: int = 1, norm=None):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
         self._resolution_src = resolution_src
         self._out = _out_code(out_dtype)
         self._seed = int(seed)
+        self._norm = norm  # NormTable (per-dataset statistics) or None: global mean/std
         self._batch_index = 0
         self.depth = max(1, int(depth))
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
@@ -139,6 +141,11 @@ class MI355XAugPipeline:
         if sl.params is None or sl.params.numel() < batch * self._aug_cfg.n_views * 64:
             with eng.on_stream():
                 sl.params = torch.empty(batch * self._aug_cfg.n_views * 64, dtype=torch.uint8, device=self.device)
+        if self._norm is not None:  # per-dataset statistics of this batch's images (DALI NormSource)
+            recs = torch.from_numpy(self._norm.batch_records(batch)).pin_memory()
+            with eng.on_stream():
+                sl.norm = recs.to(self.device, non_blocking=True)
+            eng.set_norm(sl.norm)
         views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
                                     views=views, params_out=sl.params)
         sl.info = info

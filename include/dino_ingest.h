@@ -158,6 +158,14 @@ int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t 
  * (<= max_bytes).  Synchronises the stream. */
 int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream);
 
+/* Per-dataset normalisation (reference NormSource, pipeline.py:109-180, and
+ * build_norm_arrays, norm_utils.py:51-88 — DALI-only in the reference): d_norm is a
+ * device array of n records {mean[3], std[3]} in [0, 1] scale, one per image of the
+ * batch, used by every later dino_augment / dino_run_batch on this ctx instead of
+ * cfg->mean / cfg->std (x = (p / 255 - mean) / std, as the CPU path computes).  NULL
+ * restores the global statistics.  The array must stay valid while those calls run. */
+int dino_set_norm(dino_ctx* ctx, const float* d_norm, int32_t n);
+
 /* Stage-5 cast (reference FP8Formatter.quantise, memory.py:193-214, scale 1):
  * bf16 -> OCP float8_e4m3fn, round-to-nearest-even, bit-identical to torch's
  * .to(torch.float8_e4m3fn) (c10 fp8e4m3fn_from_fp32_value: |x| >= 480 -> NaN).

@@ -374,3 +374,57 @@ def test_shm_shard_feed_matches_python_source(gpu_device, tmp_path):
             for k in a:
                 assert torch.equal(a[k], b[k]), (depth, k)
     cache.close(remove=True)
+
+
+def test_per_dataset_normalisation(gpu_device):
+    """Per-image {mean, std} (DALI NormSource semantics, reference pipeline.py:109-180) through
+    dino_set_norm, wired by MI355XBackend.build_pipeline from the specs and the source's
+    dataset-index callback: each image matches the oracle run with its dataset's stats."""
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import DinoV2AugSpec, PipelineConfig
+    from dataloader_amd.pipeline import MI355XPipelineIterator
+
+    class Spec:
+        def __init__(self, mean, std):
+            self.mean, self.std = mean, std
+
+    specs = [Spec(None, None), Spec((0.5, 0.4, 0.3), (0.25, 0.2, 0.3)), Spec((0.1, 0.2, 0.3), (0.5, 0.6, 0.7))]
+    cfg = DINOAugConfig(global_crop_size=64, local_crop_size=32, n_local_crops=2)
+    rng = np.random.default_rng(9)
+    jpegs = [make_jpeg(int(rng.integers(90, 300)), int(rng.integers(90, 300)), s) for s in range(6)]
+    ds_idx = [0, 1, 2, 1, 7, 0]  # 7 is past the table: last entry (norm_utils.py:78-86)
+
+    class Source:
+        _batch_size = 6
+        _resolution_src = None
+
+        def __init__(self):
+            self.cbs = []
+
+        def register_dataset_index_callback(self, cb):
+            self.cbs.append(cb)
+
+        def __call__(self):
+            for cb in self.cbs:
+                cb(ds_idx)
+            return jpegs
+
+    src = Source()
+    pipe = MI355XBackend().build_pipeline(src, DinoV2AugSpec(cfg), PipelineConfig(output_dtype="fp32", seed=3), specs)
+    it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], 6)
+    out = next(it)[0]
+    torch.cuda.synchronize()
+    recs = pipe.last_params()
+    nv = cfg.n_views
+    for b, jpg in enumerate(jpegs):
+        sp = specs[min(ds_idx[b], len(specs) - 1)]
+        mean = sp.mean or cfg.mean
+        std = sp.std or cfg.std
+        img = cpu_ref.decode_rgb(jpg)
+        for v in range(nv):
+            p = record_to_params(recs[b * nv + v])
+            ref = cpu_ref.augment_one(jpg, p, mean, std, out_dtype=torch.float32, decoded=img)
+            got = out[f"view_{v}"][b].cpu()
+            tol = ONE_LEVEL * max(STD_MIN / min(std), 1.0) + 1e-6 if p.blur else 0.0
+            assert (ref - got).abs().max().item() <= tol, (b, v)
+    pipe.close()
