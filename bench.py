@@ -87,8 +87,9 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
     ab = {
         "path": s_jpeg + out,                       # S_jpeg + 1 044 480 B (bf16)
-        "k_destuff": 2 * s_jpeg,
-        "k_huffman": s_jpeg + blocks * 128,          # entropy bytes in, int16 coefficients out
+        "k_destuff": s_jpeg,                         # per launch: count pass reads, write pass reads + writes
+        "k_huff1": s_jpeg,                           # first (speculative) decode reads the entropy stream
+        "k_huff3": s_jpeg + blocks * 128,            # re-decode: entropy bytes in, coefficients out (dense int16 equivalent)
         "k_idct": blocks * 128 + blocks * 64,
         "k_color": blocks * 64 + px * 3,
         "k_final_global": (3 + out_bytes * 3) * n_g * g * g,
