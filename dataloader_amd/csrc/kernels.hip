@@ -1219,42 +1219,57 @@ constexpr int kHresizeTapLds = 16 * 1024;  // taps of one slice; the rest of kHr
 __device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ rows, int pitch, int plane_bytes, int nr,
                                                  int r0, int x0, int sw, int c0, int S, const int4* __restrict__ hx,
                                                  const uint4* __restrict__ hg, uint8_t* __restrict__ tmp, int64_t cpl) {
-  for (int e = threadIdx.x; e < nr * sw; e += blockDim.x) {
-    const int r = e / sw, xl = e - r * sw;
+  // a lane computes one output column for two rows (the taps are read once for both)
+  const int npair = (nr + 1) >> 1;
+  for (int e = threadIdx.x; e < npair * sw; e += blockDim.x) {
+    const int rp = e / sw, xl = e - rp * sw;
+    const int ra = 2 * rp;
+    const bool two = ra + 1 < nr;
+    const int rb = two ? ra + 1 : ra;  // odd band height: the second row repeats the first (not stored)
     const int4 h = hx[xl];
     const int lo = h.x - c0, ng = h.y;
     const uint32_t sh = (uint32_t)(lo & 3);
-    const uint32_t* q0 = (const uint32_t*)(rows + r * pitch) + (lo >> 2);
-    const uint32_t* q1 = (const uint32_t*)((const uint8_t*)q0 + plane_bytes);
-    const uint32_t* q2 = (const uint32_t*)((const uint8_t*)q1 + plane_bytes);
-    int32_t a00 = 0, a01 = 0, a02 = 0, a10 = 0, a11 = 0, a12 = 0, a20 = 0, a21 = 0, a22 = 0;
-    uint32_t l0 = q0[0], l1 = q1[0], l2 = q2[0];
-#pragma unroll 2
+    const uint32_t* qa = (const uint32_t*)(rows + ra * pitch) + (lo >> 2);
+    const uint32_t* qb = (const uint32_t*)(rows + rb * pitch) + (lo >> 2);
+    const int pw = plane_bytes >> 2;  // plane stride in words
+    int32_t acc[2][3][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) acc[i][c][0] = acc[i][c][1] = acc[i][c][2] = 0;
+    uint32_t la[3], lb[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      la[c] = qa[c * pw];
+      lb[c] = qb[c * pw];
+    }
     for (int g = 0; g < ng; ++g) {
       const uint4 dg = hg[g * sw + xl];
-      const uint32_t u0 = q0[g + 1], u1 = q1[g + 1], u2 = q2[g + 1];
-      const int32_t p0 = (int32_t)__builtin_amdgcn_alignbyte(u0, l0, sh);
-      const int32_t p1 = (int32_t)__builtin_amdgcn_alignbyte(u1, l1, sh);
-      const int32_t p2 = (int32_t)__builtin_amdgcn_alignbyte(u2, l2, sh);
-      a00 = __builtin_amdgcn_sdot4(p0, (int32_t)dg.x, a00, false);
-      a01 = __builtin_amdgcn_sdot4(p0, (int32_t)dg.y, a01, false);
-      a02 = __builtin_amdgcn_sdot4(p0, (int32_t)dg.z, a02, false);
-      a10 = __builtin_amdgcn_sdot4(p1, (int32_t)dg.x, a10, false);
-      a11 = __builtin_amdgcn_sdot4(p1, (int32_t)dg.y, a11, false);
-      a12 = __builtin_amdgcn_sdot4(p1, (int32_t)dg.z, a12, false);
-      a20 = __builtin_amdgcn_sdot4(p2, (int32_t)dg.x, a20, false);
-      a21 = __builtin_amdgcn_sdot4(p2, (int32_t)dg.y, a21, false);
-      a22 = __builtin_amdgcn_sdot4(p2, (int32_t)dg.z, a22, false);
-      l0 = u0;
-      l1 = u1;
-      l2 = u2;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint32_t ua = qa[c * pw + g + 1], ub = qb[c * pw + g + 1];
+        const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(ua, la[c], sh);
+        const int32_t pb = (int32_t)__builtin_amdgcn_alignbyte(ub, lb[c], sh);
+        acc[0][c][0] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.x, acc[0][c][0], false);
+        acc[0][c][1] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.y, acc[0][c][1], false);
+        acc[0][c][2] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.z, acc[0][c][2], false);
+        acc[1][c][0] = __builtin_amdgcn_sdot4(pb, (int32_t)dg.x, acc[1][c][0], false);
+        acc[1][c][1] = __builtin_amdgcn_sdot4(pb, (int32_t)dg.y, acc[1][c][1], false);
+        acc[1][c][2] = __builtin_amdgcn_sdot4(pb, (int32_t)dg.z, acc[1][c][2], false);
+        la[c] = ua;
+        lb[c] = ub;
+      }
     }
-    const int64_t o = (int64_t)(r0 + r) * S + x0 + xl;
     // int32 wrap-around is harmless: the true sum (Pillow's int32 ss) fits in int32
-    tmp[o] = clip8_acc((int32_t)((uint32_t)a00 + ((uint32_t)a01 << 8) + ((uint32_t)a02 << 16) + (uint32_t)h.z));
-    tmp[cpl + o] = clip8_acc((int32_t)((uint32_t)a10 + ((uint32_t)a11 << 8) + ((uint32_t)a12 << 16) + (uint32_t)h.z));
-    tmp[2 * cpl + o] =
-        clip8_acc((int32_t)((uint32_t)a20 + ((uint32_t)a21 << 8) + ((uint32_t)a22 << 16) + (uint32_t)h.z));
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && !two) break;
+      const int64_t o = (int64_t)(r0 + ra + i) * S + x0 + xl;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        tmp[c * cpl + o] = clip8_acc((int32_t)((uint32_t)acc[i][c][0] + ((uint32_t)acc[i][c][1] << 8) +
+                                               ((uint32_t)acc[i][c][2] << 16) + (uint32_t)h.z));
+    }
   }
 }
 
