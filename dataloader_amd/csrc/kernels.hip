@@ -1408,7 +1408,8 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
         for (int c = 0; c < 3; ++c) {
           const uint8_t* q = htmp + c * cpl + (int64_t)ymin * S + 4 * xq;
           int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0, a3 = a0;
-          for (int t = 0; t < ycnt; ++t) {
+#pragma unroll 4
+          for (int t = 0; t < ycnt; ++t) {  // unrolled: four row loads in flight per wait
             const uint32_t u = *(const uint32_t*)(q + (int64_t)t * S);
             const int32_t kk = k[t];
             a0 += (int32_t)(u & 255u) * kk;
