@@ -851,17 +851,28 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
   int32_t* dcd = (int32_t*)(ws + d.dcd_off);
   const int per = (T + kDcScanThreads - 1) / kDcScanThreads;
   const int b0 = min(T, threadIdx.x * per), b1 = min(T, b0 + per);
+  // block-in-MCU position tracked incrementally (no per-block modulo); loops unrolled
+  // so that several DC loads are in flight per wait
+  const int pos0 = b0 % bpm;
   int32_t s[kMaxComp] = {0, 0, 0};
-  for (int b = b0; b < b1; ++b) add3(s, (int)((mc >> (2 * (b % bpm))) & 3u), dcd[b]);
+  int pos = pos0;
+#pragma unroll 4
+  for (int b = b0; b < b1; ++b) {
+    add3(s, (int)((mc >> (2 * pos)) & 3u), dcd[b]);
+    pos = pos + 1 == bpm ? 0 : pos + 1;
+  }
   uint32_t tot;
   int32_t pfx[kMaxComp];
   pfx[0] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[0], s_wave, &tot);
   pfx[1] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[1], s_wave, &tot);
   pfx[2] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[2], s_wave, &tot);
+  pos = pos0;
+#pragma unroll 4
   for (int b = b0; b < b1; ++b) {
-    const int c = (int)((mc >> (2 * (b % bpm))) & 3u);
+    const int c = (int)((mc >> (2 * pos)) & 3u);
     add3(pfx, c, dcd[b]);
     dcd[b] = (int32_t)(int16_t)get3(pfx, c);  // in place: JCOEF (int16) DC, as libjpeg stores it
+    pos = pos + 1 == bpm ? 0 : pos + 1;
   }
 }
 
@@ -1018,10 +1029,12 @@ __global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc,
   uint32_t* rgb = (uint32_t*)(ws + d.rgb_off);
   const int W = d.width;
   const int64_t npx = (int64_t)W * d.height;
-  const int64_t nq = (npx + 3) >> 2;
+  const int64_t nq = (npx + 3) >> 2;  // npx < 2^31 (max_image_dim <= 16384 is enforced by k_parse limits)
+#pragma unroll 2
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i0 = q * 4;
-    int y = (int)(i0 / W), x = (int)(i0 - (int64_t)y * W);
+    const uint32_t iu = (uint32_t)i0;
+    int y = (int)(iu / (uint32_t)W), x = (int)(iu - (uint32_t)y * (uint32_t)W);  // 32-bit division
     union {
       uint8_t b[12];
       uint32_t w[3];
