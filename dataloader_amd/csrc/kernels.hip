@@ -912,31 +912,55 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   }
   const int grp = threadIdx.x >> 3, l = threadIdx.x & 7;
   int32_t* sb = s_blk[grp];
-  for (int64_t g0 = (int64_t)blockIdx.x * kIdctBlocksPerWg; g0 < tot; g0 += (int64_t)gridDim.x * kIdctBlocksPerWg) {
-    const int64_t g = g0 + grp;
-    const bool valid = g < tot;
-    const int64_t gg = valid ? g : 0;
-    const int c = gg < nb0 ? 0 : (gg < nb0 + nb1 ? 1 : 2);
-    const int64_t k = gg - (c == 0 ? 0 : (c == 1 ? nb0 : nb0 + nb1));
-    const CompDesc& cd = d.comp[c];
-    const int by = (int)(k / cd.bw), bx = (int)(k - (int64_t)by * cd.bw);
-    // decode-order index of plane block (bx, by); a plane block no MCU covers stays all zero
-    int64_t b;
+  // plane block g -> component, position and decode-order index (32-bit: a plane has < 2^31 blocks);
+  // a plane block no MCU covers has b = -1 and stays all zero
+  struct Blk {
+    int c, bx, by, b;
+  };
+  auto locate = [&](int g) {
+    Blk r;
+    r.c = g < nb0 ? 0 : (g < nb0 + nb1 ? 1 : 2);
+    const int k = g - (r.c == 0 ? 0 : (r.c == 1 ? (int)nb0 : (int)(nb0 + nb1)));
+    const CompDesc& cd = d.comp[r.c];
+    r.by = k / cd.bw;
+    r.bx = k - r.by * cd.bw;
     if (ncomp == 1) {
-      b = bx < d.mcus_x ? (int64_t)by * d.mcus_x + bx : -1;
+      r.b = r.bx < d.mcus_x ? r.by * d.mcus_x + r.bx : -1;
     } else {
-      const int mo = c == 0 ? moff[0] : (c == 1 ? moff[1] : moff[2]);
-      b = ((int64_t)(by / cd.v) * d.mcus_x + bx / cd.h) * d.blocks_per_mcu + mo + (by % cd.v) * cd.h + bx % cd.h;
+      const int mo = r.c == 0 ? moff[0] : (r.c == 1 ? moff[1] : moff[2]);
+      const int my = r.by / cd.v, mx = r.bx / cd.h;
+      r.b = (my * d.mcus_x + mx) * d.blocks_per_mcu + mo + (r.by - my * cd.v) * cd.h + (r.bx - mx * cd.h);
     }
-    uint2 bi = make_uint2(0u, 0u);
-    int32_t dc = 0;
-    if (valid && b >= 0 && b < d.total_blocks) {
-      bi = binfo[b];
-      dc = dcv[b];
-    }
+    return r;
+  };
+  const int T = (int)tot, step = gridDim.x * kIdctBlocksPerWg;
+  // the next iteration's block info and DC are loaded one iteration ahead
+  int gn = blockIdx.x * kIdctBlocksPerWg + grp;
+  Blk nx = locate(gn < T ? gn : 0);
+  uint2 bin = make_uint2(0u, 0u);
+  int32_t dcn = 0;
+  if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) {
+    bin = binfo[nx.b];
+    dcn = dcv[nx.b];
+  }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
-    __syncthreads();
+  for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
+  __syncthreads();
+  for (int g0 = blockIdx.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
+    const bool valid = gn < T;
+    const Blk cur = nx;
+    const uint2 bi = bin;
+    const int32_t dc = dcn;
+    gn += step;
+    if (gn < T) {  // prefetch the next block's record while this one is transformed
+      nx = locate(gn);
+      bin = make_uint2(0u, 0u);
+      dcn = 0;
+      if (nx.b >= 0 && nx.b < d.total_blocks) {
+        bin = binfo[nx.b];
+        dcn = dcv[nx.b];
+      }
+    }
     if (valid) {
       if (l == 0) sb[0] = dc;
       for (uint32_t j = l; j < bi.y; j += 8) {
@@ -945,6 +969,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
       }
     }
     __syncthreads();
+    const CompDesc& cd = d.comp[cur.c];
     if (valid) {  // dequantize + pass 1 on column l (reads and writes only this lane's column)
       const uint16_t* q = d.qt[cd.tq];
       int32_t col[8], wcol[8];
@@ -955,17 +980,19 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
       for (int r = 0; r < 8; ++r) sb[r * 8 + l] = wcol[r];
     }
     __syncthreads();
-    if (valid) {  // pass 2 on row l
+    if (valid) {  // pass 2 on row l, then the row is cleared for the next block
       int32_t row[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) row[j] = sb[l * 8 + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
       union {
         uint8_t b[8];
         uint64_t u;
       } o;
       idct_pass2(row, o.b);
       const int pitch = cd.bw * 8;
-      *(uint64_t*)(planes + cd.plane_off + ((int64_t)by * 8 + l) * pitch + bx * 8) = o.u;
+      *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = o.u;
     }
     __syncthreads();
   }
