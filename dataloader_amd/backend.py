@@ -162,8 +162,19 @@ class MI355XBackend:
         return InProcessShardCache(job_id, node_master, max_gb, prefetch_window, timeout_s, warn_threshold)
 
     def build_pipeline(self, source: Any, aug_spec: Any, pipeline_cfg: Any, specs: Any = None) -> MI355XAugPipeline:
-        if not _is_dinov2_spec(aug_spec):
-            raise TypeError(f"MI355XBackend: unsupported aug_spec type {type(aug_spec).__name__}.")
+        """Dispatch as CPUBackend.build_pipeline (cpu.py:649-709): DinoV2 multi-crop, LeJEPA
+        (context + targets) and Eval (resize + centre crop) run on the same kernels with their
+        own view recipe; UserAugSpec (a Python aug_fn on decoded tensors) is not offered."""
+        kind = type(aug_spec).__name__
+        if _is_dinov2_spec(aug_spec):
+            aug_cfg = aug_spec.aug_cfg
+            names = None
+        elif kind in ("LeJEPAAugSpec", "EvalAugSpec"):
+            from .config import recipe_aug_config
+            aug_cfg = recipe_aug_config(aug_spec)
+            names = list(aug_spec.output_map)
+        else:
+            raise TypeError(f"MI355XBackend: unsupported aug_spec type {kind}.")
         out = pipeline_cfg.output_dtype
         if getattr(pipeline_cfg, "dali_fp8_output", False) or getattr(aug_spec, "fp8_output", False):
             out = "fp8"
@@ -171,20 +182,21 @@ class MI355XBackend:
         if getattr(pipeline_cfg, "fuse_normalization", False) and specs is not None:
             # per-dataset mean/std as DALIBackend wires NormSource (dali_backend.py:142-153)
             from .norm import NormTable
-            norm = NormTable(aug_spec.aug_cfg, specs)
+            norm = NormTable(aug_cfg, specs)
             if hasattr(source, "register_dataset_index_callback"):
                 source.register_dataset_index_callback(norm.set_dataset_indices)
         return MI355XAugPipeline(
             source=source,
-            aug_cfg=aug_spec.aug_cfg,
+            aug_cfg=aug_cfg,
             batch_size=getattr(source, "_batch_size", 1),
-            resolution_src=getattr(source, "_resolution_src", None),
+            resolution_src=getattr(source, "_resolution_src", None) if names is None else None,
             seed=pipeline_cfg.seed,
             out_dtype=out,
             device=pipeline_cfg.device_id,
             max_image_dim=self._max_image_dim,
             workspace_bytes=self._workspace_bytes,
             norm=norm,
+            view_names=names,
         )
 
     def build_pipeline_iterator(self, pipeline: Any, aug_spec: Any, output_map: list[str],

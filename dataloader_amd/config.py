@@ -142,3 +142,97 @@ class ResolutionSource:
     def __call__(self):
         with self._lock:
             return np.array(self._g, dtype=np.int32), np.array(self._l, dtype=np.int32)
+
+
+@dataclass
+class EvalAugSpec:
+    """Reference ``EvalAugSpec`` (augmentation.py:290-334): resize shorter side + centre crop."""
+
+    crop_size: int = 224
+    mean: tuple = (0.485, 0.456, 0.406)
+    std: tuple = (0.229, 0.224, 0.225)
+    interpolation: str = "bicubic"
+
+    @property
+    def output_map(self) -> list[str]:
+        return ["view_0"]
+
+    @property
+    def norm_stats(self) -> NormStats:
+        return NormStats(mean=self.mean, std=self.std)
+
+    @property
+    def initial_global_size(self) -> int:
+        return self.crop_size
+
+    @property
+    def initial_local_size(self) -> int:
+        return self.crop_size
+
+    @property
+    def supports_masking(self) -> bool:
+        return False
+
+
+@dataclass
+class LeJEPAAugSpec:
+    """Reference ``LeJEPAAugSpec`` (augmentation.py:336-399): one context crop + N target crops."""
+
+    context_crop_size: int = 224
+    target_crop_size: int = 96
+    n_target_views: int = 4
+    context_scale: tuple = (0.85, 1.0)
+    target_scale: tuple = (0.15, 0.30)
+    mean: tuple = (0.485, 0.456, 0.406)
+    std: tuple = (0.229, 0.224, 0.225)
+
+    @property
+    def output_map(self) -> list[str]:
+        return ["context", *[f"target_{i}" for i in range(self.n_target_views)]]
+
+    @property
+    def norm_stats(self) -> NormStats:
+        return NormStats(mean=self.mean, std=self.std)
+
+    @property
+    def initial_global_size(self) -> int:
+        return self.context_crop_size
+
+    @property
+    def initial_local_size(self) -> int:
+        return self.target_crop_size
+
+    @property
+    def supports_masking(self) -> bool:
+        return False
+
+
+def recipe_aug_config(spec: Any) -> DINOAugConfig:
+    """The view recipe of an Eval / LeJEPA spec as a ``DINOAugConfig`` + ``recipe`` code
+    (``DINO_RECIPE_*``), so that the same kernels and sampler serve every spec:
+
+    * LeJEPA (reference cpu.py:447-459): view 0 = context, RandomResizedCrop(context_crop_size,
+      context_scale) + ``_color_jitter(ctx, 0.8, 0.8, 0.8, 0.2, 0.8)`` + flip(0.5); views 1..N =
+      RandomResizedCrop(target_crop_size, target_scale) only;
+    * Eval (reference cpu.py:400-411): one view, resize shorter side to int(S * 256 / 224)
+      (BICUBIC) then centre crop S.
+    """
+    from .params import RECIPE_EVAL, RECIPE_LEJEPA
+    kind = type(spec).__name__
+    if kind == "LeJEPAAugSpec":
+        cfg = DINOAugConfig(global_crop_size=spec.context_crop_size, local_crop_size=spec.target_crop_size,
+                            n_global_crops=1, n_local_crops=spec.n_target_views,
+                            global_crops_scale=tuple(spec.context_scale), local_crops_scale=tuple(spec.target_scale),
+                            blur_prob_global1=0.0, blur_prob_global2=0.0, blur_prob_local=0.0, solarize_prob=0.0,
+                            color_jitter_prob=0.8, grayscale_prob=0.0, brightness=0.8, contrast=0.8, saturation=0.8,
+                            hue=0.2, flip_prob=0.5, mean=tuple(spec.mean), std=tuple(spec.std))
+        cfg.recipe = RECIPE_LEJEPA
+        return cfg
+    if kind == "EvalAugSpec":
+        cfg = DINOAugConfig(global_crop_size=spec.crop_size, local_crop_size=spec.crop_size, n_global_crops=1,
+                            n_local_crops=0, blur_prob_global1=0.0, blur_prob_global2=0.0, blur_prob_local=0.0,
+                            solarize_prob=0.0, color_jitter_prob=0.0, grayscale_prob=0.0, flip_prob=0.0,
+                            mean=tuple(spec.mean), std=tuple(spec.std))
+        cfg.recipe = RECIPE_EVAL
+        return cfg
+    raise TypeError(f"no view recipe for {kind}")

@@ -141,6 +141,8 @@ static int check_cfg(const dino_ctx* c, const dino_aug_config* cfg) {
     return fail(DINO_EINVAL, "crop size outside (4, max_crop_size]%s%lld");
   if (cfg->out_dtype < DINO_OUT_BF16 || cfg->out_dtype > DINO_OUT_FP8_E4M3)
     return fail(DINO_EINVAL, "unknown out_dtype %s%lld", "", cfg->out_dtype);
+  if (cfg->recipe < DINO_RECIPE_DINOV2 || cfg->recipe > DINO_RECIPE_EVAL)
+    return fail(DINO_EINVAL, "unknown recipe %s%lld", "", cfg->recipe);
   return DINO_OK;
 }
 

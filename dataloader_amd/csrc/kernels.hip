@@ -1129,10 +1129,14 @@ __device__ __forceinline__ int64_t hdot_table_bytes(int S, int kh) {
   return kh ? (int64_t)S * 16 * (1 + (kh + 3) / 4) : 0;
 }
 
+// Resample target of a view's crop box (0 in the record means the view size S).
+__device__ __forceinline__ int view_rw(const dino_view_params& p) { return p.resize_w > 0 ? p.resize_w : p.out_size; }
+__device__ __forceinline__ int view_rh(const dino_view_params& p) { return p.resize_h > 0 ? p.resize_h : p.out_size; }
+
 __device__ void view_sizes(const dino_view_params& p, int ok, int64_t* htmp, int64_t* rcoef, int32_t* kh, int32_t* kv) {
   const int S = p.out_size;
-  *kh = ok && p.crop_w != S ? resample_ksize(p.crop_w, S) : 0;
-  *kv = ok && p.crop_h != S ? resample_ksize(p.crop_h, S) : 0;
+  *kh = ok && p.crop_w != view_rw(p) ? resample_ksize(p.crop_w, view_rw(p)) : 0;
+  *kv = ok && p.crop_h != view_rh(p) ? resample_ksize(p.crop_h, view_rh(p)) : 0;
   *htmp = (*kh) ? align16((int64_t)p.crop_h * S * 3) : 0;
   *rcoef = ok ? align16((int64_t)S * (4 + *kh + *kv) * 4) + hdot_table_bytes(S, *kh) : 0;
 }
@@ -1146,6 +1150,12 @@ __device__ bool params_valid(const dino_view_params& p, const ImgDesc& d, int S)
     return false;  // torch reflect padding needs pad < S
   for (int k = 0; k < 4; ++k)
     if (p.order[k] > 3) return false;
+  // window of the resampled box: inside it, and an axis that is not resampled has no window
+  const int rw = view_rw(p), rh = view_rh(p);
+  if (rw < S || rh < S || rw > 65536 || rh > 65536 || p.out_x < 0 || p.out_y < 0) return false;
+  if (p.out_x + S > rw || p.out_y + S > rh) return false;
+  if (p.crop_w == rw && (rw != S || p.out_x != 0)) return false;
+  if (p.crop_h == rh && (rh != S || p.out_y != 0)) return false;
   return true;
 }
 
@@ -1214,7 +1224,7 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
   for (int x = threadIdx.x; x < S; x += blockDim.x) {
     if (vp.kh) {
       int32_t* k = ht + (int64_t)x * vp.kh;
-      resample_coeffs_one(p.crop_w, S, x, vp.kh, &hb[2 * x], &hb[2 * x + 1], k);
+      resample_coeffs_one(p.crop_w, view_rw(p), p.out_x + x, vp.kh, &hb[2 * x], &hb[2 * x + 1], k);
       // sum_t p_t k_t = sum_t (p_t - 128) k_t + 128 sum_t k_t, and k_t = D0 + 256 D1 + 65536 D2
       // with signed digits D in [-128, 127] (exact for |k| < 2^23 - 2^15; normalised bicubic
       // taps stay below 1.1 x 2^22): three v_dot4 products per 4 taps
@@ -1238,7 +1248,8 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
       }
       hx[x] = make_int4(hb[2 * x], ng, 128 * ksum + (1 << (kPrecisionBits - 1)), 0);
     }
-    if (vp.kv) resample_coeffs_one(p.crop_h, S, x, vp.kv, &vb[2 * x], &vb[2 * x + 1], vt + (int64_t)x * vp.kv);
+    if (vp.kv)
+      resample_coeffs_one(p.crop_h, view_rh(p), p.out_y + x, vp.kv, &vb[2 * x], &vb[2 * x + 1], vt + (int64_t)x * vp.kv);
   }
 }
 

@@ -159,6 +159,58 @@ DHD void sample_view(const dino_aug_config& cfg, uint64_t seed, uint64_t batch_i
   p.solarize = (sol_p > 0.0f) && su < (double)sol_p;
   p.pad0[0] = p.pad0[1] = p.pad0[2] = 0;
   p.pad1 = ok ? 0 : 1;
+  p.resize_w = p.resize_h = 0;
+  p.out_x = p.out_y = 0;
+  if (cfg.recipe == DINO_RECIPE_LEJEPA) {
+    // CPULeJEPAPipeline (cpu.py:447-459): the context view keeps RRC + ColorJitter (with
+    // probability color_jitter_prob) + flip; targets are RRC only; no grayscale, blur, solarize
+    p.gray = 0;
+    p.blur = 0;
+    p.sigma = 1.0;
+    p.ksize = 3;
+    p.solarize = 0;
+    if (!global) {
+      p.flip = 0;
+      p.jitter = 0;
+    }
+  } else if (cfg.recipe == DINO_RECIPE_EVAL) {
+    // CPUEvalPipeline (cpu.py:400-411): Resize(int(S * 256 / 224)) of the shorter side, then
+    // CenterCrop(S); deterministic.  The crop box is the whole image, resampled to the
+    // torchvision output size, and the view is the centred window of it.
+    const int S = p.out_size;
+    const int size = (int)((double)S * 256.0 / 224.0);
+    int nw, nh;
+    if (W <= H) {
+      nw = size;
+      nh = (int)((double)size * (double)H / (double)W);
+    } else {
+      nw = (int)((double)size * (double)W / (double)H);
+      nh = size;
+    }
+    p.flip = p.jitter = p.gray = p.blur = p.solarize = 0;
+    p.sigma = 1.0;
+    p.ksize = 3;
+    p.crop_top = p.crop_left = 0;
+    p.crop_w = W;
+    p.crop_h = H;
+    p.resize_w = nw;
+    p.resize_h = nh;
+    p.out_x = (int)py_round((double)(nw - S) / 2.0);
+    p.out_y = (int)py_round((double)(nh - S) / 2.0);
+    // an axis that is not resampled is a plain crop: fold its window into the crop box
+    if (nw == W) {
+      p.crop_left = p.out_x;
+      p.crop_w = S;
+      p.resize_w = S;
+      p.out_x = 0;
+    }
+    if (nh == H) {
+      p.crop_top = p.out_y;
+      p.crop_h = S;
+      p.resize_h = S;
+      p.out_y = 0;
+    }
+  }
   if (!p.jitter) {
     p.brightness = p.contrast = p.saturation = 1.0f;
     p.hue = 0.0f;

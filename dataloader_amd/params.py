@@ -1,6 +1,6 @@
 """Host mirrors of the C ABI structs in ``include/dino_ingest.h``.
 
-``VIEW_PARAMS_DTYPE`` is the numpy layout of ``dino_view_params`` (64 bytes):
+``VIEW_PARAMS_DTYPE`` is the numpy layout of ``dino_view_params`` (80 bytes):
 every random decision ``_augment_one`` makes for one (sample, view)
 (reference ``src/dino_loader/backends/cpu.py:172-267``).  Records are stored
 sample-major: ``params[b * n_views + v]``.
@@ -21,8 +21,11 @@ VIEW_PARAMS_DTYPE = np.dtype([
     ("brightness", "<f4"), ("contrast", "<f4"), ("saturation", "<f4"), ("hue", "<f4"),
     ("sigma", "<f8"),
     ("ksize", "<i4"), ("pad1", "<i4"),
+    ("resize_w", "<i4"), ("resize_h", "<i4"), ("out_x", "<i4"), ("out_y", "<i4"),
 ])
-assert VIEW_PARAMS_DTYPE.itemsize == 64
+assert VIEW_PARAMS_DTYPE.itemsize == 80
+RECORD_BYTES = VIEW_PARAMS_DTYPE.itemsize
+RECIPE_DINOV2, RECIPE_LEJEPA, RECIPE_EVAL = 0, 1, 2
 
 OUT_BF16, OUT_FP32, OUT_FP8_E4M3 = 0, 1, 2
 
@@ -50,13 +53,15 @@ class DinoAugConfig(ctypes.Structure):
         ("brightness", ctypes.c_float), ("contrast", ctypes.c_float),
         ("saturation", ctypes.c_float), ("hue", ctypes.c_float),
         ("mean", ctypes.c_float * 3), ("std", ctypes.c_float * 3),
-        ("out_dtype", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("out_dtype", ctypes.c_int32), ("recipe", ctypes.c_int32),
     ]
 
 
 def make_aug_config(aug_cfg, global_size: int, local_size: int, out_dtype: int) -> DinoAugConfig:
-    """Build the C struct from a ``DINOAugConfig``-shaped object (reference config.py:243-272)."""
+    """Build the C struct from a ``DINOAugConfig``-shaped object (reference config.py:243-272);
+    ``aug_cfg.recipe`` (default DINOv2) selects the view recipe (``DINO_RECIPE_*``)."""
     c = DinoAugConfig()
+    c.recipe = int(getattr(aug_cfg, "recipe", RECIPE_DINOV2))
     c.n_global = int(aug_cfg.n_global_crops)
     c.n_local = int(aug_cfg.n_local_crops)
     c.global_size = int(global_size)

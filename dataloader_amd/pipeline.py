@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from .engine import IngestEngine, pack_jpegs, params_from_device
-from .params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, make_aug_config
+from .params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, RECORD_BYTES, make_aug_config
 
 _DTYPES = {"bf16": OUT_BF16, "fp32": OUT_FP32, "fp8": OUT_FP8_E4M3}
 
@@ -60,7 +60,8 @@ class MI355XAugPipeline:
 
     def __init__(self, source: Any, aug_cfg, batch_size: int, resolution_src=None, seed: int = 0,
                  out_dtype="bf16", device: int = 0, max_image_dim: int = 8192, workspace_bytes: int = 0,
-                 engine: IngestEngine | None = None, depth: int = 1, norm=None):
+                 engine: IngestEngine | None = None, depth: int = 1, norm=None,
+                 view_names: list[str] | None = None):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -68,6 +69,7 @@ class MI355XAugPipeline:
         self._out = _out_code(out_dtype)
         self._seed = int(seed)
         self._norm = norm  # NormTable (per-dataset statistics) or None: global mean/std
+        self._names = list(view_names) if view_names else [f"view_{i}" for i in range(aug_cfg.n_views)]
         self._batch_index = 0
         self.depth = max(1, int(depth))
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
@@ -138,9 +140,10 @@ class MI355XAugPipeline:
         g, l = self._sizes()
         cfg = self._cfg(g, l)
         eng = sl.engine
-        if sl.params is None or sl.params.numel() < batch * self._aug_cfg.n_views * 64:
+        if sl.params is None or sl.params.numel() < batch * self._aug_cfg.n_views * RECORD_BYTES:
             with eng.on_stream():
-                sl.params = torch.empty(batch * self._aug_cfg.n_views * 64, dtype=torch.uint8, device=self.device)
+                sl.params = torch.empty(batch * self._aug_cfg.n_views * RECORD_BYTES, dtype=torch.uint8,
+                                        device=self.device)
         if self._norm is not None:  # per-dataset statistics of this batch's images (DALI NormSource)
             recs = torch.from_numpy(self._norm.batch_records(batch)).pin_memory()
             with eng.on_stream():
@@ -149,7 +152,7 @@ class MI355XAugPipeline:
         views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
                                     views=views, params_out=sl.params)
         sl.info = info
-        sl.outputs = {f"view_{i}": v for i, v in enumerate(views)}
+        sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
         if eng.stream is not None:
             sl.event = torch.cuda.Event()
             sl.event.record(eng.stream)
@@ -226,7 +229,7 @@ class MI355XAugPipeline:
         if sl.event is not None:
             sl.event.synchronize()
         n = sl.engine.last_batch * self._aug_cfg.n_views
-        return params_from_device(sl.params[: n * 64])
+        return params_from_device(sl.params[: n * RECORD_BYTES])
 
     def last_status(self) -> np.ndarray:
         sl = self._last

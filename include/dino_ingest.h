@@ -82,11 +82,26 @@ typedef struct dino_aug_config {
   float brightness, contrast, saturation, hue;
   float mean[3], std[3];
   int32_t out_dtype;           /* DINO_OUT_* */
-  int32_t reserved;
+  int32_t recipe;              /* DINO_RECIPE_*: how dino_sample_params draws the views */
 } dino_aug_config;
 
+/* View recipes of dino_sample_params (reference backends/cpu.py):
+ *  DINOV2  n_global + n_local multi-crop (CPUAugPipeline, cpu.py:309-367);
+ *  LEJEPA  view 0 = context: RandomResizedCrop(global_size, global_scale), ColorJitter with
+ *          probability color_jitter_prob, flip with probability flip_prob; views 1.. =
+ *          targets: RandomResizedCrop(local_size, local_scale) only (CPULeJEPAPipeline,
+ *          cpu.py:421-461);
+ *  EVAL    one view: Resize(shorter side -> int(global_size * 256 / 224), BICUBIC) then
+ *          CenterCrop(global_size) (CPUEvalPipeline, cpu.py:380-413). */
+#define DINO_RECIPE_DINOV2 0
+#define DINO_RECIPE_LEJEPA 1
+#define DINO_RECIPE_EVAL 2
+
 /* Every random decision of one (sample, view) — reference cpu.py:172-267.
- * 64 bytes, layout shared with dataloader_amd/params.py (numpy dtype). */
+ * 80 bytes, layout shared with dataloader_amd/params.py (numpy dtype).
+ * Geometry: the view is the window [out_x, out_x + S) x [out_y, out_y + S) of the
+ * crop box resized (Pillow BICUBIC) to resize_w x resize_h; resize_w/h = 0 mean S
+ * (RandomResizedCrop), a window needs the crop box itself to be resampled. */
 typedef struct dino_view_params {
   int32_t crop_top, crop_left, crop_h, crop_w;   /* RandomResizedCrop (i, j, h, w) */
   int32_t out_size;                              /* S */
@@ -97,6 +112,8 @@ typedef struct dino_view_params {
   double sigma;                                  /* blur sigma */
   int32_t ksize;                                 /* blur kernel size */
   int32_t pad1;
+  int32_t resize_w, resize_h;                    /* resample target of the crop box (0 -> S) */
+  int32_t out_x, out_y;                          /* view window inside the resampled box */
 } dino_view_params;
 
 /* Library / context */

@@ -9,6 +9,10 @@ Follows, op for op, reference ``src/dino_loader/backends/cpu.py``:
 * ``_to_tensor_normalized``  cpu.py:223-232  -> :func:`to_tensor_normalized`
 * ``CPUAugPipeline.run_one_batch`` view-param table cpu.py:325-341 -> :func:`view_table`,
   stacking cpu.py:362-367 -> :func:`run_batch`
+* ``CPUEvalPipeline.run_one_batch`` cpu.py:395-413 (``_resize_shorter`` cpu.py:190-191,
+  ``_center_crop`` cpu.py:186-187) -> :func:`eval_one`, :func:`eval_geometry`
+* ``CPULeJEPAPipeline.run_one_batch`` cpu.py:435-461 -> :func:`lejepa_one` (views replayed
+  from their :class:`ViewParams`, as the multi-crop ones)
 
 The reference draws every random quantity from process-global RNGs inside the
 ops (torch global RNG for RandomResizedCrop/ColorJitter, Python ``random`` for
@@ -66,6 +70,10 @@ class ViewParams:
     sigma: float = 1.0
     ksize: int = 3
     solarize: bool = False
+    resize_w: int = 0        # resample target of the crop box (0 -> out_size)
+    resize_h: int = 0
+    out_x: int = 0           # view window inside the resampled box
+    out_y: int = 0
 
 
 @dataclass
@@ -256,9 +264,49 @@ def to_tensor_normalized(img: Image.Image, mean=IMAGENET_MEAN, std=IMAGENET_STD,
 # The per-view op chain (cpu.py:235-267)
 # ---------------------------------------------------------------------------
 
+def eval_geometry(w: int, h: int, crop_size: int) -> tuple[int, int, int, int]:
+    """(new_w, new_h, left, top) of CPUEvalPipeline: torchvision ``Resize(int(crop * 256 / 224))``
+    of the shorter side (``_compute_resized_output_size``: long side = int(size * long / short)),
+    then ``CenterCrop`` offsets ``int(round((dim - crop) / 2.0))`` (torchvision F.center_crop)."""
+    size = int(crop_size * 256 / 224)
+    if w <= h:
+        new_w, new_h = size, int(size * h / w)
+    else:
+        new_w, new_h = int(size * w / h), size
+    return new_w, new_h, int(round((new_w - crop_size) / 2.0)), int(round((new_h - crop_size) / 2.0))
+
+
+def eval_one(jpeg_bytes: bytes, crop_size: int, mean=IMAGENET_MEAN, std=IMAGENET_STD,
+             out_dtype=torch.bfloat16, decoded: Image.Image | None = None) -> torch.Tensor:
+    """CPUEvalPipeline for one sample (cpu.py:405-411): decode, resize shorter side (BICUBIC),
+    centre crop, normalise; undecodable -> zeros."""
+    img = decoded if decoded is not None else decode_rgb(jpeg_bytes)
+    if img is None:
+        return torch.zeros(3, crop_size, crop_size, dtype=out_dtype)
+    new_w, new_h, left, top = eval_geometry(img.size[0], img.size[1], crop_size)
+    img = img.resize((new_w, new_h), Image.BICUBIC)
+    img = img.crop((left, top, left + crop_size, top + crop_size))
+    return to_tensor_normalized(img, mean, std, out_dtype)
+
+
+def lejepa_one(jpeg_bytes: bytes, params: list, mean=IMAGENET_MEAN, std=IMAGENET_STD,
+               out_dtype=torch.bfloat16, decoded: Image.Image | None = None) -> list[torch.Tensor]:
+    """CPULeJEPAPipeline for one sample (cpu.py:447-459), with its draws as records:
+    context = RRC + ColorJitter + flip (flip commutes with the per-pixel jitter ops),
+    targets = RRC only."""
+    img = decoded if decoded is not None else decode_rgb(jpeg_bytes)
+    return [augment_one(jpeg_bytes, p, mean, std, out_dtype, decoded=img) for p in params]
+
+
 def augment_image(img: Image.Image, p: ViewParams) -> Image.Image:
     """All uint8 stages of ``_augment_one`` after decode, with explicit params."""
-    img = resized_crop(img, p.crop_top, p.crop_left, p.crop_h, p.crop_w, p.out_size)
+    if p.resize_w:  # a window of the resampled crop box (Eval: resize shorter side + centre crop)
+        img = img.crop((p.crop_left, p.crop_top, p.crop_left + p.crop_w, p.crop_top + p.crop_h))
+        if (p.resize_w, p.resize_h) != img.size:
+            img = img.resize((p.resize_w, p.resize_h), Image.BICUBIC)
+        img = img.crop((p.out_x, p.out_y, p.out_x + p.out_size, p.out_y + p.out_size))
+    else:
+        img = resized_crop(img, p.crop_top, p.crop_left, p.crop_h, p.crop_w, p.out_size)
     if p.flip:
         img = img.transpose(Image.FLIP_LEFT_RIGHT)
     if p.jitter:

@@ -25,7 +25,8 @@ def record_to_params(rec) -> ViewParams:
         brightness=float(rec["brightness"]), contrast=float(rec["contrast"]),
         saturation=float(rec["saturation"]), hue=float(rec["hue"]), gray=bool(rec["gray"]),
         blur=bool(rec["blur"]), sigma=float(rec["sigma"]), ksize=int(rec["ksize"]),
-        solarize=bool(rec["solarize"]))
+        solarize=bool(rec["solarize"]), resize_w=int(rec["resize_w"]), resize_h=int(rec["resize_h"]),
+        out_x=int(rec["out_x"]), out_y=int(rec["out_y"]))
 
 
 def params_to_record(p: ViewParams) -> np.ndarray:
@@ -36,6 +37,7 @@ def params_to_record(p: ViewParams) -> np.ndarray:
     r["order"] = np.asarray(p.order, np.uint8)
     r["brightness"], r["contrast"], r["saturation"], r["hue"] = p.brightness, p.contrast, p.saturation, p.hue
     r["sigma"], r["ksize"] = p.sigma, p.ksize
+    r["resize_w"], r["resize_h"], r["out_x"], r["out_y"] = p.resize_w, p.resize_h, p.out_x, p.out_y
     return r
 
 

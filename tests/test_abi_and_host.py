@@ -81,11 +81,11 @@ def test_backend_protocol_surface():
     env = be.init_distributed(rank=2, world_size=8, local_rank=2, local_world_size=8)
     assert (env.rank, env.world_size, env.topology.is_nvl72) == (2, 8, False)
 
-    class EvalAugSpec:  # unsupported spec types raise TypeError like CPUBackend (cpu.py:708-709)
+    class CustomSpec:  # unsupported spec types raise TypeError like CPUBackend (cpu.py:708-709)
         pass
     from dataloader_amd.config import PipelineConfig
     with pytest.raises(TypeError):
-        be.build_pipeline(lambda: [], EvalAugSpec(), PipelineConfig())
+        be.build_pipeline(lambda: [], CustomSpec(), PipelineConfig())
 
 
 def test_shard_cache_lru(tmp_path):

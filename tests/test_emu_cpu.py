@@ -207,6 +207,6 @@ def test_sampler_records_valid(emu):
 
 
 def test_view_params_layout_matches_c():
-    assert VIEW_PARAMS_DTYPE.itemsize == 64
+    assert VIEW_PARAMS_DTYPE.itemsize == 80
     assert VIEW_PARAMS_DTYPE.fields["sigma"][1] == 48 and VIEW_PARAMS_DTYPE.fields["order"][1] == 28
     assert ctypes.sizeof(DinoAugConfig) == 4 * 29  # dino_aug_config: 29 x 32-bit fields

@@ -20,7 +20,7 @@ import torch
 
 from dataloader_amd.config import DINOAugConfig
 from dataloader_amd.engine import IngestEngine, pack_jpegs, params_from_device, params_to_device
-from dataloader_amd.params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, make_aug_config
+from dataloader_amd.params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, VIEW_PARAMS_DTYPE, make_aug_config
 from dataloader_amd.synthetic import encode_jpeg, make_jpeg, textured_rgb
 from oracle import cpu_ref
 from oracle.masking_ref import RefMaskingGenerator
@@ -100,7 +100,7 @@ def test_augment_parity_device_params(gpu_device, out_code, tdtype):
     eng = IngestEngine(gpu_device, max_batch=B, max_views=cfg.n_views, max_crop_size=224)
     ccfg = make_aug_config(cfg, 224, 96, out_code)
     d_bytes, d_off = _to_dev(jpegs, gpu_device)
-    params = torch.empty(B * cfg.n_views * 64, dtype=torch.uint8, device=gpu_device)
+    params = torch.empty(B * cfg.n_views * VIEW_PARAMS_DTYPE.itemsize, dtype=torch.uint8, device=gpu_device)
     views, info = eng.run_batch(d_bytes, d_off, B, ccfg, seed=1234, batch_index=3, params_out=params)
     torch.cuda.synchronize()
     recs = params_from_device(params)
@@ -427,4 +427,71 @@ def test_per_dataset_normalisation(gpu_device):
             got = out[f"view_{v}"][b].cpu()
             tol = ONE_LEVEL * max(STD_MIN / min(std), 1.0) + 1e-6 if p.blur else 0.0
             assert (ref - got).abs().max().item() <= tol, (b, v)
+    pipe.close()
+
+
+@pytest.mark.parametrize("dtype,tdtype", [("fp32", torch.float32), ("bf16", torch.bfloat16)])
+def test_eval_spec_parity(gpu_device, dtype, tdtype):
+    """EvalAugSpec (reference CPUEvalPipeline, cpu.py:395-413): resize shorter side to
+    int(S*256/224) BICUBIC + centre crop on the same kernels (a window of the resampled
+    image); bit-exact vs the oracle, including images whose one axis is not resampled."""
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import EvalAugSpec, PipelineConfig
+    from dataloader_amd.pipeline import MI355XPipelineIterator
+    rng = np.random.default_rng(21)
+    sizes = [(640, 480), (480, 640), (256, 400), (300, 256), (257, 1000), (1111, 333), (256, 256), (90, 70)]
+    jpegs = [encode_jpeg(textured_rgb(w, h, rng), quality=90) for w, h in sizes] + [b"corrupt"]
+    spec = EvalAugSpec(crop_size=224)
+
+    class Src:
+        _batch_size = len(jpegs)
+        _resolution_src = None
+
+        def __call__(self):
+            return jpegs
+
+    pipe = MI355XBackend().build_pipeline(Src(), spec, PipelineConfig(output_dtype=dtype), None)
+    out = next(MI355XPipelineIterator(pipe, spec.output_map, len(jpegs)))[0]["view_0"].cpu()
+    torch.cuda.synchronize()
+    assert out.shape == (len(jpegs), 3, 224, 224) and out.dtype == tdtype
+    for b, j in enumerate(jpegs):
+        ref = cpu_ref.eval_one(j, 224, out_dtype=tdtype)
+        assert torch.equal(ref, out[b]), f"{sizes[b] if b < len(sizes) else 'corrupt'}: {(ref.float() - out[b].float()).abs().max()}"
+    pipe.close()
+
+
+def test_lejepa_spec_parity(gpu_device):
+    """LeJEPAAugSpec (reference CPULeJEPAPipeline, cpu.py:435-461): context view with RRC +
+    ColorJitter + flip, targets with RRC only, on the same kernels; every view matches the
+    oracle replay of its record and the recipe's flags hold."""
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import LeJEPAAugSpec, PipelineConfig
+    from dataloader_amd.pipeline import MI355XPipelineIterator
+    rng = np.random.default_rng(22)
+    jpegs = [make_jpeg(int(rng.integers(150, 500)), int(rng.integers(150, 500)), s) for s in range(6)]
+    spec = LeJEPAAugSpec(n_target_views=3)
+
+    class Src:
+        _batch_size = len(jpegs)
+        _resolution_src = None
+
+        def __call__(self):
+            return jpegs
+
+    pipe = MI355XBackend().build_pipeline(Src(), spec, PipelineConfig(output_dtype="fp32", seed=5), None)
+    out = next(MI355XPipelineIterator(pipe, spec.output_map, len(jpegs)))[0]
+    torch.cuda.synchronize()
+    assert list(out) == spec.output_map
+    recs = pipe.last_params()
+    nv = 1 + spec.n_target_views
+    assert not recs["blur"].any() and not recs["gray"].any() and not recs["solarize"].any()
+    r2 = recs.reshape(-1, nv)
+    assert not r2[:, 1:]["flip"].any() and not r2[:, 1:]["jitter"].any()
+    assert r2[:, 0]["jitter"].any() and (r2[:, 0]["out_size"] == 224).all() and (r2[:, 1:]["out_size"] == 96).all()
+    for b, j in enumerate(jpegs):
+        img = cpu_ref.decode_rgb(j)
+        for v, name in enumerate(spec.output_map):
+            p = record_to_params(recs[b * nv + v])
+            ref = cpu_ref.augment_one(j, p, spec.mean, spec.std, out_dtype=torch.float32, decoded=img)
+            assert torch.equal(ref, out[name][b].cpu()), (b, name)
     pipe.close()

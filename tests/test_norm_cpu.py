@@ -44,3 +44,33 @@ def test_set_norm_rejects_bad_arguments():
     lib = _lib.load()
     assert lib.dino_set_norm(None, None, 0) == -1
     assert b"null ctx" in lib.dino_last_error()
+
+
+def test_eval_geometry_follows_torchvision_rules():
+    from oracle.cpu_ref import eval_geometry
+    # Resize(256) of the shorter side, long side int(256 * long / short); CenterCrop offsets
+    # int(round((dim - 224) / 2.0)) with Python's half-to-even round
+    assert eval_geometry(640, 480, 224) == (341, 256, 58, 16)
+    assert eval_geometry(480, 640, 224) == (256, 341, 16, 58)
+    assert eval_geometry(256, 256, 224) == (256, 256, 16, 16)
+    assert eval_geometry(300, 257, 224) == (298, 256, 37, 16)
+
+
+def test_recipe_configs_and_spec_dispatch():
+    import pytest
+
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import EvalAugSpec, LeJEPAAugSpec, PipelineConfig, recipe_aug_config
+    from dataloader_amd.params import RECIPE_EVAL, RECIPE_LEJEPA, make_aug_config
+    c = recipe_aug_config(LeJEPAAugSpec(n_target_views=5))
+    assert (c.n_global_crops, c.n_local_crops, c.global_crop_size, c.local_crop_size) == (1, 5, 224, 96)
+    k = make_aug_config(c, 224, 96, 0)
+    assert k.recipe == RECIPE_LEJEPA and k.color_jitter_prob == pytest.approx(0.8) and k.blur_prob_local == 0
+    e = make_aug_config(recipe_aug_config(EvalAugSpec(crop_size=192)), 192, 192, 0)
+    assert e.recipe == RECIPE_EVAL and (e.n_global, e.n_local, e.global_size) == (1, 0, 192)
+
+    class UserAugSpec:
+        pass
+
+    with pytest.raises(TypeError):
+        MI355XBackend().build_pipeline(None, UserAugSpec(), PipelineConfig(), None)
