@@ -18,6 +18,11 @@ P = ctypes.c_void_p
 
 
 def record_to_params(rec) -> ViewParams:
+    names = rec.dtype.names or ()
+
+    def opt(k):  # records saved before the window fields existed (golden fixtures) have none
+        return int(rec[k]) if k in names else 0
+
     return ViewParams(
         out_size=int(rec["out_size"]), crop_top=int(rec["crop_top"]), crop_left=int(rec["crop_left"]),
         crop_h=int(rec["crop_h"]), crop_w=int(rec["crop_w"]), flip=bool(rec["flip"]),
@@ -25,8 +30,8 @@ def record_to_params(rec) -> ViewParams:
         brightness=float(rec["brightness"]), contrast=float(rec["contrast"]),
         saturation=float(rec["saturation"]), hue=float(rec["hue"]), gray=bool(rec["gray"]),
         blur=bool(rec["blur"]), sigma=float(rec["sigma"]), ksize=int(rec["ksize"]),
-        solarize=bool(rec["solarize"]), resize_w=int(rec["resize_w"]), resize_h=int(rec["resize_h"]),
-        out_x=int(rec["out_x"]), out_y=int(rec["out_y"]))
+        solarize=bool(rec["solarize"]), resize_w=opt("resize_w"), resize_h=opt("resize_h"),
+        out_x=opt("out_x"), out_y=opt("out_y"))
 
 
 def params_to_record(p: ViewParams) -> np.ndarray:
