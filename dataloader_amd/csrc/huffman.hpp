@@ -414,17 +414,17 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
 // ac(zigzag_index, int16) receives one non-zero AC coefficient (zigzag indices are
 // strictly increasing within a block; an index > 63 only comes from a corrupt
 // stream and is the block's last, mapped to natural position 63 as libjpeg's
-// jpeg_natural_order does), dc(int16) the absolute DC value (only with `pred`),
-// end() closes the block.
+// jpeg_natural_order does), dc(int16) the block's DC, end() closes the block.
 // Decode from `st` (a true state) and emit every block whose DC step starts before
 // `end`, finishing the last one past `end`; the leading partial block (st.z != 0)
 // belongs to the previous lane and is decoded without being emitted.  Stops at
-// `total_blocks`.  DC: with `pred` the absolute value goes to the sink (DC
-// predictors carried by the caller); without, the difference goes to dcd[block]
-// for the DC prefix pass (k_dcscan).  Returns the bit position.
+// `total_blocks`.  DC: with `pred` the sink gets the absolute value (DC predictors
+// carried by the caller); without, the difference (summed later by the DC prefix
+// pass, k_dcscan).  A difference fits int16: DC categories are <= 15.  Returns the
+// bit position.
 template <int kWin, typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
-                          int32_t total_blocks, int32_t* pred, int32_t* dcd, Sink& sink) {
+                          int32_t total_blocks, int32_t* pred, Sink& sink) {
   st = sanitize(st, im.blocks_per_mcu);
   BitCursor cur;
   bc_init<kWin>(cur, br, st.pos);
@@ -439,12 +439,8 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
     for (;;) {
       StepOut o = huff_step<kWin>(cur, br, im, blk, z);
       if (o.kind == 0) {
-        if (pred) {
-          add3(pred, comp, o.value);
-          sink.dc((int16_t)get3(pred, comp));
-        } else {
-          dcd[b] = o.value;
-        }
+        if (pred) add3(pred, comp, o.value);
+        sink.dc((int16_t)(pred ? get3(pred, comp) : o.value));
       } else if (o.kind == 1) {
         sink.ac(o.zz, (int16_t)o.value);
       }

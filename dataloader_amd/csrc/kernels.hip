@@ -75,11 +75,11 @@ __device__ int32_t huff_lanes_cap(const ImgDesc& d) {
 // Byte sizes of an image's workspace regions, in chunk order: destuffed entropy
 // bytes, restart offsets, sparse coefficient entries (64 u32 per block, see
 // SparseSink), block info (uint2 per block), component planes, RGB, speculative
-// checkpoints, DC values (int32 per block).
+// checkpoints.
 struct ChunkSizes {
-  int64_t ent, rst, coef, binfo, plane, rgb, cps, dcd, htab, hlane, dspart;
+  int64_t ent, rst, coef, binfo, plane, rgb, cps, htab, hlane, dspart;
   __device__ int64_t total() const {
-    return ent + rst + coef + binfo + plane + rgb + cps + dcd + htab + hlane + dspart;
+    return ent + rst + coef + binfo + plane + rgb + cps + htab + hlane + dspart;
   }
 };
 
@@ -103,7 +103,6 @@ __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   z.rgb = align16((int64_t)d.width * d.height * 3 + 16);
   const int64_t lanes = huff_lanes_cap(d);
   z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
-  z.dcd = align16(4 * (int64_t)d.total_blocks);
   z.htab = align16(6 * (int64_t)sizeof(HuffTable));
   z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
   z.dspart = 16 * (int64_t)ds_parts(d);
@@ -158,8 +157,7 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
       d.plane_off = d.binfo_off + z.binfo;
       d.rgb_off = d.plane_off + z.plane;
       d.cps_off = d.rgb_off + z.rgb;
-      d.dcd_off = d.cps_off + z.cps;
-      d.htab_off = d.dcd_off + z.dcd;
+      d.htab_off = d.cps_off + z.cps;
       d.hlane_off = d.htab_off + z.htab;
       d.dspart_off = d.hlane_off + z.hlane;
       d.h_lanes_cap = huff_lanes_cap(d);
@@ -516,17 +514,17 @@ constexpr int kHuff3LdsBytes = (int)((sizeof(HuffLds3) + 15) & ~(size_t)15);
 // (a block has at most 63 AC entries, so regions never overlap), buffered four at
 // a time into 16-byte stores so that each lane writes whole contiguous lines
 // instead of scattered 2-byte coefficients into a dense block.  binfo[b] =
-// {first entry, entry count}; the DC value lives in dcd[b] (absolute after
-// k_dcscan, or written here with restart intervals).  k_idct scatters the entries
-// into its LDS block.
+// {first entry, (int16 DC << 16) | entry count}: one 8-byte record per block carries
+// the DC too (a difference until k_dcscan sums it in place; absolute with restart
+// intervals).  k_idct scatters the entries into its LDS block.
 struct SparseSink {
   uint32_t* ent;   // image entry area
   uint2* binfo;    // image block info
-  int32_t* dcd;    // image DC values
   uint32_t n;      // entries written (relative to the image entry area), multiple of 4
   uint32_t k;      // entries buffered in e0..e3
   uint32_t e0, e1, e2, e3;
   uint32_t bstart;
+  uint32_t dcw;    // DC of the open block in the high half
   int32_t b;
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * 64u;
@@ -535,6 +533,7 @@ struct SparseSink {
   __device__ void begin(int32_t blk) {
     b = blk;
     bstart = n + k;
+    dcw = 0;
   }
   __device__ void push(uint32_t e) {
     e0 = k == 0 ? e : e0;
@@ -548,8 +547,8 @@ struct SparseSink {
     }
   }
   __device__ void ac(int zz, int16_t v) { push(((uint32_t)(uint16_t)v << 16) | (uint32_t)zz); }
-  __device__ void dc(int16_t v) { dcd[b] = (int32_t)v; }
-  __device__ void end() { binfo[b] = make_uint2(bstart, n + k - bstart); }
+  __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
+  __device__ void end() { binfo[b] = make_uint2(bstart, (n + k - bstart) | dcw); }
   __device__ void close() {  // the region is a multiple of 4 entries: a whole-word tail store stays inside it
     if (k) *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
   }
@@ -803,7 +802,6 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
     SparseSink sink;
     sink.ent = (uint32_t*)(ws + sd.coef_off);
     sink.binfo = (uint2*)(ws + sd.binfo_off);
-    sink.dcd = (int32_t*)(ws + sd.dcd_off);
     const int i = (item - sd.h_item_base) * kHuffThreads + t;
     if (sd.restart_interval > 0) {
       // restart intervals are independent: one lane per interval, absolute DC
@@ -817,7 +815,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
         const int first = i * per, last = min(first + per, sd.total_blocks);
         if (first < last) {
           sink.open(first);
-          decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+          decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
           sink.close();
         }
       }
@@ -825,8 +823,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
       sink.open(r.blk0);
-      decode_write<kSrcPadded>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr, sink.dcd,
-                          sink);
+      decode_write<kSrcPadded>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr, sink);
       sink.close();
     }
     __syncthreads();
@@ -836,43 +833,53 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
 // ---------------------------------------------------------------------------
 // k_dcscan: DC predictors of a speculatively decoded image (no restart
 // intervals): per-component running sums of the DC differences k_huffman left
-// in decode order, replaced in place by the absolute (int16) DC values.  One workgroup per
-// image, a contiguous run of blocks per lane.
+// in decode order (the high half of each block record), replaced in place by the
+// absolute (int16) DC values.  One workgroup per image, tiles of 2048 blocks.
 // ---------------------------------------------------------------------------
 constexpr int kDcScanThreads = 256;
 
 __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  constexpr int K = 8;  // blocks per lane per tile: a wave covers 512 consecutive blocks
   __shared__ uint32_t s_wave[kDcScanThreads / 64];
   const ImgDesc& d = desc[blockIdx.x];
   if (d.status != DINO_IMG_OK || d.restart_interval > 0) return;
   const int T = d.total_blocks, bpm = d.blocks_per_mcu;
   uint32_t mc = 0;
   for (int i = 0; i < bpm && i < kMaxBlocksPerMcu; ++i) mc |= (uint32_t)(d.mcu_comp[i] & 3) << (2 * i);
-  int32_t* dcd = (int32_t*)(ws + d.dcd_off);
-  const int per = (T + kDcScanThreads - 1) / kDcScanThreads;
-  const int b0 = min(T, threadIdx.x * per), b1 = min(T, b0 + per);
-  // block-in-MCU position tracked incrementally (no per-block modulo); loops unrolled
-  // so that several DC loads are in flight per wait
-  const int pos0 = b0 % bpm;
-  int32_t s[kMaxComp] = {0, 0, 0};
-  int pos = pos0;
-#pragma unroll 4
-  for (int b = b0; b < b1; ++b) {
-    add3(s, (int)((mc >> (2 * pos)) & 3u), dcd[b]);
-    pos = pos + 1 == bpm ? 0 : pos + 1;
-  }
-  uint32_t tot;
-  int32_t pfx[kMaxComp];
-  pfx[0] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[0], s_wave, &tot);
-  pfx[1] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[1], s_wave, &tot);
-  pfx[2] = (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[2], s_wave, &tot);
-  pos = pos0;
-#pragma unroll 4
-  for (int b = b0; b < b1; ++b) {
-    const int c = (int)((mc >> (2 * pos)) & 3u);
-    add3(pfx, c, dcd[b]);
-    dcd[b] = (int32_t)(int16_t)get3(pfx, c);  // in place: JCOEF (int16) DC, as libjpeg stores it
-    pos = pos + 1 == bpm ? 0 : pos + 1;
+  // the .y word of each block's record: (int16 DC << 16) | entry count
+  uint32_t* info = (uint32_t*)(ws + d.binfo_off) + 1;
+  int32_t carry[kMaxComp] = {0, 0, 0};
+  for (int t0 = 0; t0 < T; t0 += kDcScanThreads * K) {
+    // a tile: lane t owns K consecutive blocks, so each lane's loads and stores fill
+    // its own 64-byte span at once (no partially written lines left behind)
+    const int b0 = t0 + (int)threadIdx.x * K;
+    uint32_t y[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) y[j] = b0 + j < T ? info[2 * (int64_t)(b0 + j)] : 0u;
+    const int pos0 = b0 % bpm;
+    int32_t s[kMaxComp] = {0, 0, 0};
+    int pos = pos0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      add3(s, (int)((mc >> (2 * pos)) & 3u), (int32_t)y[j] >> 16);
+      pos = pos + 1 == bpm ? 0 : pos + 1;
+    }
+    uint32_t tot[kMaxComp];
+    int32_t pfx[kMaxComp];
+#pragma unroll
+    for (int c = 0; c < kMaxComp; ++c)
+      pfx[c] = carry[c] + (int32_t)block_excl_scan<kDcScanThreads>((uint32_t)s[c], s_wave, &tot[c]);
+    pos = pos0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const int c = (int)((mc >> (2 * pos)) & 3u);
+      add3(pfx, c, (int32_t)y[j] >> 16);
+      // in place: JCOEF (int16) DC, as libjpeg stores it
+      if (b0 + j < T) info[2 * (int64_t)(b0 + j)] = (y[j] & 0xFFFFu) | ((uint32_t)get3(pfx, c) << 16);
+      pos = pos + 1 == bpm ? 0 : pos + 1;
+    }
+#pragma unroll
+    for (int c = 0; c < kMaxComp; ++c) carry[c] += (int32_t)tot[c];
   }
 }
 
@@ -900,7 +907,6 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   const int64_t tot = nb0 + nb1 + nb2;
   const uint32_t* ent = (const uint32_t*)(ws + d.coef_off);
   const uint2* binfo = (const uint2*)(ws + d.binfo_off);
-  const int32_t* dcv = (const int32_t*)(ws + d.dcd_off);
   uint8_t* planes = ws + d.plane_off;
   // first position of each component inside the MCU (interleaved scans)
   int moff[kMaxComp] = {0, 0, 0};
@@ -938,11 +944,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   int gn = blockIdx.x * kIdctBlocksPerWg + grp;
   Blk nx = locate(gn < T ? gn : 0);
   uint2 bin = make_uint2(0u, 0u);
-  int32_t dcn = 0;
-  if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) {
-    bin = binfo[nx.b];
-    dcn = dcv[nx.b];
-  }
+  if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
 #pragma unroll
   for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
   __syncthreads();
@@ -950,20 +952,16 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     const bool valid = gn < T;
     const Blk cur = nx;
     const uint2 bi = bin;
-    const int32_t dc = dcn;
     gn += step;
     if (gn < T) {  // prefetch the next block's record while this one is transformed
       nx = locate(gn);
       bin = make_uint2(0u, 0u);
-      dcn = 0;
-      if (nx.b >= 0 && nx.b < d.total_blocks) {
-        bin = binfo[nx.b];
-        dcn = dcv[nx.b];
-      }
+      if (nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
     }
     if (valid) {
-      if (l == 0) sb[0] = dc;
-      for (uint32_t j = l; j < bi.y; j += 8) {
+      if (l == 0) sb[0] = (int32_t)bi.y >> 16;  // DC (int16, absolute after k_dcscan)
+      const uint32_t cnt = bi.y & 0xFFFFu;
+      for (uint32_t j = l; j < cnt; j += 8) {
         const uint32_t e = ent[bi.x + j];
         sb[s_nat[e & 0x7Fu]] = (int32_t)(int16_t)(e >> 16);
       }

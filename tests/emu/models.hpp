@@ -55,14 +55,22 @@ inline Destuffed model_destuff(const uint8_t* r, int n) {
 
 struct CoefSink {
   const ImgDesc* d;
-  int16_t* coef;  // image coefficient area
+  int16_t* coef;            // image coefficient area
+  int32_t* dcd = nullptr;   // set: DC differences per block (speculative mode), else absolute DC
   int16_t* blk = nullptr;
-  void begin(int32_t b) {
+  int32_t b = 0;
+  void begin(int32_t blk_index) {
+    b = blk_index;
     blk = coef + coef_block_offset(*d, b);
     memset(blk, 0, 128);
   }
   void ac(int zz, int16_t v) { blk[kNaturalOrder[zz]] = v; }
-  void dc(int16_t v) { blk[0] = v; }
+  void dc(int16_t v) {
+    if (dcd)
+      dcd[b] = v;
+    else
+      blk[0] = v;
+  }
   void end() {}
 };
 
@@ -137,10 +145,12 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
     }
   }
   int32_t blk0 = 0;
+  sink.dcd = dcd;
   for (int i = 0; i < n; ++i) {
-    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, dcd, sink);
+    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, sink);
     blk0 += R[i].nblk;
   }
+  sink.dcd = nullptr;
   model_dcscan(d, im, dcd, sink.coef);
   if (stats) {
     stats[0] = rounds;
@@ -188,14 +198,14 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
       int first = k * per, last = std::min(first + per, d.total_blocks);
       if (mode == 2) {  // segments read from the staged (swapped) words, as k_huffman's LDS window
         BitReader sw{win.data(), k + 1 < nseg ? (uint32_t)ds.rst[k] : (uint32_t)ds.len};
-        decode_write<true>(sw, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+        decode_write<true>(sw, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
       } else {
-        decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, (int32_t*)nullptr, sink);
+        decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
       }
     }
   } else if (mode == 0) {
     int32_t pred[kMaxComp] = {0, 0, 0};
-    decode_write<false>(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, (int32_t*)nullptr, sink);
+    decode_write<false>(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, sink);
   } else {
     std::vector<int32_t> dcd(d.total_blocks, 0);
     if (mode == 2) {
