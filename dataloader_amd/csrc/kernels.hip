@@ -895,11 +895,13 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
 constexpr int kIdctBlocksPerWg = 32;
 
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  __shared__ int32_t s_blk[kIdctBlocksPerWg][65];
+  // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
+  // (pass 2) accesses of a wave's 8 groups x 8 lanes hit 64 distinct banks
+  __shared__ int32_t s_blk[kIdctBlocksPerWg][72];
   __shared__ uint8_t s_nat[80];
   const ImgDesc& d = desc[blockIdx.y];
   if (d.status != DINO_IMG_OK) return;
-  if (threadIdx.x < 80) s_nat[threadIdx.x] = kNaturalOrder[threadIdx.x];
+  if (threadIdx.x < 80) s_nat[threadIdx.x] = (uint8_t)((kNaturalOrder[threadIdx.x] >> 3) * 9 + (kNaturalOrder[threadIdx.x] & 7));
   const int ncomp = d.ncomp;
   const int64_t nb0 = (int64_t)d.comp[0].bw * d.comp[0].bh;
   const int64_t nb1 = ncomp > 1 ? (int64_t)d.comp[1].bw * d.comp[1].bh : 0;
@@ -946,7 +948,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   uint2 bin = make_uint2(0u, 0u);
   if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
+  for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
   __syncthreads();
   for (int g0 = blockIdx.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
     const bool valid = gn < T;
@@ -972,18 +974,18 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
       const uint16_t* q = d.qt[cd.tq];
       int32_t col[8], wcol[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) col[r] = sb[r * 8 + l] * (int32_t)(int16_t)q[r * 8 + l];
+      for (int r = 0; r < 8; ++r) col[r] = sb[r * 9 + l] * (int32_t)(int16_t)q[r * 8 + l];
       idct_pass1(col, wcol);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sb[r * 8 + l] = wcol[r];
+      for (int r = 0; r < 8; ++r) sb[r * 9 + l] = wcol[r];
     }
     __syncthreads();
     if (valid) {  // pass 2 on row l, then the row is cleared for the next block
       int32_t row[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) row[j] = sb[l * 8 + j];
+      for (int j = 0; j < 8; ++j) row[j] = sb[l * 9 + j];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sb[l * 8 + j] = 0;
+      for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
       union {
         uint8_t b[8];
         uint64_t u;
