@@ -1259,7 +1259,36 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
 // staged in LDS too when they fit.  Each lane then resamples one (row, x) with
 // one LDS word per tap and writes the three channels to planar temp rows
 // [3][crop_h][S].  Crops too wide for LDS take a direct (global) path.
-constexpr int kHresizeTapLds = 16 * 1024;  // taps of one slice; the rest of kHresizeLds stages rows
+#ifndef DINO_HRESIZE_MIN_ROWS
+#define DINO_HRESIZE_MIN_ROWS 8
+#endif
+constexpr int kHresizeMinRows = DINO_HRESIZE_MIN_ROWS;  // rows per band the slice width is chosen for
+
+// Tile shape of a view's horizontal pass: the widest slice of outputs (all of S,
+// else a multiple of 8) whose taps (16 bytes per output + 16 per output and group
+// of 4 taps) and kHresizeMinRows staged rows fit kHresizeLds; then as many rows per
+// band as fit (<= 16).  R = 0: even 8 outputs do not fit (direct path).
+struct HrTile {
+  int sw, pitch, R;
+};
+__device__ __forceinline__ int hresize_pitch(int S, int cw, int kh, int sw) {
+  // widest source span of a slice (+ 4 for the word alignment of its first column)
+  const int span = min(cw, (int)(((int64_t)sw * cw + S - 1) / S) + kh + 2) + 4;
+  return ((span + 3) & ~3) + 8;  // + slack for the last group's upper word
+}
+__device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
+  const int tap_bytes = 16 * (1 + (kh + 3) / 4);
+  HrTile t{0, 0, 0};
+  int sw = S;
+  while (tap_bytes * sw + kHresizeMinRows * 3 * hresize_pitch(S, cw, kh, sw) > kHresizeLds) {
+    sw = sw == S ? ((S - 1) & ~7) : sw - 8;
+    if (sw < 8) return t;
+  }
+  t.sw = sw;
+  t.pitch = hresize_pitch(S, cw, kh, sw);
+  t.R = min(16, (kHresizeLds - tap_bytes * sw) / (3 * t.pitch));
+  return t;
+}
 
 // One tile: nr staged rows x the outputs [x0, x0 + sw) of a slice.  Lane (r, x)
 // accumulates three signed-dot4 digit products per channel and group of 4 taps.
@@ -1324,10 +1353,10 @@ __device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ row
   }
 }
 
-// Horizontal pass in tiles of (slice of outputs) x (band of rows).  A slice is as
-// many outputs as fit their taps in kHresizeTapLds, so the taps always come from
-// LDS; the band stages only the source columns the slice reads
-// [xmin(x0), xmin(x1-1) + xcnt(x1-1)), so narrower slices also mean more rows per band.
+// Horizontal pass in tiles of (slice of outputs) x (band of rows), shaped by
+// hresize_tile: the slice's taps always come from LDS, and the band stages only the
+// source columns the slice reads [xmin(x0), xmin(x1-1) + xcnt(x1-1)), so wide crops
+// take narrower slices to keep >= kHresizeMinRows rows per band.
 __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  const ViewPlan* __restrict__ plan, int nv, int v0,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
@@ -1347,14 +1376,9 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   uint8_t* tmp = aws + vp.htmp_off;
   const int64_t cpl = (int64_t)p.crop_h * S;
   const int ng_max = (kh + 3) / 4;
-  int sw = kHresizeTapLds / (16 * (1 + ng_max));
-  sw = sw >= S ? S : (sw & ~7);
+  const HrTile tl = hresize_tile(S, cw, kh);
+  const int sw = tl.sw, pitch = tl.pitch, R = tl.R;
   const int nsl = sw > 0 ? (S + sw - 1) / sw : 0;
-  // widest source span of a slice (+ 4 for the word alignment of its first column)
-  const int span = min(cw, (int)(((int64_t)sw * cw + S - 1) / S) + kh + 2) + 4;
-  const int pitch = ((span + 3) & ~3) + 8;  // + slack for the last group's upper word
-  int R = sw > 0 ? (kHresizeLds - kHresizeTapLds) / (3 * pitch) : 0;
-  R = R > 16 ? 16 : R;
   if (R < 1) {  // direct path: taps and pixels from global memory (crops too wide for LDS)
     const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
     const CoefView cv{gb, gt, kh};
@@ -1366,7 +1390,7 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   }
   int4* lx = (int4*)smem;
   uint4* lg = (uint4*)(lx + sw);
-  uint8_t* rows = smem + kHresizeTapLds;
+  uint8_t* rows = smem + 16 * sw * (1 + ng_max);
   const int plane_bytes = R * pitch;
   const int nbands = (p.crop_h + R - 1) / R;
   int cur = -1;

@@ -18,8 +18,11 @@ constexpr int kHuffThreads = DINO_HUFF_THREADS;
 #endif
 constexpr int64_t kHuffSegBits = (int64_t)DINO_HUFF_SEG_KBITS * 1024;
 
-// LDS of k_hresize: taps (when they fit in 16 KiB) + RGBX rows of one band.
-constexpr int kHresizeLds = 40 * 1024;
+// LDS of k_hresize: taps (when they fit in kHresizeTapLds) + planar rows of one band.
+#ifndef DINO_HRESIZE_LDS_KB
+#define DINO_HRESIZE_LDS_KB 26
+#endif
+constexpr int kHresizeLds = DINO_HRESIZE_LDS_KB * 1024;
 
 struct ViewPlan {
   int64_t htmp_off;   // horizontal-pass rows (crop_h x S x 3 u8) in the augment workspace
