@@ -1442,10 +1442,12 @@ __device__ __forceinline__ int64_t crop_slot(const dino_aug_config& cfg, int B, 
 }
 
 // Vertical pass (+ flip) and the ColorJitter ops that precede contrast, over a
-// band of kVertRows output rows; adds the band's L sum to the view's counter.
+// band of vert_rows(S) output rows; adds the band's L sum to the view's counter.
 // Fast path (planar temp rows, S % 4 == 0): a lane produces 4 adjacent pixels
 // from one 4-byte load per channel and tap and stores one word per plane.
 constexpr int kVertRows = 8;
+// rows per workgroup: 16 for the small (local) views, whose 8-row bands are short
+__host__ __device__ __forceinline__ int vert_rows(int S) { return S > 128 ? kVertRows : 2 * kVertRows; }
 
 __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                               ViewPlan* __restrict__ plan, int nv, int v0, int B,
@@ -1468,8 +1470,8 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   const uint8_t* htmp = aws + vp.htmp_off;
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
-  const int y0 = blockIdx.x * kVertRows;
-  const int nr = min(kVertRows, S - y0);
+  const int y0 = blockIdx.x * vert_rows(S);
+  const int nr = min(vert_rows(S), S - y0);
   uint32_t lsum = 0;
   if (need_h && (S & 3) == 0) {
     const int nq = S >> 2;
@@ -1595,12 +1597,15 @@ __device__ __forceinline__ void store_out4<uint8_t>(uint8_t* out, int64_t o, con
 }
 
 // Contrast (with the view's mean) and later ColorJitter ops, grayscale, then blur
-// + solarize + normalize + cast over a band of kFinalRows output rows.  The band
+// + solarize + normalize + cast over a band of final_rows(S) output rows.  The band
 // and its blur halo (rows and columns, reflected as torch's reflect padding) are
 // staged in LDS after the stage-1 jitter, so the blur reads a plain window.  A
 // lane produces 4 adjacent outputs of one channel; the kernel size is a template
 // parameter for the sizes the DINO sigma range yields (3..9).
 constexpr int kFinalRows = 32;
+// rows per workgroup: 16 for the large (global) views keeps their LDS tile small
+// enough for 7 workgroups per CU
+__host__ __device__ __forceinline__ int final_rows(int S) { return S > 128 ? 16 : kFinalRows; }
 constexpr int kMaxBlurPad = 7;
 
 struct FinalLds {
@@ -1685,8 +1690,8 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   const int i = b * nv + v;
   const ViewPlan vp = plan[i];
   const int64_t N = (int64_t)S * S;
-  const int y0 = blockIdx.x * kFinalRows;
-  const int nr = min(kFinalRows, S - y0);
+  const int y0 = blockIdx.x * final_rows(S);
+  const int nr = min(final_rows(S), S - y0);
   OutT* out = (OutT*)views.p[v] + (int64_t)b * 3 * N;
   if (!vp.ok) {  // reference cpu.py:253: undecodable -> zeros
     for (int e = threadIdx.x; e < 3 * nr * S; e += blockDim.x) {
@@ -1921,11 +1926,11 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   TIMED(tm, kKHresize, s,
         (k_hresize<<<dim3(16, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
   TIMED(tm, kvert, s,
-        (k_vert<<<dim3((S + kVertRows - 1) / kVertRows, nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, B,
+        (k_vert<<<dim3((S + vert_rows(S) - 1) / vert_rows(S), nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, B,
                                                                              a.ws, a.aws, a.gcrop, a.cfg, S)));
-  const int lds = (int)sizeof(FinalLds) + 3 * (kFinalRows + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
+  const int lds = (int)sizeof(FinalLds) + 3 * (final_rows(S) + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
   TIMED(tm, kfin, s,
-        (k_final<OutT><<<dim3((S + kFinalRows - 1) / kFinalRows, nvc, B), 256, lds, s>>>(
+        (k_final<OutT><<<dim3((S + final_rows(S) - 1) / final_rows(S), nvc, B), 256, lds, s>>>(
             a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S, a.norm)));
   return hipGetLastError();
 }
