@@ -19,18 +19,34 @@
 namespace dino {
 
 // Derived decoding table for one Huffman table (jpeg_make_d_derived_tbl).
-// Lookahead entry for each kLookBits-bit prefix: (symbol << 5) | code length, 0
-// when the code is longer than kLookBits (16 bits: six tables take 14.7 KiB of LDS).
-struct HuffTable {
+// Lookahead entry for each LB-bit prefix: (symbol << 5) | code length, 0 when the
+// code is longer than LB.  AC tables look ahead kLookBits = 11 bits; DC tables
+// kDcLookBits = 9 (the standard DC codes are <= 9 bits for luma and only the rare
+// categories >= 10 of chroma need the slow path), which keeps an image's six tables
+// at 17.3 KiB of LDS.
+constexpr int kDcLookBits = 9;
+template <int LB>
+struct HuffTableT {
   int32_t maxcode[18];     // maxcode[l], -1 if no codes of length l; [17] sentinel
   int32_t valoffset[18];
   uint8_t huffval[256];
-  uint16_t look[1 << kLookBits];
+  uint16_t look[1 << LB];
 };
+using HuffTable = HuffTableT<kLookBits>;
+using DcTable = HuffTableT<kDcLookBits>;
+
+// The six tables of an image: AC tables of components 0..2, then DC tables.  Both
+// kinds share the layout up to `look`, so the slow path reads either through one type.
+struct HuffTables {
+  HuffTable ac[3];
+  DcTable dc[3];
+};
+static_assert(sizeof(HuffTables) % 16 == 0, "HuffTables is copied in 16-byte words");
 
 // Build maxcode/valoffset/huffval (not the lookahead) from BITS[16] + HUFFVAL.
 // Returns false on an invalid table (libjpeg JERR_BAD_HUFF_TABLE).
-DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTable* t) {
+template <int LB>
+DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTableT<LB>* t) {
   int p = 0;
   int code = 0;
   for (int l = 1; l <= 16; ++l) {
@@ -68,11 +84,11 @@ DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTable* t) {
 
 DHD int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(((unsigned)-1) << s) + 1 : x; }
 
-// Lookahead entry for the kLookBits-bit prefix `idx` (computable independently per entry).
-DHD uint16_t huff_look_entry(const HuffTable* t, int idx, bool is_dc) {
-  (void)is_dc;
-  for (int l = 1; l <= kLookBits; ++l) {
-    const int code = idx >> (kLookBits - l);
+// Lookahead entry for the LB-bit prefix `idx` (computable independently per entry).
+template <int LB>
+DHD uint16_t huff_look_entry(const HuffTableT<LB>* t, int idx) {
+  for (int l = 1; l <= LB; ++l) {
+    const int code = idx >> (LB - l);
     if (code <= t->maxcode[l]) {  // canonical code: first length whose maxcode covers the prefix
       const int sym = t->huffval[(code + t->valoffset[l]) & 255];
       return (uint16_t)((sym << 5) | l);
@@ -185,22 +201,23 @@ DHD void bc_skip(BitCursor& c, int n) {
   c.pos += n;
 }
 
-// Symbol whose code is longer than kLookBits (jpeg_huff_decode's bit-serial loop,
+// Symbol whose code is longer than LB bits (jpeg_huff_decode's bit-serial loop,
 // incl. the l = 17 "fake zero").  The maxcode values are read up front and the
 // length found by comparisons, so the lane waits on LDS once, not per bit.
-DHD void huff_slow(const BitCursor& c, const HuffTable* t, int* sym, int* len) {
+template <int LB>
+DHD void huff_slow(const BitCursor& c, const HuffTableT<LB>* t, int* sym, int* len) {
   const uint32_t p17 = bc_peek(c, 17);  // code of up to 16 bits + sentinel
-  int32_t mc[17 - kLookBits], vo[17 - kLookBits];
+  int32_t mc[17 - LB], vo[17 - LB];
 #pragma unroll
-  for (int k = 0; k < 17 - kLookBits; ++k) {
-    mc[k] = t->maxcode[kLookBits + 1 + k];
-    vo[k] = t->valoffset[kLookBits + 1 + k];
+  for (int k = 0; k < 17 - LB; ++k) {
+    mc[k] = t->maxcode[LB + 1 + k];
+    vo[k] = t->valoffset[LB + 1 + k];
   }
   int l = 17, off = 0;
 #pragma unroll
-  for (int k = 16 - kLookBits; k >= 0; --k) {
-    if ((int32_t)(p17 >> (16 - kLookBits - k)) <= mc[k]) {
-      l = kLookBits + 1 + k;
+  for (int k = 16 - LB; k >= 0; --k) {
+    if ((int32_t)(p17 >> (16 - LB - k)) <= mc[k]) {
+      l = LB + 1 + k;
       off = vo[k];
     }
   }
@@ -227,12 +244,12 @@ DHD bool hstate_eq(const HState& a, const HState& b) { return a.pos == b.pos && 
 // Everything a lane indexes per step is a base pointer or a packed word, so that
 // no per-lane array is dynamically indexed (which would spill it to scratch).
 struct HuffImage {
-  const HuffTable* tabs;   // [6]: DC tables of components 0..2, then AC tables 0..2
+  const HuffTables* tabs;
   uint32_t mcu_comp;       // component of block b of the MCU in bits [2b, 2b+2)
   int32_t blocks_per_mcu;
 };
 
-DHD void hi_init(HuffImage& im, const HuffTable* tabs, const uint8_t* mcu_comp, int blocks_per_mcu) {
+DHD void hi_init(HuffImage& im, const HuffTables* tabs, const uint8_t* mcu_comp, int blocks_per_mcu) {
   im.tabs = tabs;
   im.mcu_comp = 0;
   for (int i = 0; i < blocks_per_mcu && i < kMaxBlocksPerMcu; ++i) im.mcu_comp |= (uint32_t)(mcu_comp[i] & 3) << (2 * i);
@@ -282,13 +299,16 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
   bc_fill<kWin>(cur, br);
   const int comp = hi_comp(im, blk);
   const bool dc = z == 0;
-  const HuffTable* t = im.tabs + (dc ? comp : 3 + comp);
+  // both table kinds keep `look` at the same offset: one pointer, one shift select
+  const HuffTable* t = dc ? reinterpret_cast<const HuffTable*>(im.tabs->dc + comp) : im.tabs->ac + comp;
   const uint32_t hi32 = (uint32_t)(cur.buf >> 32);  // >= 32 valid bits after bc_fill
-  const uint32_t e = t->look[hi32 >> (32 - kLookBits)];
+  const uint32_t e = t->look[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
   int sym, len;
   if (e) {
     sym = (int)(e >> 5);
     len = (int)(e & 31u);
+  } else if (dc) {
+    huff_slow(cur, reinterpret_cast<const DcTable*>(t), &sym, &len);
   } else {
     huff_slow(cur, t, &sym, &len);
   }

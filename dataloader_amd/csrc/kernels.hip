@@ -103,7 +103,7 @@ __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   z.rgb = align16((int64_t)d.width * d.height * 3 + 16);
   const int64_t lanes = huff_lanes_cap(d);
   z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
-  z.htab = align16(6 * (int64_t)sizeof(HuffTable));
+  z.htab = align16((int64_t)sizeof(HuffTables));
   z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
   z.dspart = 16 * (int64_t)ds_parts(d);
   return z;
@@ -494,13 +494,13 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 
 struct HuffLds {     // k_huff1
   ImgDesc sd;
-  HuffTable tab[6];
+  HuffTables tab;
   RangeOut R[kHuffThreads];
   int32_t img, item;
 };
 struct HuffLds3 {    // k_huff3 (no lane exchange)
   ImgDesc sd;
-  HuffTable tab[6];
+  HuffTables tab;
   int32_t img, item;
 };
 
@@ -570,7 +570,7 @@ __device__ __forceinline__ uint32_t lane_write_end(const ImgDesc& d, int i) {
 __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict__ bytes,
                                                        const int64_t* __restrict__ offsets,
                                                        ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  __shared__ HuffTable s_tab[6];
+  __shared__ HuffTables s_tab;
   __shared__ int32_t s_bad;
   ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
@@ -580,23 +580,27 @@ __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict
   __syncthreads();
   if (t < 2 * d.ncomp) {
     const int c = t >> 1, ac = t & 1;
-    const int slot = ac ? 3 + c : c;
-    const int off = ac ? d.huff_off[4 + d.comp[c].ta] : d.huff_off[d.comp[c].td];
-    if (!huff_build_derived(p + off, !ac, &s_tab[slot])) atomicOr(&s_bad, 1);
+    const bool ok = ac ? huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &s_tab.ac[c])
+                       : huff_build_derived(p + d.huff_off[d.comp[c].td], true, &s_tab.dc[c]);
+    if (!ok) atomicOr(&s_bad, 1);
   }
   __syncthreads();
   if (s_bad) {
     if (t == 0) d.status = DINO_IMG_CORRUPT;
     return;
   }
-  for (int e = t; e < 6 * (1 << kLookBits); e += kHuffThreads) {
-    const int slot = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
-    if (slot % 3 < d.ncomp) s_tab[slot].look[idx] = huff_look_entry(&s_tab[slot], idx, slot < 3);
+  for (int e = t; e < 3 * (1 << kLookBits); e += kHuffThreads) {
+    const int c = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
+    if (c < d.ncomp) s_tab.ac[c].look[idx] = huff_look_entry(&s_tab.ac[c], idx);
+  }
+  for (int e = t; e < 3 * (1 << kDcLookBits); e += kHuffThreads) {
+    const int c = e >> kDcLookBits, idx = e & ((1 << kDcLookBits) - 1);
+    if (c < d.ncomp) s_tab.dc[c].look[idx] = huff_look_entry(&s_tab.dc[c], idx);
   }
   __syncthreads();
   uint4* dst = (uint4*)(ws + d.htab_off);
-  const uint4* src = (const uint4*)s_tab;
-  for (int k = t; k < (int)(sizeof(HuffTable) * 6 / 16); k += kHuffThreads) dst[k] = src[k];
+  const uint4* src = (const uint4*)&s_tab;
+  for (int k = t; k < (int)(sizeof(HuffTables) / 16); k += kHuffThreads) dst[k] = src[k];
   if (t == 0) {
     const int64_t nbits = (int64_t)d.ent_len * 8;
     if (d.restart_interval > 0) {
@@ -669,8 +673,8 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
   __syncthreads();
   if (L.img < 0) return false;
   const uint4* src = (const uint4*)(ws + L.sd.htab_off);
-  uint4* dst = (uint4*)L.tab;
-  for (int k = threadIdx.x; k < (int)(sizeof(HuffTable) * 6 / 16); k += kHuffThreads) dst[k] = src[k];
+  uint4* dst = (uint4*)&L.tab;
+  for (int k = threadIdx.x; k < (int)(sizeof(HuffTables) / 16); k += kHuffThreads) dst[k] = src[k];
   __syncthreads();
   return true;
 }
@@ -688,7 +692,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       continue;
     }
     HuffImage im;
-    hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
+    hi_init(im, &L.tab, sd.mcu_comp, sd.blocks_per_mcu);
     const BitReader br{(const uint32_t*)(ws + sd.ent_off), (uint32_t)sd.ent_len};
     const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
     const int i = (item - sd.h_item_base) * kHuffThreads + t;  // lane index within the image
@@ -735,7 +739,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
 constexpr int kHuff2Threads = 256;
 
 __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  __shared__ HuffTable s_tab[6];
+  __shared__ HuffTables s_tab;
   __shared__ uint32_t s_wave[kHuff2Threads / 64];
   const ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
@@ -745,12 +749,12 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
   if (n > kHuffThreads) {  // several segments: their first lanes started from guesses
     {
       const uint4* src = (const uint4*)(ws + d.htab_off);
-      uint4* dst = (uint4*)s_tab;
-      for (int k = t; k < (int)(sizeof(HuffTable) * 6 / 16); k += kHuff2Threads) dst[k] = src[k];
+      uint4* dst = (uint4*)&s_tab;
+      for (int k = t; k < (int)(sizeof(HuffTables) / 16); k += kHuff2Threads) dst[k] = src[k];
     }
     __syncthreads();
     HuffImage im;
-    hi_init(im, s_tab, d.mcu_comp, d.blocks_per_mcu);
+    hi_init(im, &s_tab, d.mcu_comp, d.blocks_per_mcu);
     const BitReader br{(const uint32_t*)(ws + d.ent_off), (uint32_t)d.ent_len};
     const uint32_t nbits = (uint32_t)d.ent_len * 8u;
     const Checkpoint* cps = (const Checkpoint*)(ws + d.cps_off);
@@ -797,7 +801,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
     if (!huff_load_item(L, desc, B, ws, item)) return;
     const ImgDesc& sd = L.sd;
     HuffImage im;
-    hi_init(im, L.tab, sd.mcu_comp, sd.blocks_per_mcu);
+    hi_init(im, &L.tab, sd.mcu_comp, sd.blocks_per_mcu);
     const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
     SparseSink sink;
     sink.ent = (uint32_t*)(ws + sd.coef_off);

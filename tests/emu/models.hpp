@@ -84,14 +84,12 @@ inline void model_dcscan(const ImgDesc& d, const HuffImage& im, const int32_t* d
   }
 }
 
-inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTable* tabs /* [6] */, HuffImage& im) {
+inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTables* tabs, HuffImage& im) {
   for (int c = 0; c < d.ncomp; ++c) {
-    if (!huff_build_derived(p + d.huff_off[d.comp[c].td], true, &tabs[c])) return false;
-    if (!huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &tabs[3 + c])) return false;
-    for (int i = 0; i < (1 << kLookBits); ++i) {
-      tabs[c].look[i] = huff_look_entry(&tabs[c], i, true);
-      tabs[3 + c].look[i] = huff_look_entry(&tabs[3 + c], i, false);
-    }
+    if (!huff_build_derived(p + d.huff_off[d.comp[c].td], true, &tabs->dc[c])) return false;
+    if (!huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &tabs->ac[c])) return false;
+    for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->dc[c].look[i] = huff_look_entry(&tabs->dc[c], i);
+    for (int i = 0; i < (1 << kLookBits); ++i) tabs->ac[c].look[i] = huff_look_entry(&tabs->ac[c], i);
   }
   hi_init(im, tabs, d.mcu_comp, d.blocks_per_mcu);
   return true;
@@ -176,9 +174,9 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     cap->ent.assign(ds.bytes.begin(), ds.bytes.begin() + ds.len);
   }
   if (!ds.terminated) return DINO_IMG_TRUNCATED;
-  HuffTable tabs[6];
+  HuffTables tabs;
   HuffImage im;
-  if (!model_tables(p, d, tabs, im)) return DINO_IMG_CORRUPT;
+  if (!model_tables(p, d, &tabs, im)) return DINO_IMG_CORRUPT;
   std::vector<int16_t> coef(d.coef_bytes / 2, 0);
   CoefSink sink;
   sink.d = &d;

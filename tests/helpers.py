@@ -102,3 +102,13 @@ def emu_resized_crop(lib, rgb: np.ndarray, rec) -> np.ndarray:
     out = np.zeros(S * S * 3, np.uint8)
     lib.emu_resized_crop(rgb.ctypes.data_as(P), W, H, recarr.ctypes.data_as(P), out.ctypes.data_as(P))
     return out.reshape(S, S, 3)
+
+
+def dc_extremes_rgb(w: int, h: int, rng, cell: int = 16) -> np.ndarray:
+    """Saturated colour cells (black/white/blue/yellow/red/cyan) in cell x cell squares:
+    neighbouring blocks differ by DC categories 10-11 in luma and chroma, whose chroma
+    codes are longer than the DC lookahead (the decoder's slow path)."""
+    pal = np.array([[0, 0, 0], [255, 255, 255], [0, 0, 255], [255, 255, 0], [255, 0, 0], [0, 255, 255]], np.uint8)
+    idx = rng.integers(0, len(pal), size=((h + cell - 1) // cell, (w + cell - 1) // cell))
+    img = pal[np.repeat(np.repeat(idx, cell, axis=0), cell, axis=1)[:h, :w]]
+    return np.ascontiguousarray(img)

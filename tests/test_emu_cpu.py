@@ -23,7 +23,7 @@ from dataloader_amd.params import VIEW_PARAMS_DTYPE, DinoAugConfig
 from dataloader_amd.synthetic import encode_jpeg, textured_rgb
 from oracle import cpu_ref
 from oracle.masking_ref import RefMaskingGenerator
-from tests.helpers import P, emu_augment, emu_decode, emu_resized_crop, params_to_record, record_to_params
+from tests.helpers import dc_extremes_rgb, P, emu_augment, emu_decode, emu_resized_crop, params_to_record, record_to_params
 
 GOLD = Path(__file__).resolve().parent / "golden"
 ONE_LEVEL = 1.0 / 255.0 / min(cpu_ref.IMAGENET_STD)
@@ -90,6 +90,8 @@ def _zoo():
     out.append(encode_jpeg(textured_rgb(320, 240, rng), restart_mcus=7))
     out.append(encode_jpeg(textured_rgb(99, 77, rng), quality=30))
     out.append(encode_jpeg(textured_rgb(99, 77, rng), quality=100))
+    for sub, q in ((0, 95), (2, 95), (2, 50)):
+        out.append(encode_jpeg(dc_extremes_rgb(160, 96, rng), quality=q, subsampling=sub))
     return out
 
 

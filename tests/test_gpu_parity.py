@@ -24,7 +24,7 @@ from dataloader_amd.params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, VIEW_PARAMS_
 from dataloader_amd.synthetic import encode_jpeg, make_jpeg, textured_rgb
 from oracle import cpu_ref
 from oracle.masking_ref import RefMaskingGenerator
-from tests.helpers import record_to_params
+from tests.helpers import dc_extremes_rgb, record_to_params
 
 pytestmark = pytest.mark.gpu
 
@@ -43,6 +43,8 @@ def _jpeg_zoo():
     out.append(encode_jpeg(textured_rgb(321, 123, rng), restart_mcus=40, subsampling=0))
     out.append(encode_jpeg(textured_rgb(300, 200, rng), quality=50))
     out.append(encode_jpeg(textured_rgb(300, 200, rng), quality=95))
+    for sub, q in ((0, 95), (2, 95), (2, 50)):
+        out.append(encode_jpeg(dc_extremes_rgb(160, 96, rng), quality=q, subsampling=sub))
     return out
 
 
