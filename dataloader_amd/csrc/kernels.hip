@@ -898,6 +898,15 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
 // stores output row l as one 8-byte word.
 constexpr int kIdctBlocksPerWg = 32;
 
+// A wave's 8 blocks live only in its own 8 LDS slots, so the steps of one block need
+// no workgroup barrier: a wave's LDS operations execute in issue order, and the
+// wavefront-scope fences keep the compiler from moving LDS accesses across this point.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
   // (pass 2) accesses of a wave's 8 groups x 8 lanes hit 64 distinct banks
@@ -946,11 +955,20 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     return r;
   };
   const int T = (int)tot, step = gridDim.x * kIdctBlocksPerWg;
-  // the next iteration's block info and DC are loaded one iteration ahead
+  // The next block's record is loaded one iteration ahead, and its first 16 entries
+  // at the end of the current iteration (once the record has arrived), so the
+  // scatter at the top of an iteration normally waits on nothing.
   int gn = blockIdx.x * kIdctBlocksPerWg + grp;
   Blk nx = locate(gn < T ? gn : 0);
   uint2 bin = make_uint2(0u, 0u);
   if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
+  uint32_t ea = 0, eb = 0;  // entries l and l + 8 of the next block
+  auto first_entries = [&]() {
+    const uint32_t c = bin.y & 0xFFFFu;
+    ea = l < c ? ent[bin.x + l] : 0u;
+    eb = l + 8 < c ? ent[bin.x + l + 8] : 0u;
+  };
+  if (gn < T) first_entries();
 #pragma unroll
   for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
   __syncthreads();
@@ -967,12 +985,14 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     if (valid) {
       if (l == 0) sb[0] = (int32_t)bi.y >> 16;  // DC (int16, absolute after k_dcscan)
       const uint32_t cnt = bi.y & 0xFFFFu;
-      for (uint32_t j = l; j < cnt; j += 8) {
+      if (l < cnt) sb[s_nat[ea & 0x7Fu]] = (int32_t)(int16_t)(ea >> 16);
+      if (l + 8 < cnt) sb[s_nat[eb & 0x7Fu]] = (int32_t)(int16_t)(eb >> 16);
+      for (uint32_t j = l + 16; j < cnt; j += 8) {
         const uint32_t e = ent[bi.x + j];
         sb[s_nat[e & 0x7Fu]] = (int32_t)(int16_t)(e >> 16);
       }
     }
-    __syncthreads();
+    wave_lds_sync();
     const CompDesc& cd = d.comp[cur.c];
     if (valid) {  // dequantize + pass 1 on column l (reads and writes only this lane's column)
       const uint16_t* q = d.qt[cd.tq];
@@ -983,7 +1003,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
 #pragma unroll
       for (int r = 0; r < 8; ++r) sb[r * 9 + l] = wcol[r];
     }
-    __syncthreads();
+    wave_lds_sync();
     if (valid) {  // pass 2 on row l, then the row is cleared for the next block
       int32_t row[8];
 #pragma unroll
@@ -998,7 +1018,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
       const int pitch = cd.bw * 8;
       *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = o.u;
     }
-    __syncthreads();
+    if (gn < T) first_entries();
+    wave_lds_sync();
   }
 }
 
