@@ -355,7 +355,18 @@ struct RangeOut {
   int32_t nblk;    // blocks whose DC step starts in the range
 };
 
-constexpr int kHuffCheckpoints = 32;  // block boundaries recorded per lane by the first decode
+#ifndef DINO_HUFF_CHECKPOINTS
+#define DINO_HUFF_CHECKPOINTS 16
+#endif
+constexpr int kHuffCheckpoints = DINO_HUFF_CHECKPOINTS;  // block boundaries recorded per lane by the first decode
+#ifndef DINO_HUFF_CP_DENSE
+#define DINO_HUFF_CP_DENSE 4
+#endif
+#ifndef DINO_HUFF_CP_STRIDE
+#define DINO_HUFF_CP_STRIDE 8
+#endif
+constexpr int kHuffCpDense = DINO_HUFF_CP_DENSE;    // leading blocks that all get a checkpoint
+constexpr int kHuffCpStride = DINO_HUFF_CP_STRIDE;  // then every kHuffCpStride-th block (power of 2)
 
 // A block boundary (state before a DC step) seen by a lane's first decode:
 // bit position, block-in-MCU index c and the blocks started before it.
@@ -385,7 +396,10 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
   int32_t blk = st.c, z = st.z;
   while (cur.pos < end) {
     if (z == 0) {
-      if (n < kmax) cps[n++] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
+      // every block boundary at first (where a re-decode from a corrected state
+      // usually meets the first decode), then every kHuffCpStride-th: fewer stores
+      if (n < kmax && (r.nblk < kHuffCpDense || (r.nblk & (kHuffCpStride - 1)) == 0))
+        cps[n++] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
       r.nblk++;
     }
     huff_step<kWin>(cur, br, im, blk, z);
