@@ -383,10 +383,12 @@ DHD HState sanitize(HState st, int bpm) {
   return st;
 }
 
-// First (speculative) decode of a range; records up to kmax block boundaries.
+// First (speculative) decode of a range; records up to kmax block boundaries at
+// cps[0], cps[cstride], ... (the kernels interleave the lanes' checkpoints, so that
+// the lanes of a wave recording their n-th checkpoint write neighbouring words).
 template <int kWin>
 DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, uint32_t end, Checkpoint* cps,
-                          int kmax, int32_t* ncp) {
+                          int cstride, int kmax, int32_t* ncp) {
   st = sanitize(st, im.blocks_per_mcu);
   RangeOut r;
   r.nblk = 0;
@@ -399,7 +401,7 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
       // every block boundary at first (where a re-decode from a corrected state
       // usually meets the first decode), then every kHuffCpStride-th: fewer stores
       if (n < kmax && (r.nblk < kHuffCpDense || (r.nblk & (kHuffCpStride - 1)) == 0))
-        cps[n++] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
+        cps[(n++) * cstride] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
       r.nblk++;
     }
     huff_step<kWin>(cur, br, im, blk, z);
@@ -417,7 +419,7 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 // decode already found: its end state and remaining block count are reused.
 template <int kWin>
 DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
-                               const Checkpoint* cps, int ncp, RangeOut first) {
+                               const Checkpoint* cps, int cstride, int ncp, RangeOut first) {
   st = sanitize(st, im.blocks_per_mcu);
   int32_t nblk = 0;
   int j = 0;
@@ -426,10 +428,10 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
   int32_t blk = st.c, z = st.z;
   while (cur.pos < end) {
     if (z == 0) {
-      while (j < ncp && cps[j].pos < cur.pos) ++j;
-      if (j < ncp && cps[j].pos == cur.pos && (int32_t)(cps[j].cn & 15u) == blk) {
+      while (j < ncp && cps[j * cstride].pos < cur.pos) ++j;
+      if (j < ncp && cps[j * cstride].pos == cur.pos && (int32_t)(cps[j * cstride].cn & 15u) == blk) {
         RangeOut r = first;
-        r.nblk = nblk + first.nblk - (int32_t)(cps[j].cn >> 4);
+        r.nblk = nblk + first.nblk - (int32_t)(cps[j * cstride].cn >> 4);
         return r;
       }
       nblk++;

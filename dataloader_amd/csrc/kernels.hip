@@ -699,12 +699,14 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     const bool active = i < sd.h_lanes;
     const uint32_t rend = lane_range_end(sd, i, nbits);
     LaneRec* lr = (LaneRec*)(ws + sd.hlane_off);
-    Checkpoint* cps = (Checkpoint*)(ws + sd.cps_off) + (int64_t)i * kHuffCheckpoints;
+    // checkpoint k of lane i at [k][lane]: a wave's lanes write neighbouring words
+    Checkpoint* cps = (Checkpoint*)(ws + sd.cps_off) + i;
+    const int cstride = sd.h_lanes_cap;
     int32_t ncp = 0;
     HState myS{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};  // this lane's start state and first-decode
     RangeOut myR1{};                                      // result stay in registers; only R is shared
     if (active) {
-      myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, kHuffCheckpoints, &ncp);
+      myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
       L.R[t] = myR1;
     }
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
@@ -718,7 +720,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       __syncthreads();
       if (redo) {
         myS = want;
-        L.R[t] = decode_range_sync<kSrcPadded>(br, im, want, rend, cps, ncp, myR1);
+        L.R[t] = decode_range_sync<kSrcPadded>(br, im, want, rend, cps, cstride, ncp, myR1);
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
@@ -773,7 +775,7 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
           const HState want = lr[i].W;
           lr[i].S = want;
           lr[i].R = decode_range_sync<kSrcPadded>(br, im, want, lane_range_end(d, i, nbits),
-                                             cps + (int64_t)i * kHuffCheckpoints, lr[i].ncp, lr[i].R1);
+                                             cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1);
         }
       }
       __syncthreads();

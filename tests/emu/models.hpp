@@ -118,7 +118,7 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
   for (int i = 0; i < n; ++i) {
     S[i] = HState{(uint32_t)i * sub, 0, 0};
-    R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], kHuffCheckpoints, &ncp[i]);
+    R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, kHuffCheckpoints, &ncp[i]);
   }
   int rounds = 0, redone = 0;
   for (int pass = 0; pass < 2; ++pass) {  // 0: inside segments (k_huff1), 1: whole image (k_huff2)
@@ -134,7 +134,7 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
       for (int i = 1; i < n; ++i) {
         if (!redo[i]) continue;
         S[i] = want[i];
-        R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], ncp[i], R1[i]);
+        R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i], R1[i]);
         any = true;
         ++redone;
       }
