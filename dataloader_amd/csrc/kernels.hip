@@ -1084,11 +1084,22 @@ __global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc,
   const int W = d.width;
   const int64_t npx = (int64_t)W * d.height;
   const int64_t nq = (npx + 3) >> 2;  // npx < 2^31 (max_image_dim <= 16384 is enforced by k_parse limits)
+  // (y, x) of the lane's first quad by one division; later quads advance by the
+  // grid stride (dy rows + dx pixels) without dividing again
+  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, qs = (int64_t)gridDim.x * blockDim.x;
+  const uint32_t pstride = (uint32_t)(qs * 4);
+  const int dy = (int)(pstride / (uint32_t)W), dx = (int)(pstride - (uint32_t)dy * (uint32_t)W);
+  int yq = (int)((uint32_t)(q0 * 4) / (uint32_t)W), xq = (int)((uint32_t)(q0 * 4) - (uint32_t)yq * (uint32_t)W);
 #pragma unroll 2
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t q = q0; q < nq; q += qs) {
     const int64_t i0 = q * 4;
-    const uint32_t iu = (uint32_t)i0;
-    int y = (int)(iu / (uint32_t)W), x = (int)(iu - (uint32_t)y * (uint32_t)W);  // 32-bit division
+    int y = yq, x = xq;
+    xq += dx;
+    yq += dy;
+    if (xq >= W) {
+      xq -= W;
+      ++yq;
+    }
     union {
       uint8_t b[12];
       uint32_t w[3];
