@@ -1057,12 +1057,17 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, int* o
   int cs[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) cs[j] = 3 * (int)((n >> (8 * j)) & 255u) + (int)((f >> (8 * j)) & 255u);
-  const int c0 = x0 >> 1;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int x = x0 + j, c = (x >> 1) - c0 + 1;  // index of column x>>1 in cs
-    out[j] = (x & 1) ? (cs[c] * 3 + cs[c + 1] + 7) >> 4 : (cs[c] * 3 + cs[c - 1] + 8) >> 4;
-  }
+  // an even pixel x blends column x/2 with its left neighbour ((3a + b + 8) >> 4), an odd
+  // one with its right neighbour ((3a + b + 7) >> 4); with cs[1] = column x0/2 the four
+  // pixels use fixed columns for each parity of x0 (no dynamically indexed cs)
+  const int e0 = (cs[1] * 3 + cs[0] + 8) >> 4, e1 = (cs[1] * 3 + cs[2] + 7) >> 4;
+  const int e2 = (cs[2] * 3 + cs[1] + 8) >> 4, e3 = (cs[2] * 3 + cs[3] + 7) >> 4;
+  const int o3 = (cs[3] * 3 + cs[2] + 8) >> 4;
+  const bool odd = x0 & 1;
+  out[0] = odd ? e1 : e0;
+  out[1] = odd ? e2 : e1;
+  out[2] = odd ? e3 : e2;
+  out[3] = odd ? o3 : e3;
 }
 
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
