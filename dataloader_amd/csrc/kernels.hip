@@ -76,6 +76,9 @@ __device__ int32_t huff_lanes_cap(const ImgDesc& d) {
 // bytes, restart offsets, sparse coefficient entries (64 u32 per block, see
 // SparseSink), block info (uint2 per block), component planes, RGB, speculative
 // checkpoints.
+// Sparse entry capacity per block (see SparseSink): 63 u32 entries + 1 alignment halfword.
+constexpr int kEntHalfwordsPerBlock = 128;
+
 struct ChunkSizes {
   int64_t ent, rst, coef, binfo, plane, rgb, cps, htab, hlane, dspart;
   __device__ int64_t total() const {
@@ -95,7 +98,7 @@ __device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   if (d.status != DINO_IMG_OK) return z;
   z.ent = align16((int64_t)d.scan_len + 64);
   z.rst = align16(4 * ((int64_t)d.n_rst_max + 1));
-  z.coef = (int64_t)d.total_blocks * 256;
+  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;
   z.binfo = align16((int64_t)d.total_blocks * 8);
   int64_t p = 0;
   for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
@@ -509,48 +512,69 @@ constexpr int kHuffLdsBytes = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
 constexpr int kHuff3LdsBytes = (int)((sizeof(HuffLds3) + 15) & ~(size_t)15);
 
 // Sparse coefficient output.  A lane appends its blocks' non-zero AC coefficients
-// as u32 entries ((int16 value << 16) | zigzag index) to a private region of the
-// image's entry area that starts at 64 entries per block before its first block
-// (a block has at most 63 AC entries, so regions never overlap), buffered four at
-// a time into 16-byte stores so that each lane writes whole contiguous lines
-// instead of scattered 2-byte coefficients into a dense block.  binfo[b] =
-// {first entry, (int16 DC << 16) | entry count}: one 8-byte record per block carries
-// the DC too (a difference until k_dcscan sums it in place; absolute with restart
-// intervals).  k_idct scatters the entries into its LDS block.
+// to a private region of the image's entry area that starts at 128 halfwords per
+// block before its first block (a block needs at most 127, so regions never
+// overlap), buffered eight halfwords at a time into 16-byte stores so that each lane
+// writes whole contiguous lines instead of scattered 2-byte coefficients into a
+// dense block.  A coefficient takes one halfword, zigzag index | (int10 value << 6),
+// while its value fits 10 bits; from the block's first coefficient that does not,
+// the rest of the block is written as u32 entries (zigzag | int16 value << 16) at the
+// next even halfword.  binfo[b] = {first halfword, n16 | n32 << 7 | (int16 DC << 16)}:
+// one 8-byte record per block carries the DC too (a difference until k_dcscan sums
+// it in place; absolute with restart intervals).  k_idct scatters the entries into
+// its LDS block.
 struct SparseSink {
   uint32_t* ent;   // image entry area
   uint2* binfo;    // image block info
-  uint32_t n;      // entries written (relative to the image entry area), multiple of 4
-  uint32_t k;      // entries buffered in e0..e3
-  uint32_t e0, e1, e2, e3;
-  uint32_t bstart;
-  uint32_t dcw;    // DC of the open block in the high half
+  uint32_t n;      // halfwords stored (relative to the image entry area), multiple of 8
+  uint32_t k;      // halfwords buffered in w0..w3
+  uint32_t w0, w1, w2, w3;
+  uint32_t bstart, dcw, n16, n32;
+  bool wide;       // the open block has switched to u32 entries
   int32_t b;
   __device__ void open(int32_t first_block) {
-    n = (uint32_t)first_block * 64u;
+    n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
   }
   __device__ void begin(int32_t blk) {
     b = blk;
     bstart = n + k;
     dcw = 0;
+    n16 = n32 = 0;
+    wide = false;
   }
-  __device__ void push(uint32_t e) {
-    e0 = k == 0 ? e : e0;
-    e1 = k == 1 ? e : e1;
-    e2 = k == 2 ? e : e2;
-    e3 = k == 3 ? e : e3;
-    if (++k == 4) {
-      *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
-      n += 4;
+  __device__ void put(uint32_t h) {
+    const uint32_t sh = (k & 1u) * 16u, m = 0xFFFFu << sh, hv = (h & 0xFFFFu) << sh;
+    const uint32_t q = k >> 1;
+    w0 = q == 0 ? (w0 & ~m) | hv : w0;
+    w1 = q == 1 ? (w1 & ~m) | hv : w1;
+    w2 = q == 2 ? (w2 & ~m) | hv : w2;
+    w3 = q == 3 ? (w3 & ~m) | hv : w3;
+    if (++k == 8) {
+      *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
+      n += 8;
       k = 0;
     }
   }
-  __device__ void ac(int zz, int16_t v) { push(((uint32_t)(uint16_t)v << 16) | (uint32_t)zz); }
+  __device__ void ac(int zz, int16_t v) {
+    const uint32_t z = (uint32_t)(zz > 63 ? 63 : zz);  // 64..79 (corrupt streams) share natural position 63
+    if (!wide && v >= -512 && v <= 511) {
+      put(z | ((uint32_t)(v & 0x3FF) << 6));
+      ++n16;
+      return;
+    }
+    if (!wide) {
+      wide = true;
+      if ((n + k) & 1u) put(0u);  // u32 entries start at an even halfword
+    }
+    put(z);
+    put((uint32_t)(uint16_t)v);
+    ++n32;
+  }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void end() { binfo[b] = make_uint2(bstart, (n + k - bstart) | dcw); }
-  __device__ void close() {  // the region is a multiple of 4 entries: a whole-word tail store stays inside it
-    if (k) *(uint4*)(ent + n) = make_uint4(e0, e1, e2, e3);
+  __device__ void end() { binfo[b] = make_uint2(bstart, n16 | (n32 << 7) | dcw); }
+  __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
+    if (k) *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
   }
 };
 
@@ -964,11 +988,12 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   Blk nx = locate(gn < T ? gn : 0);
   uint2 bin = make_uint2(0u, 0u);
   if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
-  uint32_t ea = 0, eb = 0;  // entries l and l + 8 of the next block
+  const uint16_t* ent16 = (const uint16_t*)ent;
+  uint32_t ea = 0, eb = 0;  // halfword entries l and l + 8 of the next block
   auto first_entries = [&]() {
-    const uint32_t c = bin.y & 0xFFFFu;
-    ea = l < c ? ent[bin.x + l] : 0u;
-    eb = l + 8 < c ? ent[bin.x + l + 8] : 0u;
+    const uint32_t c = bin.y & 0x7Fu;
+    ea = l < c ? ent16[bin.x + l] : 0u;
+    eb = l + 8 < c ? ent16[bin.x + l + 8] : 0u;
   };
   if (gn < T) first_entries();
 #pragma unroll
@@ -986,12 +1011,19 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     }
     if (valid) {
       if (l == 0) sb[0] = (int32_t)bi.y >> 16;  // DC (int16, absolute after k_dcscan)
-      const uint32_t cnt = bi.y & 0xFFFFu;
-      if (l < cnt) sb[s_nat[ea & 0x7Fu]] = (int32_t)(int16_t)(ea >> 16);
-      if (l + 8 < cnt) sb[s_nat[eb & 0x7Fu]] = (int32_t)(int16_t)(eb >> 16);
-      for (uint32_t j = l + 16; j < cnt; j += 8) {
-        const uint32_t e = ent[bi.x + j];
-        sb[s_nat[e & 0x7Fu]] = (int32_t)(int16_t)(e >> 16);
+      // halfword entries (zigzag | int10 value << 6), then u32 entries from the next
+      // even halfword (see SparseSink)
+      const uint32_t c16 = bi.y & 0x7Fu, c32 = (bi.y >> 7) & 0x7Fu;
+      if (l < c16) sb[s_nat[ea & 63u]] = (int32_t)(int16_t)ea >> 6;
+      if (l + 8 < c16) sb[s_nat[eb & 63u]] = (int32_t)(int16_t)eb >> 6;
+      for (uint32_t j = l + 16; j < c16; j += 8) {
+        const uint32_t h = ent16[bi.x + j];
+        sb[s_nat[h & 63u]] = (int32_t)(int16_t)h >> 6;
+      }
+      const uint32_t* e32 = ent + ((bi.x + c16 + 1) >> 1);
+      for (uint32_t j = l; j < c32; j += 8) {
+        const uint32_t e = e32[j];
+        sb[s_nat[e & 63u]] = (int32_t)(int16_t)(e >> 16);
       }
     }
     wave_lds_sync();
