@@ -543,13 +543,16 @@ struct SparseSink {
     n16 = n32 = 0;
     wide = false;
   }
+  // w0..w3 are a shift register of halfwords: a new one enters at the top and the
+  // eighth push has moved the first to the bottom (four v_alignbyte per push)
+  __device__ void shift_in(uint32_t h) {
+    w0 = __builtin_amdgcn_alignbyte(w1, w0, 2);
+    w1 = __builtin_amdgcn_alignbyte(w2, w1, 2);
+    w2 = __builtin_amdgcn_alignbyte(w3, w2, 2);
+    w3 = __builtin_amdgcn_alignbyte(h, w3, 2);
+  }
   __device__ void put(uint32_t h) {
-    const uint32_t sh = (k & 1u) * 16u, m = 0xFFFFu << sh, hv = (h & 0xFFFFu) << sh;
-    const uint32_t q = k >> 1;
-    w0 = q == 0 ? (w0 & ~m) | hv : w0;
-    w1 = q == 1 ? (w1 & ~m) | hv : w1;
-    w2 = q == 2 ? (w2 & ~m) | hv : w2;
-    w3 = q == 3 ? (w3 & ~m) | hv : w3;
+    shift_in(h);
     if (++k == 8) {
       *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
       n += 8;
@@ -574,7 +577,10 @@ struct SparseSink {
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
   __device__ void end() { binfo[b] = make_uint2(bstart, n16 | (n32 << 7) | dcw); }
   __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
-    if (k) *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
+    if (k) {
+      for (uint32_t j = k; j < 8; ++j) shift_in(0u);
+      *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
+    }
   }
 };
 
