@@ -29,6 +29,21 @@ DHD int rgb_to_l(int r, int g, int b) { return (r * 19595 + g * 38470 + b * 7471
 
 DHD int clip8i(int v) { return v <= 0 ? 0 : (v >= 255 ? 255 : v); }
 
+// 1/d (d = 1..255) as correctly rounded doubles.  For integers 0 <= n <= d <= 255,
+// (float)(n * (1/d)) equals the float quotient n / d: the double product is within
+// 2^-52 (relative) of n/d, and a quotient with a denominator <= 255 that is not exact
+// in float lies >= 2^-32 (relative) away from every float rounding midpoint.  The
+// same holds for the rationals k/255 below.  (The exhaustive test of both
+// conversions against Pillow over all 2^24 inputs, tests/test_emu_cpu.py, checks it.)
+struct RcpU8 {
+  double v[256];
+  constexpr RcpU8() : v() {
+    for (int d = 1; d < 256; ++d) v[d] = 1.0 / (double)d;
+  }
+};
+inline constexpr RcpU8 kRcpU8{};
+constexpr double kRcp255 = 1.0 / 255.0;
+
 DHD void rgb_to_hsv(int r, int g, int b, int* oh, int* os, int* ov) {
   int maxc = r > g ? (r > b ? r : b) : (g > b ? g : b);
   int minc = r < g ? (r < b ? r : b) : (g < b ? g : b);
@@ -38,11 +53,13 @@ DHD void rgb_to_hsv(int r, int g, int b, int* oh, int* os, int* ov) {
     *os = 0;
     return;
   }
-  float cr = (float)(maxc - minc);
-  float s = cr / (float)maxc;
-  float rc = ((float)(maxc - r)) / cr;
-  float gc = ((float)(maxc - g)) / cr;
-  float bc = ((float)(maxc - b)) / cr;
+  // Convert.c rgb2hsv_row: float quotients (via the exact reciprocal products above)
+  const int cri = maxc - minc;
+  const double rcr = kRcpU8.v[cri];
+  float s = (float)((double)cri * kRcpU8.v[maxc]);
+  float rc = (float)((double)(maxc - r) * rcr);
+  float gc = (float)((double)(maxc - g) * rcr);
+  float bc = (float)((double)(maxc - b) * rcr);
   float h;
   if (r == maxc) {
     h = bc - gc;
@@ -51,7 +68,10 @@ DHD void rgb_to_hsv(int r, int g, int b, int* oh, int* os, int* ov) {
   } else {
     h = (float)(4.0 + (double)gc - (double)rc);
   }
-  h = (float)fmod(((double)h / 6.0 + 1.0), 1.0);
+  // fmod(h / 6.0 + 1.0, 1.0): h is in [-1, 5], so the argument is in (0, 2) and the
+  // remainder is the argument minus 1 when >= 1 (exact)
+  const double x = (double)h / 6.0 + 1.0;
+  h = (float)(x >= 1.0 ? x - 1.0 : x);
   *oh = clip8i((int)((double)h * 255.0));
   *os = clip8i((int)((double)s * 255.0));
 }
@@ -61,9 +81,12 @@ DHD void hsv_to_rgb(int h, int s, int v, int* r, int* g, int* b) {
     *r = *g = *b = v;
     return;
   }
-  int i = (int)floor((double)(float)h * 6.0 / 255.0);
-  float f = (float)((double)(float)h * 6.0 / 255.0 - (double)(float)i);
-  float fs = (float)((double)(float)s / 255.0);
+  // Convert.c hsv2rgb: i = floor(h * 6 / 255), f = its fraction (0 exactly when h * 6
+  // is a multiple of 255), fs = s / 255 — the same values without double divisions
+  const int h6 = h * 6;
+  const int i = h6 / 255;
+  float f = h6 - 255 * i == 0 ? 0.0f : (float)((double)h6 * kRcp255 - (double)i);
+  float fs = (float)((double)s * kRcp255);
   int p = (int)round((double)(float)v * (1.0 - (double)fs));
   int q = (int)round((double)(float)v * (1.0 - (double)(fs * f)));  // fs * f is a float product in C
   int t = (int)round((double)(float)v * (1.0 - (double)fs * (1.0 - (double)f)));
