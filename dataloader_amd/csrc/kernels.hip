@@ -1629,51 +1629,38 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   }
 }
 
+// The normalize + cast epilogue of one u8 value (to_tensor / 255, (x - mean) / std in
+// float32, then the output type); k_final tabulates it per channel.
 template <typename OutT>
-__device__ __forceinline__ void store_out(OutT* out, int64_t o, float f);
+__device__ __forceinline__ OutT out_cast(float f);
 template <>
-__device__ __forceinline__ void store_out<uint16_t>(uint16_t* out, int64_t o, float f) {
-  out[o] = f32_to_bf16(f);
+__device__ __forceinline__ uint16_t out_cast<uint16_t>(float f) {
+  return f32_to_bf16(f);
 }
 template <>
-__device__ __forceinline__ void store_out<float>(float* out, int64_t o, float f) {
-  out[o] = f;
+__device__ __forceinline__ float out_cast<float>(float f) {
+  return f;
 }
 template <>
-__device__ __forceinline__ void store_out<uint8_t>(uint8_t* out, int64_t o, float f) {
-  out[o] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f)));
+__device__ __forceinline__ uint8_t out_cast<uint8_t>(float f) {
+  return f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f)));
 }
 
-// Four adjacent outputs; one vector store when all four are in the row and aligned.
+// Four adjacent output values; one vector store when all four are in the row and aligned.
 template <typename OutT>
-__device__ __forceinline__ void store_out4(OutT* out, int64_t o, const float* f, int n, bool vec);
-template <>
-__device__ __forceinline__ void store_out4<uint16_t>(uint16_t* out, int64_t o, const float* f, int n, bool vec) {
+__device__ __forceinline__ void store_vals4(OutT* out, int64_t o, const OutT* v, int n, bool vec) {
   if (vec) {
-    uint2 u;
-    u.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
-    u.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
-    *(uint2*)(out + o) = u;
+    if (sizeof(OutT) == 2) {
+      *(uint2*)(out + o) = make_uint2((uint32_t)(uint16_t)v[0] | ((uint32_t)(uint16_t)v[1] << 16),
+                                      (uint32_t)(uint16_t)v[2] | ((uint32_t)(uint16_t)v[3] << 16));
+    } else if (sizeof(OutT) == 4) {
+      *(float4*)(out + o) = make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+    } else {
+      *(uint32_t*)(out + o) = (uint32_t)(uint8_t)v[0] | ((uint32_t)(uint8_t)v[1] << 8) |
+                              ((uint32_t)(uint8_t)v[2] << 16) | ((uint32_t)(uint8_t)v[3] << 24);
+    }
   } else {
-    for (int j = 0; j < n; ++j) out[o + j] = f32_to_bf16(f[j]);
-  }
-}
-template <>
-__device__ __forceinline__ void store_out4<float>(float* out, int64_t o, const float* f, int n, bool vec) {
-  if (vec) {
-    *(float4*)(out + o) = make_float4(f[0], f[1], f[2], f[3]);
-  } else {
-    for (int j = 0; j < n; ++j) out[o + j] = f[j];
-  }
-}
-template <>
-__device__ __forceinline__ void store_out4<uint8_t>(uint8_t* out, int64_t o, const float* f, int n, bool vec) {
-  uint8_t q[4];
-  for (int j = 0; j < 4; ++j) q[j] = f32_to_fp8e4m3(bf16_to_f32(f32_to_bf16(f[j])));
-  if (vec) {
-    *(uint32_t*)(out + o) = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
-  } else {
-    for (int j = 0; j < n; ++j) out[o + j] = q[j];
+    for (int j = 0; j < n; ++j) out[o + j] = v[j];
   }
 }
 
@@ -1695,12 +1682,15 @@ struct FinalLds {
 };
 
 __host__ __device__ __forceinline__ int final_tile_pitch(int S, int pad) { return (((S + 3) & ~3) + 2 * pad + 3) & ~3; }
+// LDS reserved for the tile (the largest blur halo)
+__host__ __device__ __forceinline__ int final_tile_bytes(int S) {
+  return 3 * (final_rows(S) + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
+}
 
 template <int KS, typename OutT>
 __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, int tp, int64_t tplane, int nr, int y0,
                                               int S, int ks_rt, const float* __restrict__ k2, bool solarize,
-                                              const dino_aug_config& cfg, const float* __restrict__ nb,
-                                              OutT* __restrict__ out) {
+                                              const OutT* __restrict__ ntab, OutT* __restrict__ out) {
   const int ks = KS > 0 ? KS : ks_rt;
   const int nq = (S + 3) >> 2;
   const int64_t N = (int64_t)S * S;
@@ -1750,12 +1740,12 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
         val[j] = rr <= 0.0f ? 0 : (rr >= 255.0f ? 255 : (int)rr);
       }
     }
-    const float mean = nb ? nb[ch] : cfg.mean[ch], sd = nb ? nb[3 + ch] : cfg.std[ch];
-    float f[4];
+    const OutT* tb = ntab + 256 * ch;
+    OutT o4[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) f[j] = u8_normalize(solarize ? solarize_u8(val[j]) : val[j], mean, sd);
+    for (int j = 0; j < 4; ++j) o4[j] = tb[solarize ? solarize_u8(val[j]) : val[j]];
     const int n = min(4, S - x0);
-    store_out4<OutT>(out, ch * N + (int64_t)(y0 + y) * S + x0, f, n, vec_ok);
+    store_vals4<OutT>(out, ch * N + (int64_t)(y0 + y) * S + x0, o4, n, vec_ok);
   }
 }
 
@@ -1790,6 +1780,14 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   const int tp = final_tile_pitch(S, pad);
   const int64_t tplane = (int64_t)tr * tp;
   if (p.blur && threadIdx.x == 0) gaussian_kernel1d(ks, p.sigma, H.k1);
+  // the epilogue of each u8 value per channel (global or per-image statistics), after
+  // the largest tile the launch reserves
+  OutT* ntab = reinterpret_cast<OutT*>(tile + final_tile_bytes(S));
+  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
+  for (int e = threadIdx.x; e < 3 * 256; e += blockDim.x) {
+    const int c = e >> 8;
+    ntab[e] = out_cast<OutT>(u8_normalize(e & 255, nb ? nb[c] : cfg.mean[c], nb ? nb[3 + c] : cfg.std[c]));
+  }
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
   const int cmean = contrast_mean_from_sum(vp.lsum, N);
@@ -1808,14 +1806,13 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   if (p.blur && threadIdx.x < ks * ks) H.k2[threadIdx.x] = H.k1[threadIdx.x / ks] * H.k1[threadIdx.x % ks];
   __syncthreads();
   const bool sol = p.solarize != 0;
-  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
   switch (ks) {
-    case 1: final_compute<1, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
-    case 3: final_compute<3, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
-    case 5: final_compute<5, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
-    case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
-    case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
-    default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, cfg, nb, out); break;
+    case 1: final_compute<1, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+    case 3: final_compute<3, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+    case 5: final_compute<5, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+    case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+    case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+    default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
   }
 }
 
@@ -2009,7 +2006,7 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   TIMED(tm, kvert, s,
         (k_vert<<<dim3((S + vert_rows(S) - 1) / vert_rows(S), nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, B,
                                                                              a.ws, a.aws, a.gcrop, a.cfg, S)));
-  const int lds = (int)sizeof(FinalLds) + 3 * (final_rows(S) + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
+  const int lds = (int)sizeof(FinalLds) + final_tile_bytes(S) + 3 * 256 * (int)sizeof(OutT);
   TIMED(tm, kfin, s,
         (k_final<OutT><<<dim3((S + final_rows(S) - 1) / final_rows(S), nvc, B), 256, lds, s>>>(
             a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S, a.norm)));
