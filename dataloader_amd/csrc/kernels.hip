@@ -1522,6 +1522,15 @@ __device__ __forceinline__ int64_t crop_slot(const dino_aug_config& cfg, int B, 
   return (int64_t)B * cfg.n_global * g3 + ((int64_t)b * cfg.n_local + (v - cfg.n_global)) * l3;
 }
 
+// Division of non-negative ints by a workgroup-uniform divisor d by one 64-bit
+// multiply: exact whenever e * d < 2^32 (the rounding of m = ceil(2^32 / d) stays
+// below 1/d over that range; here e * d < 2^27 for any view size <= 16384).
+struct FastDiv {
+  uint64_t m;
+  __device__ explicit FastDiv(uint32_t d) : m(((1ull << 32) + d - 1) / d) {}
+  __device__ uint32_t div(uint32_t e) const { return (uint32_t)(((uint64_t)e * m) >> 32); }
+};
+
 // Vertical pass (+ flip) and the ColorJitter ops that precede contrast, over a
 // band of vert_rows(S) output rows; adds the band's L sum to the view's counter.
 // Fast path (planar temp rows, S % 4 == 0): a lane produces 4 adjacent pixels
@@ -1556,8 +1565,10 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   uint32_t lsum = 0;
   if (need_h && (S & 3) == 0) {
     const int nq = S >> 2;
+    const FastDiv dq((uint32_t)nq);
     for (int e = threadIdx.x; e < nr * nq; e += blockDim.x) {
-      const int y = y0 + e / nq, xq = e % nq;
+      const int yl = (int)dq.div((uint32_t)e);
+      const int y = y0 + yl, xq = e - yl * nq;
       uint32_t w[3];
       if (need_v) {
         const int ymin = cvv.bounds[2 * y], ycnt = cvv.bounds[2 * y + 1];
@@ -1695,9 +1706,10 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
   const int nq = (S + 3) >> 2;
   const int64_t N = (int64_t)S * S;
   const bool vec_ok = (S & 3) == 0;
+  const FastDiv dplane((uint32_t)(nr * nq)), drow((uint32_t)nq);
   for (int e = threadIdx.x; e < 3 * nr * nq; e += blockDim.x) {
-    const int ch = e / (nr * nq), rem = e - ch * nr * nq;
-    const int y = rem / nq, x0 = 4 * (rem - (rem / nq) * nq);
+    const int ch = (int)dplane.div((uint32_t)e), rem = e - ch * nr * nq;
+    const int y = (int)drow.div((uint32_t)rem), x0 = 4 * (rem - y * nq);
     const uint8_t* pl = tile + ch * tplane;
     int val[4];
     if (KS == 1) {
@@ -1791,8 +1803,9 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
   const int cmean = contrast_mean_from_sum(vp.lsum, N);
+  const FastDiv dtw((uint32_t)tw);
   for (int e = threadIdx.x; e < tr * tw; e += blockDim.x) {
-    const int lr = e / tw, tc = e - lr * tw;
+    const int lr = (int)dtw.div((uint32_t)e), tc = e - lr * tw;
     const int sr = reflect_idx(y0 - pad + lr, S), sc = reflect_idx(tc - pad, S);
     const int64_t so = (int64_t)sr * S + sc;
     int r = crop[so], g = crop[N + so], bb = crop[2 * N + so];
