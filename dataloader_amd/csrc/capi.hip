@@ -64,6 +64,8 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
   dino_limits L = *limits;
   if (L.max_batch <= 0 || L.max_views <= 0 || L.max_crop_size <= 0)
     return fail(DINO_EINVAL, "dino_ctx_create: max_batch/max_views/max_crop_size must be > 0%s%lld");
+  if (L.max_crop_size > 1024)  // k_final's LDS tile and its 32-bit index arithmetic are sized for S <= 1024
+    return fail(DINO_EINVAL, "dino_ctx_create: max_crop_size %s%lld > 1024", "", L.max_crop_size);
   if (L.max_image_dim <= 0) L.max_image_dim = 8192;
   if (L.max_image_dim > 16384)  // pixel indices of the colour/resize kernels are 32-bit
     return fail(DINO_EINVAL, "dino_ctx_create: max_image_dim %s%lld > 16384", "", L.max_image_dim);

@@ -1524,7 +1524,8 @@ __device__ __forceinline__ int64_t crop_slot(const dino_aug_config& cfg, int B, 
 
 // Division of non-negative ints by a workgroup-uniform divisor d by one 64-bit
 // multiply: exact whenever e * d < 2^32 (the rounding of m = ceil(2^32 / d) stays
-// below 1/d over that range; here e * d < 2^27 for any view size <= 16384).
+// below 1/d over that range; here e * d < 2^26 for any view size <= 1024, the
+// dino_ctx_create limit).
 struct FastDiv {
   uint64_t m;
   __device__ explicit FastDiv(uint32_t d) : m(((1ull << 32) + d - 1) / d) {}

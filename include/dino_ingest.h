@@ -66,7 +66,7 @@ typedef struct dino_ctx dino_ctx;
 typedef struct dino_limits {
   int32_t max_batch;           /* images per call */
   int32_t max_views;           /* views per image (n_global + n_local) */
-  int32_t max_crop_size;       /* largest S of any view */
+  int32_t max_crop_size;       /* largest S of any view (<= 1024) */
   int32_t max_image_dim;       /* largest JPEG width or height accepted (<= 16384; 0 -> 8192) */
   int64_t workspace_bytes;     /* decode workspace (HBM); 0 -> default */
 } dino_limits;

@@ -41,6 +41,8 @@ def test_bad_arguments_rejected_before_any_launch():
     ctx = ctypes.c_void_p()
     assert lib.dino_ctx_create(0, ctypes.byref(DinoLimits(0, 10, 224, 4096, 0)), ctypes.byref(ctx)) == -1
     assert b"max_batch" in lib.dino_last_error()
+    assert lib.dino_ctx_create(0, ctypes.byref(DinoLimits(4, 10, 2048, 4096, 0)), ctypes.byref(ctx)) == -1
+    assert b"max_crop_size" in lib.dino_last_error()
     assert lib.dino_decode(None, None, None, 1, None, None) == -1
     assert lib.dino_masks(0, 4, 2, 1, 2, 0.0, 1.0, 1, None, None, None, None) == -1
 
