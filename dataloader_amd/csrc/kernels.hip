@@ -499,6 +499,7 @@ struct HuffLds {     // k_huff1
   ImgDesc sd;
   HuffTables tab;
   RangeOut R[kHuffThreads];
+  uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
 struct HuffLds3 {    // k_huff3 (no lane exchange)
@@ -693,15 +694,31 @@ __device__ int huff_item_image(const ImgDesc* desc, int B, int item) {
   return lo;
 }
 
+// An image of one segment without restart intervals and with short lane ranges is
+// decoded completely by k_huff1 (its lanes' start states are final after the
+// in-segment rounds).  Long ranges stay with k_huff3: in k_huff1 their second
+// decode would double the longest serial chain of the launch.
+#ifndef DINO_HUFF_FUSE_SUB_BITS
+#define DINO_HUFF_FUSE_SUB_BITS 3072
+#endif
+__device__ __forceinline__ bool huff_single_segment(const ImgDesc& d) {
+  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= DINO_HUFF_FUSE_SUB_BITS;
+}
+
 // Loads work item `item`'s image descriptor and tables into LDS; false past the end.
+// With skip_single, the tables of a single-segment image are not loaded (L.img = -2).
 template <typename LdsT>
-__device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_t* ws, int item) {
+__device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_t* ws, int item, bool skip_single = false) {
   if (threadIdx.x == 0) {
     L.img = huff_item_image(desc, B, item);
-    if (L.img >= 0) L.sd = desc[L.img];
+    if (L.img >= 0) {
+      L.sd = desc[L.img];
+      if (skip_single && huff_single_segment(L.sd)) L.img = -2;
+    }
   }
   __syncthreads();
-  if (L.img < 0) return false;
+  if (L.img == -1) return false;
+  if (L.img == -2) return true;
   const uint4* src = (const uint4*)(ws + L.sd.htab_off);
   uint4* dst = (uint4*)&L.tab;
   for (int k = threadIdx.x; k < (int)(sizeof(HuffTables) / 16); k += kHuffThreads) dst[k] = src[k];
@@ -754,7 +771,21 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
-    if (active) {
+    if (huff_single_segment(sd)) {
+      // the whole image is this segment: its start states are final, so the blocks
+      // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
+      uint32_t tot;
+      const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)L.R[t].nblk : 0u, L.wave, &tot);
+      if (active) {
+        SparseSink sink;
+        sink.ent = (uint32_t*)(ws + sd.coef_off);
+        sink.binfo = (uint2*)(ws + sd.binfo_off);
+        sink.open((int32_t)blk0);
+        decode_write<kSrcPadded>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
+                                 sink);
+        sink.close();
+      }
+    } else if (active) {
       LaneRec& o = lr[i];
       o.S = myS;
       o.R = L.R[t];
@@ -775,7 +806,7 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
   __shared__ uint32_t s_wave[kHuff2Threads / 64];
   const ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
-  if (d.status != DINO_IMG_OK || d.restart_interval > 0) return;
+  if (d.status != DINO_IMG_OK || d.restart_interval > 0 || huff_single_segment(d)) return;
   const int n = d.h_lanes;
   LaneRec* lr = (LaneRec*)(ws + d.hlane_off);
   if (n > kHuffThreads) {  // several segments: their first lanes started from guesses
@@ -830,7 +861,11 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
   HuffLds3& L = *reinterpret_cast<HuffLds3*>(smem);
   const int t = threadIdx.x;
   for (int item = blockIdx.x;; item += gridDim.x) {
-    if (!huff_load_item(L, desc, B, ws, item)) return;
+    if (!huff_load_item(L, desc, B, ws, item, true)) return;
+    if (L.img == -2) {  // decoded by k_huff1
+      __syncthreads();
+      continue;
+    }
     const ImgDesc& sd = L.sd;
     HuffImage im;
     hi_init(im, &L.tab, sd.mcu_comp, sd.blocks_per_mcu);
