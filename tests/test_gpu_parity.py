@@ -35,7 +35,9 @@ ONE_LEVEL = 1.0 / 255.0 / STD_MIN
 def _jpeg_zoo():
     rng = np.random.default_rng(123)
     out = []
-    for (w, h) in [(64, 64), (225, 333), (640, 480), (17, 9), (8, 8), (33, 17), (1, 1), (1601, 1203)]:
+    # 640x480: one segment, short lanes (finished by k_huff1); 1024x768: one segment, long
+    # lanes (k_huff3); 1601x1203: several segments (k_huff2 cross-segment sync)
+    for (w, h) in [(64, 64), (225, 333), (640, 480), (17, 9), (8, 8), (33, 17), (1, 1), (1024, 768), (1601, 1203)]:
         for sub in (0, 1, 2):
             out.append(encode_jpeg(textured_rgb(w, h, rng), quality=85, subsampling=sub))
     out.append(encode_jpeg(textured_rgb(200, 150, rng), gray=True))
