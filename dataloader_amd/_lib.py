@@ -16,8 +16,10 @@ _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "libdino_ingest.so"
 
 DINO_OK = 0
-IMG_STATUS = {0: "ok", -1: "corrupt", -2: "truncated", -3: "bad-data", -4: "too-large",
-              1: "unsupported", 2: "multi-scan"}
+IMG_STATUS = {0: "ok", -1: "corrupt", -2: "truncated", -3: "bad-data", -4: "too-large (Pillow bomb check)",
+              1: "unsupported", 2: "multi-scan", 3: "no-space", 4: "over max_image_dim"}
+ABI_VERSION = 2
+RAW_MAGIC = 0x42475244  # "DRGB": pre-decoded RGB container (include/dino_ingest.h)
 
 _lib = None
 
@@ -57,6 +59,12 @@ def load() -> ctypes.CDLL:
         "dino_tar_last_error": (ctypes.c_char_p, []),
         "dino_gather": (i32, [vp, vp, i64, vp, i64, vp, i32]),
         "dino_set_norm": (i32, [vp, vp, i32]),
+        "dino_batch_info": (i32, [vp, vp, vp]),
+        "dino_probe": (i32, [vp, vp, i32, i32, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(i64),
+                             ctypes.POINTER(i64)]),
+        "dino_reserve": (i32, [vp, i64, i64]),
+        "dino_workspace_sizes": (i32, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+        "dino_masks_host": (i32, [i32, i32, i32, i32, i32, dbl, dbl, i32, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -76,4 +84,5 @@ def exported_symbols() -> list[str]:
     return ["dino_abi_version", "dino_last_error", "dino_ctx_create", "dino_ctx_destroy", "dino_decode",
             "dino_copy_rgb", "dino_sample_params", "dino_augment", "dino_run_batch", "dino_masks",
             "dino_bf16_to_fp8", "dino_debug_region", "dino_set_timing", "dino_kernel_times",
-            "dino_tar_index", "dino_tar_last_error", "dino_gather", "dino_set_norm"]
+            "dino_tar_index", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
+            "dino_probe", "dino_reserve", "dino_workspace_sizes", "dino_masks_host"]

@@ -11,8 +11,13 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
+#include "jpeg_parse.hpp"
 #include "kernels.hpp"
+#include "mask.hpp"
+#include "plan.hpp"
+#include "progressive.hpp"
 
 using namespace dino;
 
@@ -48,6 +53,7 @@ struct dino_ctx {
   const float* d_norm = nullptr;  // per-image normalisation (dino_set_norm), nullable
   int32_t norm_n = 0;
   int32_t last_batch = -1;
+  LaunchGeom geom{};
   KernelTimer* timer = nullptr;
   KernelTimer* tm() { return timer && timer->enabled ? timer : nullptr; }
 };
@@ -66,7 +72,7 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
     return fail(DINO_EINVAL, "dino_ctx_create: max_batch/max_views/max_crop_size must be > 0%s%lld");
   if (L.max_crop_size > 1024)  // k_final's LDS tile and its 32-bit index arithmetic are sized for S <= 1024
     return fail(DINO_EINVAL, "dino_ctx_create: max_crop_size %s%lld > 1024", "", L.max_crop_size);
-  if (L.max_image_dim <= 0) L.max_image_dim = 8192;
+  if (L.max_image_dim <= 0) L.max_image_dim = 16384;
   if (L.max_image_dim > 16384)  // pixel indices of the colour/resize kernels are 32-bit
     return fail(DINO_EINVAL, "dino_ctx_create: max_image_dim %s%lld > 16384", "", L.max_image_dim);
   hipError_t e = hipSetDevice(device);
@@ -74,6 +80,10 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
   dino_ctx* c = new dino_ctx();
   c->device = device;
   c->lim = L;
+  if ((e = init_launch_geom(device, &c->geom)) != hipSuccess) {
+    delete c;
+    return hip_fail(e, "dino_ctx_create: launch geometry");
+  }
   // decode workspace: default 16 MiB per image of the batch (a 1600x2133 JPEG needs ~26 MiB,
   // a 640x480 one ~2.4 MiB; images that do not fit are reported DINO_IMG_TOO_LARGE)
   c->ws_size = L.workspace_bytes > 0 ? L.workspace_bytes : (int64_t)L.max_batch * (16ll << 20);
@@ -119,7 +129,7 @@ int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, i
   if (batch < 0 || batch > c->lim.max_batch)
     return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
   hipStream_t s = (hipStream_t)stream;
-  DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size};
+  DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size, c->geom};
   hipError_t e = launch_decode(a, s, c->tm());
   if (e != hipSuccess) return hip_fail(e, "dino_decode");
   if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
@@ -194,10 +204,89 @@ int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets
   if (!c) return fail(DINO_EINVAL, "dino_run_batch: null ctx%s%lld");
   int r = check_cfg(c, cfg);
   if (r) return r;
-  if ((r = dino_decode(c, d_bytes, d_offsets, batch, d_info, stream))) return r;
+  if ((r = dino_decode(c, d_bytes, d_offsets, batch, nullptr, stream))) return r;
   dino_view_params* prm = d_params_out ? d_params_out : c->d_params;
   if ((r = dino_sample_params(c, cfg, seed, batch_index, prm, stream))) return r;
-  return dino_augment(c, cfg, prm, d_views, stream);
+  if ((r = dino_augment(c, cfg, prm, d_views, stream))) return r;
+  return d_info ? dino_batch_info(c, d_info, stream) : DINO_OK;
+}
+
+int dino_batch_info(dino_ctx* c, int32_t* d_info, void* stream) {
+  if (!c || !d_info) return fail(DINO_EINVAL, "dino_batch_info: null argument%s%lld");
+  if (c->last_batch < 0) return fail(DINO_EINVAL, "dino_batch_info: no decoded batch%s%lld");
+  hipError_t e = launch_info(c->d_desc, c->last_batch, d_info, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_batch_info");
+}
+
+int dino_reserve(dino_ctx* c, int64_t ws_bytes, int64_t aws_bytes) {
+  if (!c || ws_bytes < 0 || aws_bytes < 0) return fail(DINO_EINVAL, "dino_reserve: bad arguments%s%lld");
+  if (ws_bytes <= c->ws_size && aws_bytes <= c->aws_size) return DINO_OK;
+  hipError_t e = hipSetDevice(c->device);
+  if (e == hipSuccess) e = hipDeviceSynchronize();  // in-flight batches may still use the old buffers
+  if (e != hipSuccess) return hip_fail(e, "dino_reserve: synchronize");
+  if (ws_bytes > c->ws_size) {
+    const int64_t n = ws_bytes + ws_bytes / 8;  // headroom: fewer regrowths
+    (void)hipFree(c->d_ws);
+    c->d_ws = nullptr;
+    c->ws_size = 0;
+    if ((e = hipMalloc(&c->d_ws, n)) != hipSuccess) return hip_fail(e, "dino_reserve: hipMalloc(workspace)");
+    c->ws_size = n;
+  }
+  if (aws_bytes > c->aws_size) {
+    const int64_t n = aws_bytes + aws_bytes / 8;
+    (void)hipFree(c->d_aws);
+    c->d_aws = nullptr;
+    c->aws_size = 0;
+    if ((e = hipMalloc(&c->d_aws, n)) != hipSuccess) return hip_fail(e, "dino_reserve: hipMalloc(augment workspace)");
+    c->aws_size = n;
+  }
+  c->last_batch = -1;  // the decoded batch (if any) lived in the old workspace
+  return DINO_OK;
+}
+
+int dino_workspace_sizes(dino_ctx* c, int64_t* ws_bytes, int64_t* aws_bytes) {
+  if (!c || !ws_bytes || !aws_bytes) return fail(DINO_EINVAL, "dino_workspace_sizes: null argument%s%lld");
+  *ws_bytes = c->ws_size;
+  *aws_bytes = c->aws_size;
+  return DINO_OK;
+}
+
+int dino_probe(const uint8_t* bytes, const int64_t* offsets, int32_t batch, int32_t max_image_dim,
+               const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need) {
+  if ((!bytes && batch > 0) || !offsets || batch < 0 || !ws_need || !aws_need)
+    return fail(DINO_EINVAL, "dino_probe: bad arguments%s%lld");
+  if (max_image_dim <= 0) max_image_dim = 16384;
+  int64_t ws = 0, aws = 0;
+  std::vector<ScanRec> scans(kMaxScans);
+  for (int32_t i = 0; i < batch; ++i) {
+    const int64_t off = offsets[i], len = offsets[i + 1] - off;
+    ImgDesc d;
+    if (len <= 0) {
+      d.status = DINO_IMG_CORRUPT;
+      d.width = d.height = d.ncomp = 0;
+    } else {
+      parse_jpeg(bytes + off, len, max_image_dim, &d);
+      if (d.status == DINO_IMG_OK && d.kind == 1) {
+        HostMarkerFinder find;
+        prog_walk(bytes + off, len, &d, scans.data(), find);
+      }
+    }
+    if (info) {
+      info[4 * i + 0] = d.status;
+      info[4 * i + 1] = d.status == DINO_IMG_OK || d.status > 0 ? d.width : 0;
+      info[4 * i + 2] = d.status == DINO_IMG_OK || d.status > 0 ? d.height : 0;
+      info[4 * i + 3] = d.status == DINO_IMG_OK ? d.kind : -1;
+    }
+    if (d.status != DINO_IMG_OK) continue;
+    ws += image_chunk_bytes(d).total();
+    if (cfg) {
+      for (int v = 0; v < cfg->n_global + cfg->n_local; ++v)
+        aws += view_scratch_bound(v < cfg->n_global ? cfg->global_size : cfg->local_size, d.width, d.height);
+    }
+  }
+  *ws_need = ws;
+  *aws_need = aws;
+  return DINO_OK;
 }
 
 int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,
@@ -208,14 +297,30 @@ int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32
   if (num_masking_patches < 0 || num_masking_patches > height * width)
     return fail(DINO_EINVAL, "dino_masks: num_masking_patches %s%lld out of range", "", num_masking_patches);
   if (n_masks == 0) return DINO_OK;
-  hipStream_t s = (hipStream_t)stream;
-  int32_t* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, sizeof(int32_t) * height * width, s);
-  if (e != hipSuccess) return hip_fail(e, "dino_masks(scratch)");
-  e = launch_masks(height, width, num_masking_patches, min_num_patches, max_num_patches, log_aspect_min,
-                   log_aspect_max, n_masks, d_py_state, d_np_state, d_out, scratch, s);
-  (void)hipFreeAsync(scratch, s);
+  if ((int64_t)height * width > 8192)
+    return fail(DINO_EINVAL, "dino_masks: grid of %s%lld patches (> 8192; use dino_masks_host)", "",
+                (long long)height * width);
+  hipError_t e = launch_masks(height, width, num_masking_patches, min_num_patches, max_num_patches, log_aspect_min,
+                              log_aspect_max, n_masks, d_py_state, d_np_state, d_out, (hipStream_t)stream);
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_masks");
+}
+
+int dino_masks_host(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,
+                    int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
+                    uint32_t* py_state, uint32_t* np_state, uint8_t* out) {
+  if (height <= 0 || width <= 0 || n_masks < 0 || !py_state || !np_state || (!out && n_masks))
+    return fail(DINO_EINVAL, "dino_masks_host: bad arguments%s%lld");
+  if (num_masking_patches < 0 || num_masking_patches > height * width)
+    return fail(DINO_EINVAL, "dino_masks_host: num_masking_patches %s%lld out of range", "", num_masking_patches);
+  MaskParams mp{height, width, num_masking_patches, min_num_patches, max_num_patches, log_aspect_min, log_aspect_max};
+  MtState py, np;
+  mt_load(py, py_state);
+  mt_load(np, np_state);
+  std::vector<int32_t> scratch((size_t)height * width);
+  for (int32_t k = 0; k < n_masks; ++k) gen_mask(mp, py, np, out + (int64_t)k * height * width, scratch.data());
+  mt_store(py, py_state);
+  mt_store(np, np_state);
+  return DINO_OK;
 }
 
 int dino_set_timing(dino_ctx* c, int32_t enable) {

@@ -204,9 +204,9 @@ DHD void bc_skip(BitCursor& c, int n) {
 // Symbol whose code is longer than LB bits (jpeg_huff_decode's bit-serial loop,
 // incl. the l = 17 "fake zero").  The maxcode values are read up front and the
 // length found by comparisons, so the lane waits on LDS once, not per bit.
+// p17: the next 17 bits of the stream (code of up to 16 bits + sentinel).
 template <int LB>
-DHD void huff_slow(const BitCursor& c, const HuffTableT<LB>* t, int* sym, int* len) {
-  const uint32_t p17 = bc_peek(c, 17);  // code of up to 16 bits + sentinel
+DHD void huff_slow_bits(uint32_t p17, const HuffTableT<LB>* t, int* sym, int* len) {
   int32_t mc[17 - LB], vo[17 - LB];
 #pragma unroll
   for (int k = 0; k < 17 - LB; ++k) {
@@ -229,6 +229,11 @@ DHD void huff_slow(const BitCursor& c, const HuffTableT<LB>* t, int* sym, int* l
   const int code = (int)(p17 >> (17 - l));
   *sym = t->huffval[(code + off) & 255];
   *len = l;
+}
+
+template <int LB>
+DHD void huff_slow(const BitCursor& c, const HuffTableT<LB>* t, int* sym, int* len) {
+  huff_slow_bits(bc_peek(c, 17), t, sym, len);
 }
 
 // Decoder state between steps.

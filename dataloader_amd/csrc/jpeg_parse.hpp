@@ -25,16 +25,54 @@ DHD int rd16(const uint8_t* p) { return (p[0] << 8) | p[1]; }
 
 // Parse markers of one JPEG held in p[0..len).  Fills geometry, tables and the
 // entropy-data offset.  Returns d->status.
+// Pillow's DecompressionBombError threshold: 2 x Image.MAX_IMAGE_PIXELS (PIL/Image.py).
+constexpr int64_t kPilBombPixels = 2ll * 89478485;
+
+DHD uint32_t rd32le(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// Size checks shared by both image kinds: Pillow refuses decompression bombs at
+// Image.open (the reference then zero-fills); images above the ctx's dimension limit
+// are left to the caller.
+DHD int check_dims(ImgDesc* d, int max_dim) {
+  if ((int64_t)d->width * d->height > kPilBombPixels) return (d->status = DINO_IMG_TOO_LARGE);
+  if (d->width > max_dim || d->height > max_dim) return (d->status = DINO_IMG_LIMIT);
+  return d->status;
+}
+
 DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
   d->status = DINO_IMG_CORRUPT;
   d->width = d->height = d->ncomp = 0;
   d->restart_interval = 0;
   d->scan_off = d->scan_len = 0;
+  d->kind = 0;
+  d->progressive = 0;
+  d->first_sos = 0;
+  d->n_scans = 0;
+  d->qt_seen_mask = 0;
+  d->aug_status = 0;
+  d->total_blocks = 0;
   for (int i = 0; i < 8; ++i) d->huff_off[i] = -1;
   for (int t = 0; t < 4; ++t)
     for (int k = 0; k < 64; ++k) d->qt[t][k] = 0;
   bool qt_seen[4] = {false, false, false, false};
-  if (len < 4 || p[0] != 0xFF || p[1] != 0xD8) return d->status;
+  // pre-decoded RGB container (include/dino_ingest.h DINO_RAW_MAGIC)
+  if (len >= 16 && rd32le(p) == DINO_RAW_MAGIC) {
+    const uint32_t w = rd32le(p + 4), h = rd32le(p + 8);
+    if (w < 1 || h < 1 || w > 65535 || h > 65535 || (int64_t)w * h * 3 > len - 16) return d->status;
+    d->kind = 2;
+    d->width = (int32_t)w;
+    d->height = (int32_t)h;
+    d->ncomp = 3;
+    d->color = kRGB;
+    d->scan_off = 16;
+    d->scan_len = (int32_t)((int64_t)w * h * 3 > 0x7FFFFFFF ? 0x7FFFFFFF : (int64_t)w * h * 3);
+    d->status = DINO_IMG_OK;
+    return check_dims(d, max_dim);
+  }
+  // Pillow's _accept: the file must start with FF D8 FF
+  if (len < 4 || p[0] != 0xFF || p[1] != 0xD8 || p[2] != 0xFF) return d->status;
 
   bool saw_sof = false, saw_jfif = false, saw_adobe = false;
   int adobe_transform = 0;
@@ -54,16 +92,21 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
     int n = seglen - 2;
     switch (m) {
       case 0xC0:
-      case 0xC1: {  // SOF0 baseline / SOF1 extended sequential, Huffman
+      case 0xC1:
+      case 0xC2: {  // SOF0 baseline / SOF1 extended sequential / SOF2 progressive, Huffman
         if (saw_sof || n < 6) return (d->status = DINO_IMG_CORRUPT);
         saw_sof = true;
+        d->progressive = m == 0xC2;
         int prec = s[0];
         d->height = rd16(s + 1);
         d->width = rd16(s + 3);
         int nf = s[5];
         if (n < 6 + 3 * nf || nf <= 0) return (d->status = DINO_IMG_CORRUPT);
-        if (prec != 8) return (d->status = DINO_IMG_UNSUPPORTED);
-        if (nf != 1 && nf != 3) return (d->status = DINO_IMG_UNSUPPORTED);
+        // Pillow's SOF handler raises for precision != 8 and for layer counts other than
+        // 1, 3, 4 (JpegImagePlugin.SOF): the reference zero-fills those
+        if (prec != 8) return (d->status = DINO_IMG_CORRUPT);
+        if (nf != 1 && nf != 3 && nf != 4) return (d->status = DINO_IMG_CORRUPT);
+        if (nf == 4) return (d->status = DINO_IMG_UNSUPPORTED);  // CMYK / YCCK
         if (d->height == 0) return (d->status = DINO_IMG_UNSUPPORTED);  // DNL
         if (d->width == 0) return (d->status = DINO_IMG_CORRUPT);
         d->ncomp = nf;
@@ -78,8 +121,10 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
         }
         break;
       }
-      case 0xC2: case 0xC3: case 0xC5: case 0xC6: case 0xC7:
+      case 0xC3: case 0xC5: case 0xC6: case 0xC7:
       case 0xC9: case 0xCA: case 0xCB: case 0xCD: case 0xCE: case 0xCF:
+        // lossless / hierarchical / arithmetic: left to the host (Pillow decides)
+        if (n >= 1 && s[0] != 8) return (d->status = DINO_IMG_CORRUPT);  // Pillow: "cannot handle N-bit layers"
         return (d->status = DINO_IMG_UNSUPPORTED);
       case 0xCC:  // DAC: arithmetic coding
         return (d->status = DINO_IMG_UNSUPPORTED);
@@ -129,20 +174,32 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
         if (!saw_sof || n < 1) return (d->status = DINO_IMG_CORRUPT);
         int ns = s[0];
         if (n < 4 + 2 * ns || ns < 1 || ns > 4) return (d->status = DINO_IMG_CORRUPT);
-        if (ns != d->ncomp) return (d->status = DINO_IMG_MULTISCAN);
-        for (int k = 0; k < ns; ++k) {
-          int cs = s[1 + 2 * k], t = s[2 + 2 * k];
+        // One interleaved scan of every component in frame order decodes on the
+        // baseline path; anything else (progressive, components spread over several
+        // scans, another component order) on the coefficient-buffer path (k_prog),
+        // whose marker walk re-reads this SOS.
+        bool one_scan = !d->progressive && ns == d->ncomp;
+        for (int k = 0; k < ns && one_scan; ++k) {
+          int cs = s[1 + 2 * k];
           int ci = -1;
           for (int c = 0; c < d->ncomp; ++c)
             if (d->comp[c].id == cs) ci = c;
-          if (ci < 0) return (d->status = DINO_IMG_CORRUPT);        // JERR_BAD_COMPONENT_ID
-          if (ci != k) return (d->status = DINO_IMG_UNSUPPORTED);   // scan order != frame order
-          d->comp[ci].td = t >> 4;
-          d->comp[ci].ta = t & 15;
-          if (d->comp[ci].td > 3 || d->comp[ci].ta > 3) return (d->status = DINO_IMG_CORRUPT);
+          if (ci != k) one_scan = false;
         }
-        int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahal = s[3 + 2 * ns];
-        if (ss != 0 || se != 63 || ahal != 0) return (d->status = DINO_IMG_UNSUPPORTED);
+        if (!one_scan) {
+          d->kind = 1;
+          d->first_sos = (int32_t)(pos - 2);
+          d->scan_off = (int32_t)(pos + seglen);
+          d->scan_len = (int32_t)(len - d->scan_off);
+          goto have_scan;
+        }
+        for (int k = 0; k < ns; ++k) {
+          int t = s[2 + 2 * k];
+          d->comp[k].td = t >> 4;
+          d->comp[k].ta = t & 15;
+          if (d->comp[k].td > 3 || d->comp[k].ta > 3) return (d->status = DINO_IMG_CORRUPT);
+        }
+        // Ss/Se/Ah/Al of a sequential scan are ignored (libjpeg: JWRN_NOT_SEQUENTIAL warning)
         d->scan_off = (int32_t)(pos + seglen);
         d->scan_len = (int32_t)(len - d->scan_off);
         goto have_scan;
@@ -154,12 +211,17 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
   }
 
 have_scan:
-  if (d->width > max_dim || d->height > max_dim) return (d->status = DINO_IMG_TOO_LARGE);
-  for (int c = 0; c < d->ncomp; ++c) {
-    const CompDesc& cd = d->comp[c];
-    if (!qt_seen[cd.tq]) return (d->status = DINO_IMG_CORRUPT);  // libjpeg JERR_NO_QUANT_TABLE
-    if (d->huff_off[cd.td] < 0 || d->huff_off[4 + cd.ta] < 0)
-      return (d->status = DINO_IMG_CORRUPT);                      // JERR_NO_HUFF_TABLE
+  d->status = DINO_IMG_OK;
+  if (check_dims(d, max_dim) != DINO_IMG_OK) return d->status;
+  d->status = DINO_IMG_CORRUPT;
+  for (int t = 0; t < 4; ++t) d->qt_seen_mask |= qt_seen[t] ? 1 << t : 0;
+  if (d->kind == 0) {  // (kind 1: tables and quant latching are checked per scan by prog_walk)
+    for (int c = 0; c < d->ncomp; ++c) {
+      const CompDesc& cd = d->comp[c];
+      if (!qt_seen[cd.tq]) return (d->status = DINO_IMG_CORRUPT);  // libjpeg JERR_NO_QUANT_TABLE
+      if (d->huff_off[cd.td] < 0 || d->huff_off[4 + cd.ta] < 0)
+        return (d->status = DINO_IMG_CORRUPT);                      // JERR_NO_HUFF_TABLE
+    }
   }
   // colour space (jdapimin.c default_decompress_parms)
   if (d->ncomp == 1) {

@@ -23,6 +23,8 @@
 #include "jpeg_parse.hpp"
 #include "kernels.hpp"
 #include "mask.hpp"
+#include "plan.hpp"
+#include "progressive.hpp"
 #include "sampler.hpp"
 
 #include <stdio.h>
@@ -42,6 +44,8 @@ __global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __rest
   if (len <= 0) {
     d.status = DINO_IMG_CORRUPT;
     d.width = d.height = d.ncomp = 0;
+    d.kind = 0;
+    d.aug_status = 0;
   } else {
     parse_jpeg(bytes + off, len, max_dim, &d);
   }
@@ -51,67 +55,33 @@ __global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __rest
 // ---------------------------------------------------------------------------
 // k_plan: exclusive scan of per-image chunk sizes (single workgroup of 1024)
 // ---------------------------------------------------------------------------
-// Checkpoints + DC differences of the speculative Huffman decode (no restart intervals).
-// Per-lane state of the speculative decode (global, k_huff1 -> k_huff2 -> k_huff3).
-struct LaneRec {
-  HState S;       // start state used by the lane's current decode
-  RangeOut R;     // its result
-  RangeOut R1;    // result of the first (guessed-state) decode, for checkpoint syncs
-  int32_t ncp;    // checkpoints recorded by the first decode
-  int32_t blk0;   // first block the lane emits (k_huff2 scan)
-  HState W;       // k_huff2 scratch: wanted start state
-  int32_t pad;
-};
-static_assert(sizeof(LaneRec) == 68, "LaneRec layout");
-
-// Lanes reserved for the speculative Huffman decode (restart images decode per interval).
-__device__ int32_t huff_lanes_cap(const ImgDesc& d) {
-  if (d.restart_interval > 0) return 0;
-  const int64_t nbits = ((int64_t)d.scan_len + 64) * 8;  // >= the destuffed stream
-  const int64_t seg = nbits <= kHuffSegBits ? 1 : (nbits + kHuffSegBits - 1) / kHuffSegBits;
-  return (int32_t)(seg * kHuffThreads);
-}
-
-// Byte sizes of an image's workspace regions, in chunk order: destuffed entropy
-// bytes, restart offsets, sparse coefficient entries (64 u32 per block, see
-// SparseSink), block info (uint2 per block), component planes, RGB, speculative
-// checkpoints.
-// Sparse entry capacity per block (see SparseSink): 63 u32 entries + 1 alignment halfword.
-constexpr int kEntHalfwordsPerBlock = 128;
-
-struct ChunkSizes {
-  int64_t ent, rst, coef, binfo, plane, rgb, cps, htab, hlane, dspart;
-  __device__ int64_t total() const {
-    return ent + rst + coef + binfo + plane + rgb + cps + htab + hlane + dspart;
+// Places the image at `base` (or marks it DINO_IMG_NO_SPACE).
+__device__ void plan_place(ImgDesc& d, const ChunkSizes& z, int64_t base, int64_t ws_size) {
+  const int64_t sz = z.total();
+  if (sz == 0) return;
+  if (base < 0 || base + sz > ws_size) {
+    d.status = DINO_IMG_NO_SPACE;
+    return;
   }
-};
-
-// Destuff work items of an image: 32 KiB parts of its scan (>= 1, so that the
-// descriptor is always completed by k_destuff_write).
-constexpr int kDsPartBytes = 32 * 1024;
-__device__ __forceinline__ int ds_parts(const ImgDesc& d) {
-  return d.status != DINO_IMG_OK ? 0 : max(1, (d.scan_len + 16 + kDsPartBytes - 1) / kDsPartBytes);
+  d.base = base;
+  d.ent_off = base;
+  d.rst_off = d.ent_off + z.ent;
+  d.coef_off = d.rst_off + z.rst;
+  d.binfo_off = d.coef_off + z.coef;
+  d.plane_off = d.binfo_off + z.binfo;
+  d.rgb_off = d.plane_off + z.plane;
+  d.cps_off = d.rgb_off + z.rgb;
+  d.htab_off = d.cps_off + z.cps;
+  d.hlane_off = d.htab_off + z.htab;
+  d.dspart_off = d.hlane_off + z.hlane;
+  d.h_lanes_cap = huff_lanes_cap(d);
 }
 
-__device__ ChunkSizes image_chunk_bytes(const ImgDesc& d) {
-  ChunkSizes z{};
-  if (d.status != DINO_IMG_OK) return z;
-  z.ent = align16((int64_t)d.scan_len + 64);
-  z.rst = align16(4 * ((int64_t)d.n_rst_max + 1));
-  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;
-  z.binfo = align16((int64_t)d.total_blocks * 8);
-  int64_t p = 0;
-  for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
-  z.plane = align16(p);
-  z.rgb = align16((int64_t)d.width * d.height * 3 + 16);
-  const int64_t lanes = huff_lanes_cap(d);
-  z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
-  z.htab = align16((int64_t)sizeof(HuffTables));
-  z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
-  z.dspart = 16 * (int64_t)ds_parts(d);
-  return z;
-}
-
+// Exclusive scan of the images' chunk sizes.  When the batch does not fit the
+// workspace, images are accepted greedily in batch order instead (one lane), so
+// that an image that does not fit leaves its bytes to the later ones: only images
+// that cannot be placed get DINO_IMG_NO_SPACE (the host probe, dino_probe, sizes
+// the workspace so that this does not happen on the product path).
 __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size) {
   __shared__ int64_t part[1024];
   __shared__ int32_t dpart[1024];
@@ -137,35 +107,37 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
     dpart[t] += dv;
     __syncthreads();
   }
+  const bool fits = part[1023] <= ws_size;
   int64_t base = part[t] - local;
   int32_t dbase = dpart[t] - dlocal;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
     if (i >= B) continue;
     ImgDesc& d = desc[i];
-    const ChunkSizes z = image_chunk_bytes(d);
-    const int64_t sz = z.total();
     d.ds_item_base = dbase;
     d.ds_items = ds_parts(d);  // as counted by the scan above (the kernels skip images not OK)
     dbase += d.ds_items;
-    if (sz == 0) continue;
-    if (base + sz > ws_size) {
-      d.status = DINO_IMG_TOO_LARGE;
-    } else {
-      d.base = base;
-      d.ent_off = base;
-      d.rst_off = d.ent_off + z.ent;
-      d.coef_off = d.rst_off + z.rst;
-      d.binfo_off = d.coef_off + z.coef;
-      d.plane_off = d.binfo_off + z.binfo;
-      d.rgb_off = d.plane_off + z.plane;
-      d.cps_off = d.rgb_off + z.rgb;
-      d.htab_off = d.cps_off + z.cps;
-      d.hlane_off = d.htab_off + z.htab;
-      d.dspart_off = d.hlane_off + z.hlane;
-      d.h_lanes_cap = huff_lanes_cap(d);
+    const ChunkSizes z = image_chunk_bytes(d);
+    if (fits) plan_place(d, z, base, ws_size);
+    base += z.total();
+  }
+  if (!fits) {
+    __syncthreads();
+    if (t == 0) {
+      int64_t b = 0;
+      for (int i = 0; i < B; ++i) {
+        ImgDesc& d = desc[i];
+        const ChunkSizes z = image_chunk_bytes(d);
+        const int64_t sz = z.total();
+        if (sz == 0) continue;
+        if (b + sz <= ws_size) {
+          plan_place(d, z, b, ws_size);
+          b += sz;
+        } else {
+          d.status = DINO_IMG_NO_SPACE;
+        }
+      }
     }
-    base += sz;
   }
 }
 
@@ -508,7 +480,7 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
   int32_t img, item;
 };
 
-static_assert(sizeof(ImgDesc) == 960, "ImgDesc layout");
+static_assert(sizeof(ImgDesc) % 16 == 8 || sizeof(ImgDesc) % 16 == 0, "ImgDesc layout");
 constexpr int kHuffLdsBytes = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
 constexpr int kHuff3LdsBytes = (int)((sizeof(HuffLds3) + 15) & ~(size_t)15);
 
@@ -605,7 +577,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict
   __shared__ int32_t s_bad;
   ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
-  if (d.status != DINO_IMG_OK) return;
+  if (d.status != DINO_IMG_OK || d.kind != 0) return;
   const uint8_t* p = bytes + offsets[blockIdx.x];
   if (t == 0) s_bad = 0;
   __syncthreads();
@@ -659,7 +631,7 @@ __global__ void __launch_bounds__(1024) k_hseg(ImgDesc* __restrict__ desc, int B
   int32_t local = 0;
   for (int k = 0; k < per; ++k) {
     const int i = t * per + k;
-    if (i < B && desc[i].status == DINO_IMG_OK) local += desc[i].h_items;
+    if (i < B && desc[i].status == DINO_IMG_OK && desc[i].kind == 0) local += desc[i].h_items;
   }
   part[t] = local;
   __syncthreads();
@@ -675,7 +647,7 @@ __global__ void __launch_bounds__(1024) k_hseg(ImgDesc* __restrict__ desc, int B
     if (i >= B) continue;
     ImgDesc& d = desc[i];
     d.h_item_base = base;
-    if (d.status == DINO_IMG_OK) base += d.h_items;
+    if (d.status == DINO_IMG_OK && d.kind == 0) base += d.h_items;
     else d.h_items = 0;
   }
 }
@@ -806,7 +778,7 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
   __shared__ uint32_t s_wave[kHuff2Threads / 64];
   const ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
-  if (d.status != DINO_IMG_OK || d.restart_interval > 0 || huff_single_segment(d)) return;
+  if (d.status != DINO_IMG_OK || d.kind != 0 || d.restart_interval > 0 || huff_single_segment(d)) return;
   const int n = d.h_lanes;
   LaneRec* lr = (LaneRec*)(ws + d.hlane_off);
   if (n > kHuffThreads) {  // several segments: their first lanes started from guesses
@@ -902,6 +874,148 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
 }
 
 // ---------------------------------------------------------------------------
+// k_prog: progressive and multi-scan images (kind 1), one wave per image
+// (progressive.hpp).  The wave walks the marker segments together, zeroes the
+// dense coefficient buffer, then decodes scan i on lane i, one dependency level at
+// a time; the Huffman tables of a level's scans are built into an LDS pool (in
+// chunks when a level needs more tables than the pool holds).
+// ---------------------------------------------------------------------------
+constexpr int kProgThreads = 64;
+constexpr int kProgPool = 16;
+
+// Wave-cooperative search for the end of a scan's entropy data (see HostMarkerFinder):
+// each lane classifies 16 bytes per step, the first lane with a marker wins.
+struct WaveMarkerFinder {
+  __device__ int64_t operator()(const uint8_t* p, int64_t from, int64_t len) const {
+    const int lane = threadIdx.x & 63;
+    for (int64_t base = from; base + 1 < len; base += 64 * 16) {
+      const int64_t k0 = base + lane * 16;
+      uint32_t b[17];
+#pragma unroll
+      for (int j = 0; j < 17; ++j) b[j] = k0 + j < len ? p[k0 + j] : 0u;
+      int hit = 16;
+#pragma unroll
+      for (int j = 15; j >= 0; --j) {
+        const uint32_t c = b[j + 1];
+        if (k0 + j + 1 < len && b[j] == 0xFFu && c != 0x00u && c != 0xFFu && !(c >= 0xD0u && c <= 0xD7u)) hit = j;
+      }
+      const uint64_t m = __ballot(hit < 16);
+      if (m) {
+        const int first = __ffsll((long long)m) - 1;
+        return base + first * 16 + __shfl(hit, first);
+      }
+    }
+    return -1;
+  }
+};
+
+struct ProgLds {
+  ImgDesc d;
+  ScanRec scans[kMaxScans];
+  ProgTable pool[kProgPool];
+  int16_t scratch[kProgThreads][64];   // each lane's AC-refine block
+  int32_t slot_off[kProgPool];         // BITS offset of the table in each pool slot
+  int32_t slot_dc[kProgPool];
+  int8_t tslot[kMaxScans][8];          // pool slot of each scan table (dc 0..3, ac 4..7), -1 none
+  int32_t ready[kMaxScans];
+  int32_t nslots, next, bad;
+};
+
+__global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict__ bytes,
+                                                       const int64_t* __restrict__ offsets,
+                                                       ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  __shared__ ProgLds L;
+  const int img = blockIdx.x, t = threadIdx.x;
+  if (desc[img].status != DINO_IMG_OK || desc[img].kind != 1) return;
+  if (t == 0) L.d = desc[img];
+  __syncthreads();
+  const uint8_t* p = bytes + offsets[img];
+  const int64_t len = offsets[img + 1] - offsets[img];
+  WaveMarkerFinder find;
+  // every lane runs the walk on the LDS descriptor (identical values, identical writes)
+  prog_walk(p, len, &L.d, L.scans, find);
+  __syncthreads();
+  const ImgDesc& dl = L.d;
+  if (dl.status != DINO_IMG_OK) {
+    if (t == 0) desc[img].status = dl.status;
+    return;
+  }
+  const int n = dl.n_scans;
+  // zero the dense coefficient buffer (libjpeg's pre-zeroed coefficient arrays)
+  {
+    uint4* c4 = (uint4*)(ws + dl.coef_off);
+    const int64_t nq = dl.coef_bytes >> 4;
+    for (int64_t q = t; q < nq; q += kProgThreads) c4[q] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  int maxlv = 0;
+  for (int i = 0; i < n; ++i) maxlv = L.scans[i].level > maxlv ? L.scans[i].level : maxlv;
+  if (t == 0) L.bad = 0;
+  if (t < kMaxScans) L.ready[t] = 0;
+  __syncthreads();
+  int16_t* coef = (int16_t*)(ws + dl.coef_off);
+  for (int lv = 0; lv <= maxlv; ++lv) {
+    int first = 0;
+    for (;;) {
+      if (t == 0) {  // assign pool slots to the next scans of this level that fit
+        int used = 0, i = first;
+        for (; i < n; ++i) {
+          const ScanRec& sr = L.scans[i];
+          if (sr.level != lv) continue;
+          int need = 0;
+          for (int k = 0; k < 4; ++k) need += (sr.dc_tab[k] >= 0) + (sr.ac_tab[k] >= 0);
+          if (used + need > kProgPool) break;
+          for (int k = 0; k < 4; ++k) {
+            L.tslot[i][k] = -1;
+            L.tslot[i][4 + k] = -1;
+            if (sr.dc_tab[k] >= 0) {
+              L.slot_off[used] = sr.dc_tab[k];
+              L.slot_dc[used] = 1;
+              L.tslot[i][k] = (int8_t)used++;
+            }
+            if (sr.ac_tab[k] >= 0) {
+              L.slot_off[used] = sr.ac_tab[k];
+              L.slot_dc[used] = 0;
+              L.tslot[i][4 + k] = (int8_t)used++;
+            }
+          }
+          L.ready[i] = 1;
+        }
+        L.nslots = used;
+        L.next = i;
+      }
+      __syncthreads();
+      const int nslots = L.nslots;
+      if (t < nslots && !huff_build_derived(p + L.slot_off[t], L.slot_dc[t] != 0, &L.pool[t])) atomicOr(&L.bad, 1);
+      __syncthreads();
+      if (L.bad) break;
+      for (int e = t; e < nslots * (1 << kProgLookBits); e += kProgThreads) {
+        const int sl = e >> kProgLookBits, ix = e & ((1 << kProgLookBits) - 1);
+        L.pool[sl].look[ix] = huff_look_entry(&L.pool[sl], ix);
+      }
+      __syncthreads();
+      if (t < n && L.ready[t]) {
+        const ScanRec sr = L.scans[t];
+        ScanTables tb;
+        for (int k = 0; k < 4; ++k) {
+          tb.dc[k] = L.tslot[t][k] >= 0 ? &L.pool[L.tslot[t][k]] : &L.pool[0];
+          tb.ac[k] = L.tslot[t][4 + k] >= 0 ? &L.pool[L.tslot[t][4 + k]] : &L.pool[0];
+        }
+        prog_decode_scan(p, len, dl, sr, tb, coef, L.scratch[t]);
+        L.ready[t] = 0;
+      }
+      __syncthreads();  // (workgroup scope: this level's coefficient stores are visible to the next)
+      first = L.next;
+      if (first >= n) break;
+    }
+    if (L.bad) break;
+  }
+  if (t == 0) {
+    desc[img].n_scans = n;
+    if (L.bad) desc[img].status = DINO_IMG_CORRUPT;  // JERR_BAD_HUFF_TABLE
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_dcscan: DC predictors of a speculatively decoded image (no restart
 // intervals): per-component running sums of the DC differences k_huffman left
 // in decode order (the high half of each block record), replaced in place by the
@@ -913,7 +1027,7 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
   constexpr int K = 8;  // blocks per lane per tile: a wave covers 512 consecutive blocks
   __shared__ uint32_t s_wave[kDcScanThreads / 64];
   const ImgDesc& d = desc[blockIdx.x];
-  if (d.status != DINO_IMG_OK || d.restart_interval > 0) return;
+  if (d.status != DINO_IMG_OK || d.kind != 0 || d.restart_interval > 0) return;
   const int T = d.total_blocks, bpm = d.blocks_per_mcu;
   uint32_t mc = 0;
   for (int i = 0; i < bpm && i < kMaxBlocksPerMcu; ++i) mc |= (uint32_t)(d.mcu_comp[i] & 3) << (2 * i);
@@ -980,7 +1094,10 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   __shared__ int32_t s_blk[kIdctBlocksPerWg][72];
   __shared__ uint8_t s_nat[80];
   const ImgDesc& d = desc[blockIdx.y];
-  if (d.status != DINO_IMG_OK) return;
+  if (d.status != DINO_IMG_OK || d.kind == 2) return;
+  // kind 1 (progressive / multi-scan): dense int16 coefficients in natural order,
+  // component planes of bw x bh blocks (k_prog); kind 0: sparse entries + block records
+  const bool dense = d.kind == 1;
   if (threadIdx.x < 80) s_nat[threadIdx.x] = (uint8_t)((kNaturalOrder[threadIdx.x] >> 3) * 9 + (kNaturalOrder[threadIdx.x] & 7));
   const int ncomp = d.ncomp;
   const int64_t nb0 = (int64_t)d.comp[0].bw * d.comp[0].bh;
@@ -1028,10 +1145,11 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   int gn = blockIdx.x * kIdctBlocksPerWg + grp;
   Blk nx = locate(gn < T ? gn : 0);
   uint2 bin = make_uint2(0u, 0u);
-  if (gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
+  if (!dense && gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
   const uint16_t* ent16 = (const uint16_t*)ent;
   uint32_t ea = 0, eb = 0;  // halfword entries l and l + 8 of the next block
   auto first_entries = [&]() {
+    if (dense) return;
     const uint32_t c = bin.y & 0x7Fu;
     ea = l < c ? ent16[bin.x + l] : 0u;
     eb = l + 8 < c ? ent16[bin.x + l + 8] : 0u;
@@ -1048,9 +1166,15 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     if (gn < T) {  // prefetch the next block's record while this one is transformed
       nx = locate(gn);
       bin = make_uint2(0u, 0u);
-      if (nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
+      if (!dense && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
     }
-    if (valid) {
+    if (valid && dense) {  // lane l: row l of the block (8 int16 = one 16-byte load)
+      const CompDesc& cc = d.comp[cur.c];
+      const uint4 q = *(const uint4*)(ws + d.coef_off + cc.coef_off + ((int64_t)cur.by * cc.bw + cur.bx) * 128 + l * 16);
+      const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sb[l * 9 + j] = (int32_t)(int16_t)(w4[j >> 1] >> (16 * (j & 1)));
+    } else if (valid) {
       if (l == 0) sb[0] = (int32_t)bi.y >> 16;  // DC (int16, absolute after k_dcscan)
       // halfword entries (zigzag | int10 value << 6), then u32 entries from the next
       // even halfword (see SparseSink)
@@ -1148,9 +1272,23 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, int* o
 // 4:2:0 interior quads (the common case) take a vectorised path: one word of Y and
 // two words per chroma row instead of per-pixel byte loads; edges, quads that wrap
 // a row and other samplings use the per-pixel path (same arithmetic).
-__global__ void __launch_bounds__(256) k_color(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+__global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
+                                               const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const ImgDesc& d = desc[blockIdx.y];
   if (d.status != DINO_IMG_OK) return;
+  if (d.kind == 2) {  // pre-decoded RGB container: copy the pixels into the workspace
+    const uint8_t* src = bytes + offsets[blockIdx.y] + d.scan_off;
+    uint32_t* dst = (uint32_t*)(ws + d.rgb_off);
+    const int64_t n = (int64_t)d.width * d.height * 3, nw = (n + 3) >> 2;
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += (int64_t)gridDim.x * blockDim.x) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (4 * q + j < n) w |= (uint32_t)src[4 * q + j] << (8 * j);
+      dst[q] = w;
+    }
+    return;
+  }
   const int nc = d.ncomp;
   const PlaneView p0 = make_plane_view(d, ws, 0);
   const PlaneView p1 = nc > 1 ? make_plane_view(d, ws, 1) : p0;
@@ -1235,26 +1373,24 @@ __global__ void k_params(const ImgDesc* __restrict__ desc, int B, dino_aug_confi
   int b = i / nv, v = i - b * nv;
   const ImgDesc& d = desc[b];
   int ok = d.status == DINO_IMG_OK;
+  if (!ok && d.status < 0 && cfg.recipe == DINO_RECIPE_LEJEPA) {
+    // CPULeJEPAPipeline (cpu.py:446-448) crops an undecodable image's views from a black
+    // 224 x 224 canvas: the draws are those of that canvas (k_final writes its values)
+    sample_view(cfg, seed, batch_index, b, v, 224, 224, 1, &out[i]);
+    return;
+  }
   sample_view(cfg, seed, batch_index, b, v, ok ? d.width : 1, ok ? d.height : 1, ok, &out[i]);
-}
-
-// Horizontal taps in the signed-dot4 layout (k_hresize): per output x an int4
-// {xmin, groups, corr, 0}, then groups of 4 taps as signed base-256 digit planes
-// uint4 {D0, D1, D2, 0} stored [group][x] (lanes of a wave read consecutive x).
-__device__ __forceinline__ int64_t hdot_table_bytes(int S, int kh) {
-  return kh ? (int64_t)S * 16 * (1 + (kh + 3) / 4) : 0;
 }
 
 // Resample target of a view's crop box (0 in the record means the view size S).
 __device__ __forceinline__ int view_rw(const dino_view_params& p) { return p.resize_w > 0 ? p.resize_w : p.out_size; }
 __device__ __forceinline__ int view_rh(const dino_view_params& p) { return p.resize_h > 0 ? p.resize_h : p.out_size; }
 
-__device__ void view_sizes(const dino_view_params& p, int ok, int64_t* htmp, int64_t* rcoef, int32_t* kh, int32_t* kv) {
-  const int S = p.out_size;
+// Scratch of one view (plan.hpp view_scratch_bytes); 0 when the view is not rendered.
+__device__ void view_sizes(const dino_view_params& p, int ok, int64_t* bytes, int32_t* kh, int32_t* kv) {
   *kh = ok && p.crop_w != view_rw(p) ? resample_ksize(p.crop_w, view_rw(p)) : 0;
   *kv = ok && p.crop_h != view_rh(p) ? resample_ksize(p.crop_h, view_rh(p)) : 0;
-  *htmp = (*kh) ? align16((int64_t)p.crop_h * S * 3) : 0;
-  *rcoef = ok ? align16((int64_t)S * (4 + *kh + *kv) * 4) + hdot_table_bytes(S, *kh) : 0;
+  *bytes = ok ? view_scratch_bytes(p.out_size, p.crop_w, p.crop_h, *kh, *kv) : 0;
 }
 
 // Host-supplied records are validated before any kernel indexes memory with them.
@@ -1275,22 +1411,28 @@ __device__ bool params_valid(const dino_view_params& p, const ImgDesc& d, int S)
   return true;
 }
 
-__global__ void __launch_bounds__(1024) k_vplan(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+// Per-view scratch offsets: exclusive scan of the views' scratch sizes, or (when the
+// batch's views do not fit the augment workspace) greedy placement in batch order by
+// one lane.  A view that cannot be placed is not rendered and its image is marked
+// DINO_IMG_NO_SPACE (reported by dino_batch_info; the host sizes the workspace with
+// dino_probe + dino_reserve so that this does not happen on the product path).
+__global__ void __launch_bounds__(1024) k_vplan(ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                 int B, int nv, int n_global, int gsize, int lsize, int64_t aws_size,
                                                 ViewPlan* __restrict__ plan) {
   __shared__ int64_t part[1024];
   const int t = threadIdx.x, N = B * nv;
+  for (int b = t; b < B; b += 1024) desc[b].aug_status = 0;
   const int per = (N + 1023) / 1024;
   int64_t local = 0;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
     if (i < N) {
-      int64_t a, b;
+      int64_t a;
       int32_t c, e;
       const ImgDesc& d = desc[i / nv];
       int S = (i % nv) < n_global ? gsize : lsize;
-      view_sizes(prm[i], d.status == DINO_IMG_OK && params_valid(prm[i], d, S), &a, &b, &c, &e);
-      local += a + b;
+      view_sizes(prm[i], d.status == DINO_IMG_OK && params_valid(prm[i], d, S), &a, &c, &e);
+      local += a;
     }
   }
   part[t] = local;
@@ -1301,6 +1443,7 @@ __global__ void __launch_bounds__(1024) k_vplan(const ImgDesc* __restrict__ desc
     part[t] += v;
     __syncthreads();
   }
+  const bool fits = part[1023] <= aws_size;
   int64_t base = part[t] - local;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
@@ -1308,18 +1451,41 @@ __global__ void __launch_bounds__(1024) k_vplan(const ImgDesc* __restrict__ desc
     const ImgDesc& d = desc[i / nv];
     int S = (i % nv) < n_global ? gsize : lsize;
     int ok = d.status == DINO_IMG_OK && params_valid(prm[i], d, S);
-    int64_t a, b;
+    int64_t a;
     int32_t kh, kv;
-    view_sizes(prm[i], ok, &a, &b, &kh, &kv);
+    view_sizes(prm[i], ok, &a, &kh, &kv);
     ViewPlan vp;
-    vp.ok = ok && (base + a + b <= aws_size);
+    vp.ok = ok && fits;
     vp.lsum = 0;
     vp.kh = kh;
     vp.kv = kv;
     vp.htmp_off = base;
-    vp.rcoef_off = base + a;
+    vp.rcoef_off = base + (kh ? align16((int64_t)prm[i].crop_h * S * 3) : 0);
     plan[i] = vp;
-    base += a + b;
+    base += a;
+  }
+  if (!fits) {
+    __syncthreads();
+    if (t == 0) {
+      int64_t b = 0;
+      for (int i = 0; i < N; ++i) {
+        ViewPlan& vp = plan[i];
+        const ImgDesc& d = desc[i / nv];
+        int S = (i % nv) < n_global ? gsize : lsize;
+        if (!(d.status == DINO_IMG_OK && params_valid(prm[i], d, S))) continue;
+        int64_t a;
+        int32_t kh, kv;
+        view_sizes(prm[i], 1, &a, &kh, &kv);
+        if (b + a <= aws_size) {
+          vp.ok = 1;
+          vp.htmp_off = b;
+          vp.rcoef_off = b + (kh ? align16((int64_t)prm[i].crop_h * S * 3) : 0);
+          b += a;
+        } else {
+          desc[i / nv].aug_status = DINO_IMG_NO_SPACE;
+        }
+      }
+    }
   }
 }
 
@@ -1798,10 +1964,10 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
 }
 
 template <typename OutT>
-__global__ void __launch_bounds__(256) k_final(const dino_view_params* __restrict__ prm, const ViewPlan* __restrict__ plan,
-                                               int nv, int v0, int B, const uint8_t* __restrict__ gcrop,
-                                               ViewPtrs views, dino_aug_config cfg, int S,
-                                               const float* __restrict__ norm) {
+__global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                               const ViewPlan* __restrict__ plan, int nv, int v0, int B,
+                                               const uint8_t* __restrict__ gcrop, ViewPtrs views, dino_aug_config cfg,
+                                               int S, const float* __restrict__ norm) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
   uint8_t* tile = smem + sizeof(FinalLds);
@@ -1812,10 +1978,16 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   const int y0 = blockIdx.x * final_rows(S);
   const int nr = min(final_rows(S), S - y0);
   OutT* out = (OutT*)views.p[v] + (int64_t)b * 3 * N;
-  if (!vp.ok) {  // reference cpu.py:253: undecodable -> zeros
+  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
+  if (!vp.ok) {
+    // reference cpu.py:253: undecodable -> zeros; LeJEPA (cpu.py:446-448) crops a black
+    // canvas instead, whose every op (crop, resize, jitter, flip) keeps it black, so its
+    // views are the normalised value of 0
+    const bool canvas = cfg.recipe == DINO_RECIPE_LEJEPA && desc[b].status < 0;
     for (int e = threadIdx.x; e < 3 * nr * S; e += blockDim.x) {
       const int ch = e / (nr * S), rem = e - ch * nr * S;
-      out[(int64_t)ch * N + (int64_t)y0 * S + rem] = (OutT)0;
+      out[(int64_t)ch * N + (int64_t)y0 * S + rem] =
+          canvas ? out_cast<OutT>(u8_normalize(0, nb ? nb[ch] : cfg.mean[ch], nb ? nb[3 + ch] : cfg.std[ch])) : (OutT)0;
     }
     return;
   }
@@ -1831,7 +2003,6 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
   // the epilogue of each u8 value per channel (global or per-image statistics), after
   // the largest tile the launch reserves
   OutT* ntab = reinterpret_cast<OutT*>(tile + final_tile_bytes(S));
-  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
   for (int e = threadIdx.x; e < 3 * 256; e += blockDim.x) {
     const int c = e >> 8;
     ntab[e] = out_cast<OutT>(u8_normalize(e & 255, nb ? nb[c] : cfg.mean[c], nb ? nb[3 + c] : cfg.std[c]));
@@ -1866,17 +2037,33 @@ __global__ void __launch_bounds__(256) k_final(const dino_view_params* __restric
 }
 
 // ---------------------------------------------------------------------------
-// iBOT masks: one lane runs the (inherently sequential) generator
+// iBOT masks: one lane runs the (inherently sequential) generator; the mask and
+// the completion scratch live in LDS (dynamic, 5 bytes per patch), the MT states too.
 // ---------------------------------------------------------------------------
+constexpr int kMaskLdsMaxPatches = 8192;  // 40 KiB of dynamic LDS (grids up to 90 x 90)
+
 __global__ void k_masks(MaskParams mp, int n, uint32_t* __restrict__ py_state, uint32_t* __restrict__ np_state,
-                        uint8_t* __restrict__ out, int32_t* __restrict__ scratch) {
+                        uint8_t* __restrict__ out) {
   __shared__ MtState py, np;
-  if (threadIdx.x != 0) return;
-  mt_load(py, py_state);
-  mt_load(np, np_state);
-  for (int k = 0; k < n; ++k) gen_mask(mp, py, np, out + (int64_t)k * mp.H * mp.W, scratch);
-  mt_store(py, py_state);
-  mt_store(np, np_state);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int hw = mp.H * mp.W;
+  int32_t* scratch = reinterpret_cast<int32_t*>(smem);
+  uint8_t* mask = smem + 4 * hw;
+  if (threadIdx.x == 0) {
+    mt_load(py, py_state);
+    mt_load(np, np_state);
+  }
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (threadIdx.x == 0) gen_mask(mp, py, np, mask, scratch);
+    __syncthreads();
+    for (int i = threadIdx.x; i < hw; i += blockDim.x) out[(int64_t)k * hw + i] = mask[i];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    mt_store(py, py_state);
+    mt_store(np, np_state);
+  }
 }
 
 __global__ void k_bf16_to_fp8(const uint16_t* __restrict__ in, uint8_t* __restrict__ out, int64_t n) {
@@ -1898,7 +2085,7 @@ __global__ void k_info(const ImgDesc* __restrict__ desc, int B, int32_t* __restr
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
   const ImgDesc& d = desc[i];
-  info[4 * i + 0] = d.status;
+  info[4 * i + 0] = d.status != DINO_IMG_OK ? d.status : d.aug_status;
   info[4 * i + 1] = d.width;
   info[4 * i + 2] = d.height;
   info[4 * i + 3] = d.ncomp;
@@ -1972,7 +2159,7 @@ static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_d
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
                                                        "k_vert_local", "k_dcscan", "k_htab", "k_hseg", "k_huff2",
-                                                       "k_huff3"};
+                                                       "k_huff3", "k_prog"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -1993,12 +2180,27 @@ const char* g_failed_kernel = "";
 
 // Persistent grids of the segment kernels: as many workgroups as can be resident
 // on the device at once (occupancy query x CUs); items beyond them come in later turns.
-static int persistent_grid(const void* fn, int lds) {
-  int dev = 0, cus = 256, per = 4;
-  (void)hipGetDevice(&dev);
-  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+static int persistent_grid(const void* fn, int lds, int cus) {
+  int per = 4;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, kHuffThreads, lds) != hipSuccess || per < 1) per = 4;
   return per * cus;
+}
+
+// Per-device launch geometry (called by dino_ctx_create with `device` current).
+hipError_t init_launch_geom(int device, LaunchGeom* g) {
+  int cus = 256;
+  hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return e;
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff1), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kHuffLdsBytes)) != hipSuccess)
+    return e;
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff3), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kHuff3LdsBytes)) != hipSuccess)
+    return e;
+  g->grid_ds = 4 * cus;
+  g->grid3 = persistent_grid(reinterpret_cast<const void*>(&k_huff3), kHuff3LdsBytes, cus);
+  g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
+  return hipSuccess;
 }
 
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
@@ -2006,24 +2208,10 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   if (B <= 0) return hipSuccess;
   TIMED(tm, kKParse, s, (k_parse<<<(B + 63) / 64, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc)));
   TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
-  static int grid_ds = 0;
-  if (!grid_ds) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    grid_ds = 4 * cus;
-  }
+  const int grid_ds = a.geom.grid_ds, grid1 = a.geom.grid1, grid3 = a.geom.grid3;
   TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
-  static int grid1 = 0, grid3 = 0;
-  if (!grid1) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff1), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kHuffLdsBytes);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_huff3), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              kHuff3LdsBytes);
-    grid3 = persistent_grid(reinterpret_cast<const void*>(&k_huff3), kHuff3LdsBytes);
-    grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes);
-  }
+  TIMED(tm, kKProg, s, (k_prog<<<B, kProgThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
@@ -2031,7 +2219,7 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKHuff3, s, (k_huff3<<<grid3, kHuffThreads, kHuff3LdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKIdct, s, (k_idct<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
-  TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   return hipGetLastError();
 }
 
@@ -2058,7 +2246,7 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   const int lds = (int)sizeof(FinalLds) + final_tile_bytes(S) + 3 * 256 * (int)sizeof(OutT);
   TIMED(tm, kfin, s,
         (k_final<OutT><<<dim3((S + final_rows(S) - 1) / final_rows(S), nvc, B), 256, lds, s>>>(
-            a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S, a.norm)));
+            a.desc, a.params, a.plan, nv, v0, B, a.gcrop, a.views, a.cfg, S, a.norm)));
   return hipGetLastError();
 }
 
@@ -2096,9 +2284,10 @@ hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint
 }
 
 hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,
-                        uint32_t* np, uint8_t* out, int32_t* scratch, hipStream_t s) {
+                        uint32_t* np, uint8_t* out, hipStream_t s) {
   MaskParams mp{H, W, target, minp, maxp, la0, la1};
-  k_masks<<<1, 64, 0, s>>>(mp, n, py, np, out, scratch);
+  if ((int64_t)H * W > kMaskLdsMaxPatches) return hipErrorInvalidValue;
+  k_masks<<<1, 64, 5 * H * W + 16, s>>>(mp, n, py, np, out);
   return hipGetLastError();
 }
 

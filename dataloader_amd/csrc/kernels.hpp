@@ -37,7 +37,8 @@ struct ViewPlan {
 // the launch stream around each kernel; elapsed times are summed on demand.
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuff1, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
-  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKNumKernels
+  kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKProg,
+  kKNumKernels
 };
 
 struct KernelTimer {
@@ -56,6 +57,14 @@ struct KernelTimer {
   void destroy();
 };
 
+// Launch geometry of one device (computed per ctx by dino_ctx_create).
+struct LaunchGeom {
+  int32_t grid_ds;   // persistent destuff grid
+  int32_t grid1;     // persistent k_huff1 grid (occupancy x CUs)
+  int32_t grid3;     // persistent k_huff3 grid
+};
+hipError_t init_launch_geom(int device, LaunchGeom* g);
+
 struct DecodeArgs {
   const uint8_t* bytes;
   const int64_t* offsets;
@@ -64,6 +73,7 @@ struct DecodeArgs {
   ImgDesc* desc;
   uint8_t* ws;
   int64_t ws_size;
+  LaunchGeom geom;
 };
 
 // Output pointers travel as a kernel argument (no host->device copy whose source
@@ -74,7 +84,7 @@ struct ViewPtrs {
 };
 
 struct AugmentArgs {
-  const ImgDesc* desc;
+  ImgDesc* desc;
   int32_t batch;
   const dino_view_params* params;
   ViewPlan* plan;
@@ -94,7 +104,7 @@ hipError_t launch_augment(const AugmentArgs& a, hipStream_t s, KernelTimer* tm =
 hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_t s);
 hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s);
 hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,
-                        uint32_t* np, uint8_t* out, int32_t* scratch, hipStream_t s);
+                        uint32_t* np, uint8_t* out, hipStream_t s);
 hipError_t launch_bf16_to_fp8(const uint16_t* in, uint8_t* out, int64_t n, hipStream_t s);
 
 }  // namespace dino

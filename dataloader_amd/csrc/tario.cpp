@@ -45,10 +45,15 @@ bool is_zero_block(const uint8_t* h) {
 // tarfile.nti: octal (NUL/space padded) or GNU base-256 (first byte 0x80 / 0xFF).
 bool parse_number(const uint8_t* f, int n, int64_t* out) {
   if (f[0] == 0x80 || f[0] == 0xFF) {
-    int64_t v = 0;
-    for (int i = 1; i < n; ++i) v = (v << 8) | f[i];
-    if (f[0] == 0xFF) v -= (int64_t)1 << (8 * (n - 1));
-    *out = v;
+    // base-256: a value needing more than 63 bits (or a negative one) is rejected
+    // instead of wrapping; tar sizes and checksums are never that large
+    if (f[0] == 0xFF) return false;
+    uint64_t v = 0;
+    for (int i = 1; i < n; ++i) {
+      if (v >> 55) return false;
+      v = (v << 8) | f[i];
+    }
+    *out = (int64_t)v;
     return true;
   }
   int i = 0;
@@ -56,6 +61,7 @@ bool parse_number(const uint8_t* f, int n, int64_t* out) {
   int64_t v = 0;
   bool any = false;
   for (; i < n && f[i] >= '0' && f[i] <= '7'; ++i) {
+    if (v >> 59) return false;
     v = v * 8 + (f[i] - '0');
     any = true;
   }
@@ -97,7 +103,16 @@ void parse_pax(const uint8_t* p, int64_t n, std::string* path, int64_t* size) {
       std::string key = rec.substr(0, eq), val = rec.substr(eq + 1);
       if (!val.empty() && val.back() == '\n') val.pop_back();
       if (key == "path") *path = val;
-      if (key == "size") *size = std::atoll(val.c_str());
+      if (key == "size") {
+        // a size that is not a plain non-negative decimal below 2^62 is ignored
+        int64_t v = 0;
+        bool okv = !val.empty() && val.size() <= 18;
+        for (char ch : val) okv = okv && ch >= '0' && ch <= '9';
+        if (okv) {
+          for (char ch : val) v = v * 10 + (ch - '0');
+          *size = v;
+        }
+      }
     }
     i += len;
   }
@@ -167,11 +182,11 @@ int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_
     const char type = (char)h[156];
     if (pax_size >= 0 && type != 'x' && type != 'g' && type != 'L' && type != 'K') size = pax_size;
     const int64_t data = pos + 512;
-    const int64_t next = data + ((size + 511) / 512) * 512;
-    if (data + size > len) {
+    if (size > len - data) {  // (no overflow: 0 <= size, data <= len)
       status = DINO_TAR_TRUNCATED;
       break;
     }
+    const int64_t next = data + ((size + 511) / 512) * 512;
     if (type == 'L') {
       long_name = cstr(tar + data, (int)std::min<int64_t>(size, 1 << 20));
     } else if (type == 'x') {

@@ -147,6 +147,27 @@ class IngestEngine:
         self.last_batch = batch
         return views, info
 
+    def batch_info(self, info: torch.Tensor) -> torch.Tensor:
+        """Per-image status after augmentation (``dino_batch_info``) into ``info`` [B, 4] int32."""
+        _lib.check(self.lib.dino_batch_info(self._ctx, _ptr(info), self._s()), "dino_batch_info")
+        return info
+
+    def workspace_sizes(self) -> tuple[int, int]:
+        ws, aws = ctypes.c_int64(0), ctypes.c_int64(0)
+        _lib.check(self.lib.dino_workspace_sizes(self._ctx, ctypes.byref(ws), ctypes.byref(aws)),
+                   "dino_workspace_sizes")
+        return int(ws.value), int(aws.value)
+
+    def reserve(self, ws_bytes: int, aws_bytes: int) -> bool:
+        """Grow the decode / augment workspaces to at least these sizes (``dino_reserve``).
+        Returns True when it had to reallocate (which synchronises the device)."""
+        cur_ws, cur_aws = self.workspace_sizes()
+        if ws_bytes <= cur_ws and aws_bytes <= cur_aws:
+            return False
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.dino_reserve(self._ctx, int(ws_bytes), int(aws_bytes)), "dino_reserve")
+        return True
+
     def set_norm(self, d_norm: torch.Tensor | None) -> None:
         """Per-image {mean[3], std[3]} ([0, 1] scale) for the next batches (``dino_set_norm``);
         None restores the global statistics.  The tensor must outlive the batches using it."""

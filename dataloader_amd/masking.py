@@ -8,8 +8,9 @@ states, so the bits are identical to the reference's.
 Two ways to drive it:
 
 * ``gen(flat=...)`` — exact reference semantics including side effects: the
-  process-global ``random`` and ``numpy.random`` states are read, advanced on
-  the GPU, and written back (as the reference consumes them, masking.py:208-262).
+  process-global ``random`` and ``numpy.random`` states are read, advanced by the
+  C++ host twin of the kernel (``dino_masks_host``, no GPU stream involved), and
+  written back (as the reference consumes them, masking.py:208-262).
 * ``gen.generate(n)`` — device-resident fast path: ``n`` masks as a
   ``[n, H*W]`` bool tensor on the GPU from the generator's own state
   (``seed(s)`` == ``random.seed(s); np.random.seed(s)``), no host round trip.
@@ -93,17 +94,39 @@ class MaskingGenerator:
 
     # ------------------------------------------------------------ reference API
     def __call__(self, flat: bool = False) -> np.ndarray:
+        """Reference ``MaskingGenerator.__call__`` (masking.py:148-172): one mask from the
+        process-global ``random`` / ``numpy.random`` states, advanced exactly as the
+        reference advances them.  Runs the C++ host twin of ``k_masks``
+        (``dino_masks_host``): no GPU stream is touched or synchronised."""
         py_state = random.getstate()
         np_state = np.random.get_state()
-        py = torch.from_numpy(_py_state_words(py_state).copy()).to(self.device)
-        npst = torch.from_numpy(_np_state_words(np_state).copy()).to(self.device)
-        mask = self._run(1, py, npst)[0].cpu().numpy()
-        pyw = py.cpu().numpy()
-        npw = npst.cpu().numpy()
+        pyw = _py_state_words(py_state).copy()
+        npw = _np_state_words(np_state).copy()
+        mask = np.empty(self.height * self.width, np.bool_)
+        lib = _lib.load()
+        vp = ctypes.c_void_p
+        _lib.check(lib.dino_masks_host(self.height, self.width, self.num_masking_patches, self.min_num_patches,
+                                       self.max_num_patches, self.log_aspect_ratio[0], self.log_aspect_ratio[1], 1,
+                                       pyw.ctypes.data_as(vp), npw.ctypes.data_as(vp), mask.ctypes.data_as(vp)),
+                   "dino_masks_host")
         random.setstate((py_state[0], tuple(int(x) for x in pyw), py_state[2]))
         np.random.set_state((np_state[0], npw[:624].astype(np.uint32), int(npw[624]), np_state[3], np_state[4]))
         mask = mask.reshape(self.height, self.width)
         return mask.ravel() if flat else mask
+
+    @staticmethod
+    def _complete_randomly(mask: np.ndarray, target: int) -> np.ndarray:
+        """Reference ``_complete_randomly`` (masking.py:232-269): fill up to ``target`` masked
+        patches at random positions drawn with ``np.random.choice`` (legacy global state),
+        in place, also on non-contiguous arrays."""
+        shortfall = target - int(mask.sum())
+        if shortfall <= 0:
+            return mask
+        unmasked = np.flatnonzero(~mask.ravel())  # C order, like the reference's ravel
+        shortfall = min(shortfall, unmasked.size)
+        chosen = np.random.choice(unmasked, size=shortfall, replace=False)
+        mask.flat[chosen] = True  # in place whatever the memory layout
+        return mask
 
     def get_shape(self) -> tuple[int, int]:
         return self.height, self.width

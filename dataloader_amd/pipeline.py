@@ -14,16 +14,24 @@ Randomness: every (sample, view) record comes from a counter-based Philox
 stream keyed by (seed, batch index, sample, view) on the device, so the
 output does not depend on thread scheduling; ``last_params()`` exports the
 records so the CPU oracle can replay a batch exactly.
+
+Failures are never silent: every host batch is pre-screened (``fallback.py``:
+``dino_probe``, Pillow hand-over of the JPEG flavours the GPU decoder does not
+implement, ``dino_reserve``), and every batch's per-image status is read back
+asynchronously and accounted in ``stats``; an image that the reference would
+have decoded but that came back zero-filled raises a ``RuntimeWarning``.
 """
 
 from __future__ import annotations
 
-from collections import deque
+import warnings
+from collections import Counter, deque
 from typing import Any
 
 import numpy as np
 import torch
 
+from . import fallback
 from .engine import IngestEngine, pack_jpegs, params_from_device
 from .params import OUT_BF16, OUT_FP8_E4M3, OUT_FP32, RECORD_BYTES, make_aug_config
 
@@ -51,6 +59,9 @@ class _Slot:
         self.norm: torch.Tensor | None = None         # per-image normalisation records of the batch
         self.staging: torch.Tensor | None = None      # pinned JPEG bytes of a packed (native) source
         self.staging_off: torch.Tensor | None = None  # pinned int64 offsets[B+1]
+        self.info_host: torch.Tensor | None = None    # pinned copy of the batch's per-image status
+        self.done: torch.cuda.Event | None = None     # recorded after that copy (status accounting)
+        self.batch_id = -1
 
 
 class MI355XAugPipeline:
@@ -61,7 +72,7 @@ class MI355XAugPipeline:
     def __init__(self, source: Any, aug_cfg, batch_size: int, resolution_src=None, seed: int = 0,
                  out_dtype="bf16", device: int = 0, max_image_dim: int = 8192, workspace_bytes: int = 0,
                  engine: IngestEngine | None = None, depth: int = 1, norm=None,
-                 view_names: list[str] | None = None):
+                 view_names: list[str] | None = None, host_fallback: bool = True):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -71,6 +82,12 @@ class MI355XAugPipeline:
         self._norm = norm  # NormTable (per-dataset statistics) or None: global mean/std
         self._names = list(view_names) if view_names else [f"view_{i}" for i in range(aug_cfg.n_views)]
         self._batch_index = 0
+        self._max_image_dim = int(max_image_dim)
+        self._host_fallback = bool(host_fallback)
+        # per-image outcome of every batch handed over (status code -> images), images the
+        # GPU decoder left to Pillow, and workspace regrowths
+        self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0, "reserves": 0}
+        self._pending: deque = deque()
         self.depth = max(1, int(depth))
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
@@ -135,10 +152,10 @@ class MI355XAugPipeline:
             sl.engine.stream.wait_stream(torch.cuda.current_stream(self.device))
         return self._launch(sl, d_bytes, d_offsets, batch, views)
 
-    def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views):
+    def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views, cfg=None, account: bool = False):
         batch = self._batch_size if batch is None else int(batch)
-        g, l = self._sizes()
-        cfg = self._cfg(g, l)
+        if cfg is None:
+            cfg = self._cfg(*self._sizes())
         eng = sl.engine
         if sl.params is None or sl.params.numel() < batch * self._aug_cfg.n_views * RECORD_BYTES:
             with eng.on_stream():
@@ -153,12 +170,65 @@ class MI355XAugPipeline:
                                     views=views, params_out=sl.params)
         sl.info = info
         sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
+        if account:  # per-image status back to the host asynchronously (accounted at a later hand-over)
+            if any(e[0] is sl for e in self._pending):
+                self._account(until=sl)  # the slot's previous batch (long finished) is read before its copy is reused
+            if sl.info_host is None or sl.info_host.shape[0] < batch:
+                sl.info_host = torch.empty((batch, 4), dtype=torch.int32, pin_memory=True)
+            with eng.on_stream():
+                sl.info_host[:batch].copy_(info, non_blocking=True)
+            sl.done = torch.cuda.Event()
+            sl.done.record(eng.stream if eng.stream is not None else torch.cuda.current_stream(self.device))
+            sl.batch_id = self._batch_index
+            self._pending.append((sl, sl.batch_id, batch))
         if eng.stream is not None:
             sl.event = torch.cuda.Event()
             sl.event.record(eng.stream)
         self._last = sl
         self._batch_index += 1
         return sl.outputs
+
+    # ------------------------------------------------------------------ screening
+    def _screen(self, sl: _Slot, jpegs, host_buf: torch.Tensor, offsets: np.ndarray, cfg):
+        """dino_probe the packed host batch; hand the flavours the GPU does not decode to
+        Pillow (re-packing the batch); grow the slot's workspaces.  Returns the (possibly
+        re-packed) host buffer and offsets."""
+        batch = len(offsets) - 1
+        info, ws, aws = fallback.probe(host_buf.data_ptr(), offsets, batch, self._max_image_dim, cfg)
+        st = info[:, 0]
+        if self._host_fallback and (st == fallback.IMG_UNSUPPORTED).any():
+            if jpegs is None:  # packed native feed: slice the images back out of the staging buffer
+                hb = host_buf.numpy()
+                jpegs = [hb[offsets[i]:offsets[i + 1]] for i in range(batch)]
+            jpegs, n = fallback.hand_over(list(jpegs), st)
+            self.stats["host_decoded"] += n
+            host_buf, off_t = pack_jpegs(jpegs, pin=True)
+            offsets = off_t.numpy()
+            info, ws, aws = fallback.probe(host_buf.data_ptr(), offsets, batch, self._max_image_dim, cfg)
+        if sl.engine.reserve(ws, aws):
+            self.stats["reserves"] += 1
+        return host_buf, offsets
+
+    def _account(self, block: bool = False, until: _Slot | None = None) -> None:
+        """Fold the per-image status of finished batches into ``stats`` (oldest first);
+        ``until``: wait for batches up to and including that slot's pending one."""
+        while self._pending:
+            sl, bid, batch = self._pending[0]
+            waiting = block or (until is not None and any(e[0] is until for e in self._pending))
+            if not waiting and not sl.done.query():
+                break
+            sl.done.synchronize()
+            self._pending.popleft()
+            st = sl.info_host[:batch, 0].numpy()
+            self.stats["batches"] += 1
+            self.stats["images"] += batch
+            self.stats["status"].update(int(x) for x in st)
+            bad = st[st > 0]
+            if bad.size:
+                from ._lib import IMG_STATUS
+                kinds = ", ".join(f"{n} {IMG_STATUS.get(int(k), k)}" for k, n in Counter(bad.tolist()).items())
+                warnings.warn(f"MI355XAugPipeline: batch {bid}: {bad.size} decodable image(s) returned zero-filled "
+                              f"views ({kinds}); see MI355XAugPipeline.stats", RuntimeWarning, stacklevel=3)
 
     def _enqueue_packed(self) -> _Slot:
         """Native feed (``source.next_spans()``, e.g. :class:`~dataloader_amd.tario.ShardBatchFeeder`):
@@ -179,11 +249,17 @@ class MI355XAugPipeline:
             sl.staging_off = torch.empty(len(spans) + 1, dtype=torch.int64, pin_memory=True)
         off = gather(spans, sl.staging, getattr(self._source, "nthreads", 8))
         sl.staging_off.numpy()[: len(off)] = off
+        cfg = self._cfg(*self._sizes())
+        host_buf, offsets = self._screen(sl, None, sl.staging, np.asarray(off, np.int64), cfg)
+        if host_buf is sl.staging:
+            host_off, nbytes = sl.staging_off[: len(off)], need
+        else:  # re-packed after a Pillow hand-over
+            host_off, nbytes = torch.from_numpy(offsets).pin_memory(), int(offsets[-1])
         with sl.engine.on_stream():
-            d_bytes = sl.staging[:need].to(self.device, non_blocking=True)
-            d_offsets = sl.staging_off[: len(off)].to(self.device, non_blocking=True)
-        self._launch(sl, d_bytes, d_offsets, len(spans), None)
-        sl.inflight = (d_bytes, d_offsets)
+            d_bytes = host_buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
+            d_offsets = host_off.to(self.device, non_blocking=True)
+        self._launch(sl, d_bytes, d_offsets, len(spans), None, cfg=cfg, account=True)
+        sl.inflight = (host_buf, host_off, d_bytes, d_offsets)
         if sl.event is None:  # depth 1 (no side stream): the staging buffer is reused next batch
             torch.cuda.current_stream(self.device).synchronize()
         return sl
@@ -199,16 +275,20 @@ class MI355XAugPipeline:
             raise ValueError(f"source returned {len(jpeg_batch)} samples, expected {self._batch_size}")
         sl = self._next_slot()
         host_buf, offsets = pack_jpegs(jpeg_batch, pin=True)
+        cfg = self._cfg(*self._sizes())
+        host_buf, off_np = self._screen(sl, jpeg_batch, host_buf, offsets.numpy(), cfg)
+        offsets = torch.from_numpy(off_np)
         with sl.engine.on_stream():
             d_bytes = host_buf.to(self.device, non_blocking=True)
             d_offsets = offsets.to(self.device, non_blocking=True)
-        self._launch(sl, d_bytes, d_offsets, len(jpeg_batch), None)
+        self._launch(sl, d_bytes, d_offsets, len(jpeg_batch), None, cfg=cfg, account=True)
         # torch's caching host allocator keeps the pinned staging block until the copy retires
         sl.inflight = (host_buf, d_bytes, d_offsets)
         return sl
 
     def _hand_over(self, sl: _Slot) -> dict[str, torch.Tensor]:
         """Order the caller's stream after the slot's work and tie the outputs to it."""
+        self._account()
         if sl.event is not None:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_event(sl.event)
@@ -237,11 +317,19 @@ class MI355XAugPipeline:
             sl.event.synchronize()
         return sl.info[:, 0].cpu().numpy() if sl.info is not None else np.zeros(0, np.int32)
 
+    def flush_stats(self) -> dict:
+        """Wait for every launched batch and fold its status into ``stats``."""
+        self._account(block=True)
+        return self.stats
+
     def close(self) -> None:
         if not self._closed:
             self._closed = True
-            for sl in self._slots:
-                sl.engine.close()
+            try:
+                self._account(block=True)
+            finally:
+                for sl in self._slots:
+                    sl.engine.close()
 
     def __del__(self):
         try:

@@ -18,10 +18,18 @@
  *    host unless stated.
  *  - One dino_ctx per device; a ctx is not thread-safe (callers serialise),
  *    several ctx may run concurrently on different devices/streams.
- *  - Per-image status codes (d_status[i]): 0 ok, <0 the reference would have
- *    raised inside Image.open/convert (cpu.py:250-253) -> zero-filled output,
- *    >0 valid JPEG flavour this decoder does not implement (progressive,
- *    arithmetic, 12-bit, CMYK, multi-scan) -> zero-filled output.
+ *  - Per-image status codes (d_info[i][0]): 0 ok, <0 the reference would have
+ *    raised inside Image.open/convert (cpu.py:250-253) -> zero-filled output
+ *    (the reference's own semantics), >0 the reference decodes the image but this
+ *    call did not (a flavour the GPU decoder does not implement, or workspace
+ *    capacity) -> zero-filled output and the caller is expected to recover: the
+ *    Python layer pre-screens host batches with dino_probe, grows the workspaces
+ *    with dino_reserve and hands flavours it cannot decode over as pre-decoded
+ *    RGB images (DINO_RAW_MAGIC below), so the product path never zero-fills an
+ *    image the reference would have decoded.
+ *  - Input images are JPEG byte strings, or pre-decoded RGB images in the raw
+ *    container: 16-byte header {uint32 DINO_RAW_MAGIC, uint32 width, uint32
+ *    height, uint32 0} followed by width*height*3 bytes of HWC RGB.
  */
 #ifndef DINO_INGEST_H
 #define DINO_INGEST_H
@@ -32,7 +40,7 @@
 extern "C" {
 #endif
 
-#define DINO_ABI_VERSION 1
+#define DINO_ABI_VERSION 2
 
 /* return codes */
 #define DINO_OK 0
@@ -51,9 +59,18 @@ extern "C" {
 #define DINO_IMG_CORRUPT (-1)        /* not a JPEG / malformed header / bad table */
 #define DINO_IMG_TRUNCATED (-2)      /* entropy data ends before the last MCU, no EOI */
 #define DINO_IMG_BADDATA (-3)        /* libjpeg would error (bad sampling, MCU too large) */
-#define DINO_IMG_TOO_LARGE (-4)      /* exceeds ctx limits / workspace */
-#define DINO_IMG_UNSUPPORTED 1       /* progressive / arithmetic / lossless / 12-bit / CMYK */
-#define DINO_IMG_MULTISCAN 2         /* sequential JPEG with non-interleaved multi-scan */
+#define DINO_IMG_TOO_LARGE (-4)      /* > 2 x PIL.Image.MAX_IMAGE_PIXELS: Pillow raises DecompressionBombError */
+#define DINO_IMG_UNSUPPORTED 1       /* arithmetic / lossless / hierarchical / >8-bit / CMYK / 2-component,
+                                        progressive needing libjpeg block smoothing, > DINO_MAX_SCANS scans */
+#define DINO_IMG_MULTISCAN 2         /* (ABI v1; no longer produced: multi-scan files are decoded) */
+#define DINO_IMG_NO_SPACE 3          /* the ctx workspace could not hold the image or one of its views
+                                        (dino_reserve more and run again) */
+#define DINO_IMG_LIMIT 4             /* width or height above the ctx's max_image_dim */
+
+/* raw pre-decoded RGB container ("DRGB" little-endian) */
+#define DINO_RAW_MAGIC 0x42475244u
+/* scans of one progressive / multi-scan image the device decoder accepts */
+#define DINO_MAX_SCANS 64
 
 /* output dtypes */
 #define DINO_OUT_BF16 0
@@ -150,6 +167,28 @@ int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offse
                    dino_view_params* d_params_out, void* const* views, int32_t* d_info,
                    void* stream);
 
+/* Per-image status of the last batch after augmentation (the decode status, or
+ * DINO_IMG_NO_SPACE when one of the image's views did not fit the augment workspace):
+ * d_info: int32[batch][4] as dino_decode's. */
+int dino_batch_info(dino_ctx* ctx, int32_t* d_info, void* stream);
+
+/* Host pre-screen of a batch held in HOST memory (same packing as dino_decode): runs
+ * the device parser (and, for progressive / multi-scan files, its marker walk) on
+ * the CPU.  info (nullable): int32[batch][4] = {status the device decode will report,
+ * width, height, kind (0 baseline, 1 multi-scan, 2 raw RGB, -1 failed)}.  ws_need:
+ * decode workspace bytes the batch needs; aws_need: an upper bound of the augment
+ * workspace for cfg's views (0 when cfg is NULL).  Images with status > 0 are the
+ * ones the caller should decode itself and pass as raw RGB (DINO_RAW_MAGIC).
+ * Replaces nothing in the reference (its decode cannot fail for capacity). */
+int dino_probe(const uint8_t* bytes, const int64_t* offsets, int32_t batch, int32_t max_image_dim,
+               const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need);
+
+/* Grow the ctx's decode / augment workspaces to at least the given sizes (never
+ * shrinks).  Synchronises the device first when it reallocates; the last decoded
+ * batch is invalidated. */
+int dino_reserve(dino_ctx* ctx, int64_t ws_bytes, int64_t aws_bytes);
+int dino_workspace_sizes(dino_ctx* ctx, int64_t* ws_bytes, int64_t* aws_bytes);
+
 /* iBOT block masks (reference MaskingGenerator.__call__, masking.py:148-172).
  * d_py_state: uint32[625] = CPython random.getstate() words + index;
  * d_np_state: uint32[625] = numpy RandomState MT19937 key + pos.
@@ -158,11 +197,18 @@ int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offse
 int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,
                int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
                uint32_t* d_py_state, uint32_t* d_np_state, uint8_t* d_out, void* stream);
+/* The same generator on the host (HOST pointers; no GPU involved): the reference-API
+ * MaskingGenerator.__call__ uses it so that no batch synchronises a device stream.
+ * dino_masks (device) accepts grids of up to 8192 patches, the host version any. */
+int dino_masks_host(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,
+                    int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
+                    uint32_t* py_state, uint32_t* np_state, uint8_t* out);
 
 /* Per-kernel HIP-event timing of this ctx's launches (bench / profiling).
- * Kernel ids: 0 parse, 1 plan, 2 destuff, 3 huffman, 4 idct, 5 color, 6 params,
+ * Kernel ids: 0 parse, 1 plan, 2 destuff, 3 huff1, 4 idct, 5 color, 6 params,
  * 7 vplan, 8 rcoeffs, 9 hresize, 10 final(global views), 11 final(local views),
- * 12 vert(global views), 13 vert(local views), 14 dcscan.
+ * 12 vert(global views), 13 vert(local views), 14 dcscan, 15 htab, 16 hseg,
+ * 17 huff2, 18 huff3, 19 prog (progressive / multi-scan decode).
  * dino_kernel_times synchronises the recorded events, returns the sums since the
  * last call (ms, launches) and resets them. */
 int dino_set_timing(dino_ctx* ctx, int32_t enable);

@@ -13,6 +13,7 @@
 #include "../../dataloader_amd/csrc/huffman.hpp"
 #include "../../dataloader_amd/csrc/idct.hpp"
 #include "../../dataloader_amd/csrc/jpeg_parse.hpp"
+#include "../../dataloader_amd/csrc/progressive.hpp"
 
 namespace dino {
 
@@ -164,10 +165,56 @@ struct StageCapture {
   ImgDesc desc;
 };
 
+inline int model_idct_color(const ImgDesc& d, const std::vector<int16_t>& coef, uint8_t* out_rgb, StageCapture* cap);
+
+// k_prog: the marker walk, then every scan in file order (the kernel's level order
+// gives the same coefficients: scans of one level touch disjoint coefficients).
+inline int host_model_decode_multiscan(const uint8_t* p, int64_t len, ImgDesc& d, uint8_t* out_rgb, int32_t* stats,
+                                       StageCapture* cap) {
+  std::vector<ScanRec> scans(kMaxScans);
+  HostMarkerFinder find;
+  if (prog_walk(p, len, &d, scans.data(), find) != DINO_IMG_OK) return d.status;
+  std::vector<int16_t> coef(d.coef_bytes / 2, 0);
+  std::vector<ProgTable> tabs(8);
+  int16_t scratch[64];
+  for (int i = 0; i < d.n_scans; ++i) {
+    const ScanRec& sr = scans[i];
+    ScanTables tb;
+    for (int k = 0; k < 4; ++k) {
+      tb.dc[k] = tb.ac[k] = &tabs[0];
+      if (sr.dc_tab[k] >= 0) {
+        if (!prog_build_table(p + sr.dc_tab[k], true, &tabs[k])) return DINO_IMG_CORRUPT;
+        tb.dc[k] = &tabs[k];
+      }
+      if (sr.ac_tab[k] >= 0) {
+        if (!prog_build_table(p + sr.ac_tab[k], false, &tabs[4 + k])) return DINO_IMG_CORRUPT;
+        tb.ac[k] = &tabs[4 + k];
+      }
+    }
+    prog_decode_scan(p, len, d, sr, tb, coef.data(), scratch);
+  }
+  if (stats) {
+    stats[0] = d.n_scans;
+    int mx = 0;
+    for (int i = 0; i < d.n_scans; ++i) mx = std::max(mx, scans[i].level);
+    stats[1] = mx + 1;
+  }
+  if (cap) {
+    cap->desc = d;
+    cap->coef = coef;
+  }
+  return model_idct_color(d, coef, out_rgb, cap);
+}
+
 inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes, uint8_t* out_rgb, int32_t* stats,
                              StageCapture* cap = nullptr) {
   ImgDesc d;
   if (parse_jpeg(p, len, 1 << 16, &d) != DINO_IMG_OK) return d.status;
+  if (d.kind == 2) {
+    memcpy(out_rgb, p + 16, (size_t)d.width * d.height * 3);
+    return DINO_IMG_OK;
+  }
+  if (d.kind == 1) return host_model_decode_multiscan(p, len, d, out_rgb, stats, cap);
   Destuffed ds = model_destuff(p + d.scan_off, d.scan_len);
   if (cap) {
     cap->desc = d;
@@ -215,6 +262,11 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     }
   }
   if (cap) cap->coef = coef;
+  return model_idct_color(d, coef, out_rgb, cap);
+}
+
+// k_idct + k_color of the decode model (dense coefficients).
+inline int model_idct_color(const ImgDesc& d, const std::vector<int16_t>& coef, uint8_t* out_rgb, StageCapture* cap) {
   // k_idct
   std::vector<uint8_t> planes;
   int64_t psz = 0;

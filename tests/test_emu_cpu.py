@@ -123,9 +123,6 @@ def test_corrupt_and_unsupported(emu):
     for data, expect in [(b"not a jpeg", -1), (b"\xff\xd8\xff\xd9", -1), (b"", -1)]:
         buf = np.frombuffer(data + b"\0", np.uint8)
         assert emu.emu_parse(buf.ctypes.data_as(P), ctypes.c_int64(len(data)), info.ctypes.data_as(P)) == expect
-    prog = encode_jpeg(textured_rgb(40, 30, np.random.default_rng(0)), progressive=True)
-    b = np.frombuffer(prog, np.uint8)
-    assert emu.emu_parse(b.ctypes.data_as(P), ctypes.c_int64(len(prog)), info.ctypes.data_as(P)) == 1
     good = encode_jpeg(textured_rgb(200, 150, np.random.default_rng(0)))
     r, _, _ = emu_decode(emu, good[: len(good) * 4 // 5], 0, 1)  # truncated, no EOI: Pillow raises
     assert r == -2
@@ -212,3 +209,31 @@ def test_view_params_layout_matches_c():
     assert VIEW_PARAMS_DTYPE.itemsize == 80
     assert VIEW_PARAMS_DTYPE.fields["sigma"][1] == 48 and VIEW_PARAMS_DTYPE.fields["order"][1] == 28
     assert ctypes.sizeof(DinoAugConfig) == 4 * 29  # dino_aug_config: 29 x 32-bit fields
+
+
+def test_progressive_bit_exact_vs_pillow(emu):
+    """Progressive JPEGs (libjpeg's simple progression: DC first/refine, spectral bands,
+    successive approximation) through the k_prog model: bit-exact vs Pillow, with and
+    without restart intervals, every chroma sampling, gray, edge sizes."""
+    rng = np.random.default_rng(4)
+    n = 0
+    for w, h in [(1, 1), (8, 8), (17, 9), (64, 64), (225, 333), (640, 480), (1111, 71)]:
+        for sub in (0, 1, 2):
+            for q, rst in ((50, 0), (85, 3), (95, 0)):
+                j = encode_jpeg(textured_rgb(w, h, rng), quality=q, subsampling=sub, progressive=True,
+                                restart_mcus=rst)
+                b = np.frombuffer(j, np.uint8)
+                info = np.zeros(8, np.int32)
+                assert emu.emu_parse(b.ctypes.data_as(P), ctypes.c_int64(len(j)), info.ctypes.data_as(P)) == 0
+                r, out, st = emu_decode(emu, j, 0, 1)
+                assert r == 0 and st[0] >= 2, (w, h, sub, q, rst)
+                np.testing.assert_array_equal(out, np.asarray(cpu_ref.decode_rgb(j)), err_msg=f"{w}x{h} s{sub} q{q}")
+                n += 1
+    j = encode_jpeg(textured_rgb(300, 200, rng), progressive=True, gray=True)
+    r, out, _ = emu_decode(emu, j, 0, 1)
+    assert r == 0
+    np.testing.assert_array_equal(out, np.asarray(cpu_ref.decode_rgb(j)))
+    # truncated progressive file (no EOI): Pillow raises, the walk reports TRUNCATED
+    cut = j[: len(j) * 2 // 3]
+    assert cpu_ref.decode_rgb(cut) is None
+    assert emu_decode(emu, cut, 0, 1)[0] == -2

@@ -130,3 +130,38 @@ def test_corrupt_jpeg_gives_zeros():
     p = cpu_ref.ViewParams(out_size=32)
     t = cpu_ref.augment_one(b"not a valid jpeg", p)
     assert t.shape == (3, 32, 32) and torch.count_nonzero(t) == 0
+
+
+def test_r2_decodes_match_golden_hashes(emu):
+    """Round-2 fixtures (odd/large sizes, progressive files): Pillow and the kernel model
+    (emulator, incl. the progressive k_prog path) both give the committed decode hash."""
+    import hashlib
+
+    from tests.helpers import emu_decode
+    for name, m in META["jpegs_r2"].items():
+        data = (GOLD / f"{name}.jpg").read_bytes()
+        ref = np.asarray(cpu_ref.decode_rgb(data), dtype=np.uint8)
+        assert ref.shape == (m["height"], m["width"], 3)
+        assert hashlib.sha256(ref.tobytes()).hexdigest() == m["rgb_sha256"], name
+        r, out, _ = emu_decode(emu, data, 0, 1)
+        assert r == 0 and hashlib.sha256(out.tobytes()).hexdigest() == m["rgb_sha256"], name
+
+
+def test_views224_match_golden():
+    """Full DINOAugConfig (2 x 224 + 8 x 96) records and views reproduce from the oracle."""
+    g = META["views224"]
+    recs = np.load(GOLD / "views224.params.npy")
+    views = np.load(GOLD / "views224.bf16.npz")
+    cfg = cpu_ref.AugCfg()
+    gen = torch.Generator().manual_seed(1)
+    rnd = random.Random(1)
+    k = 0
+    for name in g["jpegs"]:
+        data = (GOLD / f"{name}.jpg").read_bytes()
+        img = cpu_ref.decode_rgb(data)
+        for spec in cpu_ref.view_table(cfg):
+            p = cpu_ref.draw_params_like_cpubackend(img.size[0], img.size[1], spec, cfg, gen, rnd)
+            assert p == record_to_params(recs[k]), (name, k)
+            got = cpu_ref.augment_one(data, p, decoded=img).view(torch.int16).numpy().reshape(-1)
+            np.testing.assert_array_equal(got, views[f"arr_{k}"], err_msg=f"{name} view {k}")
+            k += 1

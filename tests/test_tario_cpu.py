@@ -210,3 +210,29 @@ def test_batch_feeder_partitions_and_drops_last(tmp_path, world):
             got += [dst.numpy()[off[i]:off[i + 1]].tobytes() for i in range(3)]
         assert got == expect[:len(expect) // 3 * 3]
     cache.close(remove=True)
+
+
+def _set_header(tar: bytearray, h: int, size_field: bytes) -> None:
+    """Overwrite member header h's size field and fix its checksum."""
+    tar[h + 124:h + 136] = size_field
+    tar[h + 148:h + 156] = b" " * 8
+    tar[h + 148:h + 156] = b"%06o\x00 " % sum(tar[h:h + 512])
+
+
+def test_tar_index_forged_sizes_do_not_overflow():
+    """A base-256 or octal size near 2^63 (or a pax size) must not wrap the bounds check
+    (data + size > len overflowed): the member is reported truncated and the
+    samples before it are kept."""
+    tar = make_shard(4, seed=2)
+    full = tario.index_tar(tar)
+    h = int(full.samples[2]["img_off"]) - 512
+    for field in (b"\x80" + b"\x7f" + b"\xff" * 10,          # base-256, ~2^87: rejected
+                  b"\x80\x00\x00\x00" + b"\x7f" + b"\xff" * 7,  # base-256, ~2^63 - 1
+                  b"\xff" * 12,                              # negative base-256
+                  b"7777777777777777"[:11] + b"\x00"):      # octal, 8^11 - 1: fits, truncated
+        bad = bytearray(tar)
+        _set_header(bad, h, field)
+        t = tario.index_tar(bytes(bad))
+        assert t.status in (tario.TAR_TRUNCATED, tario.TAR_BAD_HEADER) and len(t) == 2, field
+        for r in t.samples:
+            assert 0 <= r["img_off"] and r["img_off"] + r["img_len"] <= len(bad)
