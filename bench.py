@@ -71,7 +71,27 @@ def jpeg_meta(j: bytes):
     return im.size
 
 
-def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int, recs=None) -> dict:
+def sparse_entry_bytes(pipe, dims_420) -> tuple[float, float]:
+    """Mean bytes of the sparse coefficient entries k_huff1 / k_huff3 wrote per block, read
+    back from the block records of the last decoded batch (dino_debug_region 2): a block
+    record {first halfword, n16 | n32 << 7 | DC << 16} gives n16 halfword entries + n32
+    u32 entries (+ 1 alignment halfword); 8 bytes of record per block on top."""
+    eng = pipe._last.engine
+    tot_e = tot_b = 0.0
+    for i in range(min(eng.last_batch, 16)):
+        w, h = dims_420[i % len(dims_420)]
+        nblk = ((w + 15) // 16) * ((h + 15) // 16) * 6
+        reg = eng.debug_region(i, 2, nblk * 256 + nblk * 8).cpu().numpy()
+        y = reg[nblk * 256:nblk * 256 + nblk * 8].view(np.uint32)[1::2]
+        n16 = (y & 0x7F).astype(np.int64)
+        n32 = ((y >> 7) & 0x7F).astype(np.int64)
+        tot_e += float((2 * n16 + 4 * n32 + 2 * (n32 > 0)).sum())
+        tot_b += nblk
+    return (tot_e / tot_b if tot_b else 0.0), 8.0
+
+
+def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int, recs=None,
+                      entry_bytes_per_block: float = 20.0) -> dict:
     """Per-image algorithmic bytes of the path and of each kernel's interface.
 
     ``recs`` (the last batch's view records) sizes the resize kernels' interfaces
@@ -98,15 +118,16 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     blk_fused = float(np.mean([b if f else 0 for b, f in zip(nblk, fz)]))
     s_unfused = float(np.mean([len(j) if not f else 0 for j, f in zip(jpegs, fz)]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
+    per_blk = entry_bytes_per_block + 8.0       # sparse entries + the 8-byte block record
     ab = {
         "path": s_jpeg + out,                       # S_jpeg + 1 044 480 B (bf16)
         "k_destuff": s_jpeg,                         # per launch: count pass reads, write pass reads + writes
         # first (speculative) decode reads the entropy stream; for the images it finishes
-        # itself it also writes their coefficients (dense int16 equivalent)
-        "k_huff1": s_jpeg + blk_fused * 128,
-        # re-decode of the other images: entropy bytes in, coefficients out
-        "k_huff3": s_unfused + (blocks - blk_fused) * 128,
-        "k_idct": blocks * 128 + blocks * 64,
+        # itself it also writes their sparse coefficient entries + block records (measured)
+        "k_huff1": s_jpeg + blk_fused * per_blk,
+        # re-decode of the other images: entropy bytes in, sparse entries + records out
+        "k_huff3": s_unfused + (blocks - blk_fused) * per_blk,
+        "k_idct": blocks * per_blk + blocks * 64,
         "k_color": blocks * 64 + px * 3,
         "k_final_global": (3 + out_bytes * 3) * n_g * g * g,
         "k_final_local": (3 + out_bytes * 3) * n_l * l * l,
@@ -124,13 +145,43 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     return ab
 
 
-def cpu_baseline(jpegs, seconds: float, batch: int = 32) -> dict:
-    """Reference-faithful CPUBackend restatement timed on this host's cores (oracle, kind 'port')."""
+def _measure(fn, warmup: int, iters: int, budget_s: float) -> dict:
+    """scripts/benchmark.py:161-190 of the reference: warm-up, then per-iteration wall times ->
+    mean/std/p50/p95 (ms).  ``iters`` is capped so that the timed part stays within ``budget_s``."""
+    import statistics
+    for _ in range(warmup):
+        fn()
+    times = []
+    t_start = time.perf_counter()
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        fn()
+        times.append((time.perf_counter() - t0) * 1e3)
+        if time.perf_counter() - t_start > budget_s and len(times) >= 5:
+            break
+    st = sorted(times)
+    return {"mean_ms": statistics.mean(times), "std_ms": statistics.stdev(times) if len(times) > 1 else 0.0,
+            "p50_ms": statistics.median(times), "p95_ms": st[min(len(st) - 1, int(0.95 * len(st)))],
+            "iters": len(times)}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _ref_faithful_runner(jpegs, batch: int, workers: int):
+    """CPUAugPipeline.run_one_batch restated (cpu.py:309-367): a ThreadPoolExecutor of
+    min(B, cpu_count, 16) workers created once (cpu.py:286, 303-306), every view re-decoding
+    the JPEG (cpu.py:251), per-view draws from the torch + Python RNGs, torch.stack per view."""
     import torch
 
     from oracle import cpu_ref
-    torch.set_num_threads(1)
-    workers = min(batch, os.cpu_count() or 4, 16)             # cpu.py:286, 303-306
     cfg = cpu_ref.AugCfg()
     table = cpu_ref.view_table(cfg)
     gen = torch.Generator().manual_seed(0)
@@ -140,27 +191,85 @@ def cpu_baseline(jpegs, seconds: float, batch: int = 32) -> dict:
         img = cpu_ref.decode_rgb(j)
         w, h = img.size
         outs = []
-        for spec in table:                                     # decode per view, as cpu.py:251
+        for spec in table:
             p = cpu_ref.draw_params_like_cpubackend(w, h, spec, cfg, gen, rnd)
             outs.append(cpu_ref.augment_one(j, p))
         return outs
 
-    done = 0
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(max_workers=workers) as ex:
-        k = 0
-        while True:
-            b = [jpegs[(k * batch + i) % len(jpegs)] for i in range(batch)]
-            res = list(ex.map(sample, b))
-            _ = [torch.stack([r[v] for r in res]) for v in range(len(table))]
-            done += batch
-            k += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "images/s", "cores": workers, "kind": "port",
-            "sample": f"{done} images ({batch}/batch) of the same synthetic JPEG pool, CPUBackend restatement "
-                      f"(PIL+torch), decode per view, ThreadPoolExecutor({workers}), {dt:.1f}s"}
+    ex = ThreadPoolExecutor(max_workers=workers)
+    state = {"k": 0}
+
+    def run():
+        k = state["k"]
+        state["k"] += 1
+        b = [jpegs[(k * batch + i) % len(jpegs)] for i in range(batch)]
+        res = list(ex.map(sample, b))
+        return [torch.stack([r[v] for r in res]) for v in range(len(table))]
+    return run, ex
+
+
+def _best_cpu_chunk(args):
+    """One process of the 'best CPU' pool: decode ONCE per image, then the 10 views."""
+    jpegs, seed = args
+    import torch
+
+    from oracle import cpu_ref
+    torch.set_num_threads(1)
+    cfg = cpu_ref.AugCfg()
+    table = cpu_ref.view_table(cfg)
+    gen = torch.Generator().manual_seed(seed)
+    rnd = random.Random(seed)
+    n = 0
+    for j in jpegs:
+        img = cpu_ref.decode_rgb(j)
+        for spec in table:
+            p = cpu_ref.draw_params_like_cpubackend(img.size[0], img.size[1], spec, cfg, gen, rnd)
+            cpu_ref.augment_one(j, p, decoded=img)
+        n += 1
+    return n
+
+
+def cpu_baseline(c2_jpegs, c1_jpegs, budget_s: float = 10.0, procs: int = 16) -> dict:
+    """SURVEY §8(d) CPU baseline, timed on this host (oracle restatement, kind 'port'):
+
+    * value: the reference-faithful CPUBackend on the C2 images (640x480), B = 32;
+    * c1: the same on BASELINE configs[0] (one tar shard of 256 x 256^2 JPEGs, B = 32);
+    * best_cpu: a process pool over the box's CPU share, decoding once per image.
+    Per-batch timing as reference scripts/benchmark.py:161-190 (mean/std/p50/p95)."""
+    import torch
+    from multiprocessing import get_context
+    torch.set_num_threads(1)
+    B = 32
+    workers = min(B, os.cpu_count() or 4, 16)                    # cpu.py:286
+    out = {"unit": "images/s", "cores": workers, "kind": "port", "batch": B,
+           "cpu_count": os.cpu_count(), "cpu_model": _cpu_model()}
+    run, ex = _ref_faithful_runner(c2_jpegs, B, workers)
+    m = _measure(run, 2, 30, budget_s)
+    out.update({"value": round(B / (m["mean_ms"] / 1e3), 2), "per_batch_ms": {k: round(v, 2) for k, v in m.items()},
+                "sample": f"C2: {m['iters']} timed batches of {B} synthetic 640x480 q85 JPEGs (after 2 warm-up), "
+                          f"CPUBackend restatement (Pillow + torch), decode per view, ThreadPoolExecutor({workers})"})
+    ex.shutdown()
+    run, ex = _ref_faithful_runner(c1_jpegs, B, workers)
+    m = _measure(run, 2, 30, budget_s / 2)
+    out["c1"] = {"images_per_s": round(B / (m["mean_ms"] / 1e3), 2), "per_batch_ms": {k: round(v, 2) for k, v in m.items()},
+                 "workload": "BASELINE configs[0]: 256 synthetic 256x256 JPEGs (one tar shard), B = 32, "
+                             "DINOAugConfig(n_local_crops=8), reference-faithful"}
+    ex.shutdown()
+    # best CPU: one process per core of the box's share, decode once per image
+    nb = 16 * procs
+    pool = get_context("spawn").Pool(procs)
+    try:
+        chunks = [([c2_jpegs[(i * 16 + k) % len(c2_jpegs)] for k in range(16)], i) for i in range(procs)]
+        pool.map(_best_cpu_chunk, chunks)                        # warm-up: imports, first decode
+        t0 = time.perf_counter()
+        done = sum(pool.map(_best_cpu_chunk, chunks))
+        dt = time.perf_counter() - t0
+    finally:
+        pool.close()
+        pool.join()
+    out["best_cpu"] = {"images_per_s": round(done / dt, 2), "processes": procs, "images": nb,
+                       "mode": "process pool, decode once per image, C2 images"}
+    return out
 
 
 def make_shards(jpegs, shard_size: int) -> list[bytes]:
@@ -225,7 +334,7 @@ def run_e2e(args, uniq, rank: int, world: int, dev, cfg, B: int) -> dict:
         feeder.close()
         pipe.close()
         if world > 1:
-            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            t = torch.tensor([dt], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         return {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
@@ -239,25 +348,32 @@ def run_e2e(args, uniq, rank: int, world: int, dev, cfg, B: int) -> dict:
         cache.close(remove=True)
 
 
-def load_traffic(kernel: str):
-    f = ROOT / "profiles" / "pmc_traffic.json"
-    if not f.exists():
-        return None
-    try:
-        d = json.loads(f.read_text())
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
-    except Exception:  # noqa: BLE001
-        return None
+PMC_FILES = ("r02_pmc_traffic.json", "r01_s7_pmc_traffic.json")
+
+
+def load_traffic() -> tuple[dict, str | None]:
+    """Per-launch HBM bytes per kernel from the newest committed PMC summary (FETCH_SIZE and
+    WRITE_SIZE passes of this bench under rocprofv3, scripts/gpu_pmc.sh; corrections of
+    MI355X_MICROARCH.md §HBM): {kernel: bytes}, file name."""
+    for name in PMC_FILES:
+        f = ROOT / "profiles" / name
+        if f.exists():
+            try:
+                d = json.loads(f.read_text())
+                return {k: v.get("hbm_bytes_per_launch") for k, v in d.items() if not k.startswith("_")}, name
+            except Exception:  # noqa: BLE001
+                pass
+    return {}, None
 
 
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=98, help="timed steps (98 x 512 covers the 50k set once)")
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--images", type=int, default=50000)
-    ap.add_argument("--unique", type=int, default=256)
+    ap.add_argument("--unique", type=int, default=2048, help="distinct JPEG encodes tiled to --images")
     ap.add_argument("--procs", type=int, default=-1, help="JPEG encoder processes (0: in-process)")
     ap.add_argument("--depth", type=int, default=3, help="batches in flight (slots with their own ctx + stream)")
     ap.add_argument("--width", type=int, default=640)
@@ -265,7 +381,7 @@ def main() -> None:
     ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600} (+ iBOT masks)")
     ap.add_argument("--masks", action="store_true", help="iBOT masks per batch (default with --mixed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
-    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="time budget of each CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--h2d", action="store_true", help="also time the H2D-inclusive rate (pinned host bytes)")
     ap.add_argument("--kernel-json", default="", help="write per-kernel times here (rank 0)")
@@ -288,7 +404,8 @@ def main() -> None:
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # barrier + MAX of the elapsed time only: a CPU (gloo) group, no RCCL on this path
+        dist.init_process_group("gloo")
 
     from dataloader_amd.config import DINOAugConfig
     from dataloader_amd.engine import pack_jpegs
@@ -351,8 +468,11 @@ def main() -> None:
     t_ser = time.perf_counter() - t_ser
     ktimes = pipe.kernel_times()
     pipe.set_timing(False)
+    k_last = args.warmup + 2 * args.steps - 1  # the batch the last slot still holds
+    s_last = (k_last % n_batches) * B
+    ent_b, _ = sparse_entry_bytes(pipe, [jpeg_meta(j) for j in jpegs[s_last:s_last + 16]])
     if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -375,30 +495,37 @@ def main() -> None:
     value = world * args.steps * B / dt
     out_bytes = {"bf16": 2, "fp8": 1, "fp32": 4}[args.dtype]
     ab = algorithmic_bytes(uniq, cfg.global_crop_size, cfg.local_crop_size, cfg.n_global_crops,
-                           cfg.n_local_crops, out_bytes, recs=pipe.last_params())
+                           cfg.n_local_crops, out_bytes, recs=pipe.last_params(), entry_bytes_per_block=ent_b)
     per_kernel = {k: {"avg_ms": (ms / n if n else 0.0), "launches": n, "total_ms": ms} for k, (ms, n) in ktimes.items()}
     dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
-    dom_bytes = ab.get(dom)
-    roof = None
-    if dom_bytes:
-        bytes_launch = dom_bytes * B
-        achieved = bytes_launch / (per_kernel[dom]["avg_ms"] * 1e-3) / 1e9
-        traffic = load_traffic(dom)
-        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic, "kernel": dom,
-                "algorithmic_bytes_per_launch": int(bytes_launch)}
-    # the same figure for every timed kernel whose interface bytes are defined
+    traffic, traffic_src = load_traffic()
+    # algorithmic bytes per image = S_jpeg + sum over views of 3 S^2 x out bytes;
+    # one launch of any Stage-3 kernel processes the batch of B images
+    bytes_launch = ab["path"] * B
+    achieved = bytes_launch / (per_kernel[dom]["avg_ms"] * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic.get(dom), "kernel": dom,
+            "algorithmic_bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(per_kernel[dom]["avg_ms"], 4),
+            "definition": "SURVEY 8(d) bytes per image (S_jpeg + 3*sum(S_v^2)*out_bytes) x batch / dominant kernel's "
+                          "mean launch time (HIP events on its stream, serialized pass after the timed region)",
+            "traffic_source": f"profiles/{traffic_src}" if traffic_src else None}
+    # each kernel on its own interface bytes (what it must read + write; huffman entries measured)
     roof_all = {}
     for k, v in per_kernel.items():
         if ab.get(k) and v["avg_ms"] > 0:
             gbs = ab[k] * B / (v["avg_ms"] * 1e-3) / 1e9
             roof_all[k] = {"achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 4),
-                           "avg_ms": round(v["avg_ms"], 4)}
+                           "avg_ms": round(v["avg_ms"], 4), "interface_bytes_per_launch": int(ab[k] * B),
+                           "traffic_bytes_per_launch": traffic.get(k)}
     ms_step = dt / args.steps * 1e3
     path_gbs = ab["path"] * B * world / (dt / args.steps) / 1e9
+    step_traffic = None
+    if traffic:
+        step_traffic = sum((traffic.get(k) or 0) * v["launches"] / max(args.steps, 1) for k, v in per_kernel.items())
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(uniq, args.cpu_seconds)
+        c1 = make_unique(256, 256, 256, 7, False, procs)
+        cpu = cpu_baseline(uniq, c1, args.cpu_seconds)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world,
@@ -414,7 +541,10 @@ def main() -> None:
             "roofline": roof,
             "roofline_kernels": roof_all,
             "path_roofline": {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
-                              "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5)},
+                              "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5),
+                              "pmc_traffic_bytes_per_step": int(step_traffic) if step_traffic else None,
+                              "algorithmic_bytes_per_step": int(ab["path"] * B),
+                              "sparse_entry_bytes_per_block": round(ent_b, 2)},
             "kernels_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in per_kernel.items()},
             "serialized_ms_per_step": round(t_ser / args.steps * 1e3, 3),
             "cpu_baseline": cpu,

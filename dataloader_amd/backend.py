@@ -7,8 +7,10 @@ runs Stage 3 on the GPU.  Method-by-method:
 
 * ``name`` / ``supports_fp8`` / ``supports_gpu``     protocol.py:22-29
 * ``build_shard_cache``   -> in-process LRU (Stage 1 stays host-side; cpu.py:86-145)
-* ``build_pipeline``      -> :class:`MI355XAugPipeline` (dispatch as cpu.py:649-709;
-  DinoV2 multi-crop only — Eval/LeJEPA/User specs raise TypeError)
+* ``build_pipeline``      -> :class:`MI355XAugPipeline` (dispatch as cpu.py:649-709):
+  DinoV2 multi-crop, LeJEPA and Eval view recipes on the same kernels; UserAugSpec ->
+  :class:`MI355XUserAugPipeline` (decode-only recipe, ``dino_resize_batch``, then aug_fn);
+  anything else raises TypeError (cpu.py:708-709)
 * ``build_pipeline_iterator`` -> :class:`MI355XPipelineIterator` (cpu.py:711-722)
 * ``build_h2d_stream``    -> outputs are already device-resident: identity transfer
   that orders the consumer stream after the producer (memory.py:131-165 semantics)
@@ -164,8 +166,20 @@ class MI355XBackend:
     def build_pipeline(self, source: Any, aug_spec: Any, pipeline_cfg: Any, specs: Any = None) -> MI355XAugPipeline:
         """Dispatch as CPUBackend.build_pipeline (cpu.py:649-709): DinoV2 multi-crop, LeJEPA
         (context + targets) and Eval (resize + centre crop) run on the same kernels with their
-        own view recipe; UserAugSpec (a Python aug_fn on decoded tensors) is not offered."""
+        own view recipe; UserAugSpec decodes + resizes on the GPU and applies aug_fn."""
         kind = type(aug_spec).__name__
+        if kind == "UserAugSpec":  # decode-only recipe + the user's aug_fn (cpu.py:469-503)
+            from .pipeline import MI355XUserAugPipeline
+            norm = None
+            if getattr(pipeline_cfg, "fuse_normalization", False) and specs is not None:
+                from .norm import NormTable
+                norm = NormTable(aug_spec, specs)
+                if hasattr(source, "register_dataset_index_callback"):
+                    source.register_dataset_index_callback(norm.set_dataset_indices)
+            return MI355XUserAugPipeline(source, aug_spec, getattr(source, "_batch_size", 1),
+                                         out_dtype=pipeline_cfg.output_dtype, device=pipeline_cfg.device_id,
+                                         max_image_dim=self._max_image_dim, workspace_bytes=self._workspace_bytes,
+                                         norm=norm)
         if _is_dinov2_spec(aug_spec):
             aug_cfg = aug_spec.aug_cfg
             names = None
@@ -200,7 +214,10 @@ class MI355XBackend:
         )
 
     def build_pipeline_iterator(self, pipeline: Any, aug_spec: Any, output_map: list[str],
-                                batch_size: int) -> MI355XPipelineIterator:
+                                batch_size: int):
+        from .pipeline import MI355XUserAugIterator, MI355XUserAugPipeline
+        if isinstance(pipeline, MI355XUserAugPipeline):
+            return MI355XUserAugIterator(pipeline, output_map)
         return MI355XPipelineIterator(pipeline, output_map, batch_size)
 
     def build_h2d_stream(self, device: Any, topo: Any) -> DeviceH2DStream:

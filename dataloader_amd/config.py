@@ -207,6 +207,59 @@ class LeJEPAAugSpec:
         return False
 
 
+@dataclass
+class UserAugSpec:
+    """Reference ``UserAugSpec`` (augmentation.py:400-473): decode + resize the shorter side to
+    ``decode_size`` + normalise, then ``aug_fn(Tensor[B,C,H,W]) -> dict[str, Tensor]``."""
+
+    aug_fn: Any
+    _output_map: list
+    decode_size: int = 256
+    mean: tuple = (0.485, 0.456, 0.406)
+    std: tuple = (0.229, 0.224, 0.225)
+    warn_not_dali: bool = True
+
+    @property
+    def output_map(self) -> list[str]:
+        return self._output_map
+
+    @property
+    def n_views(self) -> int:
+        return len(self.output_map)
+
+    @property
+    def norm_stats(self) -> NormStats:
+        return NormStats(mean=self.mean, std=self.std)
+
+    @property
+    def initial_global_size(self) -> int:
+        return self.decode_size
+
+    @property
+    def initial_local_size(self) -> int:
+        return self.decode_size
+
+    def split_views(self, views: list) -> tuple[list, list]:
+        mid = max(1, len(views) // 2)
+        return views[:mid], views[mid:]
+
+    def __post_init__(self) -> None:
+        if not callable(self.aug_fn):
+            raise TypeError("UserAugSpec.aug_fn must be callable.")
+        if not self.output_map:
+            raise ValueError("UserAugSpec.output_map must be a non-empty list of view names.")
+        if self.decode_size < 1:
+            raise ValueError(f"UserAugSpec.decode_size must be >= 1, got {self.decode_size}.")
+
+
+def resize_shorter_size(width: int, height: int, size: int) -> tuple[int, int]:
+    """torchvision ``Resize(size)`` output (w, h) for an int size (``_compute_resized_output_size``):
+    the shorter side becomes ``size``, the longer ``int(size * long / short)`` (reference cpu.py:190-191)."""
+    if width <= height:
+        return size, int(size * height / width)
+    return int(size * width / height), size
+
+
 def recipe_aug_config(spec: Any) -> DINOAugConfig:
     """The view recipe of an Eval / LeJEPA spec as a ``DINOAugConfig`` + ``recipe`` code
     (``DINO_RECIPE_*``), so that the same kernels and sampler serve every spec:

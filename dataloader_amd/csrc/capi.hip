@@ -211,6 +211,23 @@ int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets
   return d_info ? dino_batch_info(c, d_info, stream) : DINO_OK;
 }
 
+int dino_resize_batch(dino_ctx* c, int32_t out_w, int32_t out_h, const float* mean, const float* stdv,
+                      int32_t out_dtype, void* d_out, void* stream) {
+  if (!c || !mean || !stdv || !d_out) return fail(DINO_EINVAL, "dino_resize_batch: null argument%s%lld");
+  if (c->last_batch < 0) return fail(DINO_EINVAL, "dino_resize_batch: no decoded batch%s%lld");
+  if (out_w < 1 || out_h < 1 || out_w > 65535 || out_h > 65535)
+    return fail(DINO_EINVAL, "dino_resize_batch: output size %s%lld out of range", "", (long long)out_w * out_h);
+  if (out_dtype < DINO_OUT_BF16 || out_dtype > DINO_OUT_FP8_E4M3)
+    return fail(DINO_EINVAL, "dino_resize_batch: unknown out_dtype %s%lld", "", out_dtype);
+  if (c->d_norm && c->norm_n < c->last_batch)
+    return fail(DINO_EINVAL, "dino_resize_batch: dino_set_norm covers %s%lld images, fewer than the batch", "",
+                c->norm_n);
+  DecodeOnlyArgs a{c->d_desc, c->last_batch, out_w, out_h, out_dtype, c->d_plan, c->d_ws, c->d_aws, c->aws_size,
+                   {mean[0], mean[1], mean[2]}, {stdv[0], stdv[1], stdv[2]}, c->d_norm, d_out};
+  hipError_t e = launch_decode_only(a, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_resize_batch");
+}
+
 int dino_batch_info(dino_ctx* c, int32_t* d_info, void* stream) {
   if (!c || !d_info) return fail(DINO_EINVAL, "dino_batch_info: null argument%s%lld");
   if (c->last_batch < 0) return fail(DINO_EINVAL, "dino_batch_info: no decoded batch%s%lld");

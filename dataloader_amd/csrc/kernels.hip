@@ -2037,6 +2037,177 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
 }
 
 // ---------------------------------------------------------------------------
+// Decode-only recipe (reference CPUUserAugPipeline, cpu.py:484-500; DALI
+// _build_decode_only_pipeline, pipeline.py:693-756): every image of the batch
+// resampled whole (Pillow BICUBIC, horizontal pass then vertical, each only when
+// that axis changes size) to ow x oh, normalised and cast, NCHW.  Scratch per
+// image (k_dplan, the ViewPlan slot of view 0): coefficient tables of both axes +
+// the horizontal pass's rows (planar u8 [3][H][ow]).
+// ---------------------------------------------------------------------------
+__device__ void dec_sizes(const ImgDesc& d, int ow, int oh, int64_t* bytes, int32_t* kh, int32_t* kv) {
+  const bool ok = d.status == DINO_IMG_OK;
+  *kh = ok && d.width != ow ? resample_ksize(d.width, ow) : 0;
+  *kv = ok && d.height != oh ? resample_ksize(d.height, oh) : 0;
+  *bytes = ok ? align16((int64_t)ow * (2 + *kh) * 4) + align16((int64_t)oh * (2 + *kv) * 4) +
+                    (*kh ? align16((int64_t)d.height * ow * 3) : 0)
+              : 0;
+}
+
+__global__ void __launch_bounds__(1024) k_dplan(ImgDesc* __restrict__ desc, int B, int ow, int oh, int64_t aws_size,
+                                                ViewPlan* __restrict__ plan) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (B + 1023) / 1024;
+  int64_t local = 0;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i < B) {
+      desc[i].aug_status = 0;
+      int64_t a;
+      int32_t kh, kv;
+      dec_sizes(desc[i], ow, oh, &a, &kh, &kv);
+      local += a;
+    }
+  }
+  part[t] = local;
+  __syncthreads();
+  for (int s = 1; s < 1024; s <<= 1) {
+    const int64_t v = t >= s ? part[t - s] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const bool fits = part[1023] <= aws_size;
+  int64_t base = part[t] - local;
+  for (int k = 0; k < per; ++k) {
+    const int i = t * per + k;
+    if (i >= B) continue;
+    int64_t a;
+    int32_t kh, kv;
+    dec_sizes(desc[i], ow, oh, &a, &kh, &kv);
+    ViewPlan vp;
+    vp.ok = desc[i].status == DINO_IMG_OK && fits;
+    vp.kh = kh;
+    vp.kv = kv;
+    vp.lsum = 0;
+    vp.rcoef_off = base;
+    vp.htmp_off = base + align16((int64_t)ow * (2 + kh) * 4) + align16((int64_t)oh * (2 + kv) * 4);
+    plan[i] = vp;
+    base += a;
+  }
+  if (!fits) {
+    __syncthreads();
+    if (t == 0) {
+      int64_t b = 0;
+      for (int i = 0; i < B; ++i) {
+        if (desc[i].status != DINO_IMG_OK) continue;
+        int64_t a;
+        int32_t kh, kv;
+        dec_sizes(desc[i], ow, oh, &a, &kh, &kv);
+        if (b + a <= aws_size) {
+          plan[i].ok = 1;
+          plan[i].rcoef_off = b;
+          plan[i].htmp_off = b + align16((int64_t)ow * (2 + kh) * 4) + align16((int64_t)oh * (2 + kv) * 4);
+          b += a;
+        } else {
+          desc[i].aug_status = DINO_IMG_NO_SPACE;
+        }
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dcoeffs(const ImgDesc* __restrict__ desc, const ViewPlan* __restrict__ plan,
+                                                 int ow, int oh, uint8_t* __restrict__ aws) {
+  const int b = blockIdx.x;
+  const ViewPlan vp = plan[b];
+  if (!vp.ok) return;
+  const ImgDesc& d = desc[b];
+  int32_t* hb = (int32_t*)(aws + vp.rcoef_off);
+  int32_t* ht = hb + 2 * ow;
+  int32_t* vb = (int32_t*)(aws + vp.rcoef_off + align16((int64_t)ow * (2 + vp.kh) * 4));
+  int32_t* vt = vb + 2 * oh;
+  if (vp.kh)
+    for (int x = threadIdx.x; x < ow; x += blockDim.x)
+      resample_coeffs_one(d.width, ow, x, vp.kh, &hb[2 * x], &hb[2 * x + 1], ht + (int64_t)x * vp.kh);
+  if (vp.kv)
+    for (int y = threadIdx.x; y < oh; y += blockDim.x)
+      resample_coeffs_one(d.height, oh, y, vp.kv, &vb[2 * y], &vb[2 * y + 1], vt + (int64_t)y * vp.kv);
+}
+
+__global__ void __launch_bounds__(256) k_dhpass(const ImgDesc* __restrict__ desc, const ViewPlan* __restrict__ plan,
+                                                int ow, const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
+  const int b = blockIdx.y;
+  const ViewPlan vp = plan[b];
+  if (!vp.ok || !vp.kh) return;
+  const ImgDesc& d = desc[b];
+  const int32_t* hb = (const int32_t*)(aws + vp.rcoef_off);
+  const CoefView cv{hb, hb + 2 * ow, vp.kh};
+  const SrcView src{ws + d.rgb_off, (int64_t)d.width * 3, 3, 1};
+  uint8_t* tmp = aws + vp.htmp_off;
+  const int64_t n = (int64_t)d.height * ow, plane = n;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(e / ow), x = (int)(e - (int64_t)y * ow);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tmp[c * plane + e] = hresize_at(src, cv, y, x, c);
+  }
+}
+
+template <typename OutT>
+__global__ void __launch_bounds__(256) k_dvpass(const ImgDesc* __restrict__ desc, const ViewPlan* __restrict__ plan,
+                                                int ow, int oh, const uint8_t* __restrict__ ws,
+                                                const uint8_t* __restrict__ aws, OutT* __restrict__ out, float m0,
+                                                float m1, float m2, float s0, float s1, float s2,
+                                                const float* __restrict__ norm) {
+  const int b = blockIdx.y;
+  const ViewPlan vp = plan[b];
+  const ImgDesc& d = desc[b];
+  const int64_t n = (int64_t)oh * ow;
+  OutT* o = out + (int64_t)b * 3 * n;
+  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
+  const float mean[3] = {nb ? nb[0] : m0, nb ? nb[1] : m1, nb ? nb[2] : m2};
+  const float stdv[3] = {nb ? nb[3] : s0, nb ? nb[4] : s1, nb ? nb[5] : s2};
+  if (!vp.ok) {  // undecodable (cpu.py:496-497) or not placed: zeros
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < 3 * n; e += (int64_t)gridDim.x * blockDim.x)
+      o[e] = (OutT)0;
+    return;
+  }
+  const int32_t* vb = (const int32_t*)(aws + vp.rcoef_off + align16((int64_t)ow * (2 + vp.kh) * 4));
+  const CoefView cv{vb, vb + 2 * oh, vp.kv};
+  const SrcView src = vp.kh ? SrcView{aws + vp.htmp_off, (int64_t)ow, 1, (int64_t)d.height * ow}
+                            : SrcView{ws + d.rgb_off, (int64_t)d.width * 3, 3, 1};
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(e / ow), x = (int)(e - (int64_t)y * ow);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int v = vp.kv ? vresize_at(src, cv, y, x, c)
+                          : src.base[(int64_t)y * src.pitch + (int64_t)x * src.px + c * src.cs];
+      o[c * n + e] = out_cast<OutT>(u8_normalize(v, mean[c], stdv[c]));
+    }
+  }
+}
+
+template <typename OutT>
+static hipError_t launch_dec_out(const DecodeOnlyArgs& a, hipStream_t s) {
+  const int gx = 64;
+  k_dvpass<OutT><<<dim3(gx, a.batch), 256, 0, s>>>(a.desc, a.plan, a.ow, a.oh, a.ws, a.aws, (OutT*)a.out, a.mean[0],
+                                                   a.mean[1], a.mean[2], a.std[0], a.std[1], a.std[2], a.norm);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_only(const DecodeOnlyArgs& a, hipStream_t s) {
+  if (a.batch <= 0) return hipSuccess;
+  k_dplan<<<1, 1024, 0, s>>>(a.desc, a.batch, a.ow, a.oh, a.aws_size, a.plan);
+  k_dcoeffs<<<a.batch, 256, 0, s>>>(a.desc, a.plan, a.ow, a.oh, a.aws);
+  k_dhpass<<<dim3(64, a.batch), 256, 0, s>>>(a.desc, a.plan, a.ow, a.ws, a.aws);
+  switch (a.out_dtype) {
+    case DINO_OUT_FP32: return launch_dec_out<float>(a, s);
+    case DINO_OUT_FP8_E4M3: return launch_dec_out<uint8_t>(a, s);
+    default: return launch_dec_out<uint16_t>(a, s);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // iBOT masks: one lane runs the (inherently sequential) generator; the mask and
 // the completion scratch live in LDS (dynamic, 5 bytes per patch), the MT states too.
 // ---------------------------------------------------------------------------

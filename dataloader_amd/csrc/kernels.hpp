@@ -97,7 +97,21 @@ struct AugmentArgs {
   const float* norm;       // per-image {mean[3], std[3]} ([0, 1] scale), nullable -> cfg.mean / cfg.std
 };
 
+// Decode-only recipe (dino_resize_batch).
+struct DecodeOnlyArgs {
+  ImgDesc* desc;
+  int32_t batch, ow, oh, out_dtype;
+  ViewPlan* plan;
+  const uint8_t* ws;
+  uint8_t* aws;
+  int64_t aws_size;
+  float mean[3], std[3];
+  const float* norm;
+  void* out;
+};
+
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm = nullptr);
+hipError_t launch_decode_only(const DecodeOnlyArgs& a, hipStream_t s);
 hipError_t launch_params(const ImgDesc* desc, int batch, const dino_aug_config& cfg, uint64_t seed,
                          uint64_t batch_index, dino_view_params* out, hipStream_t s, KernelTimer* tm = nullptr);
 hipError_t launch_augment(const AugmentArgs& a, hipStream_t s, KernelTimer* tm = nullptr);

@@ -94,7 +94,7 @@ class IngestEngine:
 
     KERNEL_NAMES = ["k_parse", "k_plan", "k_destuff", "k_huff1", "k_idct", "k_color", "k_params", "k_vplan",
                     "k_rcoeffs", "k_hresize", "k_final_global", "k_final_local", "k_vert_global", "k_vert_local",
-                    "k_dcscan", "k_htab", "k_hseg", "k_huff2", "k_huff3"]
+                    "k_dcscan", "k_htab", "k_hseg", "k_huff2", "k_huff3", "k_prog"]
 
     def set_timing(self, enable: bool) -> None:
         _lib.check(self.lib.dino_set_timing(self._ctx, int(enable)), "dino_set_timing")
@@ -146,6 +146,19 @@ class IngestEngine:
                                            self._s()), "dino_run_batch")
         self.last_batch = batch
         return views, info
+
+    def resize_batch(self, out_w: int, out_h: int, mean, std, out_dtype: int, batch: int | None = None,
+                     out: torch.Tensor | None = None) -> torch.Tensor:
+        """Decode-only recipe on the last decoded batch (``dino_resize_batch``): [B, 3, out_h, out_w]."""
+        batch = self.last_batch if batch is None else batch
+        if out is None:
+            with self.on_stream():
+                out = torch.empty(batch, 3, out_h, out_w, dtype=_TORCH_OUT[out_dtype], device=self.device)
+        m = (ctypes.c_float * 3)(*[float(x) for x in mean])
+        sd = (ctypes.c_float * 3)(*[float(x) for x in std])
+        _lib.check(self.lib.dino_resize_batch(self._ctx, out_w, out_h, m, sd, out_dtype, _ptr(out), self._s()),
+                   "dino_resize_batch")
+        return out
 
     def batch_info(self, info: torch.Tensor) -> torch.Tensor:
         """Per-image status after augmentation (``dino_batch_info``) into ``info`` [B, 4] int32."""

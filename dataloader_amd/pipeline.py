@@ -371,3 +371,108 @@ class MI355XPipelineIterator:
         self._exhausted = False
         self._source_done = False
         self._queue.clear()
+
+
+class MI355XUserAugPipeline:
+    """``UserAugSpec`` on the GPU: the reference's ``CPUUserAugPipeline.run_one_batch``
+    (cpu.py:484-500) — decode, resize the shorter side to ``decode_size`` (Pillow BICUBIC,
+    torchvision ``Resize`` geometry), normalise — as HIP kernels (``dino_resize_batch``),
+    then ``aug_fn`` on the device tensor.  Like the reference (which ``torch.stack``s the
+    per-image tensors) every image of a batch must resize to the same shape; an
+    undecodable image contributes zeros of shape (3, decode_size, decode_size)."""
+
+    def __init__(self, source: Any, spec, batch_size: int, out_dtype="bf16", device: int = 0,
+                 max_image_dim: int = 16384, workspace_bytes: int = 0, norm=None):
+        self._source = source
+        self._spec = spec
+        self._batch_size = int(batch_size)
+        self._out = _out_code(out_dtype)
+        self._norm = norm
+        self._max_image_dim = int(max_image_dim)
+        self._engine = IngestEngine(device, max_batch=self._batch_size, max_views=1, max_crop_size=8,
+                                    max_image_dim=max_image_dim, workspace_bytes=workspace_bytes)
+        self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0}
+        self._closed = False
+
+    @property
+    def device(self) -> torch.device:
+        return self._engine.device
+
+    def run_one_batch(self) -> dict[str, torch.Tensor]:
+        if self._closed:
+            raise RuntimeError("MI355XUserAugPipeline.run_one_batch() called after close()")
+        from .config import resize_shorter_size
+        jpegs = self._source()
+        assert len(jpegs) == self._batch_size
+        host_buf, offsets = pack_jpegs(jpegs, pin=True)
+        info, ws, _ = fallback.probe(host_buf.data_ptr(), offsets.numpy(), len(jpegs), self._max_image_dim)
+        if (info[:, 0] == fallback.IMG_UNSUPPORTED).any():
+            jpegs, n = fallback.hand_over(list(jpegs), info[:, 0])
+            self.stats["host_decoded"] += n
+            host_buf, offsets = pack_jpegs(jpegs, pin=True)
+            info, ws, _ = fallback.probe(host_buf.data_ptr(), offsets.numpy(), len(jpegs), self._max_image_dim)
+        ds = int(self._spec.decode_size)
+        shapes = {resize_shorter_size(int(w), int(h), ds) if st == 0 else (ds, ds)
+                  for st, w, h, _ in info.tolist()}
+        if len(shapes) != 1:  # the reference's torch.stack raises on unequal shapes
+            raise RuntimeError(f"stack expects each tensor to be equal size, got resized shapes {sorted(shapes)}")
+        ow, oh = shapes.pop()
+        aws = 0
+        for st, w, h, _ in info.tolist():
+            if st == 0:
+                kh = 2 * (-(-2 * w // ow)) + 3
+                kv = 2 * (-(-2 * h // oh)) + 3
+                aws += ow * (2 + kh) * 4 + oh * (2 + kv) * 4 + h * ow * 3 + 64
+        self._engine.reserve(ws, aws)
+        eng = self._engine
+        d_bytes = host_buf.to(self.device, non_blocking=True)
+        d_off = offsets.to(self.device, non_blocking=True)
+        if self._norm is not None:
+            self._norm_dev = torch.from_numpy(self._norm.batch_records(len(jpegs))).to(self.device)
+            eng.set_norm(self._norm_dev)
+        d_info = eng.decode(d_bytes, d_off, len(jpegs))
+        out = eng.resize_batch(ow, oh, self._spec.mean, self._spec.std, self._out)
+        eng.batch_info(d_info)
+        st = d_info[:, 0].cpu().numpy()
+        self.stats["batches"] += 1
+        self.stats["images"] += len(st)
+        self.stats["status"].update(int(x) for x in st)
+        if (st > 0).any():
+            warnings.warn(f"MI355XUserAugPipeline: {int((st > 0).sum())} decodable image(s) returned zeros",
+                          RuntimeWarning, stacklevel=2)
+        self._inflight = (host_buf, d_bytes, d_off)
+        return self._spec.aug_fn(out)
+
+    def close(self) -> None:
+        if not self._closed:
+            self._closed = True
+            self._engine.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
+class MI355XUserAugIterator:
+    """The DALIBackend's ``_UserAugIterator`` contract (dali_backend.py:27-56): ``next()`` ->
+    ``[aug_fn(decoded)]``, with a ValueError when a view of ``output_map`` is missing."""
+
+    def __init__(self, pipeline: MI355XUserAugPipeline, output_map: list[str]) -> None:
+        self._pipe = pipeline
+        self._map = list(output_map)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self) -> list[dict[str, torch.Tensor]]:
+        augmented = self._pipe.run_one_batch()
+        missing = [k for k in self._map if k not in augmented]
+        if missing:
+            raise ValueError(f"UserAugSpec.aug_fn did not return expected view(s): {missing}. "
+                             f"Got keys: {list(augmented.keys())}")
+        return [augmented]
+
+    def reset(self) -> None:
+        """Stateless between batches."""

@@ -167,6 +167,16 @@ int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offse
                    dino_view_params* d_params_out, void* const* views, int32_t* d_info,
                    void* stream);
 
+/* Decode-only recipe (reference CPUUserAugPipeline.run_one_batch, cpu.py:484-500, and the
+ * DALI decode-only graph, pipeline.py:693-756): every image of the last decoded batch
+ * resampled whole (Pillow BICUBIC) to out_w x out_h, normalised ((p / 255 - mean) / std,
+ * or the dino_set_norm statistics) and cast into d_out = [batch, 3, out_h, out_w] NCHW.
+ * Images with status != 0 are zero-filled.  The caller applies UserAugSpec.aug_fn to the
+ * result (the reference stacks per-image tensors, so all images of a batch must resize
+ * to the same shape; the Python layer checks that before calling). */
+int dino_resize_batch(dino_ctx* ctx, int32_t out_w, int32_t out_h, const float* mean, const float* std,
+                      int32_t out_dtype, void* d_out, void* stream);
+
 /* Per-image status of the last batch after augmentation (the decode status, or
  * DINO_IMG_NO_SPACE when one of the image's views did not fit the augment workspace):
  * d_info: int32[batch][4] as dino_decode's. */

@@ -13,6 +13,7 @@ Follows, op for op, reference ``src/dino_loader/backends/cpu.py``:
   ``_center_crop`` cpu.py:186-187) -> :func:`eval_one`, :func:`eval_geometry`
 * ``CPULeJEPAPipeline.run_one_batch`` cpu.py:435-461 -> :func:`lejepa_one` (views replayed
   from their :class:`ViewParams`, as the multi-crop ones)
+* ``CPUUserAugPipeline.run_one_batch`` cpu.py:484-500 -> :func:`decode_only_one`
 
 The reference draws every random quantity from process-global RNGs inside the
 ops (torch global RNG for RandomResizedCrop/ColorJitter, Python ``random`` for
@@ -286,6 +287,21 @@ def eval_one(jpeg_bytes: bytes, crop_size: int, mean=IMAGENET_MEAN, std=IMAGENET
     new_w, new_h, left, top = eval_geometry(img.size[0], img.size[1], crop_size)
     img = img.resize((new_w, new_h), Image.BICUBIC)
     img = img.crop((left, top, left + crop_size, top + crop_size))
+    return to_tensor_normalized(img, mean, std, out_dtype)
+
+
+def decode_only_one(jpeg_bytes: bytes, decode_size: int, mean=IMAGENET_MEAN, std=IMAGENET_STD,
+                    out_dtype=torch.bfloat16) -> torch.Tensor:
+    """CPUUserAugPipeline for one sample (cpu.py:491-497): decode, torchvision
+    ``Resize(decode_size)`` of the shorter side (BICUBIC, geometry of eval_geometry),
+    normalise; undecodable -> zeros (3, decode_size, decode_size)."""
+    img = decode_rgb(jpeg_bytes)
+    if img is None:
+        return torch.zeros(3, decode_size, decode_size, dtype=out_dtype)
+    w, h = img.size
+    nw, nh = (decode_size, int(decode_size * h / w)) if w <= h else (int(decode_size * w / h), decode_size)
+    if (nw, nh) != img.size:
+        img = img.resize((nw, nh), Image.BICUBIC)
     return to_tensor_normalized(img, mean, std, out_dtype)
 
 

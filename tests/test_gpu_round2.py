@@ -247,7 +247,7 @@ def test_pipeline_hands_unsupported_flavours_to_pillow(gpu_device):
     jpegs = [good, _cmyk(240, 180, rng), encode_jpeg(textured_rgb(256, 300, rng), progressive=True), bytes(arith),
              b"\xff\xd8\xff corrupt", _cmyk(97, 131, rng)]
     cfg = DINOAugConfig(global_crop_size=64, local_crop_size=32, n_local_crops=3)
-    pipe = MI355XAugPipeline(lambda: jpegs, cfg, len(jpegs), seed=4, out_dtype="fp32", depth=2)
+    pipe = MI355XAugPipeline(lambda: jpegs, cfg, len(jpegs), seed=4, out_dtype="fp32", depth=1)
     it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], len(jpegs))
     out = next(it)[0]
     torch.cuda.synchronize()
@@ -461,3 +461,60 @@ def test_iterator_reset_with_batches_in_flight(gpu_device):
     for k in ref:
         assert torch.equal(ref[k], got[k]), k
     ser.close()
+
+
+def test_user_aug_spec_decode_only(gpu_device):
+    """UserAugSpec (reference CPUUserAugPipeline, cpu.py:484-500): decode + Resize(decode_size)
+    + normalise on the GPU, then aug_fn on the device tensor; bit-exact vs the oracle; a batch
+    whose images resize to different shapes raises like the reference's torch.stack; an
+    undecodable image contributes zeros; a missing view raises ValueError (DALI iterator)."""
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import PipelineConfig, UserAugSpec
+    rng = np.random.default_rng(40)
+    calls = []
+
+    def aug_fn(x):
+        calls.append((tuple(x.shape), x.dtype, x.device.type))
+        return {"a": x, "b": x.flip(-1)}
+
+    def src_of(jpegs):
+        class Src:
+            _batch_size = len(jpegs)
+            _resolution_src = None
+
+            def __call__(self):
+                return jpegs
+        return Src()
+
+    be = MI355XBackend()
+    for dtype, tdt in (("fp32", torch.float32), ("bf16", torch.bfloat16)):
+        spec = UserAugSpec(aug_fn=aug_fn, _output_map=["a", "b"], decode_size=256, warn_not_dali=False)
+        jpegs = [encode_jpeg(textured_rgb(w, h, rng), progressive=p) for (w, h), p in
+                 (((640, 480), False), ((320, 240), True), ((800, 600), False), ((1024, 768), False),
+                  ((341, 256), False))]
+        pipe = be.build_pipeline(src_of(jpegs), spec, PipelineConfig(output_dtype=dtype), None)
+        out = next(be.build_pipeline_iterator(pipe, spec, spec.output_map, len(jpegs)))[0]
+        torch.cuda.synchronize()
+        assert calls[-1] == ((5, 3, 256, 341), tdt, "cuda")
+        for b, j in enumerate(jpegs):
+            ref = cpu_ref.decode_only_one(j, 256, spec.mean, spec.std, out_dtype=tdt)
+            assert torch.equal(out["a"][b].cpu(), ref), (dtype, b)
+        pipe.close()
+    spec = UserAugSpec(aug_fn=aug_fn, _output_map=["a"], decode_size=64, warn_not_dali=False)
+    sq = [encode_jpeg(textured_rgb(s, s, rng)) for s in (100, 64, 300)] + [b"corrupt"]
+    pipe = be.build_pipeline(src_of(sq), spec, PipelineConfig(output_dtype="fp32"), None)
+    out = next(be.build_pipeline_iterator(pipe, spec, spec.output_map, 4))[0]["a"].cpu()
+    for b, j in enumerate(sq):
+        assert torch.equal(out[b], cpu_ref.decode_only_one(j, 64, spec.mean, spec.std, out_dtype=torch.float32)), b
+    assert torch.count_nonzero(out[3]) == 0
+    pipe.close()
+    mixed = [encode_jpeg(textured_rgb(640, 480, rng)), encode_jpeg(textured_rgb(480, 640, rng))]
+    pipe = be.build_pipeline(src_of(mixed), spec, PipelineConfig(output_dtype="fp32"), None)
+    with pytest.raises(RuntimeError, match="equal size"):
+        next(be.build_pipeline_iterator(pipe, spec, spec.output_map, 2))
+    pipe.close()
+    spec_bad = UserAugSpec(aug_fn=lambda x: {"a": x}, _output_map=["a", "zzz"], decode_size=64, warn_not_dali=False)
+    pipe = be.build_pipeline(src_of(sq[:3]), spec_bad, PipelineConfig(output_dtype="fp32"), None)
+    with pytest.raises(ValueError, match="zzz"):
+        next(be.build_pipeline_iterator(pipe, spec_bad, spec_bad.output_map, 3))
+    pipe.close()

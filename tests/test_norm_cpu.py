@@ -69,8 +69,8 @@ def test_recipe_configs_and_spec_dispatch():
     e = make_aug_config(recipe_aug_config(EvalAugSpec(crop_size=192)), 192, 192, 0)
     assert e.recipe == RECIPE_EVAL and (e.n_global, e.n_local, e.global_size) == (1, 0, 192)
 
-    class UserAugSpec:
+    class SomeOtherSpec:  # not a recipe the backend knows: TypeError, as cpu.py:708-709
         pass
 
     with pytest.raises(TypeError):
-        MI355XBackend().build_pipeline(None, UserAugSpec(), PipelineConfig(), None)
+        MI355XBackend().build_pipeline(None, SomeOtherSpec(), PipelineConfig(), None)
