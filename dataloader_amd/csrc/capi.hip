@@ -379,9 +379,9 @@ int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, i
     case 2: src = c->d_ws + d.coef_off; n = d.plane_off - d.coef_off; break;  // sparse entries + block info
     case 3: src = c->d_ws + d.plane_off; n = d.rgb_off - d.plane_off; break;
     case 4: src = c->d_ws + d.rgb_off; n = (int64_t)d.width * d.height * 3; break;
-    case 5:  // speculative-decode lane records (sizeof(LaneRec) bytes each, restart images: none)
+    case 5:  // speculative-decode lane records (68 bytes each, restart images: none)
       src = c->d_ws + d.hlane_off;
-      n = d.restart_interval > 0 ? 0 : (int64_t)d.h_lanes * (int64_t)sizeof(LaneRec);
+      n = d.restart_interval > 0 ? 0 : (int64_t)d.h_lanes * 68;
       break;
     default: return fail(DINO_EINVAL, "dino_debug_region: region %s%lld", "", region);
   }

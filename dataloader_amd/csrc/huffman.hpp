@@ -355,16 +355,9 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
 // ---------------------------------------------------------------------------
 
 // What a lane learns by decoding the steps that start in [st.pos, end).
-// sync: how the decode relates to the lane's first (speculative) decode —
-//   kSyncFirst  it IS the first decode (the lane's start state never changed),
-//   j >= 0      a re-decode that met the first decode at checkpoint j (from there on
-//               both decodes are the same: the first decode's blocks are reusable),
-//   kSyncNone   a re-decode that never met the first decode inside the range.
-constexpr int32_t kSyncFirst = -1, kSyncNone = -2;
 struct RangeOut {
   HState end;      // state at the first step boundary >= end
   int32_t nblk;    // blocks whose DC step starts in the range
-  int32_t sync;
 };
 
 #ifndef DINO_HUFF_CHECKPOINTS
@@ -421,65 +414,6 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
   r.end.pos = cur.pos;
   r.end.c = blk;
   r.end.z = z;
-  r.sync = kSyncFirst;
-  *ncp = n;
-  return r;
-}
-
-// decode_range that also emits the blocks it decodes into `sink` (begin() without a
-// block index, dc/ac, end()), finishing the block in progress at `end` (its DC step
-// started inside the range, so it is this lane's) without changing the returned end
-// state; *after: the state past that last block.  The lane's first decode: its
-// blocks become final from the checkpoint where a corrected re-decode meets it.
-template <int kWin, typename Sink>
-DHD RangeOut decode_range_emit(const BitReader& br, const HuffImage& im, HState st, uint32_t end, Checkpoint* cps,
-                               int cstride, int kmax, int32_t* ncp, Sink& sink, HState* after) {
-  st = sanitize(st, im.blocks_per_mcu);
-  RangeOut r;
-  r.nblk = 0;
-  int n = 0;
-  BitCursor cur;
-  bc_init<kWin>(cur, br, st.pos);
-  int32_t blk = st.c, z = st.z;
-  bool open = false;
-  while (cur.pos < end) {
-    if (z == 0) {
-      if (n < kmax && (r.nblk < kHuffCpDense || (r.nblk & (kHuffCpStride - 1)) == 0))
-        cps[(n++) * cstride] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
-      r.nblk++;
-      sink.begin();
-      open = true;
-    }
-    const StepOut o = huff_step<kWin>(cur, br, im, blk, z);
-    if (open) {
-      if (o.kind == 0)
-        sink.dc((int16_t)o.value);
-      else if (o.kind == 1)
-        sink.ac(o.zz, (int16_t)o.value);
-      if (o.block_done) {
-        sink.end();
-        open = false;
-      }
-    }
-  }
-  r.end.pos = cur.pos;
-  r.end.c = blk;
-  r.end.z = z;
-  r.sync = kSyncFirst;
-  while (open) {
-    const StepOut o = huff_step<kWin>(cur, br, im, blk, z);
-    if (o.kind == 0)
-      sink.dc((int16_t)o.value);
-    else if (o.kind == 1)
-      sink.ac(o.zz, (int16_t)o.value);
-    if (o.block_done) {
-      sink.end();
-      open = false;
-    }
-  }
-  after->pos = cur.pos;
-  after->c = blk;
-  after->z = z;
   *ncp = n;
   return r;
 }
@@ -503,7 +437,6 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
       if (j < ncp && cps[j * cstride].pos == cur.pos && (int32_t)(cps[j * cstride].cn & 15u) == blk) {
         RangeOut r = first;
         r.nblk = nblk + first.nblk - (int32_t)(cps[j * cstride].cn >> 4);
-        r.sync = j;
         return r;
       }
       nblk++;
@@ -515,75 +448,6 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
   r.end.c = blk;
   r.end.z = z;
   r.nblk = nblk;
-  r.sync = kSyncNone;
-  return r;
-}
-
-// decode_range_sync that also emits the blocks of the re-decode into `sink` (the
-// leading partial block, st.z != 0, belongs to the previous lane and is skipped): up
-// to the checkpoint where it meets the first decode (those are the lane's prefix
-// blocks), or, when it never meets it, every block started in the range, the last
-// one finished past `end`; *after: the state past the last emitted block (only
-// meaningful for kSyncNone).
-template <int kWin, typename Sink>
-DHD RangeOut decode_range_sync_emit(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
-                                    const Checkpoint* cps, int cstride, int ncp, RangeOut first, Sink& sink,
-                                    HState* after) {
-  st = sanitize(st, im.blocks_per_mcu);
-  int32_t nblk = 0;
-  int j = 0;
-  BitCursor cur;
-  bc_init<kWin>(cur, br, st.pos);
-  int32_t blk = st.c, z = st.z;
-  bool open = false;
-  while (cur.pos < end) {
-    if (z == 0) {
-      while (j < ncp && cps[j * cstride].pos < cur.pos) ++j;
-      if (j < ncp && cps[j * cstride].pos == cur.pos && (int32_t)(cps[j * cstride].cn & 15u) == blk) {
-        RangeOut r = first;
-        r.nblk = nblk + first.nblk - (int32_t)(cps[j * cstride].cn >> 4);
-        r.sync = j;
-        after->pos = cur.pos;
-        after->c = blk;
-        after->z = 0;
-        return r;
-      }
-      nblk++;
-      sink.begin();
-      open = true;
-    }
-    const StepOut o = huff_step<kWin>(cur, br, im, blk, z);
-    if (open) {
-      if (o.kind == 0)
-        sink.dc((int16_t)o.value);
-      else if (o.kind == 1)
-        sink.ac(o.zz, (int16_t)o.value);
-      if (o.block_done) {
-        sink.end();
-        open = false;
-      }
-    }
-  }
-  RangeOut r;
-  r.end.pos = cur.pos;
-  r.end.c = blk;
-  r.end.z = z;
-  r.nblk = nblk;
-  r.sync = kSyncNone;
-  while (open) {
-    const StepOut o = huff_step<kWin>(cur, br, im, blk, z);
-    if (o.kind == 0)
-      sink.dc((int16_t)o.value);
-    else if (o.kind == 1)
-      sink.ac(o.zz, (int16_t)o.value);
-    if (o.block_done) {
-      sink.end();
-      open = false;
-    }
-  }
-  after->pos = cur.pos;
-  after->c = blk;
-  after->z = z;
   return r;
 }
 
@@ -599,12 +463,9 @@ DHD RangeOut decode_range_sync_emit(const BitReader& br, const HuffImage& im, HS
 // carried by the caller); without, the difference (summed later by the DC prefix
 // pass, k_dcscan).  A difference fits int16: DC categories are <= 15.  Returns the
 // bit position.
-// `stop` (optional): stop at the block boundary with that bit position and block-in-MCU
-// index (the prefix of a spliced lane, see k_huff3).  *nwritten (optional): blocks emitted.
 template <int kWin, typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
-                          int32_t total_blocks, int32_t* pred, Sink& sink, const Checkpoint* stop = nullptr,
-                          int32_t* nwritten = nullptr) {
+                          int32_t total_blocks, int32_t* pred, Sink& sink) {
   st = sanitize(st, im.blocks_per_mcu);
   BitCursor cur;
   bc_init<kWin>(cur, br, st.pos);
@@ -612,10 +473,8 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
   while (z != 0) {  // skip the tail of the previous lane's block
     huff_step<kWin>(cur, br, im, blk, z);
   }
-  const uint32_t stop_pos = stop ? stop->pos : 0xFFFFFFFFu;
-  const int32_t stop_c = stop ? (int32_t)(stop->cn & 15u) : -1;
   int32_t b = first_block;
-  while (b < total_blocks && cur.pos < end && !(cur.pos == stop_pos && blk == stop_c)) {
+  while (b < total_blocks && cur.pos < end) {
     sink.begin(b);
     int comp = hi_comp(im, blk);
     for (;;) {
@@ -631,7 +490,6 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
     sink.end();
     ++b;
   }
-  if (nwritten) *nwritten = b - first_block;
   return cur.pos;
 }
 

@@ -499,42 +499,22 @@ constexpr int kHuff3LdsBytes = (int)((sizeof(HuffLds3) + 15) & ~(size_t)15);
 struct SparseSink {
   uint32_t* ent;   // image entry area
   uint2* binfo;    // image block info
-  uint2* rec;      // speculative mode (open_spec): the area's own record list, else nullptr
   uint32_t n;      // halfwords stored (relative to the image entry area), multiple of 8
   uint32_t k;      // halfwords buffered in w0..w3
-  uint32_t lim;    // end of the area (halfwords; speculative mode)
   uint32_t w0, w1, w2, w3;
   uint32_t bstart, dcw, n16, n32;
   bool wide;       // the open block has switched to u32 entries
-  bool ovf;        // speculative mode: the area overflowed (its output is unusable)
   int32_t b;
-  int32_t cnt;     // speculative mode: records appended
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
-    rec = nullptr;
-    lim = 0xFFFFFFFFu;
-    ovf = false;
   }
-  // Speculative mode: entries from halfword `base_hw` on (kSpecHw of them), records
-  // appended to `records` (kSpecRec of them), block indices unknown yet.
-  __device__ void open_spec(uint32_t base_hw, uint2* records) {
-    n = base_hw;
-    k = 0;
-    rec = records;
-    lim = base_hw + kSpecHw;
-    cnt = 0;
-    ovf = false;
-  }
-  __device__ void begin() {
+  __device__ void begin(int32_t blk) {
+    b = blk;
     bstart = n + k;
     dcw = 0;
     n16 = n32 = 0;
     wide = false;
-  }
-  __device__ void begin(int32_t blk) {
-    b = blk;
-    begin();
   }
   // w0..w3 are a shift register of halfwords: a new one enters at the top and the
   // eighth push has moved the first to the bottom (four v_alignbyte per push)
@@ -547,8 +527,7 @@ struct SparseSink {
   __device__ void put(uint32_t h) {
     shift_in(h);
     if (++k == 8) {
-      if (n + 8 <= lim) *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
-      else ovf = true;
+      *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
       n += 8;
       k = 0;
     }
@@ -569,21 +548,11 @@ struct SparseSink {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void end() {
-    const uint2 r = make_uint2(bstart, n16 | (n32 << 7) | dcw);
-    if (!rec) {
-      binfo[b] = r;
-    } else {
-      if (cnt < kSpecRec) rec[cnt] = r;
-      else ovf = true;
-      ++cnt;
-    }
-  }
+  __device__ void end() { binfo[b] = make_uint2(bstart, n16 | (n32 << 7) | dcw); }
   __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
     if (k) {
       for (uint32_t j = k; j < 8; ++j) shift_in(0u);
-      if (n + 8 <= lim) *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
-      else ovf = true;
+      *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
     }
   }
 };
@@ -729,49 +698,6 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
   return true;
 }
 
-// Final pass of one lane of a speculatively decoded image, normally without decoding:
-// its blocks are the last re-decode's (area B) up to the checkpoint where that
-// re-decode met the first decode, then the first decode's (area A) from there on;
-// B alone when it never met it, A alone when the lane was never re-decoded.  The
-// block records are copied into binfo from the lane's first block; the entries stay
-// where the areas hold them.  A lane whose needed area overflowed is re-decoded into
-// the block-indexed region; the image's last lane keeps decoding when the stream runs
-// short of blocks (zero fill, as decode_write's open-ended last lane).
-__device__ void lane_splice(const BitReader& br, const HuffImage& im, const ImgDesc& sd, uint8_t* ws, int i,
-                            const HState& S, const RangeOut& R, int32_t na, int32_t nB, int32_t ovf,
-                            const HState& afterA, const HState& afterB, const Checkpoint* cps, int cstride,
-                            int32_t blk0) {
-  uint2* binfo = (uint2*)(ws + sd.binfo_off);
-  const int32_t T = sd.total_blocks;
-  const bool useB = R.sync != kSyncFirst, useA = R.sync != kSyncNone;
-  SparseSink sink;
-  sink.ent = (uint32_t*)(ws + sd.coef_off);
-  sink.binfo = binfo;
-  if ((useA && (ovf & 1)) || (useB && (ovf & 2))) {
-    sink.open(blk0);
-    decode_write<kSrcPadded>(br, im, S, lane_write_end(sd, i), blk0, T, (int32_t*)nullptr, sink);
-    sink.close();
-    return;
-  }
-  int32_t b = blk0;
-  HState tail = afterB;
-  if (useB) {
-    const uint2* rb = (const uint2*)(ws + sd.coef_off + spec_rec_off(sd, 1, i));
-    for (int32_t k = 0; k < nB && b < T; ++k) binfo[b++] = rb[k];
-  }
-  if (useA) {
-    const int32_t kj = R.sync >= 0 ? (int32_t)(cps[R.sync * cstride].cn >> 4) : 0;
-    const uint2* ra = (const uint2*)(ws + sd.coef_off + spec_rec_off(sd, 0, i));
-    for (int32_t k = kj; k < na && b < T; ++k) binfo[b++] = ra[k];
-    tail = afterA;
-  }
-  if (i == sd.h_lanes - 1 && b < T) {
-    sink.open(b);
-    decode_write<kSrcPadded>(br, im, tail, 0xFFFFFFFFu, b, T, (int32_t*)nullptr, sink);
-    sink.close();
-  }
-}
-
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -795,18 +721,11 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     // checkpoint k of lane i at [k][lane]: a wave's lanes write neighbouring words
     Checkpoint* cps = (Checkpoint*)(ws + sd.cps_off) + i;
     const int cstride = sd.h_lanes_cap;
-    int32_t ncp = 0, ovf = 0, nB = 0;
+    int32_t ncp = 0;
     HState myS{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};  // this lane's start state and first-decode
     RangeOut myR1{};                                      // result stay in registers; only R is shared
-    HState afterA{0, 0, 0}, afterB{0, 0, 0};
     if (active) {
-      // first decode from the guessed state; its blocks go to area A
-      SparseSink sa;
-      sa.ent = (uint32_t*)(ws + sd.coef_off);
-      sa.open_spec(spec_ent_hw(sd, 0, i), (uint2*)(ws + sd.coef_off + spec_rec_off(sd, 0, i)));
-      myR1 = decode_range_emit<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp, sa, &afterA);
-      sa.close();
-      ovf = sa.ovf ? 1 : 0;
+      myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
       L.R[t] = myR1;
     }
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
@@ -818,35 +737,32 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
         redo = !hstate_eq(want, myS);
       }
       __syncthreads();
-      if (redo) {  // re-decode from the corrected state; its blocks (up to the meeting point) go to area B
+      if (redo) {
         myS = want;
-        SparseSink sb;
-        sb.ent = (uint32_t*)(ws + sd.coef_off);
-        sb.open_spec(spec_ent_hw(sd, 1, i), (uint2*)(ws + sd.coef_off + spec_rec_off(sd, 1, i)));
-        L.R[t] = decode_range_sync_emit<kSrcPadded>(br, im, want, rend, cps, cstride, ncp, myR1, sb, &afterB);
-        sb.close();
-        ovf = (ovf & 1) | (sb.ovf ? 2 : 0);
-        nB = sb.cnt;
+        L.R[t] = decode_range_sync<kSrcPadded>(br, im, want, rend, cps, cstride, ncp, myR1);
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
     if (huff_single_segment(sd)) {
-      // the whole image is this segment: its start states are final, so the lanes'
-      // blocks are spliced into place here (k_huff2 and k_huff3 skip it)
+      // the whole image is this segment: its start states are final, so the blocks
+      // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
       uint32_t tot;
       const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)L.R[t].nblk : 0u, L.wave, &tot);
-      if (active)
-        lane_splice(br, im, sd, ws, i, myS, L.R[t], myR1.nblk, nB, ovf, afterA, afterB, cps, cstride, (int32_t)blk0);
+      if (active) {
+        SparseSink sink;
+        sink.ent = (uint32_t*)(ws + sd.coef_off);
+        sink.binfo = (uint2*)(ws + sd.binfo_off);
+        sink.open((int32_t)blk0);
+        decode_write<kSrcPadded>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
+                                 sink);
+        sink.close();
+      }
     } else if (active) {
       LaneRec& o = lr[i];
       o.S = myS;
       o.R = L.R[t];
       o.R1 = myR1;
       o.ncp = ncp;
-      o.ovf = ovf;
-      o.nB = nB;
-      o.afterA = afterA;
-      o.afterB = afterB;
     }
     __syncthreads();
   }
@@ -891,16 +807,8 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
         if (lr[i].pad) {
           const HState want = lr[i].W;
           lr[i].S = want;
-          SparseSink sb;
-          sb.ent = (uint32_t*)(ws + d.coef_off);
-          sb.open_spec(spec_ent_hw(d, 1, i), (uint2*)(ws + d.coef_off + spec_rec_off(d, 1, i)));
-          HState afterB;
-          lr[i].R = decode_range_sync_emit<kSrcPadded>(br, im, want, lane_range_end(d, i, nbits), cps + i,
-                                                       d.h_lanes_cap, lr[i].ncp, lr[i].R1, sb, &afterB);
-          sb.close();
-          lr[i].afterB = afterB;
-          lr[i].ovf = (lr[i].ovf & 1) | (sb.ovf ? 2 : 0);
-          lr[i].nB = sb.cnt;
+          lr[i].R = decode_range_sync<kSrcPadded>(br, im, want, lane_range_end(d, i, nbits),
+                                             cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1);
         }
       }
       __syncthreads();
@@ -957,8 +865,9 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
     } else if (i < sd.h_lanes) {
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
-      lane_splice(br, im, sd, ws, i, r.S, r.R, r.R1.nblk, r.nB, r.ovf, r.afterA, r.afterB,
-                  (const Checkpoint*)(ws + sd.cps_off) + i, sd.h_lanes_cap, r.blk0);
+      sink.open(r.blk0);
+      decode_write<kSrcPadded>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr, sink);
+      sink.close();
     }
     __syncthreads();
   }

@@ -17,21 +17,9 @@ struct LaneRec {
   int32_t ncp;    // checkpoints recorded by the first decode
   int32_t blk0;   // first block the lane emits (k_huff2 scan)
   HState W;       // k_huff2 scratch: wanted start state
-  int32_t pad;    // k_huff2 scratch: re-decode this round
-  HState afterA;  // state past the last block the first decode emitted (area A)
-  HState afterB;  // state past the last block the last re-decode emitted (area B)
-  int32_t ovf;    // bit 0: area A overflowed, bit 1: area B overflowed
-  int32_t nB;     // blocks the last re-decode emitted
+  int32_t pad;
 };
-static_assert(sizeof(LaneRec) == 108, "LaneRec layout");
-
-// Speculative output areas of a lane (k_huff1 / k_huff2 write them, k_huff3 splices):
-// A = blocks of the first decode, B = blocks of the last re-decode.  Each area holds
-// kSpecHw halfwords of sparse entries and kSpecRec 8-byte block records; a lane whose
-// output does not fit falls back to the block-indexed region (a full re-decode).
-constexpr uint32_t kSpecHw = 2048;
-constexpr int32_t kSpecRec = 256;
-DHD int64_t spec_bytes_per_lane() { return 2 * ((int64_t)kSpecHw * 2 + (int64_t)kSpecRec * 8); }
+static_assert(sizeof(LaneRec) == 68, "LaneRec layout");
 
 // Lanes reserved for the speculative Huffman decode (restart images decode per interval).
 DHD int32_t huff_lanes_cap(const ImgDesc& d) {
@@ -77,9 +65,9 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   }
   z.ent = align16((int64_t)d.scan_len + 64);
   z.rst = align16(4 * ((int64_t)d.n_rst_max + 1));
-  const int64_t lanes = huff_lanes_cap(d);
-  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2 + lanes * spec_bytes_per_lane();
+  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;
   z.binfo = align16((int64_t)d.total_blocks * 8);
+  const int64_t lanes = huff_lanes_cap(d);
   z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
   z.htab = align16((int64_t)sizeof(HuffTables));
   z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
@@ -102,16 +90,6 @@ DHD int64_t view_scratch_bytes(int S, int crop_w, int crop_h, int kh, int kv) {
 DHD int64_t view_scratch_bound(int S, int W, int H) {
   const int kh = resample_ksize(W > S ? W : S, S), kv = resample_ksize(H > S ? H : S, S);
   return view_scratch_bytes(S, W, H, kh, kv);
-}
-
-// Halfword offset (from the image's entry area) of lane `lane`'s area (0 = A, 1 = B).
-DHD uint32_t spec_ent_hw(const ImgDesc& d, int area, int lane) {
-  return (uint32_t)d.total_blocks * kEntHalfwordsPerBlock + ((uint32_t)area * d.h_lanes_cap + lane) * kSpecHw;
-}
-// Byte offset (from the image's entry area) of that area's block records.
-DHD int64_t spec_rec_off(const ImgDesc& d, int area, int lane) {
-  return (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2 + 2 * (int64_t)d.h_lanes_cap * kSpecHw * 2 +
-         ((int64_t)area * d.h_lanes_cap + lane) * kSpecRec * 8;
 }
 
 }  // namespace dino

@@ -96,19 +96,6 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTables* tabs, H
   return true;
 }
 
-// Phase-1 block list of one lane (the model of SpecSink): DC difference + (zz, value) pairs.
-struct ModelBlock {
-  int16_t dc = 0;
-  std::vector<std::pair<int, int16_t>> ac;
-};
-struct ModelSpecSink {
-  std::vector<ModelBlock> blocks;
-  void begin() { blocks.emplace_back(); }
-  void dc(int16_t v) { blocks.back().dc = v; }
-  void ac(int zz, int16_t v) { blocks.back().ac.emplace_back(zz, v); }
-  void end() {}
-};
-
 // ---- k_huffman, speculative mode over `lanes` lanes in segments of `seg` lanes ----
 // k_huff1: every range decoded from a guessed state recording checkpoints, then
 // rounds inside each segment re-decode the ranges whose start state changed
@@ -128,14 +115,11 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   std::vector<RangeOut> R(n), R1(n);
   std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
   std::vector<int32_t> ncp(n);
-  std::vector<ModelSpecSink> spec(n), redo_out(n);  // area A (first decode) and B (last re-decode)
-  std::vector<HState> after(n), redo_after(n);
   auto rend = [&](int i) -> uint32_t { return i == n - 1 ? nbits : (uint32_t)(i + 1) * sub; };
   auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
   for (int i = 0; i < n; ++i) {
     S[i] = HState{(uint32_t)i * sub, 0, 0};
-    R[i] = R1[i] = decode_range_emit<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1,
-                                           kHuffCheckpoints, &ncp[i], spec[i], &after[i]);
+    R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, kHuffCheckpoints, &ncp[i]);
   }
   int rounds = 0, redone = 0;
   for (int pass = 0; pass < 2; ++pass) {  // 0: inside segments (k_huff1), 1: whole image (k_huff2)
@@ -151,9 +135,7 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
       for (int i = 1; i < n; ++i) {
         if (!redo[i]) continue;
         S[i] = want[i];
-        redo_out[i].blocks.clear();
-        R[i] = decode_range_sync_emit<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i],
-                                            R1[i], redo_out[i], &redo_after[i]);
+        R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i], R1[i]);
         any = true;
         ++redone;
       }
@@ -161,40 +143,10 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
       if (!any) break;
     }
   }
-  // final pass (k_huff3 / the end of k_huff1): a lane's blocks are the prefix its true
-  // decode produces before the checkpoint where it met the first decode, then the
-  // first decode's blocks from that checkpoint on; the image's last lane continues past
-  // them (a stream that runs short of blocks); a lane that never met its first decode
-  // is decoded whole
-  // final pass (k_huff3 / the end of k_huff1), no decoding: a lane's blocks are its last
-  // re-decode's blocks (B) up to the checkpoint where it met the first decode, then the
-  // first decode's blocks (A) from that checkpoint on; B alone when it never met it; A
-  // alone when the lane was never re-decoded.  The image's last lane continues past
-  // them when the stream runs short of blocks (zero-fill decode).
   int32_t blk0 = 0;
   sink.dcd = dcd;
-  int spliced = 0;
-  auto put = [&](const ModelBlock& m, int32_t b) {
-    sink.begin(b);
-    sink.dc(m.dc);
-    for (auto& e : m.ac) sink.ac(e.first, e.second);
-    sink.end();
-  };
   for (int i = 0; i < n; ++i) {
-    const RangeOut& r = R[i];
-    int32_t b = blk0;
-    HState tail = after[i];
-    if (r.sync != kSyncFirst)
-      for (size_t t = 0; t < redo_out[i].blocks.size() && b < total_blocks; ++t) put(redo_out[i].blocks[t], b++);
-    if (r.sync == kSyncNone) {
-      tail = redo_after[i];
-    } else {
-      const int32_t kj = r.sync >= 0 ? (int32_t)(cps[(size_t)i * kHuffCheckpoints + r.sync].cn >> 4) : 0;
-      for (int t = kj; t < (int)spec[i].blocks.size() && b < total_blocks; ++t) put(spec[i].blocks[t], b++);
-    }
-    if (i == n - 1 && b < total_blocks)
-      decode_write<kWin>(br, im, tail, 0xFFFFFFFFu, b, total_blocks, (int32_t*)nullptr, sink);
-    ++spliced;
+    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, sink);
     blk0 += R[i].nblk;
   }
   sink.dcd = nullptr;
@@ -203,7 +155,6 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
     stats[0] = rounds;
     stats[1] = redone;
     stats[2] = n;
-    stats[3] = spliced;
   }
 }
 
