@@ -391,6 +391,14 @@ int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, i
   return e == hipSuccess ? (int)0 : hip_fail(e, "dino_debug_region");
 }
 
+#ifdef DINO_HUFF_PHASES
+// Instrumented builds only: copy the k_huff1 phase timestamps of the last launch.
+int dino_debug_huff_phases(uint64_t* host_out, int64_t n_items) {
+  hipError_t e = copy_huff_phases(host_out, n_items);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_debug_huff_phases");
+}
+#endif
+
 int dino_bf16_to_fp8(const uint16_t* d_in, uint8_t* d_out, int64_t n, void* stream) {
   if ((!d_in || !d_out) && n > 0) return fail(DINO_EINVAL, "dino_bf16_to_fp8: null argument%s%lld");
   hipError_t e = launch_bf16_to_fp8(d_in, d_out, n, (hipStream_t)stream);

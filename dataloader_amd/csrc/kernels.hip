@@ -698,6 +698,21 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
   return true;
 }
 
+#ifdef DINO_HUFF_PHASES
+// Phase timestamps of k_huff1 work items (instrumented builds only, scripts/huff_phases.py):
+// [item][0..4] = start, after the first decode, after the sync rounds, end; [item][4] = rounds.
+constexpr int kPhaseItems = 8192;
+__device__ uint64_t g_huff_phase[kPhaseItems][5];
+#define HUFF_PHASE(k, v)                                              \
+  do {                                                               \
+    if (threadIdx.x == 0 && item < kPhaseItems) g_huff_phase[item][k] = (v); \
+  } while (0)
+#else
+#define HUFF_PHASE(k, v) \
+  do {                   \
+  } while (0)
+#endif
+
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -724,12 +739,15 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     int32_t ncp = 0;
     HState myS{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};  // this lane's start state and first-decode
     RangeOut myR1{};                                      // result stay in registers; only R is shared
+    HUFF_PHASE(0, wall_clock64());
     if (active) {
       myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
       L.R[t] = myR1;
     }
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
-    for (int round = 0; round < kHuffThreads + 1; ++round) {
+    HUFF_PHASE(1, wall_clock64());
+    int round = 0;
+    for (; round < kHuffThreads + 1; ++round) {
       HState want;
       bool redo = false;
       if (active && t >= 1) {
@@ -743,6 +761,8 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
+    HUFF_PHASE(2, wall_clock64());
+    HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
     if (huff_single_segment(sd)) {
       // the whole image is this segment: its start states are final, so the blocks
       // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
@@ -765,6 +785,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       o.ncp = ncp;
     }
     __syncthreads();
+    HUFF_PHASE(3, wall_clock64());
   }
 }
 
@@ -2461,6 +2482,15 @@ hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0
   k_masks<<<1, 64, 5 * H * W + 16, s>>>(mp, n, py, np, out);
   return hipGetLastError();
 }
+
+#ifdef DINO_HUFF_PHASES
+hipError_t copy_huff_phases(uint64_t* host, int64_t n_items) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return e;
+  const int64_t n = n_items < kPhaseItems ? n_items : kPhaseItems;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_huff_phase), sizeof(uint64_t) * 5 * n);
+}
+#endif
 
 hipError_t launch_bf16_to_fp8(const uint16_t* in, uint8_t* out, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;

@@ -119,6 +119,9 @@ hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_
 hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s);
 hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,
                         uint32_t* np, uint8_t* out, hipStream_t s);
+#ifdef DINO_HUFF_PHASES
+hipError_t copy_huff_phases(uint64_t* host, int64_t n_items);
+#endif
 hipError_t launch_bf16_to_fp8(const uint16_t* in, uint8_t* out, int64_t n, hipStream_t s);
 
 }  // namespace dino

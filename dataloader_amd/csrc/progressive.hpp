@@ -134,14 +134,17 @@ DHD int prog_walk(const uint8_t* p, int64_t len, ImgDesc* d, ScanRec* scans, Fin
       for (int k = 0; k < 4; ++k) sr.comp[k] = 0, sr.dc_tab[k] = sr.ac_tab[k] = -1;
       int tds[4] = {0, 0, 0, 0}, tas[4] = {0, 0, 0, 0};
       for (int k = 0; k < ns; ++k) {
+        // get_sos: the first frame component with this id whose cur_comp_info slot (indexed
+        // by FRAME position) is still empty, i.e. frame index >= k; none -> JERR_BAD_COMPONENT_ID
         const int cs = s[1 + 2 * k];
         int ci = -1;
-        for (int c = 0; c < d->ncomp; ++c)
-          if (d->comp[c].id == cs && !(used & (1 << c))) {
+        for (int c = k; c < d->ncomp; ++c)
+          if (d->comp[c].id == cs) {
             ci = c;
             break;
           }
-        if (ci < 0) return (d->status = DINO_IMG_CORRUPT);  // JERR_BAD_COMPONENT_ID (unknown or repeated)
+        if (ci < 0) return (d->status = DINO_IMG_CORRUPT);
+        if (used & (1 << ci)) return (d->status = DINO_IMG_UNSUPPORTED);  // a component twice in one scan
         used |= 1 << ci;
         sr.comp[k] = ci;
         tds[k] = s[2 + 2 * k] >> 4;

@@ -136,6 +136,39 @@ def test_progressive_and_raw_decode_bit_exact(gpu_device):
     assert not bad, bad
 
 
+def test_writer_multiscan_cases_through_k_prog(gpu_device):
+    """The test writer's multi-scan sequential files, non-default progression scripts,
+    restart intervals per scan and mid-stream DQTs (tests/jpeg_writer.py) decoded by
+    k_prog in one batch, bit-exact with Pillow; reordered interleaved scans that
+    libjpeg rejects come back as zero-fill statuses like the reference's."""
+    from tests import jpeg_writer as jw
+    from tests.test_multiscan_cpu import multiscan_cases
+    rng = np.random.default_rng(33)
+    cases = multiscan_cases(rng, sizes=((83, 61), (1, 1), (130, 97), (517, 389)))
+    img = textured_rgb(40, 24, rng)
+    cases.append(("il_rev", jw.encode(img, [jw.scan((1, 0, 2))], samp=((1, 1),) * 3)))
+    jpegs = [j for _, j in cases]
+    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
+    d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    bad = []
+    for i, (name, j) in enumerate(cases):
+        ref = cpu_ref.decode_rgb(j)
+        if ref is None:
+            if info[i, 0] >= 0:
+                bad.append((name, "status", int(info[i, 0])))
+            continue
+        ref = np.asarray(ref)
+        if info[i, 0] != 0:
+            bad.append((name, "status", int(info[i, 0])))
+            continue
+        got = eng.copy_rgb(i, ref.shape[1], ref.shape[0]).cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad.append((name, int((got != ref).sum())))
+    eng.close()
+    assert not bad, bad
+
+
 def test_progressive_augmented_views(gpu_device):
     """The augment kernels on progressive-decoded images: views equal the oracle's."""
     rng = np.random.default_rng(32)
