@@ -71,13 +71,13 @@ struct ImgDesc {
   int32_t ent_len;         // destuffed entropy bytes
   int32_t n_rst;           // RST markers found
   int32_t terminated;      // a terminating marker (EOI/other) was found
-  int32_t pad1;
+  int32_t rst_bad;         // an RST marker out of sequence (k_destuff_write)
   // decode path (k_parse): 0 baseline single scan (speculative Huffman kernels),
   // 1 coefficient buffer (progressive or multi-scan sequential, k_prog),
   // 2 pre-decoded RGB container (DINO_RAW_MAGIC, copied by k_color)
   int32_t kind;
   int32_t progressive;     // SOF2
-  int32_t first_sos;       // kind 1: the FF of the first SOS marker (image-relative)
+  int32_t first_sos;       // the FF of the first SOS marker (image-relative; k_prog's walk starts there)
   int32_t n_scans;         // kind 1: scans (k_prog)
   int32_t qt_seen_mask;    // DQT slots defined before the first SOS
   int32_t aug_status;      // DINO_IMG_NO_SPACE when k_vplan could not place one of its views

@@ -422,50 +422,90 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 // reaches a block boundary the first decode also passed through (same bit
 // position, same block-in-MCU index), everything after it is what the first
 // decode already found: its end state and remaining block count are reused.
+// Resumable: redo_begin sets the walk up, each redo_run call advances it by at most
+// `budget` steps and returns true once the range result is known (k_huff1 polls its
+// predecessor between calls and restarts the walk when that lane's end changes).
+struct RedoState {
+  BitCursor cur;
+  int32_t blk, z, nblk, j;
+};
+
+template <int kWin>
+DHD void redo_begin(RedoState& r, const BitReader& br, const HuffImage& im, HState st) {
+  st = sanitize(st, im.blocks_per_mcu);
+  bc_init<kWin>(r.cur, br, st.pos);
+  r.blk = st.c;
+  r.z = st.z;
+  r.nblk = 0;
+  r.j = 0;
+}
+
+template <int kWin>
+DHD bool redo_run(RedoState& r, const BitReader& br, const HuffImage& im, uint32_t end, const Checkpoint* cps,
+                  int cstride, int ncp, const RangeOut& first, int budget, RangeOut* out) {
+  for (int s = 0; s < budget; ++s) {
+    if (r.cur.pos >= end) {
+      out->end = HState{r.cur.pos, r.blk, r.z};
+      out->nblk = r.nblk;
+      return true;
+    }
+    if (r.z == 0) {
+      while (r.j < ncp && cps[r.j * cstride].pos < r.cur.pos) ++r.j;
+      if (r.j < ncp && cps[r.j * cstride].pos == r.cur.pos && (int32_t)(cps[r.j * cstride].cn & 15u) == r.blk) {
+        *out = first;
+        out->nblk = r.nblk + first.nblk - (int32_t)(cps[r.j * cstride].cn >> 4);
+        return true;
+      }
+      r.nblk++;
+    }
+    huff_step<kWin>(r.cur, br, im, r.blk, r.z);
+  }
+  return false;
+}
+
 template <int kWin>
 DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
                                const Checkpoint* cps, int cstride, int ncp, RangeOut first) {
-  st = sanitize(st, im.blocks_per_mcu);
-  int32_t nblk = 0;
-  int j = 0;
-  BitCursor cur;
-  bc_init<kWin>(cur, br, st.pos);
-  int32_t blk = st.c, z = st.z;
-  while (cur.pos < end) {
-    if (z == 0) {
-      while (j < ncp && cps[j * cstride].pos < cur.pos) ++j;
-      if (j < ncp && cps[j * cstride].pos == cur.pos && (int32_t)(cps[j * cstride].cn & 15u) == blk) {
-        RangeOut r = first;
-        r.nblk = nblk + first.nblk - (int32_t)(cps[j * cstride].cn >> 4);
-        return r;
-      }
-      nblk++;
-    }
-    huff_step<kWin>(cur, br, im, blk, z);
+  RedoState r;
+  redo_begin<kWin>(r, br, im, st);
+  RangeOut out;
+  while (!redo_run<kWin>(r, br, im, end, cps, cstride, ncp, first, 1 << 30, &out)) {
   }
-  RangeOut r;
-  r.end.pos = cur.pos;
-  r.end.c = blk;
-  r.end.z = z;
-  r.nblk = nblk;
-  return r;
+  return out;
+}
+
+// A lane's range end state as one 64-bit word (k_huff1 publishes it in LDS):
+// pos | c << 32 | z << 36, bit 63 = final (the start it came from is the true one).
+constexpr uint64_t kEndFinal = 1ull << 63;
+DHD uint64_t pack_end(const HState& s) {
+  return (uint64_t)s.pos | ((uint64_t)(s.c & 15) << 32) | ((uint64_t)(s.z & 127) << 36);
+}
+DHD HState unpack_end(uint64_t w) {
+  return HState{(uint32_t)w, (int32_t)((w >> 32) & 15u), (int32_t)((w >> 36) & 127u)};
 }
 
 // Block sink interface (duck-typed): begin(absolute_block) opens a block,
 // ac(zigzag_index, int16) receives one non-zero AC coefficient (zigzag indices are
 // strictly increasing within a block; an index > 63 only comes from a corrupt
 // stream and is the block's last, mapped to natural position 63 as libjpeg's
-// jpeg_natural_order does), dc(int16) the block's DC, end() closes the block.
+// jpeg_natural_order does), dc(int16) the block's DC, end() closes the block;
+// zero(absolute_block) records an all-zero block whose DC is an absolute 0.
 // Decode from `st` (a true state) and emit every block whose DC step starts before
 // `end`, finishing the last one past `end`; the leading partial block (st.z != 0)
 // belongs to the previous lane and is decoded without being emitted.  Stops at
 // `total_blocks`.  DC: with `pred` the sink gets the absolute value (DC predictors
 // carried by the caller); without, the difference (summed later by the DC prefix
-// pass, k_dcscan).  A difference fits int16: DC categories are <= 15.  Returns the
-// bit position.
+// pass, k_dcscan).  A difference fits int16: DC categories are <= 15.
+// `avail`: bits of entropy data before the terminating marker.  libjpeg
+// (jdhuff.c jpeg_fill_bit_buffer / decode_mcu) zero-fills a step that needs bits
+// past it, sets insufficient_data and finishes that MCU from zero bits; every later
+// MCU of the segment is left all zero (DC 0, not predicted).  So an MCU that starts
+// past `avail` and everything after it become zero blocks.  Only the lane whose
+// range runs to the end of the segment reaches them (any other stops at its range
+// end first).  Returns the bit position.
 template <int kWin, typename Sink>
 DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, uint32_t end, int32_t first_block,
-                          int32_t total_blocks, int32_t* pred, Sink& sink) {
+                          int32_t total_blocks, int32_t* pred, uint32_t avail, Sink& sink) {
   st = sanitize(st, im.blocks_per_mcu);
   BitCursor cur;
   bc_init<kWin>(cur, br, st.pos);
@@ -475,6 +515,10 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
   }
   int32_t b = first_block;
   while (b < total_blocks && cur.pos < end) {
+    if (blk == 0 && cur.pos > avail) {  // insufficient_data before this MCU: the rest stays zero
+      for (; b < total_blocks; ++b) sink.zero(b);
+      break;
+    }
     sink.begin(b);
     int comp = hi_comp(im, blk);
     for (;;) {

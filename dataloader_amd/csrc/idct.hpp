@@ -1,7 +1,10 @@
 // idct.hpp — libjpeg-turbo jidctint.c jpeg_idct_islow (CONST_BITS 13,
 // PASS1_BITS 2) with libjpeg's post-IDCT range-limit table semantics.  This is
-// the DCT method Pillow's decoder uses (default JDCT_ISLOW); the SIMD versions
-// in libjpeg-turbo are bit-exact with this C formulation.
+// the DCT method Pillow's decoder uses (default JDCT_ISLOW).  libjpeg-turbo's SIMD
+// versions (the code Pillow runs on x86) equal this C formulation for every block
+// of valid 8-bit data; for the out-of-range coefficients of damaged streams they
+// differ, and the SIMD arithmetic is restated below (idct_simd_*), used for blocks
+// outside the bounds where the two provably agree (idct_col_safe / idct_row_safe).
 #pragma once
 
 #include "common.hpp"
@@ -179,16 +182,132 @@ DHD void idct_pass2(const int32_t* w, uint8_t* o) {
     idct_pass2_t<int64_t>(w, o);
 }
 
-// Whole block through the two passes (host emulator; the kernel runs one pass per lane).
+// ---- libjpeg-turbo SIMD islow (simd/x86_64/jidctint-sse2.asm, -avx2.asm) -------------
+// The same butterfly on 16-bit lanes: dequantisation keeps the low 16 bits of the
+// product (pmullw); in0 +/- in4, in7 + in3 and in5 + in1 are 16-bit sums (paddw/psubw);
+// the rotations are pmaddwd pairs with the constants pre-combined (z1 folded into
+// both of its products) and the 32-bit sums wrap; pass 1 saturates to int16
+// (packssdw), pass 2 to [-128, 127] (packssdw, packsswb) before adding 128.  A block
+// whose rows 1..7 are all zero takes pass 1 as (dc * q) << 2 in 16 bits (psllw).
+DHD int32_t wrap16(int32_t x) { return (int32_t)(int16_t)x; }
+DHD int32_t clamp_i32(int32_t x, int32_t lo, int32_t hi) { return x < lo ? lo : (x > hi ? hi : x); }
+DHD int32_t add_w32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+DHD int32_t sub_w32(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+DHD int32_t pmaddwd(int32_t a, int32_t ca, int32_t b, int32_t cb) {
+  return (int32_t)(uint32_t)((int64_t)a * ca + (int64_t)b * cb);
+}
+
+// One 1-D pass on eight int16 inputs; o[0..7] = the output sums before the descale.
+DHD void idct_simd_core(const int32_t* in, int32_t* o) {
+  const int32_t tmp3 = pmaddwd(in[2], F0_541 + F0_765, in[6], F0_541);
+  const int32_t tmp2 = pmaddwd(in[2], F0_541, in[6], F0_541 - F1_847);
+  const int32_t tmp0 = wrap16(in[0] + in[4]) * (1 << kConstBits);
+  const int32_t tmp1 = wrap16(in[0] - in[4]) * (1 << kConstBits);
+  const int32_t t10 = add_w32(tmp0, tmp3), t13 = sub_w32(tmp0, tmp3);
+  const int32_t t11 = add_w32(tmp1, tmp2), t12 = sub_w32(tmp1, tmp2);
+  const int32_t z3s = wrap16(in[7] + in[3]), z4s = wrap16(in[5] + in[1]);
+  const int32_t z3 = pmaddwd(z3s, F1_175 - F1_961, z4s, F1_175);
+  const int32_t z4 = pmaddwd(z3s, F1_175, z4s, F1_175 - F0_390);
+  const int32_t u0 = add_w32(pmaddwd(in[7], F0_298 - F0_899, in[1], -F0_899), z3);
+  const int32_t u3 = add_w32(pmaddwd(in[7], -F0_899, in[1], F1_501 - F0_899), z4);
+  const int32_t u1 = add_w32(pmaddwd(in[5], F2_053 - F2_562, in[3], -F2_562), z4);
+  const int32_t u2 = add_w32(pmaddwd(in[5], -F2_562, in[3], F3_072 - F2_562), z3);
+  o[0] = add_w32(t10, u3);
+  o[7] = sub_w32(t10, u3);
+  o[1] = add_w32(t11, u2);
+  o[6] = sub_w32(t11, u2);
+  o[2] = add_w32(t12, u1);
+  o[5] = sub_w32(t12, u1);
+  o[3] = add_w32(t13, u0);
+  o[4] = sub_w32(t13, u0);
+}
+
+DHD int32_t simd_descale(int32_t x, int n) { return add_w32(x, 1 << (n - 1)) >> n; }
+
+// Pass 1 of one column: raw coefficients c[0..7] (rows) and their quant values;
+// dc_only = rows 1..7 of the whole block are zero.  w: int16 workspace column.
+DHD void idct_simd_pass1(const int32_t* c, const int32_t* q, bool dc_only, int32_t* w) {
+  int32_t in[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) in[r] = wrap16(c[r] * q[r]);
+  if (dc_only) {
+    const int32_t v = wrap16(in[0] * (1 << kPass1Bits));
+#pragma unroll
+    for (int r = 0; r < 8; ++r) w[r] = v;
+    return;
+  }
+  int32_t o[8];
+  idct_simd_core(in, o);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) w[r] = clamp_i32(simd_descale(o[r], kConstBits - kPass1Bits), -32768, 32767);
+}
+
+// Pass 2 of one row of int16 workspace values -> 8 samples.
+DHD void idct_simd_pass2(const int32_t* w, uint8_t* out) {
+  int32_t o[8];
+  idct_simd_core(w, o);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) out[k] = (uint8_t)(clamp_i32(simd_descale(o[k], kConstBits + kPass1Bits + 3), -128, 127) + 128);
+}
+
+// Bounds under which the C and the SIMD formulation give the same result.  Pass 1 of
+// a column of dequantised values d: every 1-D output is d0 + sum_k d_k sqrt2 cos(.)
+// times 4 (PASS1_BITS), so |d0| + 1.4143 sum_{k>=1} |d_k| <= 8190 keeps it inside
+// int16 (no saturation), keeps every product and 16-bit sum from wrapping, and makes
+// the DC-only shortcut equal to the general path.  Pass 2 of a row w: sum |w| <= 11500
+// keeps the 16-bit sums and bounds the output by 11500 * 1.4143 / 32 + 0.5 < 512,
+// the range where the C range-limit table clamps instead of wrapping.
+DHD bool idct_col_safe(const int32_t* d) {
+  int32_t s = 0;
+#pragma unroll
+  for (int r = 1; r < 8; ++r) {
+    const int32_t a = iabs32(d[r]);
+    s += a > 8190 ? 8191 : a;
+  }
+  const int32_t a0 = iabs32(d[0]);
+  return a0 <= 8190 && 10000 * a0 + 14143 * s <= 81900000;
+}
+DHD bool idct_row_safe(const int32_t* w) {
+  int32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int32_t a = iabs32(w[k]);
+    s += a > 11500 ? 11501 : a;
+  }
+  return s <= 11500;
+}
+
+// Whole block through the two passes as the kernel runs them (host emulator; k_idct
+// runs one pass per lane): the C passes when every column is within its bound, else
+// the SIMD pass 1 for the block; per row, the C pass 2 within its bound, else SIMD.
 DHD void idct_islow_fast(const int16_t* coef, const uint16_t* q, uint8_t* out, int64_t pitch) {
   int32_t ws[64];
+  bool safe = true, dc_only = true;
+  for (int c = 0; c < 8; ++c) {
+    int32_t d[8];
+    for (int r = 0; r < 8; ++r) d[r] = (int32_t)coef[r * 8 + c] * (int32_t)(int16_t)q[r * 8 + c];
+    safe = safe && idct_col_safe(d);
+    for (int r = 1; r < 8; ++r) dc_only = dc_only && coef[r * 8 + c] == 0;
+  }
   for (int c = 0; c < 8; ++c) {
     int32_t d[8], w[8];
-    for (int r = 0; r < 8; ++r) d[r] = (int32_t)coef[r * 8 + c] * (int32_t)(int16_t)q[r * 8 + c];
-    idct_pass1(d, w);
+    if (safe) {
+      for (int r = 0; r < 8; ++r) d[r] = (int32_t)coef[r * 8 + c] * (int32_t)(int16_t)q[r * 8 + c];
+      idct_pass1(d, w);
+    } else {
+      int32_t cc[8], qq[8];
+      for (int r = 0; r < 8; ++r) {
+        cc[r] = coef[r * 8 + c];
+        qq[r] = (int32_t)(int16_t)q[r * 8 + c];
+      }
+      idct_simd_pass1(cc, qq, dc_only, w);
+    }
     for (int r = 0; r < 8; ++r) ws[r * 8 + c] = w[r];
   }
-  for (int r = 0; r < 8; ++r) idct_pass2(ws + r * 8, out + r * pitch);
+  for (int r = 0; r < 8; ++r) {
+    if (idct_row_safe(ws + r * 8)) idct_pass2(ws + r * 8, out + r * pitch);
+    else idct_simd_pass2(ws + r * 8, out + r * pitch);
+  }
 }
 
 }  // namespace dino

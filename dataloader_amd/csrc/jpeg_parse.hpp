@@ -52,6 +52,7 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
   d->n_scans = 0;
   d->qt_seen_mask = 0;
   d->aug_status = 0;
+  d->rst_bad = 0;
   d->total_blocks = 0;
   for (int i = 0; i < 8; ++i) d->huff_off[i] = -1;
   for (int t = 0; t < 4; ++t)
@@ -178,6 +179,7 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
         // baseline path; anything else (progressive, components spread over several
         // scans, another component order) on the coefficient-buffer path (k_prog),
         // whose marker walk re-reads this SOS.
+        d->first_sos = (int32_t)(pos - 2);  // (a baseline image may still move to k_prog, k_destuff_write)
         bool one_scan = !d->progressive && ns == d->ncomp;
         for (int k = 0; k < ns && one_scan; ++k) {
           int cs = s[1 + 2 * k];
@@ -188,7 +190,6 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
         }
         if (!one_scan) {
           d->kind = 1;
-          d->first_sos = (int32_t)(pos - 2);
           d->scan_off = (int32_t)(pos + seglen);
           d->scan_len = (int32_t)(len - d->scan_off);
           goto have_scan;

@@ -411,6 +411,9 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
             out[o++] = (uint8_t)((ch.wv[j >> 2] >> (8 * (j & 3))) & 255);
           } else {
             if ((int)ro < nrst_cap) rst[ro] = (int32_t)o;
+            // RSTn must count 0..7 in order; otherwise libjpeg's read_restart_marker
+            // resyncs (jdmarker.c jpeg_resync_to_restart), which k_prog restates
+            if ((g.r[16 * c - g.lead + j + 1] & 7u) != (ro & 7u)) atomicOr(&d->rst_bad, 1);
             ++ro;
           }
         }
@@ -428,8 +431,9 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
           d->ent_len = total;
           d->n_rst = (int32_t)rc_run;
           d->terminated = term;
-          if (!term) d->status = DINO_IMG_TRUNCATED;
-          else if (d->restart_interval > 0 && d->n_rst < d->n_rst_max - 1) d->status = DINO_IMG_BADDATA;
+          if (!term) {
+            d->status = DINO_IMG_TRUNCATED;
+          }
         }
       }
     }
@@ -459,6 +463,11 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
 //                           restart intervals decode one interval per lane here
 // ---------------------------------------------------------------------------
 constexpr int kMinSubBits = 1024;  // shortest lane range of a one-segment image
+#ifndef DINO_HUFF_REDO_BUDGET
+#define DINO_HUFF_REDO_BUDGET 8
+#endif
+constexpr int kHuffRedoBudget = DINO_HUFF_REDO_BUDGET;  // re-decode steps between two polls of the predecessor
+constexpr int kHuffMaxPolls = 1 << 22;
 
 
 // Work items (segments) an image needs for a stream of `nbits` bits, and the
@@ -470,7 +479,7 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 struct HuffLds {     // k_huff1
   ImgDesc sd;
   HuffTables tab;
-  RangeOut R[kHuffThreads];
+  uint64_t E[kHuffThreads];  // each lane's published range end (pack_end, kEndFinal)
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
@@ -483,6 +492,9 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
 static_assert(sizeof(ImgDesc) % 16 == 8 || sizeof(ImgDesc) % 16 == 0, "ImgDesc layout");
 constexpr int kHuffLdsBytes = (int)((sizeof(HuffLds) + 15) & ~(size_t)15);
 constexpr int kHuff3LdsBytes = (int)((sizeof(HuffLds3) + 15) & ~(size_t)15);
+
+// Block record flag: the DC field is an absolute value (k_dcscan keeps it).
+constexpr uint32_t kBinfoAbsDc = 1u << 15;
 
 // Sparse coefficient output.  A lane appends its blocks' non-zero AC coefficients
 // to a private region of the image's entry area that starts at 128 halfwords per
@@ -549,6 +561,8 @@ struct SparseSink {
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
   __device__ void end() { binfo[b] = make_uint2(bstart, n16 | (n32 << 7) | dcw); }
+  // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
+  __device__ void zero(int32_t blk) { binfo[blk] = make_uint2(n + k, kBinfoAbsDc); }
   __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
     if (k) {
       for (uint32_t j = k; j < 8; ++j) shift_in(0u);
@@ -578,6 +592,17 @@ __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict
   ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
   if (d.status != DINO_IMG_OK || d.kind != 0) return;
+  if (d.restart_interval > 0 && (d.n_rst < d.n_rst_max - 1 || d.rst_bad)) {
+    // missing or out-of-sequence restart markers (counted by k_destuff_write, which
+    // has completed): libjpeg resyncs (jdmarker.c jpeg_resync_to_restart) and decodes
+    // what it finds, empty segments once the data has ended; the coefficient-buffer
+    // path restates that walk, and its dense buffer fits in the sparse entry area
+    if (t == 0) {
+      if (align16(d.coef_bytes) <= (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2) d.kind = 1;
+      else d.status = DINO_IMG_BADDATA;
+    }
+    return;
+  }
   const uint8_t* p = bytes + offsets[blockIdx.x];
   if (t == 0) s_bad = 0;
   __syncthreads();
@@ -740,47 +765,78 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     HState myS{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};  // this lane's start state and first-decode
     RangeOut myR1{};                                      // result stay in registers; only R is shared
     HUFF_PHASE(0, wall_clock64());
-    if (active) {
-      myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
-      L.R[t] = myR1;
-    }
-    __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
+    if (active) myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
+    // Rounds without barriers: every lane publishes its range end; a lane whose
+    // predecessor's end differs from its own start re-decodes from that end (and
+    // restarts if the end changes again).  The item's first lane is the anchor (its
+    // start is exact, or k_huff2's to fix); a lane is final once its predecessor is
+    // final and its result comes from that final end, so finality runs up the lanes
+    // while the re-decodes of different lanes overlap instead of waiting per round.
+    bool fin = t == 0 || !active;
+    L.E[t] = pack_end(myR1.end) | (fin ? kEndFinal : 0ull);
+    __syncthreads();  // every first decode is published before anyone polls
     HUFF_PHASE(1, wall_clock64());
-    int round = 0;
-    for (; round < kHuffThreads + 1; ++round) {
-      HState want;
-      bool redo = false;
-      if (active && t >= 1) {
-        want = L.R[t - 1].end;
-        redo = !hstate_eq(want, myS);
+    RangeOut res = myR1;
+    RedoState rd;
+    bool working = false;
+    int iters = 0;
+    const int wl = t & 63;  // lane within the wave
+    // (the iteration cap only guards against a protocol fault: a wrong decode beats a hung GPU)
+    while (!__all(fin) && iters < kHuffMaxPolls) {
+      ++iters;
+      bool pred_final = false, published = false;
+      if (!fin) {
+        const uint64_t w = __hip_atomic_load(&L.E[t - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const HState pe = unpack_end(w);
+        pred_final = (w & kEndFinal) != 0;
+        if (!hstate_eq(pe, myS)) {  // a new start: (re)start the walk from it
+          myS = pe;
+          redo_begin<kSrcPadded>(rd, br, im, pe);
+          working = true;
+        }
+        if (working && redo_run<kSrcPadded>(rd, br, im, rend, cps, cstride, ncp, myR1, kHuffRedoBudget, &res)) {
+          working = false;
+          published = true;
+          __hip_atomic_store(&L.E[t], pack_end(res.end), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
-      __syncthreads();
-      if (redo) {
-        myS = want;
-        L.R[t] = decode_range_sync<kSrcPadded>(br, im, want, rend, cps, cstride, ncp, myR1);
+      // Finality for a whole run of lanes at once: lane i becomes final when every lane
+      // from the wave's final prefix up to i is idle on the end its predecessor had
+      // when it was read (no predecessor published a new one in this iteration), and
+      // the lane before the run is final (in the wave, or the loaded flag for lane 0).
+      const uint64_t F = __ballot(fin);
+      const uint64_t N = __ballot(published);
+      uint64_t P = F | (__ballot(!working) & ~(N << 1));
+      if (!(F & 1ull) && !(__ballot(pred_final) & 1ull)) P &= ~1ull;
+      const uint64_t run = ~P == 0ull ? ~0ull : (((~P) & (P + 1ull)) - 1ull);  // P's trailing ones
+      if (!fin && ((run >> wl) & 1ull)) {
+        fin = true;
+        __hip_atomic_store(&L.E[t], pack_end(res.end) | kEndFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (!__syncthreads_or(redo ? 1 : 0)) break;
+      if (!__any(working)) __builtin_amdgcn_s_sleep(1);  // the wave only waits on an earlier lane
     }
+    __syncthreads();
+    const int round = iters;
     HUFF_PHASE(2, wall_clock64());
     HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
     if (huff_single_segment(sd)) {
       // the whole image is this segment: its start states are final, so the blocks
       // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
       uint32_t tot;
-      const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)L.R[t].nblk : 0u, L.wave, &tot);
+      const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)res.nblk : 0u, L.wave, &tot);
       if (active) {
         SparseSink sink;
         sink.ent = (uint32_t*)(ws + sd.coef_off);
         sink.binfo = (uint2*)(ws + sd.binfo_off);
         sink.open((int32_t)blk0);
         decode_write<kSrcPadded>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
-                                 sink);
+                                 nbits, sink);
         sink.close();
       }
     } else if (active) {
       LaneRec& o = lr[i];
       o.S = myS;
-      o.R = L.R[t];
+      o.R = res;
       o.R1 = myR1;
       o.ncp = ncp;
     }
@@ -879,7 +935,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
         const int first = i * per, last = min(first + per, sd.total_blocks);
         if (first < last) {
           sink.open(first);
-          decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+          decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sb.nbytes * 8u, sink);
           sink.close();
         }
       }
@@ -887,7 +943,8 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
       sink.open(r.blk0);
-      decode_write<kSrcPadded>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr, sink);
+      decode_write<kSrcPadded>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr,
+                               br.nbytes * 8u, sink);
       sink.close();
     }
     __syncthreads();
@@ -1080,8 +1137,9 @@ __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __rest
     for (int j = 0; j < K; ++j) {
       const int c = (int)((mc >> (2 * pos)) & 3u);
       add3(pfx, c, (int32_t)y[j] >> 16);
-      // in place: JCOEF (int16) DC, as libjpeg stores it
-      if (b0 + j < T) info[2 * (int64_t)(b0 + j)] = (y[j] & 0xFFFFu) | ((uint32_t)get3(pfx, c) << 16);
+      // in place: JCOEF (int16) DC, as libjpeg stores it; a zero block after the data
+      // ran out (kBinfoAbsDc, always the image's tail) keeps its absolute 0
+      if (b0 + j < T && !(y[j] & kBinfoAbsDc)) info[2 * (int64_t)(b0 + j)] = (y[j] & 0xFFFFu) | ((uint32_t)get3(pfx, c) << 16);
       pos = pos + 1 == bpm ? 0 : pos + 1;
     }
 #pragma unroll
@@ -1216,10 +1274,24 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     const CompDesc& cd = d.comp[cur.c];
     if (valid) {  // dequantize + pass 1 on column l (reads and writes only this lane's column)
       const uint16_t* q = d.qt[cd.tq];
-      int32_t col[8], wcol[8];
+      int32_t raw[8], qq[8], col[8], wcol[8];
 #pragma unroll
-      for (int r = 0; r < 8; ++r) col[r] = sb[r * 9 + l] * (int32_t)(int16_t)q[r * 8 + l];
-      idct_pass1(col, wcol);
+      for (int r = 0; r < 8; ++r) {
+        raw[r] = sb[r * 9 + l];
+        qq[r] = (int32_t)(int16_t)q[r * 8 + l];
+        col[r] = raw[r] * qq[r];
+      }
+      // a block with a column outside the C/SIMD agreement bound (damaged data only)
+      // runs libjpeg-turbo's SIMD pass 1, whose DC-only shortcut is decided per block
+      const int gsh = threadIdx.x & 56;  // this group's first lane within the wave
+      if (((__ballot(!idct_col_safe(col)) >> gsh) & 0xFFu) == 0) {
+        idct_pass1(col, wcol);
+      } else {
+        bool acz = true;
+#pragma unroll
+        for (int r = 1; r < 8; ++r) acz = acz && raw[r] == 0;
+        idct_simd_pass1(raw, qq, ((__ballot(acz) >> gsh) & 0xFFu) == 0xFFu, wcol);
+      }
 #pragma unroll
       for (int r = 0; r < 8; ++r) sb[r * 9 + l] = wcol[r];
     }
@@ -1234,7 +1306,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
         uint8_t b[8];
         uint64_t u;
       } o;
-      idct_pass2(row, o.b);
+      if (idct_row_safe(row)) idct_pass2(row, o.b);
+      else idct_simd_pass2(row, o.b);
       const int pitch = cd.bw * 8;
       *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = o.u;
     }
@@ -2403,8 +2476,8 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int grid_ds = a.geom.grid_ds, grid1 = a.geom.grid1, grid3 = a.geom.grid3;
   TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
-  TIMED(tm, kKProg, s, (k_prog<<<B, kProgThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  TIMED(tm, kKProg, s, (k_prog<<<B, kProgThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));  // after k_htab's kind switch
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));

@@ -23,6 +23,7 @@ struct Destuffed {
   std::vector<int32_t> rst;     // destuffed byte offset where each restart segment starts
   int32_t len = 0;
   int32_t terminated = 0;
+  int32_t rst_bad = 0;  // an RST out of sequence (k_destuff_write)
 };
 
 inline Destuffed model_destuff(const uint8_t* r, int n) {
@@ -40,7 +41,10 @@ inline Destuffed model_destuff(const uint8_t* r, int n) {
     if (r[k] == 0xFF) {
       int nx = k + 1 < n ? r[k + 1] : -1;
       if (nx == 0x00) d.bytes.push_back(0xFF);
-      else if (nx >= 0xD0 && nx <= 0xD7) d.rst.push_back((int32_t)d.bytes.size());
+      else if (nx >= 0xD0 && nx <= 0xD7) {
+        if ((nx & 7) != (int)(d.rst.size() & 7)) d.rst_bad = 1;
+        d.rst.push_back((int32_t)d.bytes.size());
+      }
       // fill byte: dropped
     } else if (k > 0 && r[k - 1] == 0xFF) {
       // second byte of FF00 / FFDx: dropped
@@ -53,6 +57,8 @@ inline Destuffed model_destuff(const uint8_t* r, int n) {
   for (int i = 0; i < 8; ++i) d.bytes.push_back(0);
   return d;
 }
+
+constexpr int32_t kDcAbsZero = INT32_MIN;  // dcd marker: an absolute DC of 0 (insufficient data)
 
 struct CoefSink {
   const ImgDesc* d;
@@ -73,6 +79,10 @@ struct CoefSink {
       blk[0] = v;
   }
   void end() {}
+  void zero(int32_t blk_index) {
+    begin(blk_index);
+    if (dcd) dcd[b] = kDcAbsZero;
+  }
 };
 
 // k_dcscan: running DC sums per component over the blocks in decode order.
@@ -80,6 +90,10 @@ inline void model_dcscan(const ImgDesc& d, const HuffImage& im, const int32_t* d
   int32_t p[kMaxComp] = {0, 0, 0};
   for (int32_t b = 0; b < d.total_blocks; ++b) {
     const int c = hi_comp(im, b % d.blocks_per_mcu);
+    if (dcd[b] == kDcAbsZero) {
+      coef[coef_block_offset(d, b)] = 0;
+      continue;
+    }
     add3(p, c, dcd[b]);
     coef[coef_block_offset(d, b)] = (int16_t)get3(p, c);
   }
@@ -110,6 +124,7 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   uint32_t sub = (nbits + n - 1) / n;
   sub = (sub + 31) & ~31u;
   if (sub == 0) sub = 32;
+  n = std::max(1, std::min(n, (int)((nbits + sub - 1) / sub)));  // as k_htab's h_lanes: no range starts past the data
   if (seg <= 0) seg = n;
   std::vector<HState> S(n);
   std::vector<RangeOut> R(n), R1(n);
@@ -146,7 +161,7 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   int32_t blk0 = 0;
   sink.dcd = dcd;
   for (int i = 0; i < n; ++i) {
-    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, sink);
+    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, nbits, sink);
     blk0 += R[i].nblk;
   }
   sink.dcd = nullptr;
@@ -154,6 +169,126 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   if (stats) {
     stats[0] = rounds;
     stats[1] = redone;
+    stats[2] = n;
+  }
+}
+
+// ---- k_huff1's barrier-free rounds, one segment of `seg` lanes at a time ----
+// Waves of `wave` lanes run one loop iteration at a time in a pseudo-random order
+// (every lane of the wave reads its predecessor's published end before any lane of
+// the wave stores, as in lockstep execution); afterwards the cross-segment rounds of
+// k_huff2 and the writes follow as in model_huffman_spec.  Same result expected.
+template <int kWin>
+inline void model_huffman_async(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
+                                int seg, int wave, int budget, uint32_t seed, CoefSink& sink, int32_t* dcd,
+                                int32_t* stats) {
+  const int total_blocks = d.total_blocks;
+  int n = lanes;
+  uint32_t sub = (nbits + n - 1) / n;
+  sub = (sub + 31) & ~31u;
+  if (sub == 0) sub = 32;
+  n = std::max(1, std::min(n, (int)((nbits + sub - 1) / sub)));
+  if (seg <= 0) seg = n;
+  std::vector<HState> S(n);
+  std::vector<RangeOut> R(n), R1(n);
+  std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
+  std::vector<int32_t> ncp(n);
+  auto rend = [&](int i) -> uint32_t { return i == n - 1 ? nbits : (uint32_t)(i + 1) * sub; };
+  auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
+  for (int i = 0; i < n; ++i) {
+    S[i] = HState{(uint32_t)i * sub, 0, 0};
+    R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, kHuffCheckpoints,
+                                      &ncp[i]);
+  }
+  uint32_t rng = seed * 2654435761u + 12345u;
+  long iters = 0;
+  for (int s0 = 0; s0 < n; s0 += seg) {
+    const int s1 = std::min(n, s0 + seg);
+    std::vector<uint64_t> E(s1 - s0);
+    std::vector<char> fin(s1 - s0), working(s1 - s0, 0);
+    std::vector<RedoState> rd(s1 - s0);
+    for (int i = s0; i < s1; ++i) {
+      fin[i - s0] = i == s0;
+      E[i - s0] = pack_end(R1[i].end) | (fin[i - s0] ? kEndFinal : 0ull);
+    }
+    const int nw = (s1 - s0 + wave - 1) / wave;
+    for (;;) {
+      bool all = true;
+      for (char f : fin) all = all && f;
+      if (all) break;
+      rng = rng * 1664525u + 1013904223u;
+      const int w0 = s0 + (int)((rng >> 8) % (uint32_t)nw) * wave, w1 = std::min(s1, w0 + wave);
+      bool wave_fin = true;
+      for (int i = w0; i < w1; ++i) wave_fin = wave_fin && fin[i - s0];
+      if (wave_fin) continue;
+      ++iters;
+      std::vector<uint64_t> seen(w1 - w0);
+      for (int i = w0; i < w1; ++i) seen[i - w0] = i > s0 ? E[i - 1 - s0] : 0;
+      uint64_t F = 0, N = 0, idle = 0, pf = 0;
+      for (int i = w0; i < w1; ++i) {
+        const int k = i - s0, wl = i - w0;
+        if (!fin[k]) {
+          const uint64_t w = seen[wl];
+          const HState pe = unpack_end(w);
+          if (w & kEndFinal) pf |= 1ull << wl;
+          if (!hstate_eq(pe, S[i])) {
+            S[i] = pe;
+            redo_begin<kWin>(rd[k], br, im, pe);
+            working[k] = 1;
+          }
+          if (working[k] && redo_run<kWin>(rd[k], br, im, rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i],
+                                           R1[i], budget, &R[i])) {
+            working[k] = 0;
+            N |= 1ull << wl;
+            E[k] = pack_end(R[i].end);
+          }
+        }
+        if (fin[k]) F |= 1ull << wl;
+        if (!working[k]) idle |= 1ull << wl;
+      }
+      for (int wl = w1 - w0; wl < 64; ++wl) F |= 1ull << wl;  // lanes past the segment: as inactive lanes
+      uint64_t P = F | (idle & ~(N << 1));
+      if (!(F & 1ull) && !(pf & 1ull)) P &= ~1ull;
+      const uint64_t run = ~P == 0ull ? ~0ull : (((~P) & (P + 1ull)) - 1ull);
+      for (int i = w0; i < w1; ++i) {
+        const int k = i - s0;
+        if (!fin[k] && ((run >> (i - w0)) & 1ull)) {
+          fin[k] = 1;
+          E[k] = pack_end(R[i].end) | kEndFinal;
+        }
+      }
+    }
+  }
+  // k_huff2: rounds across the segments
+  int rounds = 0;
+  for (;;) {
+    std::vector<HState> want(n);
+    std::vector<char> redo(n, 0);
+    for (int i = 1; i < n; ++i) {
+      want[i] = R[i - 1].end;
+      redo[i] = !hstate_eq(want[i], S[i]);
+    }
+    bool any = false;
+    for (int i = 1; i < n; ++i) {
+      if (!redo[i]) continue;
+      S[i] = want[i];
+      R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i], R1[i]);
+      any = true;
+    }
+    ++rounds;
+    if (!any) break;
+  }
+  int32_t blk0 = 0;
+  sink.dcd = dcd;
+  for (int i = 0; i < n; ++i) {
+    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, nbits, sink);
+    blk0 += R[i].nblk;
+  }
+  sink.dcd = nullptr;
+  model_dcscan(d, im, dcd, sink.coef);
+  if (stats) {
+    stats[0] = (int32_t)std::min<long>(iters, 1 << 30);
+    stats[1] = rounds;
     stats[2] = n;
   }
 }
@@ -221,6 +356,10 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     cap->ent.assign(ds.bytes.begin(), ds.bytes.begin() + ds.len);
   }
   if (!ds.terminated) return DINO_IMG_TRUNCATED;
+  if (d.restart_interval > 0 && ((int)ds.rst.size() < d.n_rst_max - 1 || ds.rst_bad)) {
+    d.kind = 1;  // k_htab: resync semantics on the coefficient-buffer path
+    return host_model_decode_multiscan(p, len, d, out_rgb, stats, cap);
+  }
   HuffTables tabs;
   HuffImage im;
   if (!model_tables(p, d, &tabs, im)) return DINO_IMG_CORRUPT;
@@ -243,19 +382,22 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
       int first = k * per, last = std::min(first + per, d.total_blocks);
       if (mode == 2) {  // segments read from the staged (swapped) words, as k_huffman's LDS window
         BitReader sw{win.data(), k + 1 < nseg ? (uint32_t)ds.rst[k] : (uint32_t)ds.len};
-        decode_write<true>(sw, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+        decode_write<true>(sw, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sw.nbytes * 8u, sink);
       } else {
-        decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sink);
+        decode_write<false>(sb, im, HState{start, 0, 0}, 0xFFFFFFFFu, first, last, pred, sb.nbytes * 8u, sink);
       }
     }
   } else if (mode == 0) {
     int32_t pred[kMaxComp] = {0, 0, 0};
-    decode_write<false>(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, sink);
+    decode_write<false>(br, im, HState{0, 0, 0}, 0xFFFFFFFFu, 0, d.total_blocks, pred, br.nbytes * 8u, sink);
   } else {
     std::vector<int32_t> dcd(d.total_blocks, 0);
     if (mode == 2) {
       BitReader bw{win.data(), (uint32_t)win.size() * 4};
       model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, 0, sink, dcd.data(), stats);
+    } else if (mode >= 4) {  // 4: k_huff1's barrier-free rounds, segments of 64 lanes in waves of 16
+      model_huffman_async<kSrcPadded>(br, im, d, (uint32_t)ds.len * 8, lanes, 64, 16, mode == 4 ? 8 : 1, (uint32_t)mode,
+                                      sink, dcd.data(), stats);
     } else {
       model_huffman_spec<kSrcPadded>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
                                 stats);

@@ -345,7 +345,7 @@ def _rgb_to_ycc(rgb: np.ndarray) -> np.ndarray:
 
 def encode(img: np.ndarray, scans: list[dict], quality: int = 85, samp=((2, 2), (1, 1), (1, 1)),
            progressive: bool = False, restart=None, comp_ids=(1, 2, 3), jfif: bool = True,
-           before_scan: dict | None = None) -> bytes:
+           before_scan: dict | None = None, coef_hook=None) -> bytes:
     """Encode ``img`` (H x W x 3 RGB or H x W gray) with an explicit scan script.
 
     scans: [{"comps": (frame component indices in scan order), "ss", "se", "ah", "al"}];
@@ -353,6 +353,9 @@ def encode(img: np.ndarray, scans: list[dict], quality: int = 85, samp=((2, 2), 
     (one DRI before the first scan) or a list with one restart interval per scan (a DRI
     segment before each scan whose interval changes).  One DHT per scan (optimal tables).
     ``before_scan``: {scan index: raw marker segments inserted before that scan's tables}.
+    ``coef_hook(coefs, qts) -> (coefs, qts)``: replaces the quantized coefficients
+    ([bh, bw, 64] natural order per component) and quantization tables (<= 255) before
+    coding, for tests that need chosen coefficient values.
     """
     gray = img.ndim == 2
     planes_full = [img.astype(np.float64)] if gray else list(np.moveaxis(_rgb_to_ycc(img), -1, 0))
@@ -376,6 +379,8 @@ def encode(img: np.ndarray, scans: list[dict], quality: int = 85, samp=((2, 2), 
         coefs.append(_component_coefs(p, bw, bh, q))
         dims.append((dw, dh))
         qts.append(q)
+    if coef_hook is not None:
+        coefs, qts = coef_hook(coefs, qts)
     frame = {"dims": dims, "samp": list(samp), "mcus": (mx, my), "progressive": progressive}
     out = bytearray(b"\xff\xd8")
     if jfif:

@@ -95,7 +95,8 @@ def _zoo():
     return out
 
 
-@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024)])
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024),
+                                        (4, 5), (4, 256), (5, 300), (6, 1024)])
 def test_decode_bit_exact_vs_pillow(emu, mode, lanes):
     for j in _zoo():
         r, out, _ = emu_decode(emu, j, mode, lanes)
@@ -109,6 +110,72 @@ def test_decode_golden(emu):
         r, out, _ = emu_decode(emu, (GOLD / f"{name}.jpg").read_bytes(), 1, 16)
         assert r == 0, name
         np.testing.assert_array_equal(out, np.load(GOLD / f"{name}.rgb.npy"), err_msg=name)
+
+
+def _damaged_streams(rng):
+    """Valid entropy data cut mid-scan with the EOI kept (libjpeg: insufficient_data ->
+    the MCU finishes from zero bits, later MCUs of the segment stay zero) and restart
+    markers renumbered / dropped / duplicated (jpeg_resync_to_restart): Pillow decodes
+    all of them (with warnings)."""
+    out = []
+    for sub in (0, 1, 2):
+        for rst_mcus in (0, 5):
+            base = encode_jpeg(textured_rgb(160, 120, rng), quality=85, subsampling=sub, restart_mcus=rst_mcus)
+            sos = base.index(b"\xff\xda")
+            s0 = sos + 2 + int.from_bytes(base[sos + 2:sos + 4], "big")
+            for frac in (0.03, 0.3, 0.61, 0.97):
+                cut = s0 + int((len(base) - 2 - s0) * frac)
+                cut -= base[cut - 1] == 0xFF
+                out.append((f"cut{sub}{rst_mcus}_{frac}", base[:cut] + b"\xff\xd9"))
+    base = encode_jpeg(textured_rgb(200, 136, rng), quality=80, subsampling=2, restart_mcus=3)
+    rst = [i for i in range(len(base) - 1) if base[i] == 0xFF and 0xD0 <= base[i + 1] <= 0xD7]
+    for k in (0, len(rst) // 2, len(rst) - 1):
+        for nv in (1, 2, 7):
+            b = bytearray(base)
+            b[rst[k] + 1] = 0xD0 + ((b[rst[k] + 1] - 0xD0 + nv) & 7)
+            out.append((f"renum{k}_{nv}", bytes(b)))
+        b = bytearray(base)
+        del b[rst[k]:rst[k] + 2]
+        out.append((f"drop{k}", bytes(b)))
+        b = bytearray(base)
+        b[rst[k]:rst[k]] = bytes([0xFF, 0xD0 + (k & 7)])
+        out.append((f"dup{k}", bytes(b)))
+    return out
+
+
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 64), (4, 100), (6, 300)])
+def test_damaged_streams_bit_exact_vs_pillow(emu, mode, lanes):
+    for name, j in _damaged_streams(np.random.default_rng(1)):
+        ref = cpu_ref.decode_rgb(j)
+        assert ref is not None, name
+        r, out, _ = emu_decode(emu, j, mode, lanes)
+        assert r == 0, (name, r)
+        np.testing.assert_array_equal(out, np.asarray(ref), err_msg=name)
+
+
+def test_barrier_free_rounds_corrupt_streams(emu):
+    """k_huff1's barrier-free rounds (modes 4-6: random wave order, poll budgets 8 and 1)
+    reach the same start states as the synchronous rounds on damaged entropy data:
+    bytes overwritten inside the scan, many lanes.  (Pixels are compared between the
+    decode modes only: such streams can yield dequantised coefficients beyond 16 bits,
+    where libjpeg-turbo's SIMD IDCT saturates and its C IDCT, restated here, does not;
+    DESIGN.md §8.)"""
+    from dataloader_amd.synthetic import make_jpeg
+    rng = np.random.default_rng(5)
+    base = make_jpeg(320, 240, 3)
+    sos = base.index(b"\xff\xda")
+    for k in range(6):
+        b = bytearray(base)
+        for _ in range(4):
+            p = int(rng.integers(sos + 20, len(b) - 4))
+            v = int(rng.integers(0, 255))
+            if b[p - 1] != 0xFF and v != 0xFF:
+                b[p] = v
+        j = bytes(b)
+        outs = [emu_decode(emu, j, m, lanes) for m, lanes in ((0, 1), (1, 200), (4, 200), (5, 77), (6, 513))]
+        for r, out, _ in outs:
+            assert r == outs[0][0]
+            np.testing.assert_array_equal(out, outs[0][1])
 
 
 def test_speculative_sync_converges(emu):

@@ -136,6 +136,30 @@ def test_progressive_and_raw_decode_bit_exact(gpu_device):
     assert not bad, bad
 
 
+def test_damaged_streams_through_the_abi(gpu_device):
+    """Entropy data cut mid-scan with EOI kept (insufficient_data zero fill) and restart
+    markers renumbered / dropped / duplicated (resync on the k_prog path) in one batch with
+    clean images, bit-exact with Pillow, which decodes them all."""
+    from tests.test_emu_cpu import _damaged_streams
+    rng = np.random.default_rng(41)
+    cases = _damaged_streams(rng) + [("clean", encode_jpeg(textured_rgb(640, 480, rng)))]
+    jpegs = [j for _, j in cases]
+    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
+    d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    bad = []
+    for i, (name, j) in enumerate(cases):
+        ref = np.asarray(cpu_ref.decode_rgb(j))
+        if info[i, 0] != 0:
+            bad.append((name, "status", int(info[i, 0])))
+            continue
+        got = eng.copy_rgb(i, ref.shape[1], ref.shape[0]).cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad.append((name, int((got != ref).sum())))
+    eng.close()
+    assert not bad, bad
+
+
 def test_writer_multiscan_cases_through_k_prog(gpu_device):
     """The test writer's multi-scan sequential files, non-default progression scripts,
     restart intervals per scan and mid-stream DQTs (tests/jpeg_writer.py) decoded by
