@@ -422,66 +422,33 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 // reaches a block boundary the first decode also passed through (same bit
 // position, same block-in-MCU index), everything after it is what the first
 // decode already found: its end state and remaining block count are reused.
-// Resumable: redo_begin sets the walk up, each redo_run call advances it by at most
-// `budget` steps and returns true once the range result is known (k_huff1 polls its
-// predecessor between calls and restarts the walk when that lane's end changes).
-struct RedoState {
-  BitCursor cur;
-  int32_t blk, z, nblk, j;
-};
-
-template <int kWin>
-DHD void redo_begin(RedoState& r, const BitReader& br, const HuffImage& im, HState st) {
-  st = sanitize(st, im.blocks_per_mcu);
-  bc_init<kWin>(r.cur, br, st.pos);
-  r.blk = st.c;
-  r.z = st.z;
-  r.nblk = 0;
-  r.j = 0;
-}
-
-template <int kWin>
-DHD bool redo_run(RedoState& r, const BitReader& br, const HuffImage& im, uint32_t end, const Checkpoint* cps,
-                  int cstride, int ncp, const RangeOut& first, int budget, RangeOut* out) {
-  for (int s = 0; s < budget; ++s) {
-    if (r.cur.pos >= end) {
-      out->end = HState{r.cur.pos, r.blk, r.z};
-      out->nblk = r.nblk;
-      return true;
-    }
-    if (r.z == 0) {
-      while (r.j < ncp && cps[r.j * cstride].pos < r.cur.pos) ++r.j;
-      if (r.j < ncp && cps[r.j * cstride].pos == r.cur.pos && (int32_t)(cps[r.j * cstride].cn & 15u) == r.blk) {
-        *out = first;
-        out->nblk = r.nblk + first.nblk - (int32_t)(cps[r.j * cstride].cn >> 4);
-        return true;
-      }
-      r.nblk++;
-    }
-    huff_step<kWin>(r.cur, br, im, r.blk, r.z);
-  }
-  return false;
-}
-
 template <int kWin>
 DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
                                const Checkpoint* cps, int cstride, int ncp, RangeOut first) {
-  RedoState r;
-  redo_begin<kWin>(r, br, im, st);
-  RangeOut out;
-  while (!redo_run<kWin>(r, br, im, end, cps, cstride, ncp, first, 1 << 30, &out)) {
+  st = sanitize(st, im.blocks_per_mcu);
+  int32_t nblk = 0;
+  int j = 0;
+  BitCursor cur;
+  bc_init<kWin>(cur, br, st.pos);
+  int32_t blk = st.c, z = st.z;
+  while (cur.pos < end) {
+    if (z == 0) {
+      while (j < ncp && cps[j * cstride].pos < cur.pos) ++j;
+      if (j < ncp && cps[j * cstride].pos == cur.pos && (int32_t)(cps[j * cstride].cn & 15u) == blk) {
+        RangeOut r = first;
+        r.nblk = nblk + first.nblk - (int32_t)(cps[j * cstride].cn >> 4);
+        return r;
+      }
+      nblk++;
+    }
+    huff_step<kWin>(cur, br, im, blk, z);
   }
-  return out;
-}
-
-// A lane's range end state as one 64-bit word (k_huff1 publishes it in LDS):
-// pos | c << 32 | z << 36, bit 63 = final (the start it came from is the true one).
-constexpr uint64_t kEndFinal = 1ull << 63;
-DHD uint64_t pack_end(const HState& s) {
-  return (uint64_t)s.pos | ((uint64_t)(s.c & 15) << 32) | ((uint64_t)(s.z & 127) << 36);
-}
-DHD HState unpack_end(uint64_t w) {
-  return HState{(uint32_t)w, (int32_t)((w >> 32) & 15u), (int32_t)((w >> 36) & 127u)};
+  RangeOut r;
+  r.end.pos = cur.pos;
+  r.end.c = blk;
+  r.end.z = z;
+  r.nblk = nblk;
+  return r;
 }
 
 // Block sink interface (duck-typed): begin(absolute_block) opens a block,

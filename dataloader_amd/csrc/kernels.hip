@@ -463,11 +463,6 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
 //                           restart intervals decode one interval per lane here
 // ---------------------------------------------------------------------------
 constexpr int kMinSubBits = 1024;  // shortest lane range of a one-segment image
-#ifndef DINO_HUFF_REDO_BUDGET
-#define DINO_HUFF_REDO_BUDGET 8
-#endif
-constexpr int kHuffRedoBudget = DINO_HUFF_REDO_BUDGET;  // re-decode steps between two polls of the predecessor
-constexpr int kHuffMaxPolls = 1 << 22;
 
 
 // Work items (segments) an image needs for a stream of `nbits` bits, and the
@@ -479,7 +474,7 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 struct HuffLds {     // k_huff1
   ImgDesc sd;
   HuffTables tab;
-  uint64_t E[kHuffThreads];  // each lane's published range end (pack_end, kEndFinal)
+  RangeOut R[kHuffThreads];
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
@@ -765,58 +760,28 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     HState myS{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};  // this lane's start state and first-decode
     RangeOut myR1{};                                      // result stay in registers; only R is shared
     HUFF_PHASE(0, wall_clock64());
-    if (active) myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
-    // Rounds without barriers: every lane publishes its range end; a lane whose
-    // predecessor's end differs from its own start re-decodes from that end (and
-    // restarts if the end changes again).  The item's first lane is the anchor (its
-    // start is exact, or k_huff2's to fix); a lane is final once its predecessor is
-    // final and its result comes from that final end, so finality runs up the lanes
-    // while the re-decodes of different lanes overlap instead of waiting per round.
-    bool fin = t == 0 || !active;
-    L.E[t] = pack_end(myR1.end) | (fin ? kEndFinal : 0ull);
-    __syncthreads();  // every first decode is published before anyone polls
-    HUFF_PHASE(1, wall_clock64());
-    RangeOut res = myR1;
-    RedoState rd;
-    bool working = false;
-    int iters = 0;
-    const int wl = t & 63;  // lane within the wave
-    // (the iteration cap only guards against a protocol fault: a wrong decode beats a hung GPU)
-    while (!__all(fin) && iters < kHuffMaxPolls) {
-      ++iters;
-      bool pred_final = false, published = false;
-      if (!fin) {
-        const uint64_t w = __hip_atomic_load(&L.E[t - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const HState pe = unpack_end(w);
-        pred_final = (w & kEndFinal) != 0;
-        if (!hstate_eq(pe, myS)) {  // a new start: (re)start the walk from it
-          myS = pe;
-          redo_begin<kSrcPadded>(rd, br, im, pe);
-          working = true;
-        }
-        if (working && redo_run<kSrcPadded>(rd, br, im, rend, cps, cstride, ncp, myR1, kHuffRedoBudget, &res)) {
-          working = false;
-          published = true;
-          __hip_atomic_store(&L.E[t], pack_end(res.end), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-      // Finality for a whole run of lanes at once: lane i becomes final when every lane
-      // from the wave's final prefix up to i is idle on the end its predecessor had
-      // when it was read (no predecessor published a new one in this iteration), and
-      // the lane before the run is final (in the wave, or the loaded flag for lane 0).
-      const uint64_t F = __ballot(fin);
-      const uint64_t N = __ballot(published);
-      uint64_t P = F | (__ballot(!working) & ~(N << 1));
-      if (!(F & 1ull) && !(__ballot(pred_final) & 1ull)) P &= ~1ull;
-      const uint64_t run = ~P == 0ull ? ~0ull : (((~P) & (P + 1ull)) - 1ull);  // P's trailing ones
-      if (!fin && ((run >> wl) & 1ull)) {
-        fin = true;
-        __hip_atomic_store(&L.E[t], pack_end(res.end) | kEndFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      if (!__any(working)) __builtin_amdgcn_s_sleep(1);  // the wave only waits on an earlier lane
+    if (active) {
+      myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
+      L.R[t] = myR1;
     }
-    __syncthreads();
-    const int round = iters;
+    __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
+    HUFF_PHASE(1, wall_clock64());
+    int round = 0;
+    for (; round < kHuffThreads + 1; ++round) {
+      HState want;
+      bool redo = false;
+      if (active && t >= 1) {
+        want = L.R[t - 1].end;
+        redo = !hstate_eq(want, myS);
+      }
+      __syncthreads();
+      if (redo) {
+        myS = want;
+        L.R[t] = decode_range_sync<kSrcPadded>(br, im, want, rend, cps, cstride, ncp, myR1);
+      }
+      if (!__syncthreads_or(redo ? 1 : 0)) break;
+    }
+    const RangeOut res = L.R[t];
     HUFF_PHASE(2, wall_clock64());
     HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
     if (huff_single_segment(sd)) {

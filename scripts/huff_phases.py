@@ -15,7 +15,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-LIB = ROOT / "build" / "lib_phases.so"
+LIB = Path(os.environ.get("DINO_PHASE_LIB", ROOT / "build" / "lib_phases.so"))
 
 
 def main():

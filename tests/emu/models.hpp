@@ -173,126 +173,6 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   }
 }
 
-// ---- k_huff1's barrier-free rounds, one segment of `seg` lanes at a time ----
-// Waves of `wave` lanes run one loop iteration at a time in a pseudo-random order
-// (every lane of the wave reads its predecessor's published end before any lane of
-// the wave stores, as in lockstep execution); afterwards the cross-segment rounds of
-// k_huff2 and the writes follow as in model_huffman_spec.  Same result expected.
-template <int kWin>
-inline void model_huffman_async(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
-                                int seg, int wave, int budget, uint32_t seed, CoefSink& sink, int32_t* dcd,
-                                int32_t* stats) {
-  const int total_blocks = d.total_blocks;
-  int n = lanes;
-  uint32_t sub = (nbits + n - 1) / n;
-  sub = (sub + 31) & ~31u;
-  if (sub == 0) sub = 32;
-  n = std::max(1, std::min(n, (int)((nbits + sub - 1) / sub)));
-  if (seg <= 0) seg = n;
-  std::vector<HState> S(n);
-  std::vector<RangeOut> R(n), R1(n);
-  std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
-  std::vector<int32_t> ncp(n);
-  auto rend = [&](int i) -> uint32_t { return i == n - 1 ? nbits : (uint32_t)(i + 1) * sub; };
-  auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
-  for (int i = 0; i < n; ++i) {
-    S[i] = HState{(uint32_t)i * sub, 0, 0};
-    R[i] = R1[i] = decode_range<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, kHuffCheckpoints,
-                                      &ncp[i]);
-  }
-  uint32_t rng = seed * 2654435761u + 12345u;
-  long iters = 0;
-  for (int s0 = 0; s0 < n; s0 += seg) {
-    const int s1 = std::min(n, s0 + seg);
-    std::vector<uint64_t> E(s1 - s0);
-    std::vector<char> fin(s1 - s0), working(s1 - s0, 0);
-    std::vector<RedoState> rd(s1 - s0);
-    for (int i = s0; i < s1; ++i) {
-      fin[i - s0] = i == s0;
-      E[i - s0] = pack_end(R1[i].end) | (fin[i - s0] ? kEndFinal : 0ull);
-    }
-    const int nw = (s1 - s0 + wave - 1) / wave;
-    for (;;) {
-      bool all = true;
-      for (char f : fin) all = all && f;
-      if (all) break;
-      rng = rng * 1664525u + 1013904223u;
-      const int w0 = s0 + (int)((rng >> 8) % (uint32_t)nw) * wave, w1 = std::min(s1, w0 + wave);
-      bool wave_fin = true;
-      for (int i = w0; i < w1; ++i) wave_fin = wave_fin && fin[i - s0];
-      if (wave_fin) continue;
-      ++iters;
-      std::vector<uint64_t> seen(w1 - w0);
-      for (int i = w0; i < w1; ++i) seen[i - w0] = i > s0 ? E[i - 1 - s0] : 0;
-      uint64_t F = 0, N = 0, idle = 0, pf = 0;
-      for (int i = w0; i < w1; ++i) {
-        const int k = i - s0, wl = i - w0;
-        if (!fin[k]) {
-          const uint64_t w = seen[wl];
-          const HState pe = unpack_end(w);
-          if (w & kEndFinal) pf |= 1ull << wl;
-          if (!hstate_eq(pe, S[i])) {
-            S[i] = pe;
-            redo_begin<kWin>(rd[k], br, im, pe);
-            working[k] = 1;
-          }
-          if (working[k] && redo_run<kWin>(rd[k], br, im, rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i],
-                                           R1[i], budget, &R[i])) {
-            working[k] = 0;
-            N |= 1ull << wl;
-            E[k] = pack_end(R[i].end);
-          }
-        }
-        if (fin[k]) F |= 1ull << wl;
-        if (!working[k]) idle |= 1ull << wl;
-      }
-      for (int wl = w1 - w0; wl < 64; ++wl) F |= 1ull << wl;  // lanes past the segment: as inactive lanes
-      uint64_t P = F | (idle & ~(N << 1));
-      if (!(F & 1ull) && !(pf & 1ull)) P &= ~1ull;
-      const uint64_t run = ~P == 0ull ? ~0ull : (((~P) & (P + 1ull)) - 1ull);
-      for (int i = w0; i < w1; ++i) {
-        const int k = i - s0;
-        if (!fin[k] && ((run >> (i - w0)) & 1ull)) {
-          fin[k] = 1;
-          E[k] = pack_end(R[i].end) | kEndFinal;
-        }
-      }
-    }
-  }
-  // k_huff2: rounds across the segments
-  int rounds = 0;
-  for (;;) {
-    std::vector<HState> want(n);
-    std::vector<char> redo(n, 0);
-    for (int i = 1; i < n; ++i) {
-      want[i] = R[i - 1].end;
-      redo[i] = !hstate_eq(want[i], S[i]);
-    }
-    bool any = false;
-    for (int i = 1; i < n; ++i) {
-      if (!redo[i]) continue;
-      S[i] = want[i];
-      R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i], R1[i]);
-      any = true;
-    }
-    ++rounds;
-    if (!any) break;
-  }
-  int32_t blk0 = 0;
-  sink.dcd = dcd;
-  for (int i = 0; i < n; ++i) {
-    decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, nbits, sink);
-    blk0 += R[i].nblk;
-  }
-  sink.dcd = nullptr;
-  model_dcscan(d, im, dcd, sink.coef);
-  if (stats) {
-    stats[0] = (int32_t)std::min<long>(iters, 1 << 30);
-    stats[1] = rounds;
-    stats[2] = n;
-  }
-}
-
 struct StageCapture {
   std::vector<uint8_t> ent;
   std::vector<int16_t> coef;
@@ -395,9 +275,6 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     if (mode == 2) {
       BitReader bw{win.data(), (uint32_t)win.size() * 4};
       model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, 0, sink, dcd.data(), stats);
-    } else if (mode >= 4) {  // 4: k_huff1's barrier-free rounds, segments of 64 lanes in waves of 16
-      model_huffman_async<kSrcPadded>(br, im, d, (uint32_t)ds.len * 8, lanes, 64, 16, mode == 4 ? 8 : 1, (uint32_t)mode,
-                                      sink, dcd.data(), stats);
     } else {
       model_huffman_spec<kSrcPadded>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
                                 stats);

@@ -95,8 +95,7 @@ def _zoo():
     return out
 
 
-@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024),
-                                        (4, 5), (4, 256), (5, 300), (6, 1024)])
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024)])
 def test_decode_bit_exact_vs_pillow(emu, mode, lanes):
     for j in _zoo():
         r, out, _ = emu_decode(emu, j, mode, lanes)
@@ -143,7 +142,7 @@ def _damaged_streams(rng):
     return out
 
 
-@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 64), (4, 100), (6, 300)])
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 64), (1, 300), (3, 1000)])
 def test_damaged_streams_bit_exact_vs_pillow(emu, mode, lanes):
     for name, j in _damaged_streams(np.random.default_rng(1)):
         ref = cpu_ref.decode_rgb(j)
@@ -153,13 +152,10 @@ def test_damaged_streams_bit_exact_vs_pillow(emu, mode, lanes):
         np.testing.assert_array_equal(out, np.asarray(ref), err_msg=name)
 
 
-def test_barrier_free_rounds_corrupt_streams(emu):
-    """k_huff1's barrier-free rounds (modes 4-6: random wave order, poll budgets 8 and 1)
-    reach the same start states as the synchronous rounds on damaged entropy data:
-    bytes overwritten inside the scan, many lanes.  (Pixels are compared between the
-    decode modes only: such streams can yield dequantised coefficients beyond 16 bits,
-    where libjpeg-turbo's SIMD IDCT saturates and its C IDCT, restated here, does not;
-    DESIGN.md §8.)"""
+def test_corrupt_bytes_all_decode_modes_vs_pillow(emu):
+    """Bytes overwritten inside the scan: the speculative decode modes agree with the
+    sequential one and with Pillow, including blocks whose dequantised coefficients
+    leave the range where libjpeg-turbo's SIMD and C IDCTs agree (idct_simd_*)."""
     from dataloader_amd.synthetic import make_jpeg
     rng = np.random.default_rng(5)
     base = make_jpeg(320, 240, 3)
@@ -172,10 +168,14 @@ def test_barrier_free_rounds_corrupt_streams(emu):
             if b[p - 1] != 0xFF and v != 0xFF:
                 b[p] = v
         j = bytes(b)
-        outs = [emu_decode(emu, j, m, lanes) for m, lanes in ((0, 1), (1, 200), (4, 200), (5, 77), (6, 513))]
+        ref = cpu_ref.decode_rgb(j)
+        outs = [emu_decode(emu, j, m, lanes) for m, lanes in ((0, 1), (1, 200), (1, 77), (3, 513))]
         for r, out, _ in outs:
             assert r == outs[0][0]
             np.testing.assert_array_equal(out, outs[0][1])
+        if ref is not None:
+            assert outs[0][0] == 0
+            np.testing.assert_array_equal(outs[0][1], np.asarray(ref))
 
 
 def test_speculative_sync_converges(emu):

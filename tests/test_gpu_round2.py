@@ -160,6 +160,27 @@ def test_damaged_streams_through_the_abi(gpu_device):
     assert not bad, bad
 
 
+def test_extreme_coefficients_through_k_idct(gpu_device):
+    """Blocks whose coefficients leave the range where libjpeg-turbo's C and SIMD IDCTs
+    agree (damaged data): k_idct's SIMD-arithmetic path, bit-exact with Pillow."""
+    from tests.test_idct_simd_cpu import extreme_cases
+    jpegs = extreme_cases(12, 28)
+    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
+    d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    bad = []
+    for i, j in enumerate(jpegs):
+        ref = np.asarray(cpu_ref.decode_rgb(j))
+        if info[i, 0] != 0:
+            bad.append((i, "status", int(info[i, 0])))
+            continue
+        got = eng.copy_rgb(i, ref.shape[1], ref.shape[0]).cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad.append((i, int((got != ref).sum())))
+    eng.close()
+    assert not bad, bad
+
+
 def test_writer_multiscan_cases_through_k_prog(gpu_device):
     """The test writer's multi-scan sequential files, non-default progression scripts,
     restart intervals per scan and mid-stream DQTs (tests/jpeg_writer.py) decoded by
