@@ -142,7 +142,14 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
         for name, sl, S in (("k_vert_global", slice(0, n_g), g), ("k_vert_local", slice(n_g, nv), l)):
             rr = r[:, sl]
             ab[name] = float((rr["crop_h"].astype(np.float64) * 3 * S + 3 * S * S).sum(1).mean())
+        if l <= VFINAL_MAX_S:  # local views: k_vfinal (timed as k_final_local) reads the h-pass rows, writes the view
+            rr = r[:, n_g:nv]
+            ab["k_final_local"] = float((rr["crop_h"].astype(np.float64) * 3 * l).sum(1).mean()) + out_bytes * 3 * n_l * l * l
+            ab.pop("k_vert_local")
     return ab
+
+
+VFINAL_MAX_S = 128  # kernels.hip kVFinalMaxS: views up to this size run k_vfinal (vertical pass + epilogue fused)
 
 
 def _measure(fn, warmup: int, iters: int, budget_s: float) -> dict:

@@ -257,6 +257,17 @@ DHD void idct_simd_pass2(const int32_t* w, uint8_t* out) {
 // the DC-only shortcut equal to the general path.  Pass 2 of a row w: sum |w| <= 11500
 // keeps the 16-bit sums and bounds the output by 11500 * 1.4143 / 32 + 0.5 < 512,
 // the range where the C range-limit table clamps instead of wrapping.
+// Cheap sufficient forms: |d0| <= 2047 with every other |d_k| <= 600 (2047 + 1.4143 *
+// 7 * 600 < 8190); every |w| <= 1437 (8 * 1437 <= 11500).
+DHD bool idct_col_safe_fast(const int32_t* d) {
+  int32_t m = 0;
+#pragma unroll
+  for (int r = 1; r < 8; ++r) {
+    const int32_t a = iabs32(d[r]);
+    m = a > m ? a : m;
+  }
+  return iabs32(d[0]) <= 2047 && m <= 600;
+}
 DHD bool idct_col_safe(const int32_t* d) {
   int32_t s = 0;
 #pragma unroll

@@ -1249,8 +1249,9 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
       // a block with a column outside the C/SIMD agreement bound (damaged data only)
       // runs libjpeg-turbo's SIMD pass 1, whose DC-only shortcut is decided per block
       const int gsh = threadIdx.x & 56;  // this group's first lane within the wave
-      if (((__ballot(!idct_col_safe(col)) >> gsh) & 0xFFu) == 0) {
-        idct_pass1(col, wcol);
+      const bool csafe = idct_col_safe_fast(col) || idct_col_safe(col);
+      if (((__ballot(!csafe) >> gsh) & 0xFFu) == 0) {
+        idct_pass1_t<int32_t>(col, wcol);  // safe: every |d| <= 8190, inside the int32 bound
       } else {
         bool acz = true;
 #pragma unroll
@@ -1271,7 +1272,8 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
         uint8_t b[8];
         uint64_t u;
       } o;
-      if (idct_row_safe(row)) idct_pass2(row, o.b);
+      if (max_abs8(row) <= 1437) idct_pass2_t<int32_t>(row, o.b);
+      else if (idct_row_safe(row)) idct_pass2(row, o.b);
       else idct_simd_pass2(row, o.b);
       const int pitch = cd.bw * 8;
       *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = o.u;
@@ -1800,29 +1802,21 @@ constexpr int kVertRows = 8;
 // rows per workgroup: 16 for the small (local) views, whose 8-row bands are short
 __host__ __device__ __forceinline__ int vert_rows(int S) { return S > 128 ? kVertRows : 2 * kVertRows; }
 
-__global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
-                                              ViewPlan* __restrict__ plan, int nv, int v0, int B,
-                                              const uint8_t* __restrict__ ws, const uint8_t* __restrict__ aws,
-                                              uint8_t* __restrict__ gcrop, dino_aug_config cfg, int S) {
-  __shared__ uint32_t s_part[4];
-  const int b = blockIdx.z, v = v0 + blockIdx.y;
-  const int i = b * nv + v;
-  const ViewPlan vp = plan[i];
-  if (!vp.ok) return;
-  const dino_view_params p = prm[i];
-  const ImgDesc& d = desc[b];
-  const int64_t N = (int64_t)S * S;
-  uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);
+// Rows [y0, y0 + nr) of a view through the vertical pass (+ flip) and the stage-0
+// ColorJitter ops; every result goes out through put4(y, xo, w0, w1, w2) (four
+// adjacent output pixels starting at column xo, one byte per pixel and plane, in
+// output order) or put1(y, xo, r, g, b).  Returns the lane's sum of L over its
+// pixels (used only when the view has a contrast op).
+template <typename Put4, typename Put1>
+__device__ __forceinline__ uint32_t vert_apply(const ImgDesc& d, const dino_view_params& p, const ViewPlan& vp,
+                                               const uint8_t* __restrict__ ws, const uint8_t* __restrict__ aws, int S,
+                                               int y0, int nr, const JitterPlan& jp, int hd, Put4 put4, Put1 put1) {
   const int W = d.width;
   const bool need_h = vp.kh != 0, need_v = vp.kv != 0;
   const int32_t* cbase = (const int32_t*)(aws + vp.rcoef_off);
   const CoefView cvv{cbase + 2 * S, cbase + 4 * S + (int64_t)S * vp.kh, vp.kv};
   const int64_t cpl = (int64_t)p.crop_h * S;
   const uint8_t* htmp = aws + vp.htmp_off;
-  const JitterPlan jp = make_jitter_plan(p);
-  const int hd = hue_delta(p.hue);
-  const int y0 = blockIdx.x * vert_rows(S);
-  const int nr = min(vert_rows(S), S - y0);
   uint32_t lsum = 0;
   if (need_h && (S & 3) == 0) {
     const int nq = S >> 2;
@@ -1864,9 +1858,8 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
         o[1] |= (uint32_t)g << (8 * j);
         o[2] |= (uint32_t)bb << (8 * j);
       }
-      const int64_t off = (int64_t)y * S + (p.flip ? S - 4 - 4 * xq : 4 * xq);
-#pragma unroll
-      for (int c = 0; c < 3; ++c) *(uint32_t*)(crop + c * N + off) = p.flip ? __builtin_bswap32(o[c]) : o[c];
+      if (p.flip) put4(y, S - 4 - 4 * xq, __builtin_bswap32(o[0]), __builtin_bswap32(o[1]), __builtin_bswap32(o[2]));
+      else put4(y, 4 * xq, o[0], o[1], o[2]);
     }
   } else {
     const SrcView src = need_h ? SrcView{htmp, (int64_t)S, 1, cpl}
@@ -1886,18 +1879,55 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
         bb = q[2 * src.cs];
       }
       jitter_stage0(jp, r, g, bb, p, hd);
-      const int64_t o = (int64_t)y * S + (p.flip ? S - 1 - x : x);
-      crop[o] = (uint8_t)r;
-      crop[N + o] = (uint8_t)g;
-      crop[2 * N + o] = (uint8_t)bb;
+      put1(y, p.flip ? S - 1 - x : x, r, g, bb);
       if (jp.has_contrast) lsum += (uint32_t)rgb_to_l(r, g, bb);
     }
   }
+  return lsum;
+}
+
+// Sum of a value over the workgroup (256 lanes); every lane gets the total.
+__device__ __forceinline__ uint32_t wg_sum256(uint32_t v, uint32_t* s_part) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const uint32_t t = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+  __syncthreads();
+  return t;
+}
+
+__global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                              ViewPlan* __restrict__ plan, int nv, int v0, int B,
+                                              const uint8_t* __restrict__ ws, const uint8_t* __restrict__ aws,
+                                              uint8_t* __restrict__ gcrop, dino_aug_config cfg, int S) {
+  __shared__ uint32_t s_part[4];
+  const int b = blockIdx.z, v = v0 + blockIdx.y;
+  const int i = b * nv + v;
+  const ViewPlan vp = plan[i];
+  if (!vp.ok) return;
+  const dino_view_params p = prm[i];
+  const int64_t N = (int64_t)S * S;
+  uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);
+  const JitterPlan jp = make_jitter_plan(p);
+  const int y0 = blockIdx.x * vert_rows(S);
+  const int nr = min(vert_rows(S), S - y0);
+  const uint32_t lsum = vert_apply(
+      desc[b], p, vp, ws, aws, S, y0, nr, jp, hue_delta(p.hue),
+      [&](int y, int xo, uint32_t w0, uint32_t w1, uint32_t w2) {
+        const int64_t off = (int64_t)y * S + xo;
+        *(uint32_t*)(crop + off) = w0;
+        *(uint32_t*)(crop + N + off) = w1;
+        *(uint32_t*)(crop + 2 * N + off) = w2;
+      },
+      [&](int y, int xo, int r, int g, int bb) {
+        const int64_t o = (int64_t)y * S + xo;
+        crop[o] = (uint8_t)r;
+        crop[N + o] = (uint8_t)g;
+        crop[2 * N + o] = (uint8_t)bb;
+      });
   if (jp.has_contrast) {
-    for (int off = 32; off > 0; off >>= 1) lsum += __shfl_xor(lsum, off);
-    if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = lsum;
-    __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(&plan[i].lsum, s_part[0] + s_part[1] + s_part[2] + s_part[3]);
+    const uint32_t tot = wg_sum256(lsum, s_part);
+    if (threadIdx.x == 0) atomicAdd(&plan[i].lsum, tot);
   }
 }
 
@@ -2092,6 +2122,111 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
     case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
     case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
     default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+  }
+}
+
+// k_vert + k_final for small views in one workgroup per view: the vertical pass and
+// the stage-0 jitter write the view into an LDS tile, the workgroup reduces the
+// contrast mean, applies the later ops in place, reflects the blur halo and runs the
+// same blur/solarize/normalise epilogue -- the view never goes through HBM.
+// Tile: S + 2 pad rows; columns from -pad (the window base, word-aligned) to S + pad.
+__host__ __device__ __forceinline__ int vfinal_tile_bytes(int S) {
+  return 3 * (S + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad) + 16;
+}
+constexpr int kVFinalMaxS = 128;  // views up to this size take the fused kernel
+
+template <typename OutT>
+__global__ void __launch_bounds__(256) k_vfinal(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                                const ViewPlan* __restrict__ plan, int nv, int v0, const uint8_t* __restrict__ ws,
+                                                const uint8_t* __restrict__ aws, ViewPtrs views, dino_aug_config cfg, int S,
+                                                const float* __restrict__ norm) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ uint32_t s_part[4];
+  FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
+  uint8_t* tile = smem + sizeof(FinalLds);
+  const int b = blockIdx.y, v = v0 + blockIdx.x;
+  const int i = b * nv + v;
+  const ViewPlan vp = plan[i];
+  const int64_t N = (int64_t)S * S;
+  OutT* out = (OutT*)views.p[v] + (int64_t)b * 3 * N;
+  const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
+  if (!vp.ok) {  // as k_final: zeros, or LeJEPA's black canvas normalised
+    const bool canvas = cfg.recipe == DINO_RECIPE_LEJEPA && desc[b].status < 0;
+    for (int e = threadIdx.x; e < 3 * S * S; e += blockDim.x) {
+      const int ch = e / (S * S);
+      out[e] = canvas ? out_cast<OutT>(u8_normalize(0, nb ? nb[ch] : cfg.mean[ch], nb ? nb[3 + ch] : cfg.std[ch])) : (OutT)0;
+    }
+    return;
+  }
+  const dino_view_params p = prm[i];
+  const int ks = p.blur ? p.ksize : 1;
+  const int pad = ks >> 1;
+  const int tp = final_tile_pitch(S, pad);
+  const int64_t tplane = (int64_t)(S + 2 * pad) * tp;
+  OutT* ntab = reinterpret_cast<OutT*>(tile + vfinal_tile_bytes(S));
+  if (p.blur && threadIdx.x == 0) gaussian_kernel1d(ks, p.sigma, H.k1);
+  for (int e = threadIdx.x; e < 3 * 256; e += blockDim.x) {
+    const int c = e >> 8;
+    ntab[e] = out_cast<OutT>(u8_normalize(e & 255, nb ? nb[c] : cfg.mean[c], nb ? nb[3 + c] : cfg.std[c]));
+  }
+  const JitterPlan jp = make_jitter_plan(p);
+  const int hd = hue_delta(p.hue);
+  uint8_t* in0 = tile + (int64_t)pad * tp + pad;  // interior (0, 0)
+  const uint32_t lsum = vert_apply(
+      desc[b], p, vp, ws, aws, S, 0, S, jp, hd,
+      [&](int y, int xo, uint32_t w0, uint32_t w1, uint32_t w2) {
+        uint8_t* q = in0 + y * tp + xo;  // byte stores: the interior starts at column pad
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          q[j] = (uint8_t)(w0 >> (8 * j));
+          q[tplane + j] = (uint8_t)(w1 >> (8 * j));
+          q[2 * tplane + j] = (uint8_t)(w2 >> (8 * j));
+        }
+      },
+      [&](int y, int xo, int r, int g, int bb) {
+        uint8_t* q = in0 + y * tp + xo;
+        q[0] = (uint8_t)r;
+        q[tplane] = (uint8_t)g;
+        q[2 * tplane] = (uint8_t)bb;
+      });
+  __syncthreads();
+  const int cmean = jp.has_contrast ? contrast_mean_from_sum(wg_sum256(lsum, s_part), N) : 0;
+  // the ops after contrast, in place on the interior
+  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
+    const int y = e / S, x = e - y * S;
+    uint8_t* q = in0 + y * tp + x;
+    int r = q[0], g = q[tplane], bb = q[2 * tplane];
+    jitter_stage1(jp, r, g, bb, p, cmean, hd);
+    q[0] = (uint8_t)r;
+    q[tplane] = (uint8_t)g;
+    q[2 * tplane] = (uint8_t)bb;
+  }
+  if (pad > 0) {
+    __syncthreads();
+    // blur halo: torch's reflect padding of the jittered view
+    const int tw = S + 2 * pad, th = S + 2 * pad;
+    for (int e = threadIdx.x; e < th * tw; e += blockDim.x) {
+      const int r = e / tw, c = e - r * tw;
+      if (r >= pad && r < pad + S && c >= pad && c < pad + S) continue;
+      const int sr = reflect_idx(r - pad, S), sc = reflect_idx(c - pad, S);
+      const uint8_t* src = in0 + sr * tp + sc;
+      uint8_t* dst = tile + r * tp + c;
+      dst[0] = src[0];
+      dst[tplane] = src[tplane];
+      dst[2 * tplane] = src[2 * tplane];
+    }
+  }
+  __syncthreads();
+  if (p.blur && threadIdx.x < ks * ks) H.k2[threadIdx.x] = H.k1[threadIdx.x / ks] * H.k1[threadIdx.x % ks];
+  __syncthreads();
+  const bool sol = p.solarize != 0;
+  switch (ks) {
+    case 1: final_compute<1, OutT>(tile, tp, tplane, S, 0, S, ks, H.k2, sol, ntab, out); break;
+    case 3: final_compute<3, OutT>(tile, tp, tplane, S, 0, S, ks, H.k2, sol, ntab, out); break;
+    case 5: final_compute<5, OutT>(tile, tp, tplane, S, 0, S, ks, H.k2, sol, ntab, out); break;
+    case 7: final_compute<7, OutT>(tile, tp, tplane, S, 0, S, ks, H.k2, sol, ntab, out); break;
+    case 9: final_compute<9, OutT>(tile, tp, tplane, S, 0, S, ks, H.k2, sol, ntab, out); break;
+    default: final_compute<0, OutT>(tile, tp, tplane, S, 0, S, ks, H.k2, sol, ntab, out); break;
   }
 }
 
@@ -2470,6 +2605,13 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
   TIMED(tm, kKHresize, s,
         (k_hresize<<<dim3(16, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
+  if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS
+    const int lds = (int)sizeof(FinalLds) + vfinal_tile_bytes(S) + 3 * 256 * (int)sizeof(OutT);
+    TIMED(tm, kfin, s,
+          (k_vfinal<OutT><<<dim3(nvc, B), 256, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.views, a.cfg,
+                                                         S, a.norm)));
+    return hipGetLastError();
+  }
   TIMED(tm, kvert, s,
         (k_vert<<<dim3((S + vert_rows(S) - 1) / vert_rows(S), nvc, B), 256, 0, s>>>(a.desc, a.params, a.plan, nv, v0, B,
                                                                              a.ws, a.aws, a.gcrop, a.cfg, S)));
