@@ -1239,25 +1239,17 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     const CompDesc& cd = d.comp[cur.c];
     if (valid) {  // dequantize + pass 1 on column l (reads and writes only this lane's column)
       const uint16_t* q = d.qt[cd.tq];
-      int32_t raw[8], qq[8], col[8], wcol[8];
+      int32_t raw[8], qq[8], wcol[8];
+      bool acz = true;  // rows 1..7 of this column are zero
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
         raw[r] = sb[r * 9 + l];
         qq[r] = (int32_t)(int16_t)q[r * 8 + l];
-        col[r] = raw[r] * qq[r];
+        if (r) acz = acz && raw[r] == 0;
       }
-      // a block with a column outside the C/SIMD agreement bound (damaged data only)
-      // runs libjpeg-turbo's SIMD pass 1, whose DC-only shortcut is decided per block
+      // libjpeg-turbo's SIMD pass 1 decides its DC-only shortcut for the whole block
       const int gsh = threadIdx.x & 56;  // this group's first lane within the wave
-      const bool csafe = idct_col_safe_fast(col) || idct_col_safe(col);
-      if (((__ballot(!csafe) >> gsh) & 0xFFu) == 0) {
-        idct_pass1_t<int32_t>(col, wcol);  // safe: every |d| <= 8190, inside the int32 bound
-      } else {
-        bool acz = true;
-#pragma unroll
-        for (int r = 1; r < 8; ++r) acz = acz && raw[r] == 0;
-        idct_simd_pass1(raw, qq, ((__ballot(acz) >> gsh) & 0xFFu) == 0xFFu, wcol);
-      }
+      idct_pass1(raw, qq, ((__ballot(acz) >> gsh) & 0xFFu) == 0xFFu, wcol);
 #pragma unroll
       for (int r = 0; r < 8; ++r) sb[r * 9 + l] = wcol[r];
     }
@@ -1272,9 +1264,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
         uint8_t b[8];
         uint64_t u;
       } o;
-      if (max_abs8(row) <= 1437) idct_pass2_t<int32_t>(row, o.b);
-      else if (idct_row_safe(row)) idct_pass2(row, o.b);
-      else idct_simd_pass2(row, o.b);
+      idct_pass2(row, o.b);
       const int pitch = cd.bw * 8;
       *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = o.u;
     }
@@ -1886,12 +1876,14 @@ __device__ __forceinline__ uint32_t vert_apply(const ImgDesc& d, const dino_view
   return lsum;
 }
 
-// Sum of a value over the workgroup (256 lanes); every lane gets the total.
-__device__ __forceinline__ uint32_t wg_sum256(uint32_t v, uint32_t* s_part) {
+// Sum of a value over the workgroup (up to 1024 lanes, s_part holds one word per
+// wave); every lane gets the total.
+__device__ __forceinline__ uint32_t wg_sum(uint32_t v, uint32_t* s_part) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
   if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = v;
   __syncthreads();
-  const uint32_t t = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+  uint32_t t = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_part[w];
   __syncthreads();
   return t;
 }
@@ -1907,7 +1899,7 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   if (!vp.ok) return;
   const dino_view_params p = prm[i];
   const int64_t N = (int64_t)S * S;
-  uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);
+  uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);  // (256 lanes: s_part holds 4 waves)
   const JitterPlan jp = make_jitter_plan(p);
   const int y0 = blockIdx.x * vert_rows(S);
   const int nr = min(vert_rows(S), S - y0);
@@ -1926,7 +1918,7 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
         crop[2 * N + o] = (uint8_t)bb;
       });
   if (jp.has_contrast) {
-    const uint32_t tot = wg_sum256(lsum, s_part);
+    const uint32_t tot = wg_sum(lsum, s_part);
     if (threadIdx.x == 0) atomicAdd(&plan[i].lsum, tot);
   }
 }
@@ -2133,15 +2125,19 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
 __host__ __device__ __forceinline__ int vfinal_tile_bytes(int S) {
   return 3 * (S + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad) + 16;
 }
-constexpr int kVFinalMaxS = 128;  // views up to this size take the fused kernel
+#ifndef DINO_VFINAL_MAX_S
+#define DINO_VFINAL_MAX_S 128
+#endif
+constexpr int kVFinalMaxS = DINO_VFINAL_MAX_S;  // views up to this size take the fused kernel
+constexpr int kVFinalThreads = 512;  // 8 waves per view: the vertical pass is load-latency bound
 
 template <typename OutT>
-__global__ void __launch_bounds__(256) k_vfinal(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+__global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                 const ViewPlan* __restrict__ plan, int nv, int v0, const uint8_t* __restrict__ ws,
                                                 const uint8_t* __restrict__ aws, ViewPtrs views, dino_aug_config cfg, int S,
                                                 const float* __restrict__ norm) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ uint32_t s_part[4];
+  __shared__ uint32_t s_part[kVFinalThreads / 64];
   FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
   uint8_t* tile = smem + sizeof(FinalLds);
   const int b = blockIdx.y, v = v0 + blockIdx.x;
@@ -2190,7 +2186,7 @@ __global__ void __launch_bounds__(256) k_vfinal(const ImgDesc* __restrict__ desc
         q[2 * tplane] = (uint8_t)bb;
       });
   __syncthreads();
-  const int cmean = jp.has_contrast ? contrast_mean_from_sum(wg_sum256(lsum, s_part), N) : 0;
+  const int cmean = jp.has_contrast ? contrast_mean_from_sum(wg_sum(lsum, s_part), N) : 0;
   // the ops after contrast, in place on the interior
   for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
     const int y = e / S, x = e - y * S;
@@ -2608,7 +2604,7 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS
     const int lds = (int)sizeof(FinalLds) + vfinal_tile_bytes(S) + 3 * 256 * (int)sizeof(OutT);
     TIMED(tm, kfin, s,
-          (k_vfinal<OutT><<<dim3(nvc, B), 256, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.views, a.cfg,
+          (k_vfinal<OutT><<<dim3(nvc, B), kVFinalThreads, lds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws, a.views, a.cfg,
                                                          S, a.norm)));
     return hipGetLastError();
   }

@@ -296,7 +296,7 @@ inline int model_idct_color(const ImgDesc& d, const std::vector<int16_t>& coef, 
     int pitch = cd.bw * 8;
     for (int by = 0; by < cd.bh; ++by)
       for (int bx = 0; bx < cd.bw; ++bx)
-        idct_islow_fast(coef.data() + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64, d.qt[cd.tq],
+        idct_block(coef.data() + cd.coef_off / 2 + ((int64_t)by * cd.bw + bx) * 64, d.qt[cd.tq],
                    planes.data() + cd.plane_off + (int64_t)by * 8 * pitch + bx * 8, pitch);
   }
   if (cap) cap->planes = planes;

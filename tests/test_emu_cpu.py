@@ -155,7 +155,7 @@ def test_damaged_streams_bit_exact_vs_pillow(emu, mode, lanes):
 def test_corrupt_bytes_all_decode_modes_vs_pillow(emu):
     """Bytes overwritten inside the scan: the speculative decode modes agree with the
     sequential one and with Pillow, including blocks whose dequantised coefficients
-    leave the range where libjpeg-turbo's SIMD and C IDCTs agree (idct_simd_*)."""
+    leave the range where libjpeg-turbo's SIMD and C IDCTs agree (idct.hpp)."""
     from dataloader_amd.synthetic import make_jpeg
     rng = np.random.default_rng(5)
     base = make_jpeg(320, 240, 3)
