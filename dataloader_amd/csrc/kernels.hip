@@ -1318,6 +1318,14 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, int* o
   out[3] = odd ? o3 : e3;
 }
 
+#ifndef DINO_COLOR_WGS
+#define DINO_COLOR_WGS 32
+#endif
+constexpr int kColorWgs = DINO_COLOR_WGS;  // workgroups per image
+#ifndef DINO_COLOR_UNROLL
+#define DINO_COLOR_UNROLL 2
+#endif
+
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
 // the RGB area is padded by 16 bytes, so the last partial quad may store whole words).
 // 4:2:0 interior quads (the common case) take a vectorised path: one word of Y and
@@ -1357,7 +1365,7 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
   const uint32_t pstride = (uint32_t)(qs * 4);
   const int dy = (int)(pstride / (uint32_t)W), dx = (int)(pstride - (uint32_t)dy * (uint32_t)W);
   int yq = (int)((uint32_t)(q0 * 4) / (uint32_t)W), xq = (int)((uint32_t)(q0 * 4) - (uint32_t)yq * (uint32_t)W);
-#pragma unroll 2
+#pragma unroll DINO_COLOR_UNROLL
   for (int64_t q = q0; q < nq; q += qs) {
     const int64_t i0 = q * 4;
     int y = yq, x = xq;
@@ -2129,7 +2137,10 @@ __host__ __device__ __forceinline__ int vfinal_tile_bytes(int S) {
 #define DINO_VFINAL_MAX_S 128
 #endif
 constexpr int kVFinalMaxS = DINO_VFINAL_MAX_S;  // views up to this size take the fused kernel
-constexpr int kVFinalThreads = 512;  // 8 waves per view: the vertical pass is load-latency bound
+#ifndef DINO_VFINAL_THREADS
+#define DINO_VFINAL_THREADS 512
+#endif
+constexpr int kVFinalThreads = DINO_VFINAL_THREADS;  // 8 waves per view: the vertical pass is load-latency bound
 
 template <typename OutT>
 __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
@@ -2580,7 +2591,7 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKHuff3, s, (k_huff3<<<grid3, kHuffThreads, kHuff3LdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKIdct, s, (k_idct<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
-  TIMED(tm, kKColor, s, (k_color<<<dim3(64, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   return hipGetLastError();
 }
 
