@@ -39,7 +39,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
 
 def _gen_one(args):
-    w, h, seed, mixed = args
+    w, h, seed, mixed, prog = args
     from dataloader_amd.synthetic import encode_jpeg, textured_rgb
     rng = np.random.default_rng(seed)
     if mixed:
@@ -47,12 +47,14 @@ def _gen_one(args):
         aspect = float(rng.uniform(0.75, 4.0 / 3.0))
         long_ = max(short, int(round(short * max(aspect, 1.0 / aspect))))
         w, h = (long_, short) if rng.random() < 0.5 else (short, long_)
-    return encode_jpeg(textured_rgb(w, h, rng), quality=85)
+    return encode_jpeg(textured_rgb(w, h, rng), quality=85, progressive=prog)
 
 
-def make_unique(n: int, w: int, h: int, base_seed: int, mixed: bool, procs: int) -> list[bytes]:
+def make_unique(n: int, w: int, h: int, base_seed: int, mixed: bool, procs: int, prog_frac: float = 0.0) -> list[bytes]:
     # 'spawn': never fork a process that may already hold a HIP context
-    jobs = [(w, h, base_seed * 100003 + k, mixed) for k in range(n)]
+    # every round(1 / prog_frac)-th encode is progressive (libjpeg's simple progression)
+    step = int(round(1.0 / prog_frac)) if prog_frac > 0 else 0
+    jobs = [(w, h, base_seed * 100003 + k, mixed, bool(step) and k % step == step - 1) for k in range(n)]
     if procs <= 1:  # in-process (profiler runs: no worker processes to tear down)
         return [_gen_one(j) for j in jobs]
     pool = get_context("spawn").Pool(procs)
@@ -71,15 +73,17 @@ def jpeg_meta(j: bytes):
     return im.size
 
 
-def sparse_entry_bytes(pipe, dims_420) -> tuple[float, float]:
+def sparse_entry_bytes(pipe, dims_420: list[bytes]) -> tuple[float, float]:
     """Mean bytes of the sparse coefficient entries k_huff1 / k_huff3 wrote per block, read
     back from the block records of the last decoded batch (dino_debug_region 2): a block
     record {first halfword, n16 | n32 << 7 | DC << 16} gives n16 halfword entries + n32
     u32 entries (+ 1 alignment halfword); 8 bytes of record per block on top."""
     eng = pipe._last.engine
     tot_e = tot_b = 0.0
-    for i in range(min(eng.last_batch, 16)):
-        w, h = dims_420[i % len(dims_420)]
+    for i in range(min(eng.last_batch, 16, len(dims_420))):
+        if b"\xff\xc2" in dims_420[i][:4096]:  # progressive (k_prog's dense buffer, not entries)
+            continue
+        w, h = jpeg_meta(dims_420[i])
         nblk = ((w + 15) // 16) * ((h + 15) // 16) * 6
         reg = eng.debug_region(i, 2, nblk * 256 + nblk * 8).cpu().numpy()
         y = reg[nblk * 256:nblk * 256 + nblk * 8].view(np.uint32)[1::2]
@@ -386,6 +390,8 @@ def main() -> None:
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600} (+ iBOT masks)")
+    ap.add_argument("--progressive-frac", type=float, default=0.0,
+                    help="share of progressive encodes (web datasets hold some; decoded by k_prog)")
     ap.add_argument("--masks", action="store_true", help="iBOT masks per batch (default with --mixed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="time budget of each CPU-baseline leg")
@@ -403,7 +409,7 @@ def main() -> None:
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
     # synthetic data first, before anything initialises the GPU in this process
     procs = args.procs if args.procs >= 0 else min(16, os.cpu_count() or 4)
-    uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs)
+    uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs, args.progressive_frac)
 
     import torch
     import torch.distributed as dist
@@ -477,7 +483,7 @@ def main() -> None:
     pipe.set_timing(False)
     k_last = args.warmup + 2 * args.steps - 1  # the batch the last slot still holds
     s_last = (k_last % n_batches) * B
-    ent_b, _ = sparse_entry_bytes(pipe, [jpeg_meta(j) for j in jpegs[s_last:s_last + 16]])
+    ent_b, _ = sparse_entry_bytes(pipe, jpegs[s_last:s_last + 16])
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -544,7 +550,8 @@ def main() -> None:
                                     "resident in HBM") + f", 2x224^2+8x96^2 views, {args.dtype} out",
                        "global_batch": B * world, "batch_per_gpu": B, "parallelism": f"dp{world}",
                        "batches_in_flight": pipe.depth, "masks": masks_on,
-                       "mean_jpeg_bytes": round(ab["s_jpeg"]), "out_dtype": args.dtype},
+                       "mean_jpeg_bytes": round(ab["s_jpeg"]), "out_dtype": args.dtype,
+                       "progressive_frac": args.progressive_frac},
             "roofline": roof,
             "roofline_kernels": roof_all,
             "path_roofline": {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),

@@ -956,7 +956,8 @@ struct ProgLds {
   ImgDesc d;
   ScanRec scans[kMaxScans];
   ProgTable pool[kProgPool];
-  int16_t scratch[kProgThreads][64];   // each lane's AC-refine block
+  uint8_t nat[80];                     // jpeg_natural_order (+ safety entries), read per coefficient
+  __attribute__((aligned(16))) uint8_t ring[kProgThreads][64];  // each lane's staged raw bytes (RawBits)
   int32_t slot_off[kProgPool];         // BITS offset of the table in each pool slot
   int32_t slot_dc[kProgPool];
   int8_t tslot[kMaxScans][8];          // pool slot of each scan table (dc 0..3, ac 4..7), -1 none
@@ -994,6 +995,7 @@ __global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict
   for (int i = 0; i < n; ++i) maxlv = L.scans[i].level > maxlv ? L.scans[i].level : maxlv;
   if (t == 0) L.bad = 0;
   if (t < kMaxScans) L.ready[t] = 0;
+  for (int k = t; k < 80; k += kProgThreads) L.nat[k] = kNaturalOrder[k];
   __syncthreads();
   int16_t* coef = (int16_t*)(ws + dl.coef_off);
   for (int lv = 0; lv <= maxlv; ++lv) {
@@ -1043,7 +1045,7 @@ __global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict
           tb.dc[k] = L.tslot[t][k] >= 0 ? &L.pool[L.tslot[t][k]] : &L.pool[0];
           tb.ac[k] = L.tslot[t][4 + k] >= 0 ? &L.pool[L.tslot[t][4 + k]] : &L.pool[0];
         }
-        prog_decode_scan(p, len, dl, sr, tb, coef, L.scratch[t]);
+        prog_decode_scan(p, len, dl, sr, tb, coef, L.nat, L.ring[t], bytes + offsets[gridDim.x]);
         L.ready[t] = 0;
       }
       __syncthreads();  // (workgroup scope: this level's coefficient stores are visible to the next)

@@ -306,6 +306,11 @@ DHD int prog_walk(const uint8_t* p, int64_t len, ImgDesc* d, ScanRec* scans, Fin
 // ---------------------------------------------------------------------------
 // Bit reader over the raw (stuffed) entropy bytes with libjpeg's marker rules
 // ---------------------------------------------------------------------------
+// Raw bytes come through rb_byte: on the host straight from memory; on the device
+// from a 64-byte LDS ring per lane holding the bytes of absolute addresses
+// [hi - 64, hi), staged 32 aligned bytes at a time (two 16-byte loads and one wait
+// per 32 bytes instead of a dependent load per byte or word; the lane's decode is a
+// serial chain, so every exposed load latency adds to it).
 struct RawBits {
   const uint8_t* p;
   int64_t len;       // image bytes (hard bound)
@@ -315,9 +320,13 @@ struct RawBits {
   int32_t real;      // real (not zero-fill) bits among them; < 0: bits were needed past a marker
   int32_t unread;    // marker code the reader stopped at (0: none)
   int32_t insufficient;
+  uint8_t* ring;     // device: 64 bytes of LDS (16-byte aligned); nullptr: read memory directly
+  uintptr_t hi;      // device: end (absolute address) of the staged bytes
+  uintptr_t bend;    // device: end of the readable buffer (the batch's packed bytes)
 };
 
-DHD void rb_init(RawBits& r, const uint8_t* p, int64_t len, int64_t pos) {
+DHD void rb_init(RawBits& r, const uint8_t* p, int64_t len, int64_t pos, uint8_t* ring = nullptr,
+                 const uint8_t* bend = nullptr) {
   r.p = p;
   r.len = len;
   r.bp = pos;
@@ -326,6 +335,32 @@ DHD void rb_init(RawBits& r, const uint8_t* p, int64_t len, int64_t pos) {
   r.real = 0;
   r.unread = 0;
   r.insufficient = 0;
+  r.ring = ring;
+  r.hi = 0;
+  r.bend = (uintptr_t)bend;
+}
+
+// Stage the 32 bytes from the 16-byte-aligned address at or before `a` (continuing
+// from hi when a lies in the next 16 bytes) into the ring.
+DHD void rb_stage(RawBits& r, uintptr_t a) {
+  const uintptr_t A = (a >= r.hi && a < r.hi + 16 && r.hi) ? r.hi : (a & ~(uintptr_t)15);
+  uint4* dst0 = (uint4*)(r.ring + (A & 63));
+  uint4* dst1 = (uint4*)(r.ring + ((A + 16) & 63));
+  if (A + 32 <= r.bend) {
+    const uint4 c0 = *(const uint4*)A, c1 = *(const uint4*)(A + 16);
+    *dst0 = c0;
+    *dst1 = c1;
+  } else {  // the end of the batch buffer: bytewise, zeros past it
+    for (int j = 0; j < 32; ++j) r.ring[(A + j) & 63] = A + j < r.bend ? *(const uint8_t*)(A + j) : 0;
+  }
+  r.hi = A + 32;
+}
+
+DHD int rb_byte(RawBits& r, int64_t k) {
+  if (!r.ring) return r.p[k];
+  const uintptr_t a = (uintptr_t)(r.p + k);
+  if (a >= r.hi || a + 48 < r.hi) rb_stage(r, a);
+  return r.ring[a & 63];
 }
 
 // jpeg_fill_bit_buffer: bytes until >= 33 bits; an FF00 is a data FF; any other
@@ -335,8 +370,8 @@ DHD void rb_fill(RawBits& r) {
     if (!r.unread) {
       // four plain bytes at once when none of them is 0xFF
       if (r.bp + 4 <= r.len) {
-        const uint32_t w = (uint32_t)r.p[r.bp] << 24 | (uint32_t)r.p[r.bp + 1] << 16 | (uint32_t)r.p[r.bp + 2] << 8 |
-                           (uint32_t)r.p[r.bp + 3];
+        const uint32_t w = (uint32_t)rb_byte(r, r.bp) << 24 | (uint32_t)rb_byte(r, r.bp + 1) << 16 |
+                           (uint32_t)rb_byte(r, r.bp + 2) << 8 | (uint32_t)rb_byte(r, r.bp + 3);
         const uint32_t t = ~w;  // a byte of w is 0xFF <=> that byte of t is 0
         if (!((t - 0x01010101u) & ~t & 0x80808080u)) {
           r.buf |= (uint64_t)w << (32 - r.nbits);
@@ -347,7 +382,7 @@ DHD void rb_fill(RawBits& r) {
         }
       }
       if (r.bp < r.len) {
-        int c = r.p[r.bp];
+        int c = rb_byte(r, r.bp);
         if (c != 0xFF) {
           r.buf |= (uint64_t)c << (56 - r.nbits);
           r.nbits += 8;
@@ -356,15 +391,15 @@ DHD void rb_fill(RawBits& r) {
           continue;
         }
         int64_t k = r.bp + 1;
-        while (k < r.len && r.p[k] == 0xFF) ++k;
-        if (k < r.len && r.p[k] == 0) {  // stuffed FF
+        while (k < r.len && rb_byte(r, k) == 0xFF) ++k;
+        if (k < r.len && rb_byte(r, k) == 0) {  // stuffed FF
           r.buf |= (uint64_t)0xFF << (56 - r.nbits);
           r.nbits += 8;
           r.real += 8;
           r.bp = k + 1;
           continue;
         }
-        r.unread = k < r.len ? r.p[k] : 0xD9;  // (the walk guarantees a marker before the end)
+        r.unread = k < r.len ? rb_byte(r, k) : 0xD9;  // (the walk guarantees a marker before the end)
         r.bp = k + 1;
       } else {
         r.unread = 0xD9;
@@ -483,35 +518,55 @@ struct ScanTables {
   const ProgTable* dc[4];
   const ProgTable* ac[4];
 };
+// Table of scan component k (constant indices only; see ScanGeom).
+DHD const ProgTable* sel4(const ProgTable* const* t, int k) { return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3])); }
 
-// Geometry of the scan's MCUs (jdinput.c per_scan_setup).
+// Geometry of the scan's MCUs (jdinput.c per_scan_setup).  Per block of the MCU a
+// 2-bit field each of component, x and y offset and scan component index (bits
+// [2b, 2b + 2); <= 10 blocks): a lane never indexes a private array at run time
+// (that would live in scratch memory, one global-latency access per use).
 struct ScanGeom {
   int32_t mcus_x, mcus_y, bpm;
-  int8_t blk_comp[kMaxBlocksPerMcu], blk_x[kMaxBlocksPerMcu], blk_y[kMaxBlocksPerMcu], blk_k[kMaxBlocksPerMcu];
+  uint32_t comp, bx, by, kk;
+  int32_t ch[kMaxComp], cv[kMaxComp];  // sampling factors, read with constant indices
+  int64_t plane[kMaxComp];             // coefficient plane offset (int16 units) and blocks per row
+  int32_t bw[kMaxComp];
 };
+DHD int sg_field(uint32_t f, int b) { return (int)((f >> (2 * b)) & 3u); }
+template <typename T>
+DHD T sel3(const T* a, int c) { return c == 0 ? a[0] : (c == 1 ? a[1] : a[2]); }
 
 DHD ScanGeom scan_geom(const ImgDesc& d, const ScanRec& sr) {
   ScanGeom g;
+  g.comp = g.bx = g.by = g.kk = 0;
+  for (int c = 0; c < kMaxComp; ++c) {
+    const CompDesc& cd = d.comp[c < d.ncomp ? c : 0];
+    g.ch[c] = cd.h;
+    g.cv[c] = cd.v;
+    g.plane[c] = cd.coef_off / 2;
+    g.bw[c] = cd.bw;
+  }
   if (sr.ns == 1) {
     const CompDesc& cd = d.comp[sr.comp[0]];
     g.mcus_x = ceil_div(cd.dw, 8);
     g.mcus_y = ceil_div(cd.dh, 8);
     g.bpm = 1;
-    g.blk_comp[0] = (int8_t)sr.comp[0];
-    g.blk_x[0] = g.blk_y[0] = 0;
-    g.blk_k[0] = 0;
+    g.comp = (uint32_t)sr.comp[0];
   } else {
     g.mcus_x = d.mcus_x;
     g.mcus_y = d.mcus_y;
     int b = 0;
-    for (int k = 0; k < sr.ns; ++k) {
-      const CompDesc& cd = d.comp[sr.comp[k]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // constant indices into sr (no private array indexed at run time)
+      if (k >= sr.ns) break;
+      const int ci = sr.comp[k];
+      const CompDesc& cd = d.comp[ci];
       for (int y = 0; y < cd.v; ++y)
         for (int x = 0; x < cd.h; ++x) {
-          g.blk_comp[b] = (int8_t)sr.comp[k];
-          g.blk_x[b] = (int8_t)x;
-          g.blk_y[b] = (int8_t)y;
-          g.blk_k[b] = (int8_t)k;
+          g.comp |= (uint32_t)ci << (2 * b);
+          g.bx |= (uint32_t)x << (2 * b);
+          g.by |= (uint32_t)y << (2 * b);
+          g.kk |= (uint32_t)k << (2 * b);
           ++b;
         }
     }
@@ -520,18 +575,17 @@ DHD ScanGeom scan_geom(const ImgDesc& d, const ScanRec& sr) {
   return g;
 }
 
-DHD void scan_block_pos(const ImgDesc& d, const ScanRec& sr, const ScanGeom& g, int64_t m, int blk, int* c, int* bx,
-                        int* by) {
+// Coefficient block (int16 pointer) of block `blk` of MCU m, and its component.
+DHD int16_t* scan_block(int16_t* coef, const ScanRec& sr, const ScanGeom& g, int64_t m, int blk, int* c) {
   const int my = (int)(m / g.mcus_x), mx = (int)(m - (int64_t)my * g.mcus_x);
-  *c = g.blk_comp[blk];
-  if (sr.ns == 1) {
-    *bx = mx;
-    *by = my;
-  } else {
-    const CompDesc& cd = d.comp[*c];
-    *bx = mx * cd.h + g.blk_x[blk];
-    *by = my * cd.v + g.blk_y[blk];
+  const int cc = sg_field(g.comp, blk);
+  *c = cc;
+  int bx = mx, by = my;
+  if (sr.ns != 1) {
+    bx = mx * sel3(g.ch, cc) + sg_field(g.bx, blk);
+    by = my * sel3(g.cv, cc) + sg_field(g.by, blk);
   }
+  return coef + sel3(g.plane, cc) + ((int64_t)by * sel3(g.bw, cc) + bx) * 64;
 }
 
 // AC refinement of one block (decode_mcu_AC_refine).  `blk` holds the block's
@@ -539,7 +593,7 @@ DHD void scan_block_pos(const ImgDesc& d, const ScanRec& sr, const ScanGeom& g, 
 // coefficients are returned as masks over natural positions (corr: magnitude + p1,
 // nzn: new coefficient, neg: its sign) and applied by the caller.
 DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, uint64_t nz, int32_t* eobrun,
-                         uint64_t* corr_out, uint64_t* new_out, uint64_t* neg_out) {
+                         uint64_t* corr_out, uint64_t* new_out, uint64_t* neg_out, const uint8_t* nat) {
   uint64_t corr = 0, nzn = 0, neg = 0;
   int k = sr.ss;
   const int se = sr.se;
@@ -557,7 +611,7 @@ DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, ui
         break;
       }
       do {
-        const int pos = kNaturalOrder[k];
+        const int pos = nat[k];
         if ((nz >> pos) & 1u) {
           if (rb_bits(r, 1)) corr |= 1ull << pos;
         } else {
@@ -566,7 +620,7 @@ DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, ui
         k++;
       } while (k <= se);
       if (s) {
-        const int pos = kNaturalOrder[k];
+        const int pos = nat[k];
         nzn |= 1ull << pos;
         if (negative) neg |= 1ull << pos;
         else neg &= ~(1ull << pos);
@@ -575,7 +629,7 @@ DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, ui
   }
   if (*eobrun > 0) {
     for (; k <= se; k++) {
-      const int pos = kNaturalOrder[k];
+      const int pos = nat[k];
       if ((nz >> pos) & 1u)
         if (rb_bits(r, 1)) corr |= 1ull << pos;
     }
@@ -603,46 +657,82 @@ struct PlainCoefIO {
   }
 };
 
+// The scan's DC predictors, one per scan component (constant indices only).
+struct DcPred {
+  int32_t v0, v1, v2, v3;
+  DHD int32_t add(int k, int32_t s) {  // last_dc_val[ci] += s, returned (unsigned wrap as libjpeg-turbo)
+    const int32_t cur = k == 0 ? v0 : (k == 1 ? v1 : (k == 2 ? v2 : v3));
+    const int32_t r = (int32_t)((uint32_t)cur + (uint32_t)s);
+    if (k == 0) v0 = r;
+    else if (k == 1) v1 = r;
+    else if (k == 2) v2 = r;
+    else v3 = r;
+    return r;
+  }
+};
+
+// Non-zero mask of a block's coefficients (natural order).
+DHD uint64_t block_nz(const int16_t* b) {
+  uint64_t nz = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint4* b4 = (const uint4*)b;  // blocks are 128-byte aligned
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint4 v = b4[q];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      nz |= (uint64_t)((w[j] & 0xFFFFu) != 0) << (8 * q + 2 * j);
+      nz |= (uint64_t)((w[j] >> 16) != 0) << (8 * q + 2 * j + 1);
+    }
+  }
+#else
+  for (int i = 0; i < 64; ++i) nz |= (uint64_t)(b[i] != 0) << i;
+#endif
+  return nz;
+}
+
+// `nat`: jpeg_natural_order with its 16 safety entries (kNaturalOrder; the device
+// passes an LDS copy); `ring` / `bend`: the device's byte staging (see RawBits).
 DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const ScanRec& sr, const ScanTables& tb,
-                          int16_t* coef, int16_t* scratch64) {
+                          int16_t* coef, const uint8_t* nat, uint8_t* ring = nullptr, const uint8_t* bend = nullptr) {
   RawBits r;
-  rb_init(r, p, len, sr.data_off);
+  rb_init(r, p, len, sr.data_off, ring, bend);
   const ScanGeom g = scan_geom(d, sr);
   const int64_t nmcu = (int64_t)g.mcus_x * g.mcus_y;
   const int ri = sr.restart_interval;
   int rtg = ri, next_rst = 0;
-  int32_t last_dc[4] = {0, 0, 0, 0};
+  DcPred last_dc{0, 0, 0, 0};
   int32_t eobrun = 0;
   const bool prog = d.progressive != 0;
   const int al = sr.al;
+  const ProgTable* const ac0 = tb.ac[0];
   for (int64_t m = 0; m < nmcu; ++m) {
     if (ri) {
       if (rtg == 0) {
         rb_restart(r, &next_rst);
-        last_dc[0] = last_dc[1] = last_dc[2] = last_dc[3] = 0;
+        last_dc = DcPred{0, 0, 0, 0};
         eobrun = 0;
         rtg = ri;
       }
     }
     if (!r.insufficient) {
       for (int blk = 0; blk < g.bpm; ++blk) {
-        int c, bx, by;
-        scan_block_pos(d, sr, g, m, blk, &c, &bx, &by);
-        int16_t* b = coef_block(coef, d, c, bx, by);
-        const int kk = g.blk_k[blk];
+        int c;
+        int16_t* b = scan_block(coef, sr, g, m, blk, &c);
+        const int kk = sg_field(g.kk, blk);
         if (!prog) {  // jdhuff decode_mcu (sequential scan of a multi-scan file)
-          int s = rb_huff(r, tb.dc[kk]);
+          int s = rb_huff(r, sel4(tb.dc, kk));
           if (s) s = huff_extend((int)rb_bits(r, s), s);
-          const int32_t dcv = (int32_t)((uint32_t)last_dc[kk] + (uint32_t)s);
-          last_dc[kk] = dcv;
-          b[0] = (int16_t)dcv;
+          b[0] = (int16_t)last_dc.add(kk, s);
+          const ProgTable* act = sel4(tb.ac, kk);
           for (int k = 1; k < 64; k++) {
-            const int sym = rb_huff(r, tb.ac[kk]);
+            const int sym = rb_huff(r, act);
             const int rr = sym >> 4, ss = sym & 15;
             if (ss) {
               k += rr;
               const int v = huff_extend((int)rb_bits(r, ss), ss);
-              b[kNaturalOrder[k]] = (int16_t)v;
+              b[nat[k]] = (int16_t)v;
             } else {
               if (rr != 15) break;
               k += 15;
@@ -650,11 +740,9 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
           }
         } else if (sr.ss == 0) {
           if (sr.ah == 0) {  // decode_mcu_DC_first
-            int s = rb_huff(r, tb.dc[kk]);
+            int s = rb_huff(r, sel4(tb.dc, kk));
             if (s) s = huff_extend((int)rb_bits(r, s), s);
-            const int32_t dcv = (int32_t)((uint32_t)last_dc[kk] + (uint32_t)s);
-            last_dc[kk] = dcv;
-            b[0] = (int16_t)((uint32_t)dcv << al);
+            b[0] = (int16_t)((uint32_t)last_dc.add(kk, s) << al);
           } else {  // decode_mcu_DC_refine
             if (rb_bits(r, 1)) coef_or16(b, 1 << al);
           }
@@ -663,12 +751,12 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
             eobrun--;
           } else {
             for (int k = sr.ss; k <= sr.se; k++) {
-              const int sym = rb_huff(r, tb.ac[0]);
+              const int sym = rb_huff(r, ac0);
               const int rr = sym >> 4, ss = sym & 15;
               if (ss) {
                 k += rr;
                 const int v = huff_extend((int)rb_bits(r, ss), ss);
-                b[kNaturalOrder[k]] = (int16_t)((uint32_t)v << al);
+                b[nat[k]] = (int16_t)((uint32_t)v << al);
               } else if (rr == 15) {
                 k += 15;
               } else {
@@ -680,14 +768,12 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
             }
           }
         } else {  // decode_mcu_AC_refine
-          for (int i = 0; i < 64; ++i) scratch64[i] = b[i];
-          uint64_t nz = 0;
-          for (int i = 0; i < 64; ++i) nz |= (uint64_t)(scratch64[i] != 0) << i;
+          const uint64_t nz = block_nz(b);
           uint64_t corr, nzn, neg;
-          ac_refine_block(r, tb.ac[0], sr, nz, &eobrun, &corr, &nzn, &neg);
+          ac_refine_block(r, ac0, sr, nz, &eobrun, &corr, &nzn, &neg, nat);
           for (uint64_t mm = corr | nzn; mm; mm &= mm - 1) {
             const int pos = __builtin_ctzll(mm);
-            b[pos] = ac_refine_value(scratch64[pos], (corr >> pos) & 1u, (nzn >> pos) & 1u, (neg >> pos) & 1u, al);
+            b[pos] = ac_refine_value(b[pos], (corr >> pos) & 1u, (nzn >> pos) & 1u, (neg >> pos) & 1u, al);
           }
         }
       }

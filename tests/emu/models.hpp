@@ -191,7 +191,6 @@ inline int host_model_decode_multiscan(const uint8_t* p, int64_t len, ImgDesc& d
   if (prog_walk(p, len, &d, scans.data(), find) != DINO_IMG_OK) return d.status;
   std::vector<int16_t> coef(d.coef_bytes / 2, 0);
   std::vector<ProgTable> tabs(8);
-  int16_t scratch[64];
   for (int i = 0; i < d.n_scans; ++i) {
     const ScanRec& sr = scans[i];
     ScanTables tb;
@@ -206,7 +205,7 @@ inline int host_model_decode_multiscan(const uint8_t* p, int64_t len, ImgDesc& d
         tb.ac[k] = &tabs[4 + k];
       }
     }
-    prog_decode_scan(p, len, d, sr, tb, coef.data(), scratch);
+    prog_decode_scan(p, len, d, sr, tb, coef.data(), kNaturalOrder);
   }
   if (stats) {
     stats[0] = d.n_scans;
