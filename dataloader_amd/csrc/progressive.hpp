@@ -588,17 +588,38 @@ DHD int16_t* scan_block(int16_t* coef, const ScanRec& sr, const ScanGeom& g, int
   return coef + sel3(g.plane, cc) + ((int64_t)by * sel3(g.bw, cc) + bx) * 64;
 }
 
-// AC refinement of one block (decode_mcu_AC_refine).  `blk` holds the block's
-// coefficients as loaded at the start of the scan's pass over it; corrections and new
-// coefficients are returned as masks over natural positions (corr: magnitude + p1,
-// nzn: new coefficient, neg: its sign) and applied by the caller.
-DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, uint64_t nz, int32_t* eobrun,
-                         uint64_t* corr_out, uint64_t* new_out, uint64_t* neg_out, const uint8_t* nat) {
+// AC refinement of one block (decode_mcu_AC_refine), on masks in zigzag order.
+// nzz: the block's coefficients that were non-zero before the scan (bit k = zigzag
+// index k).  Returned (also zigzag): corr = correction bits read as 1, nzn = new
+// coefficients, neg = their sign.  libjpeg walks k one position at a time; here a
+// symbol's run and the correction bits it passes are found with bit operations and
+// the correction bits are read together (the bits and their order are the same).
+DHD int64_t low_bits(int n) { return n >= 64 ? -1ll : (int64_t)((1ull << n) - 1ull); }
+
+// Read one correction bit per set bit of c (increasing k) into corr.
+DHD void refine_corrections(RawBits& r, uint64_t c, uint64_t* corr) {
+  int n = __builtin_popcountll(c);
+  while (n > 0) {
+    const int take = n > 16 ? 16 : n;
+    uint32_t bits = rb_bits(r, take) << (32 - take);  // MSB first, in increasing k
+    for (int j = 0; j < take; ++j) {
+      const uint64_t lowest = c & (~c + 1ull);
+      if (bits & 0x80000000u) *corr |= lowest;
+      bits <<= 1;
+      c &= c - 1ull;
+    }
+    n -= take;
+  }
+}
+
+DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, uint64_t nzz, int32_t* eobrun,
+                         uint64_t* corr_out, uint64_t* new_out, uint64_t* neg_out) {
   uint64_t corr = 0, nzn = 0, neg = 0;
   int k = sr.ss;
   const int se = sr.se;
+  const uint64_t band = (uint64_t)low_bits(se + 1) & ~(uint64_t)low_bits(sr.ss);
   if (*eobrun == 0) {
-    for (; k <= se; k++) {
+    while (k <= se) {
       const int sym = rb_huff(r, tbl);
       int rr = sym >> 4, s = sym & 15;
       bool negative = false;
@@ -610,29 +631,24 @@ DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, ui
         if (rr) *eobrun += (int32_t)rb_bits(r, rr);
         break;
       }
-      do {
-        const int pos = nat[k];
-        if ((nz >> pos) & 1u) {
-          if (rb_bits(r, 1)) corr |= 1ull << pos;
-        } else {
-          if (--rr < 0) break;
-        }
-        k++;
-      } while (k <= se);
-      if (s) {
-        const int pos = nat[k];
-        nzn |= 1ull << pos;
-        if (negative) neg |= 1ull << pos;
-        else neg &= ~(1ull << pos);
+      // the (rr+1)-th not-yet-non-zero position at or after k (se + 1 when there is none)
+      uint64_t z = ~nzz & band & ~(uint64_t)low_bits(k);
+      for (int j = 0; j < rr && z; ++j) z &= z - 1ull;
+      const int stop = z ? __builtin_ctzll(z) : se + 1;
+      // correction bits of the non-zero coefficients passed on the way
+      refine_corrections(r, nzz & band & (uint64_t)low_bits(stop) & ~(uint64_t)low_bits(k), &corr);
+      k = stop;
+      if (s) {  // the new coefficient (k may be se + 1 on a corrupt stream: libjpeg's safety entries)
+        const uint64_t bit = k < 64 ? 1ull << k : 1ull << 63;
+        nzn |= bit;
+        if (negative) neg |= bit;
+        else neg &= ~bit;
       }
+      ++k;
     }
   }
   if (*eobrun > 0) {
-    for (; k <= se; k++) {
-      const int pos = nat[k];
-      if ((nz >> pos) & 1u)
-        if (rb_bits(r, 1)) corr |= 1ull << pos;
-    }
+    if (k <= se) refine_corrections(r, nzz & band & ~(uint64_t)low_bits(k), &corr);
     (*eobrun)--;
   }
   *corr_out = corr;
@@ -671,25 +687,30 @@ struct DcPred {
   }
 };
 
-// Non-zero mask of a block's coefficients (natural order).
-DHD uint64_t block_nz(const int16_t* b) {
-  uint64_t nz = 0;
+// Non-zero mask of a block's coefficients in zigzag order (bit k = coefficient
+// natural_order[k]): the refinement works on zigzag masks.
+DHD uint64_t block_nz_zz(const int16_t* b) {
+  uint64_t nzz = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint4* b4 = (const uint4*)b;  // blocks are 128-byte aligned
+  uint32_t w[32];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const uint4 v = b4[q];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    w[4 * q] = v.x;
+    w[4 * q + 1] = v.y;
+    w[4 * q + 2] = v.z;
+    w[4 * q + 3] = v.w;
+  }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      nz |= (uint64_t)((w[j] & 0xFFFFu) != 0) << (8 * q + 2 * j);
-      nz |= (uint64_t)((w[j] >> 16) != 0) << (8 * q + 2 * j + 1);
-    }
+  for (int k = 0; k < 64; ++k) {  // constant indices: registers only
+    const int pos = kNaturalOrder[k];
+    nzz |= (uint64_t)(((w[pos >> 1] >> (16 * (pos & 1))) & 0xFFFFu) != 0) << k;
   }
 #else
-  for (int i = 0; i < 64; ++i) nz |= (uint64_t)(b[i] != 0) << i;
+  for (int k = 0; k < 64; ++k) nzz |= (uint64_t)(b[kNaturalOrder[k]] != 0) << k;
 #endif
-  return nz;
+  return nzz;
 }
 
 // `nat`: jpeg_natural_order with its 16 safety entries (kNaturalOrder; the device
@@ -768,12 +789,13 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
             }
           }
         } else {  // decode_mcu_AC_refine
-          const uint64_t nz = block_nz(b);
+          const uint64_t nzz = block_nz_zz(b);
           uint64_t corr, nzn, neg;
-          ac_refine_block(r, ac0, sr, nz, &eobrun, &corr, &nzn, &neg, nat);
+          ac_refine_block(r, ac0, sr, nzz, &eobrun, &corr, &nzn, &neg);
           for (uint64_t mm = corr | nzn; mm; mm &= mm - 1) {
-            const int pos = __builtin_ctzll(mm);
-            b[pos] = ac_refine_value(b[pos], (corr >> pos) & 1u, (nzn >> pos) & 1u, (neg >> pos) & 1u, al);
+            const int k = __builtin_ctzll(mm);
+            const int pos = nat[k];
+            b[pos] = ac_refine_value(b[pos], (corr >> k) & 1u, (nzn >> k) & 1u, (neg >> k) & 1u, al);
           }
         }
       }
