@@ -399,6 +399,14 @@ int dino_debug_huff_phases(uint64_t* host_out, int64_t n_items) {
 }
 #endif
 
+#ifdef DINO_PROG_PHASES
+// Instrumented builds only: per-scan timestamps of k_prog ([64 images][64 scans][3]).
+int dino_debug_prog_phases(uint64_t* host_out) {
+  hipError_t e = copy_prog_phases(host_out);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_debug_prog_phases");
+}
+#endif
+
 int dino_bf16_to_fp8(const uint16_t* d_in, uint8_t* d_out, int64_t n, void* stream) {
   if ((!d_in || !d_out) && n > 0) return fail(DINO_EINVAL, "dino_bf16_to_fp8: null argument%s%lld");
   hipError_t e = launch_bf16_to_fp8(d_in, d_out, n, (hipStream_t)stream);

@@ -925,6 +925,17 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
 // ---------------------------------------------------------------------------
 constexpr int kProgThreads = 64;
 constexpr int kProgPool = 16;
+#ifdef DINO_PROG_PHASES
+// per image (first kProgPhaseImgs of the batch) and scan: start, end (wall_clock64) and
+// the scan's level / band / approximation (instrumented builds only)
+constexpr int kProgPhaseImgs = 64;
+__device__ uint64_t g_prog_phase[kProgPhaseImgs][kProgThreads][3];
+hipError_t copy_prog_phases(uint64_t* host) {
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prog_phase), sizeof(g_prog_phase));
+}
+#endif
 
 // Wave-cooperative search for the end of a scan's entropy data (see HostMarkerFinder):
 // each lane classifies 16 bytes per step, the first lane with a marker wins.
@@ -958,6 +969,7 @@ struct ProgLds {
   ProgTable pool[kProgPool];
   uint8_t nat[80];                     // jpeg_natural_order (+ safety entries), read per coefficient
   __attribute__((aligned(16))) uint8_t ring[kProgThreads][64];  // each lane's staged raw bytes (RawBits)
+  __attribute__((aligned(16))) int16_t blk[kProgThreads][64];    // each lane's AC-refinement block
   int32_t slot_off[kProgPool];         // BITS offset of the table in each pool slot
   int32_t slot_dc[kProgPool];
   int8_t tslot[kMaxScans][8];          // pool slot of each scan table (dc 0..3, ac 4..7), -1 none
@@ -1045,7 +1057,18 @@ __global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict
           tb.dc[k] = L.tslot[t][k] >= 0 ? &L.pool[L.tslot[t][k]] : &L.pool[0];
           tb.ac[k] = L.tslot[t][4 + k] >= 0 ? &L.pool[L.tslot[t][4 + k]] : &L.pool[0];
         }
-        prog_decode_scan(p, len, dl, sr, tb, coef, L.nat, L.ring[t], bytes + offsets[gridDim.x]);
+#ifdef DINO_PROG_PHASES
+        const uint64_t t0 = wall_clock64();
+#endif
+        prog_decode_scan(p, len, dl, sr, tb, coef, L.nat, L.ring[t], bytes + offsets[gridDim.x], L.blk[t]);
+#ifdef DINO_PROG_PHASES
+        if (img < kProgPhaseImgs) {
+          g_prog_phase[img][t][0] = t0;
+          g_prog_phase[img][t][1] = wall_clock64();
+          g_prog_phase[img][t][2] = (uint64_t)sr.level | ((uint64_t)sr.ss << 8) | ((uint64_t)sr.se << 16) |
+                                    ((uint64_t)sr.ah << 24) | ((uint64_t)sr.al << 28) | ((uint64_t)sr.ns << 32);
+        }
+#endif
         L.ready[t] = 0;
       }
       __syncthreads();  // (workgroup scope: this level's coefficient stores are visible to the next)

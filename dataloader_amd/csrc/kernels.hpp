@@ -122,6 +122,9 @@ hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0
 #ifdef DINO_HUFF_PHASES
 hipError_t copy_huff_phases(uint64_t* host, int64_t n_items);
 #endif
+#ifdef DINO_PROG_PHASES
+hipError_t copy_prog_phases(uint64_t* host);
+#endif
 hipError_t launch_bf16_to_fp8(const uint16_t* in, uint8_t* out, int64_t n, hipStream_t s);
 
 }  // namespace dino

@@ -429,8 +429,13 @@ DHD uint32_t rb_bits(RawBits& r, int n) {  // GET_BITS(n), 0 <= n <= 16
 }
 
 // HUFF_DECODE: one symbol (lookahead, else the bit-serial path incl. the l = 17 fake zero).
+inline long g_prog_host_symbols = 0;  // host model statistics (symbols decoded by rb_huff; never on the device)
+
 template <int LB>
 DHD int rb_huff(RawBits& r, const HuffTableT<LB>* t) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+  ++g_prog_host_symbols;
+#endif
   rb_fill(r);
   const uint32_t hi = rb_peek32(r);
   const uint32_t e = t->look[hi >> (32 - LB)];
@@ -715,8 +720,73 @@ DHD uint64_t block_nz_zz(const int16_t* b) {
 
 // `nat`: jpeg_natural_order with its 16 safety entries (kNaturalOrder; the device
 // passes an LDS copy); `ring` / `bend`: the device's byte staging (see RawBits).
+// AC refinement scan (single component: one block per MCU), device form: block m is
+// staged in the lane's LDS buffer `blkbuf` (64 int16) from registers loaded one
+// block ahead, corrections are applied there, and only the changed coefficients are
+// stored (other scans of the level may be writing other coefficients of the block).
+DHD void prog_refine_scan_staged(RawBits& r, const ScanRec& sr, const ScanGeom& g, int64_t nmcu, const ProgTable* ac0,
+                                 int16_t* coef, const uint8_t* nat, int16_t* blkbuf) {
+  const int ri = sr.restart_interval, al = sr.al;
+  int rtg = ri, next_rst = 0;
+  int32_t eobrun = 0;
+  int c;
+  uint4 nxt[8];
+  {
+    const uint4* b4 = (const uint4*)scan_block(coef, sr, g, 0, 0, &c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
+  }
+  uint4* lb = (uint4*)blkbuf;
+  for (int64_t m = 0; m < nmcu; ++m) {
+    if (ri) {
+      if (rtg == 0) {
+        rb_restart(r, &next_rst);
+        eobrun = 0;
+        rtg = ri;
+      }
+    }
+    int16_t* b = scan_block(coef, sr, g, m, 0, &c);
+    // this block (loaded one block ago) -> LDS and its zigzag non-zero mask; the next one is loaded meanwhile
+    uint64_t nzz = 0;
+    {
+      uint32_t w[32];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        lb[q] = nxt[q];
+        w[4 * q] = nxt[q].x;
+        w[4 * q + 1] = nxt[q].y;
+        w[4 * q + 2] = nxt[q].z;
+        w[4 * q + 3] = nxt[q].w;
+      }
+#pragma unroll
+      for (int k = 0; k < 64; ++k) {
+        const int pos = kNaturalOrder[k];
+        nzz |= (uint64_t)(((w[pos >> 1] >> (16 * (pos & 1))) & 0xFFFFu) != 0) << k;
+      }
+    }
+    if (m + 1 < nmcu) {
+      const uint4* b4 = (const uint4*)scan_block(coef, sr, g, m + 1, 0, &c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
+    }
+    if (!r.insufficient) {
+      uint64_t corr, nzn, neg;
+      ac_refine_block(r, ac0, sr, nzz, &eobrun, &corr, &nzn, &neg);
+      for (uint64_t mm = corr | nzn; mm; mm &= mm - 1) {
+        const int k = __builtin_ctzll(mm);
+        const int pos = nat[k];
+        const int16_t v = ac_refine_value(blkbuf[pos], (corr >> k) & 1u, (nzn >> k) & 1u, (neg >> k) & 1u, al);
+        blkbuf[pos] = v;
+        b[pos] = v;
+      }
+    }
+    if (ri) rtg--;
+  }
+}
+
 DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const ScanRec& sr, const ScanTables& tb,
-                          int16_t* coef, const uint8_t* nat, uint8_t* ring = nullptr, const uint8_t* bend = nullptr) {
+                          int16_t* coef, const uint8_t* nat, uint8_t* ring = nullptr, const uint8_t* bend = nullptr,
+                          int16_t* blkbuf = nullptr) {
   RawBits r;
   rb_init(r, p, len, sr.data_off, ring, bend);
   const ScanGeom g = scan_geom(d, sr);
@@ -728,6 +798,10 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
   const bool prog = d.progressive != 0;
   const int al = sr.al;
   const ProgTable* const ac0 = tb.ac[0];
+  if (blkbuf && prog && sr.ss > 0 && sr.ah > 0) {  // AC refinement, device
+    prog_refine_scan_staged(r, sr, g, nmcu, ac0, coef, nat, blkbuf);
+    return;
+  }
   for (int64_t m = 0; m < nmcu; ++m) {
     if (ri) {
       if (rtg == 0) {

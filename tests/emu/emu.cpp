@@ -113,6 +113,32 @@ int emu_decode_stages(const uint8_t* p, int64_t len, int mode, int lanes, uint8_
   return r;
 }
 
+// Per-scan symbol counts of a multi-scan image (analysis aid): out[i] = symbols of scan
+// i, levels[i] = its dependency level; returns the number of scans (< 0: status).
+int emu_prog_scan_stats(const uint8_t* p, int64_t len, int64_t* out, int32_t* levels, int32_t cap) {
+  ImgDesc d;
+  if (parse_jpeg(p, len, 1 << 16, &d) != DINO_IMG_OK || d.kind != 1) return -1;
+  std::vector<ScanRec> scans(kMaxScans);
+  HostMarkerFinder find;
+  if (prog_walk(p, len, &d, scans.data(), find) != DINO_IMG_OK) return d.status;
+  std::vector<int16_t> coef(d.coef_bytes / 2, 0);
+  std::vector<ProgTable> tabs(8);
+  for (int i = 0; i < d.n_scans && i < cap; ++i) {
+    const ScanRec& sr = scans[i];
+    ScanTables tb;
+    for (int k = 0; k < 4; ++k) {
+      tb.dc[k] = tb.ac[k] = &tabs[0];
+      if (sr.dc_tab[k] >= 0 && prog_build_table(p + sr.dc_tab[k], true, &tabs[k])) tb.dc[k] = &tabs[k];
+      if (sr.ac_tab[k] >= 0 && prog_build_table(p + sr.ac_tab[k], false, &tabs[4 + k])) tb.ac[k] = &tabs[4 + k];
+    }
+    const long before = g_prog_host_symbols;
+    prog_decode_scan(p, len, d, sr, tb, coef.data(), kNaturalOrder);
+    out[i] = g_prog_host_symbols - before;
+    levels[i] = sr.level;
+  }
+  return d.n_scans;
+}
+
 // ---- resize + augment ---------------------------------------------------------
 // Full per-view augment: src RGB (HWC), params, -> out (3*S*S) of dtype out_dtype.
 int emu_augment_view(const uint8_t* rgb, int W, int H, const dino_view_params* vp, const float* mean,
