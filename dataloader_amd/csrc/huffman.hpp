@@ -205,8 +205,8 @@ DHD void bc_skip(BitCursor& c, int n) {
 // incl. the l = 17 "fake zero").  The maxcode values are read up front and the
 // length found by comparisons, so the lane waits on LDS once, not per bit.
 // p17: the next 17 bits of the stream (code of up to 16 bits + sentinel).
-template <int LB>
-DHD void huff_slow_bits(uint32_t p17, const HuffTableT<LB>* t, int* sym, int* len) {
+template <int LB, typename TabPtr>
+DHD void huff_slow_bits(uint32_t p17, TabPtr t, int* sym, int* len) {
   int32_t mc[17 - LB], vo[17 - LB];
 #pragma unroll
   for (int k = 0; k < 17 - LB; ++k) {
@@ -233,7 +233,7 @@ DHD void huff_slow_bits(uint32_t p17, const HuffTableT<LB>* t, int* sym, int* le
 
 template <int LB>
 DHD void huff_slow(const BitCursor& c, const HuffTableT<LB>* t, int* sym, int* len) {
-  huff_slow_bits(bc_peek(c, 17), t, sym, len);
+  huff_slow_bits<LB>(bc_peek(c, 17), t, sym, len);
 }
 
 // Decoder state between steps.

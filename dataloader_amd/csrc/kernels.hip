@@ -1053,14 +1053,16 @@ __global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict
       if (t < n && L.ready[t]) {
         const ScanRec sr = L.scans[t];
         ScanTables tb;
+        LdsTable pool = (LdsTable)&L.pool[0];
         for (int k = 0; k < 4; ++k) {
-          tb.dc[k] = L.tslot[t][k] >= 0 ? &L.pool[L.tslot[t][k]] : &L.pool[0];
-          tb.ac[k] = L.tslot[t][4 + k] >= 0 ? &L.pool[L.tslot[t][4 + k]] : &L.pool[0];
+          tb.dc[k] = pool + (L.tslot[t][k] >= 0 ? L.tslot[t][k] : 0);
+          tb.ac[k] = pool + (L.tslot[t][4 + k] >= 0 ? L.tslot[t][4 + k] : 0);
         }
 #ifdef DINO_PROG_PHASES
         const uint64_t t0 = wall_clock64();
 #endif
-        prog_decode_scan(p, len, dl, sr, tb, coef, L.nat, L.ring[t], bytes + offsets[gridDim.x], L.blk[t]);
+        prog_decode_scan(p, len, dl, sr, tb, coef, (const DINO_LDS uint8_t*)L.nat, (DINO_LDS uint8_t*)L.ring[t],
+                         bytes + offsets[gridDim.x], (DINO_LDS int16_t*)L.blk[t]);
 #ifdef DINO_PROG_PHASES
         if (img < kProgPhaseImgs) {
           g_prog_phase[img][t][0] = t0;

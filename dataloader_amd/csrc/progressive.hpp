@@ -34,6 +34,26 @@ constexpr int kMaxScans = DINO_MAX_SCANS;
 constexpr int kProgLookBits = 9;
 using ProgTable = HuffTableT<kProgLookBits>;
 
+// LDS data of k_prog (tables, byte ring, refinement block, natural order) is reached
+// through address-space-3 pointers on the device, so its accesses are ds_* (LDS
+// counter only); through generic pointers they would be flat accesses, which also
+// wait on the lane's outstanding global loads and stores.  Empty on the host.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DINO_LDS __attribute__((address_space(3)))
+#define DINO_GLOBAL __attribute__((address_space(1)))
+#else
+#define DINO_LDS
+#define DINO_GLOBAL
+#endif
+using LdsTable = const DINO_LDS ProgTable*;
+// global coefficient / byte pointers for the device's loads and stores (global_* rather
+// than flat_*: a flat access counts against the LDS counter too, so every LDS wait
+// would also wait for the lane's outstanding global loads and stores)
+template <typename T>
+DHD DINO_GLOBAL T* gmem(T* p) { return (DINO_GLOBAL T*)p; }
+template <typename T>
+DHD const DINO_GLOBAL T* gmem(const T* p) { return (const DINO_GLOBAL T*)p; }
+
 // One scan of a multi-scan image (image-relative byte offsets).
 struct ScanRec {
   int32_t data_off;          // first entropy-coded byte
@@ -320,12 +340,12 @@ struct RawBits {
   int32_t real;      // real (not zero-fill) bits among them; < 0: bits were needed past a marker
   int32_t unread;    // marker code the reader stopped at (0: none)
   int32_t insufficient;
-  uint8_t* ring;     // device: 64 bytes of LDS (16-byte aligned); nullptr: read memory directly
+  DINO_LDS uint8_t* ring;  // device: 64 bytes of LDS (16-byte aligned); nullptr: read memory directly
   uintptr_t hi;      // device: end (absolute address) of the staged bytes
   uintptr_t bend;    // device: end of the readable buffer (the batch's packed bytes)
 };
 
-DHD void rb_init(RawBits& r, const uint8_t* p, int64_t len, int64_t pos, uint8_t* ring = nullptr,
+DHD void rb_init(RawBits& r, const uint8_t* p, int64_t len, int64_t pos, DINO_LDS uint8_t* ring = nullptr,
                  const uint8_t* bend = nullptr) {
   r.p = p;
   r.len = len;
@@ -344,14 +364,14 @@ DHD void rb_init(RawBits& r, const uint8_t* p, int64_t len, int64_t pos, uint8_t
 // from hi when a lies in the next 16 bytes) into the ring.
 DHD void rb_stage(RawBits& r, uintptr_t a) {
   const uintptr_t A = (a >= r.hi && a < r.hi + 16 && r.hi) ? r.hi : (a & ~(uintptr_t)15);
-  uint4* dst0 = (uint4*)(r.ring + (A & 63));
-  uint4* dst1 = (uint4*)(r.ring + ((A + 16) & 63));
+  DINO_LDS uint4* dst0 = (DINO_LDS uint4*)(r.ring + (A & 63));
+  DINO_LDS uint4* dst1 = (DINO_LDS uint4*)(r.ring + ((A + 16) & 63));
   if (A + 32 <= r.bend) {
-    const uint4 c0 = *(const uint4*)A, c1 = *(const uint4*)(A + 16);
+    const uint4 c0 = *gmem((const uint4*)A), c1 = *gmem((const uint4*)(A + 16));
     *dst0 = c0;
     *dst1 = c1;
   } else {  // the end of the batch buffer: bytewise, zeros past it
-    for (int j = 0; j < 32; ++j) r.ring[(A + j) & 63] = A + j < r.bend ? *(const uint8_t*)(A + j) : 0;
+    for (int j = 0; j < 32; ++j) r.ring[(A + j) & 63] = A + j < r.bend ? *gmem((const uint8_t*)(A + j)) : 0;
   }
   r.hi = A + 32;
 }
@@ -431,8 +451,9 @@ DHD uint32_t rb_bits(RawBits& r, int n) {  // GET_BITS(n), 0 <= n <= 16
 // HUFF_DECODE: one symbol (lookahead, else the bit-serial path incl. the l = 17 fake zero).
 inline long g_prog_host_symbols = 0;  // host model statistics (symbols decoded by rb_huff; never on the device)
 
-template <int LB>
-DHD int rb_huff(RawBits& r, const HuffTableT<LB>* t) {
+template <typename TabPtr>
+DHD int rb_huff(RawBits& r, TabPtr t) {
+  constexpr int LB = kProgLookBits;
 #if !defined(__HIP_DEVICE_COMPILE__)
   ++g_prog_host_symbols;
 #endif
@@ -444,7 +465,7 @@ DHD int rb_huff(RawBits& r, const HuffTableT<LB>* t) {
     sym = (int)(e >> 5);
     len = (int)(e & 31u);
   } else {
-    huff_slow_bits(hi >> 15, t, &sym, &len);
+    huff_slow_bits<LB>(hi >> 15, t, &sym, &len);
   }
   rb_skip(r, len);
   return sym;
@@ -509,22 +530,23 @@ DHD int16_t* coef_block(int16_t* coef, const ImgDesc& d, int c, int bx, int by) 
 
 // OR v into the int16 at p.  Other lanes may write the other half of its 32-bit word
 // at the same time (scans of one level): the device uses a word atomic.
-DHD void coef_or16(int16_t* p, int v) {
+template <typename P>
+DHD void coef_or16(P p, int v) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t* w = (uint32_t*)((uintptr_t)p & ~(uintptr_t)3);
+  DINO_GLOBAL uint32_t* w = gmem((uint32_t*)((uintptr_t)p & ~(uintptr_t)3));
   const uint32_t sh = ((uintptr_t)p & 2) ? 16u : 0u;
-  atomicOr(w, ((uint32_t)(uint16_t)v) << sh);
+  __hip_atomic_fetch_or(w, ((uint32_t)(uint16_t)v) << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
   *p = (int16_t)(*p | v);
 #endif
 }
 
 struct ScanTables {
-  const ProgTable* dc[4];
-  const ProgTable* ac[4];
+  LdsTable dc[4];
+  LdsTable ac[4];
 };
 // Table of scan component k (constant indices only; see ScanGeom).
-DHD const ProgTable* sel4(const ProgTable* const* t, int k) { return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3])); }
+DHD LdsTable sel4(const LdsTable* t, int k) { return k == 0 ? t[0] : (k == 1 ? t[1] : (k == 2 ? t[2] : t[3])); }
 
 // Geometry of the scan's MCUs (jdinput.c per_scan_setup).  Per block of the MCU a
 // 2-bit field each of component, x and y offset and scan component index (bits
@@ -617,7 +639,7 @@ DHD void refine_corrections(RawBits& r, uint64_t c, uint64_t* corr) {
   }
 }
 
-DHD void ac_refine_block(RawBits& r, const ProgTable* tbl, const ScanRec& sr, uint64_t nzz, int32_t* eobrun,
+DHD void ac_refine_block(RawBits& r, LdsTable tbl, const ScanRec& sr, uint64_t nzz, int32_t* eobrun,
                          uint64_t* corr_out, uint64_t* new_out, uint64_t* neg_out) {
   uint64_t corr = 0, nzn = 0, neg = 0;
   int k = sr.ss;
@@ -694,10 +716,11 @@ struct DcPred {
 
 // Non-zero mask of a block's coefficients in zigzag order (bit k = coefficient
 // natural_order[k]): the refinement works on zigzag masks.
-DHD uint64_t block_nz_zz(const int16_t* b) {
+template <typename P>
+DHD uint64_t block_nz_zz(P b) {
   uint64_t nzz = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
-  const uint4* b4 = (const uint4*)b;  // blocks are 128-byte aligned
+  const DINO_GLOBAL uint4* b4 = gmem((const uint4*)b);  // blocks are 128-byte aligned
   uint32_t w[32];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
@@ -724,19 +747,19 @@ DHD uint64_t block_nz_zz(const int16_t* b) {
 // staged in the lane's LDS buffer `blkbuf` (64 int16) from registers loaded one
 // block ahead, corrections are applied there, and only the changed coefficients are
 // stored (other scans of the level may be writing other coefficients of the block).
-DHD void prog_refine_scan_staged(RawBits& r, const ScanRec& sr, const ScanGeom& g, int64_t nmcu, const ProgTable* ac0,
-                                 int16_t* coef, const uint8_t* nat, int16_t* blkbuf) {
+DHD void prog_refine_scan_staged(RawBits& r, const ScanRec& sr, const ScanGeom& g, int64_t nmcu, LdsTable ac0,
+                                 int16_t* coef, const DINO_LDS uint8_t* nat, DINO_LDS int16_t* blkbuf) {
   const int ri = sr.restart_interval, al = sr.al;
   int rtg = ri, next_rst = 0;
   int32_t eobrun = 0;
   int c;
   uint4 nxt[8];
   {
-    const uint4* b4 = (const uint4*)scan_block(coef, sr, g, 0, 0, &c);
+    const DINO_GLOBAL uint4* b4 = gmem((const uint4*)scan_block(coef, sr, g, 0, 0, &c));
 #pragma unroll
     for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
   }
-  uint4* lb = (uint4*)blkbuf;
+  DINO_LDS uint4* lb = (DINO_LDS uint4*)blkbuf;
   for (int64_t m = 0; m < nmcu; ++m) {
     if (ri) {
       if (rtg == 0) {
@@ -745,7 +768,7 @@ DHD void prog_refine_scan_staged(RawBits& r, const ScanRec& sr, const ScanGeom& 
         rtg = ri;
       }
     }
-    int16_t* b = scan_block(coef, sr, g, m, 0, &c);
+    DINO_GLOBAL int16_t* b = gmem(scan_block(coef, sr, g, m, 0, &c));
     // this block (loaded one block ago) -> LDS and its zigzag non-zero mask; the next one is loaded meanwhile
     uint64_t nzz = 0;
     {
@@ -765,7 +788,7 @@ DHD void prog_refine_scan_staged(RawBits& r, const ScanRec& sr, const ScanGeom& 
       }
     }
     if (m + 1 < nmcu) {
-      const uint4* b4 = (const uint4*)scan_block(coef, sr, g, m + 1, 0, &c);
+      const DINO_GLOBAL uint4* b4 = gmem((const uint4*)scan_block(coef, sr, g, m + 1, 0, &c));
 #pragma unroll
       for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
     }
@@ -785,8 +808,8 @@ DHD void prog_refine_scan_staged(RawBits& r, const ScanRec& sr, const ScanGeom& 
 }
 
 DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const ScanRec& sr, const ScanTables& tb,
-                          int16_t* coef, const uint8_t* nat, uint8_t* ring = nullptr, const uint8_t* bend = nullptr,
-                          int16_t* blkbuf = nullptr) {
+                          int16_t* coef, const DINO_LDS uint8_t* nat, DINO_LDS uint8_t* ring = nullptr,
+                          const uint8_t* bend = nullptr, DINO_LDS int16_t* blkbuf = nullptr) {
   RawBits r;
   rb_init(r, p, len, sr.data_off, ring, bend);
   const ScanGeom g = scan_geom(d, sr);
@@ -797,7 +820,7 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
   int32_t eobrun = 0;
   const bool prog = d.progressive != 0;
   const int al = sr.al;
-  const ProgTable* const ac0 = tb.ac[0];
+  const LdsTable ac0 = tb.ac[0];
   if (blkbuf && prog && sr.ss > 0 && sr.ah > 0) {  // AC refinement, device
     prog_refine_scan_staged(r, sr, g, nmcu, ac0, coef, nat, blkbuf);
     return;
@@ -814,13 +837,13 @@ DHD void prog_decode_scan(const uint8_t* p, int64_t len, const ImgDesc& d, const
     if (!r.insufficient) {
       for (int blk = 0; blk < g.bpm; ++blk) {
         int c;
-        int16_t* b = scan_block(coef, sr, g, m, blk, &c);
+        DINO_GLOBAL int16_t* b = gmem(scan_block(coef, sr, g, m, blk, &c));
         const int kk = sg_field(g.kk, blk);
         if (!prog) {  // jdhuff decode_mcu (sequential scan of a multi-scan file)
           int s = rb_huff(r, sel4(tb.dc, kk));
           if (s) s = huff_extend((int)rb_bits(r, s), s);
           b[0] = (int16_t)last_dc.add(kk, s);
-          const ProgTable* act = sel4(tb.ac, kk);
+          const LdsTable act = sel4(tb.ac, kk);
           for (int k = 1; k < 64; k++) {
             const int sym = rb_huff(r, act);
             const int rr = sym >> 4, ss = sym & 15;

@@ -16,3 +16,5 @@ for f in ("0.02", "0.1"):
         if line.startswith("{"):
             d = json.loads(line); print(f, "k_prog ms/step", d["kernels_ms_per_step"].get("k_prog")); break
 PY
+timeout -k 10 200 python scripts/prog_phases.py > gpurun_out/${TAG}_phases.txt 2>&1 || true
+tail -16 gpurun_out/${TAG}_phases.txt

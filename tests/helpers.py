@@ -50,7 +50,8 @@ def build_emu() -> ctypes.CDLL:
     src = ROOT / "tests" / "emu" / "emu.cpp"
     deps = [src, ROOT / "tests" / "emu" / "models.hpp", *sorted((ROOT / "dataloader_amd" / "csrc").glob("*.hpp"))]
     if not EMU_SO.exists() or EMU_SO.stat().st_mtime < max(d.stat().st_mtime for d in deps):
-        cmd = (f"hipcc -O2 -ffp-contract=off -fPIC -shared -o {EMU_SO} {src}")
+        # host-only: the emulator runs the device functions on the CPU (no device pass)
+        cmd = (f"hipcc --cuda-host-only -O2 -ffp-contract=off -fPIC -shared -o {EMU_SO} {src}")
         if os.system(cmd) != 0:
             raise RuntimeError(f"emulator build failed: {cmd}")
     return ctypes.CDLL(str(EMU_SO))
