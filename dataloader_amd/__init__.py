@@ -4,12 +4,36 @@ Drop-in backend for the ``dino_loader`` backend abstraction (reference
 ``src/dino_loader/backends/protocol.py``): JPEG decode, random-resized crop x N,
 colour jitter, grayscale, gaussian blur, solarize, normalize (bf16/fp32/fp8) and
 iBOT masks as hand-written HIP kernels for gfx950.  See DESIGN.md.
+
+The public names are resolved on first access (PEP 562), so that a process that
+only needs the host hand-over (``fallback.pillow_container`` in the Pillow worker
+pool) does not import torch.
 """
 
-from .backend import MI355XBackend
-from .config import DINOAugConfig, DinoV2AugSpec, NormStats, PipelineConfig, ResolutionSource
-from .masking import MaskingGenerator
-from .params import VIEW_PARAMS_DTYPE
+from importlib import import_module
 
-__all__ = ["MI355XBackend", "DINOAugConfig", "DinoV2AugSpec", "NormStats", "PipelineConfig",
-           "ResolutionSource", "MaskingGenerator", "VIEW_PARAMS_DTYPE"]
+_EXPORTS = {
+    "MI355XBackend": ".backend",
+    "DINOAugConfig": ".config",
+    "DinoV2AugSpec": ".config",
+    "NormStats": ".config",
+    "PipelineConfig": ".config",
+    "ResolutionSource": ".config",
+    "MaskingGenerator": ".masking",
+    "VIEW_PARAMS_DTYPE": ".params",
+}
+
+__all__ = list(_EXPORTS)
+
+
+def __getattr__(name):
+    mod = _EXPORTS.get(name)
+    if mod is None:
+        raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+    value = getattr(import_module(mod, __name__), name)
+    globals()[name] = value
+    return value
+
+
+def __dir__():
+    return sorted(list(globals()) + __all__)

@@ -66,13 +66,64 @@ def probe(host_buf_ptr: int, offsets: np.ndarray, batch: int, max_image_dim: int
     return info, int(ws.value), int(aws.value)
 
 
-def hand_over(jpegs: list, status: np.ndarray) -> tuple[list, int]:
-    """Replace the images the GPU decoder does not implement by Pillow-decoded raw RGB
-    containers (zero bytes where Pillow raises).  Returns (new list, images handed over)."""
+def pillow_container(jpeg) -> bytes:
+    """One hand-over: the Pillow decode as a raw container, or b"" where Pillow raises."""
+    rgb = decode_with_pillow(jpeg)
+    return raw_container(rgb) if rgb is not None else b""
+
+
+def hand_over(jpegs: list, status: np.ndarray, mask: np.ndarray | None = None,
+              pool: "HostDecoder | None" = None) -> tuple[list, int]:
+    """Replace the images the GPU decoder does not implement (``status == IMG_UNSUPPORTED``,
+    or ``mask`` when given) by Pillow-decoded raw RGB containers (zero bytes where Pillow
+    raises), in ``pool``'s worker processes when given.  Returns (new list, images handed over)."""
+    idx = np.flatnonzero(status == IMG_UNSUPPORTED if mask is None else mask)
     out = list(jpegs)
-    n = 0
-    for i in np.flatnonzero(status == IMG_UNSUPPORTED):
-        rgb = decode_with_pillow(jpegs[i])
-        out[i] = raw_container(rgb) if rgb is not None else b""
-        n += 1
-    return out, n
+    if pool is not None and len(idx) > 1:
+        for i, f in zip(idx, [pool.submit(jpegs[i]) for i in idx]):
+            out[i] = f.result()
+    else:
+        for i in idx:
+            out[i] = pillow_container(jpegs[i])
+    return out, len(idx)
+
+
+def route_mask(info: np.ndarray, host_fallback: bool, multiscan_route: str, host_max: int) -> np.ndarray:
+    """Images of a probed batch to decode with Pillow on the host.
+
+    * ``DINO_IMG_UNSUPPORTED`` images, always (when ``host_fallback``);
+    * coefficient-buffer images (``info[:, 3] == 1``: progressive, multi-scan sequential,
+      damaged restart intervals), which ``k_prog`` decodes one image per workgroup with
+      every scan serial — about 100 ms of latency for a batch holding any — so that
+      a batch with a few of them would wait on the slowest: ``"host"`` sends them all to
+      Pillow, ``"device"`` none, ``"auto"`` all of them when the batch has at most
+      ``host_max`` (the host decodes ~6 ms per 640x480 image per worker, off the
+      critical path when prepared one batch ahead), else none."""
+    mask = (info[:, 0] == IMG_UNSUPPORTED) if host_fallback else np.zeros(len(info), bool)
+    ms = (info[:, 0] == 0) & (info[:, 3] == 1)
+    if multiscan_route == "host" or (multiscan_route == "auto" and 0 < ms.sum() <= host_max):
+        mask |= ms
+    return mask
+
+
+class HostDecoder:
+    """A pool of worker processes for the Pillow hand-over.  Pillow's decode of one JPEG
+    holds the GIL for most of its run (threads give no speed-up), so the workers are
+    processes, started with ``spawn`` (a fork of a process that has initialised HIP is not
+    safe) and only when the first image is submitted."""
+
+    def __init__(self, workers: int):
+        self.workers = max(1, int(workers))
+        self._pool = None
+
+    def submit(self, jpeg):
+        if self._pool is None:
+            import multiprocessing as mp
+            from concurrent.futures import ProcessPoolExecutor
+            self._pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"))
+        return self._pool.submit(pillow_container, bytes(jpeg))
+
+    def close(self) -> None:
+        if self._pool is not None:
+            self._pool.shutdown(wait=True, cancel_futures=True)
+            self._pool = None

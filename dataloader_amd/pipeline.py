@@ -24,6 +24,7 @@ have decoded but that came back zero-filled raises a ``RuntimeWarning``.
 
 from __future__ import annotations
 
+import os
 import warnings
 from collections import Counter, deque
 from typing import Any
@@ -64,6 +65,16 @@ class _Slot:
         self.batch_id = -1
 
 
+class _Prepared:
+    """A pulled, probed host batch whose host-routed images are decoding in the pool."""
+
+    def __init__(self, jpegs, host_buf: torch.Tensor, offsets: np.ndarray, futures: dict):
+        self.jpegs = jpegs
+        self.host_buf = host_buf
+        self.offsets = offsets
+        self.futures = futures
+
+
 class MI355XAugPipeline:
     """``depth`` > 1 keeps that many batches in flight: each slot owns a ctx and a
     HIP stream, consecutive batches alternate slots, so one batch's entropy
@@ -72,7 +83,9 @@ class MI355XAugPipeline:
     def __init__(self, source: Any, aug_cfg, batch_size: int, resolution_src=None, seed: int = 0,
                  out_dtype="bf16", device: int = 0, max_image_dim: int = 8192, workspace_bytes: int = 0,
                  engine: IngestEngine | None = None, depth: int = 1, norm=None,
-                 view_names: list[str] | None = None, host_fallback: bool = True):
+                 view_names: list[str] | None = None, host_fallback: bool = True,
+                 multiscan_route: str = "auto", host_workers: int | None = None,
+                 multiscan_host_max: int | None = None):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -84,6 +97,14 @@ class MI355XAugPipeline:
         self._batch_index = 0
         self._max_image_dim = int(max_image_dim)
         self._host_fallback = bool(host_fallback)
+        if multiscan_route not in ("auto", "device", "host"):
+            raise ValueError(f"multiscan_route must be 'auto', 'device' or 'host', not {multiscan_route!r}")
+        self._multiscan_route = multiscan_route
+        workers = int(host_workers) if host_workers else min(8, os.cpu_count() or 1)
+        self._host = fallback.HostDecoder(workers)
+        # "auto": the host takes a batch's coefficient-buffer images while its workers finish
+        # them in about the time k_prog needs for any number of them (~100 ms vs ~6 ms/image)
+        self._host_max = int(multiscan_host_max) if multiscan_host_max is not None else 8 * workers
         # per-image outcome of every batch handed over (status code -> images), images the
         # GPU decoder left to Pillow, and workspace regrowths
         self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0, "reserves": 0}
@@ -189,22 +210,42 @@ class MI355XAugPipeline:
         return sl.outputs
 
     # ------------------------------------------------------------------ screening
-    def _screen(self, sl: _Slot, jpegs, host_buf: torch.Tensor, offsets: np.ndarray, cfg):
-        """dino_probe the packed host batch; hand the flavours the GPU does not decode to
-        Pillow (re-packing the batch); grow the slot's workspaces.  Returns the (possibly
-        re-packed) host buffer and offsets."""
+    def _prepare(self, jpegs=None, host_buf: torch.Tensor | None = None,
+                 offsets: np.ndarray | None = None) -> "_Prepared":
+        """Pull a batch from the source (unless given), pack and ``dino_probe`` it, and start
+        the Pillow decodes of the images routed to the host (``fallback.route_mask``) in the
+        worker pool.  ``_enqueue_prepared`` waits for them and launches the batch."""
+        if jpegs is None and host_buf is None:
+            jpegs = self._source()  # may raise StopIteration (end of epoch)
+            if len(jpegs) != self._batch_size:
+                raise ValueError(f"source returned {len(jpegs)} samples, expected {self._batch_size}")
+            host_buf, off_t = pack_jpegs(jpegs, pin=True)
+            offsets = off_t.numpy()
         batch = len(offsets) - 1
-        info, ws, aws = fallback.probe(host_buf.data_ptr(), offsets, batch, self._max_image_dim, cfg)
-        st = info[:, 0]
-        if self._host_fallback and (st == fallback.IMG_UNSUPPORTED).any():
+        info, _, _ = fallback.probe(host_buf.data_ptr(), offsets, batch, self._max_image_dim)
+        mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
+        idx = np.flatnonzero(mask)
+        futures = {}
+        if len(idx):
             if jpegs is None:  # packed native feed: slice the images back out of the staging buffer
                 hb = host_buf.numpy()
                 jpegs = [hb[offsets[i]:offsets[i + 1]] for i in range(batch)]
-            jpegs, n = fallback.hand_over(list(jpegs), st)
-            self.stats["host_decoded"] += n
+            futures = {int(i): self._host.submit(jpegs[i]) for i in idx}
+        return _Prepared(jpegs, host_buf, offsets, futures)
+
+    def _screen(self, sl: _Slot, pb: "_Prepared", cfg):
+        """Collect a prepared batch's host decodes (re-packing the batch if there were any)
+        and grow the slot's workspaces to ``dino_probe``'s numbers for ``cfg``.  Returns
+        the (possibly re-packed) host buffer and offsets."""
+        host_buf, offsets = pb.host_buf, pb.offsets
+        if pb.futures:
+            jpegs = list(pb.jpegs)
+            for i, f in pb.futures.items():
+                jpegs[i] = f.result()
+            self.stats["host_decoded"] += len(pb.futures)
             host_buf, off_t = pack_jpegs(jpegs, pin=True)
             offsets = off_t.numpy()
-            info, ws, aws = fallback.probe(host_buf.data_ptr(), offsets, batch, self._max_image_dim, cfg)
+        _, ws, aws = fallback.probe(host_buf.data_ptr(), offsets, len(offsets) - 1, self._max_image_dim, cfg)
         if sl.engine.reserve(ws, aws):
             self.stats["reserves"] += 1
         return host_buf, offsets
@@ -250,7 +291,8 @@ class MI355XAugPipeline:
         off = gather(spans, sl.staging, getattr(self._source, "nthreads", 8))
         sl.staging_off.numpy()[: len(off)] = off
         cfg = self._cfg(*self._sizes())
-        host_buf, offsets = self._screen(sl, None, sl.staging, np.asarray(off, np.int64), cfg)
+        pb = self._prepare(host_buf=sl.staging, offsets=np.asarray(off, np.int64))
+        host_buf, offsets = self._screen(sl, pb, cfg)
         if host_buf is sl.staging:
             host_off, nbytes = sl.staging_off[: len(off)], need
         else:  # re-packed after a Pillow hand-over
@@ -270,18 +312,19 @@ class MI355XAugPipeline:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
         if hasattr(self._source, "next_spans"):
             return self._enqueue_packed()
-        jpeg_batch = self._source()  # may raise StopIteration (end of epoch)
-        if len(jpeg_batch) != self._batch_size:
-            raise ValueError(f"source returned {len(jpeg_batch)} samples, expected {self._batch_size}")
+        return self._enqueue_prepared(self._prepare())
+
+    def _enqueue_prepared(self, pb: "_Prepared") -> _Slot:
+        if self._closed:
+            raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
         sl = self._next_slot()
-        host_buf, offsets = pack_jpegs(jpeg_batch, pin=True)
         cfg = self._cfg(*self._sizes())
-        host_buf, off_np = self._screen(sl, jpeg_batch, host_buf, offsets.numpy(), cfg)
+        host_buf, off_np = self._screen(sl, pb, cfg)
         offsets = torch.from_numpy(off_np)
         with sl.engine.on_stream():
             d_bytes = host_buf.to(self.device, non_blocking=True)
             d_offsets = offsets.to(self.device, non_blocking=True)
-        self._launch(sl, d_bytes, d_offsets, len(jpeg_batch), None, cfg=cfg, account=True)
+        self._launch(sl, d_bytes, d_offsets, len(off_np) - 1, None, cfg=cfg, account=True)
         # torch's caching host allocator keeps the pinned staging block until the copy retires
         sl.inflight = (host_buf, d_bytes, d_offsets)
         return sl
@@ -328,6 +371,7 @@ class MI355XAugPipeline:
             try:
                 self._account(block=True)
             finally:
+                self._host.close()
                 for sl in self._slots:
                     sl.engine.close()
 
@@ -342,13 +386,16 @@ class MI355XPipelineIterator:
     """DALIGenericIterator-shaped wrapper: ``next()`` -> ``[ {view_name: Tensor} ]``.
 
     Keeps ``pipeline.depth`` batches in flight (DALI's prefetch queue): each
-    ``next()`` tops the queue up, then hands over the oldest batch."""
+    ``next()`` tops the queue up, then hands over the oldest batch.  With a callable
+    source one more batch is pulled and probed ahead of the queue, so that the Pillow
+    decodes of the images it routes to the host run while the GPU works."""
 
     def __init__(self, pipeline: MI355XAugPipeline, output_map: list[str], batch_size: int) -> None:
         self._pipe = pipeline
         self._output_map = list(output_map)
         self._exhausted = False
         self._queue: deque = deque()
+        self._ahead: deque = deque()  # prepared (pulled, probed, host decodes started) batches
         self._source_done = False
 
     def __iter__(self):
@@ -357,9 +404,16 @@ class MI355XPipelineIterator:
     def __next__(self) -> list[dict[str, torch.Tensor]]:
         if self._exhausted:
             raise StopIteration
-        while not self._source_done and len(self._queue) < self._pipe.depth:
+        pipe = self._pipe
+        lookahead = not hasattr(pipe._source, "next_spans")
+        while not self._source_done and len(self._queue) < pipe.depth:
             try:
-                self._queue.append(self._pipe._enqueue_one())
+                if not lookahead:
+                    self._queue.append(pipe._enqueue_one())
+                    continue
+                pb = self._ahead.popleft() if self._ahead else pipe._prepare()
+                self._queue.append(pipe._enqueue_prepared(pb))
+                self._ahead.append(pipe._prepare())
             except StopIteration:
                 self._source_done = True
         if not self._queue:
@@ -370,7 +424,7 @@ class MI355XPipelineIterator:
     def reset(self) -> None:
         self._exhausted = False
         self._source_done = False
-        self._queue.clear()
+        self._queue.clear()  # the prepared batch (not launched yet) is the source's next one: kept
 
 
 class MI355XUserAugPipeline:

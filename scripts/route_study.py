@@ -1,0 +1,64 @@
+"""Progressive routing through the product iterator (host JPEG feed, depth 3): images/s
+for batches of B 640x480 JPEGs of which k are progressive, per ``multiscan_route``.
+Writes one JSON line per (k, route) to stdout."""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+
+import torch  # noqa: E402
+
+from bench import make_unique  # noqa: E402
+from dataloader_amd.config import DINOAugConfig  # noqa: E402
+from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator  # noqa: E402
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batches", type=int, default=24)
+    ap.add_argument("--ks", default="0,1,4,16,64")
+    ap.add_argument("--routes", default="device,auto,host")
+    args = ap.parse_args()
+    B = args.batch
+    base = make_unique(B, 640, 480, 1, False, 8)
+    prog = make_unique(64, 640, 480, 2, False, 8, prog_frac=1.0)
+    cfg = DINOAugConfig()
+    for k in [int(x) for x in args.ks.split(",")]:
+        # the k progressive images spread over the batch, a different set each batch
+        batches = []
+        for b in range(args.batches):
+            j = list(base)
+            for t in range(k):
+                j[(t * B) // max(k, 1) + b % max(1, B // max(k, 1))] = prog[(b * k + t) % len(prog)]
+            batches.append(j)
+        for route in args.routes.split(","):
+            if k == 0 and route != "auto":
+                continue
+            src = iter(batches)
+            pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=1, depth=3, multiscan_route=route)
+            it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
+            n = 0
+            t0 = None
+            for i, _ in enumerate(it):
+                if i == 3:
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                elif i > 3:
+                    n += B
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            stats = pipe.flush_stats()
+            pipe.close()
+            print(json.dumps({"k_progressive": k, "route": route, "batch": B, "images_per_s": round(n / dt, 1),
+                              "host_decoded": stats["host_decoded"], "status": dict(stats["status"])}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

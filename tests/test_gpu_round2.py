@@ -312,10 +312,13 @@ def _cmyk(w, h, rng):
     return b.getvalue()
 
 
-def test_pipeline_hands_unsupported_flavours_to_pillow(gpu_device):
+@pytest.mark.parametrize("route", ["device", "auto", "host"])
+def test_pipeline_hands_unsupported_flavours_to_pillow(gpu_device, route):
     """CMYK and arithmetic-coded files (not decoded by the GPU) go through Pillow on the
-    host and are augmented on the GPU; progressive files decode on the GPU; a corrupt
-    file is zero-filled.  Every view equals the oracle's; nothing is silently dropped."""
+    host and are augmented on the GPU; the progressive file decodes in k_prog
+    (``multiscan_route="device"``) or in the Pillow worker pool ("auto": one such image
+    in the batch; "host"); a corrupt file is zero-filled.  Every view equals the
+    oracle's on every route; nothing is silently dropped."""
     from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
     rng = np.random.default_rng(35)
     good = encode_jpeg(textured_rgb(300, 200, rng))
@@ -325,7 +328,8 @@ def test_pipeline_hands_unsupported_flavours_to_pillow(gpu_device):
     jpegs = [good, _cmyk(240, 180, rng), encode_jpeg(textured_rgb(256, 300, rng), progressive=True), bytes(arith),
              b"\xff\xd8\xff corrupt", _cmyk(97, 131, rng)]
     cfg = DINOAugConfig(global_crop_size=64, local_crop_size=32, n_local_crops=3)
-    pipe = MI355XAugPipeline(lambda: jpegs, cfg, len(jpegs), seed=4, out_dtype="fp32", depth=1)
+    pipe = MI355XAugPipeline(lambda: jpegs, cfg, len(jpegs), seed=4, out_dtype="fp32", depth=1,
+                             multiscan_route=route, host_workers=2)
     it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], len(jpegs))
     out = next(it)[0]
     torch.cuda.synchronize()
@@ -343,7 +347,8 @@ def test_pipeline_hands_unsupported_flavours_to_pillow(gpu_device):
             ref = cpu_ref.augment_one(j, p, cfg.mean, cfg.std, out_dtype=torch.float32, decoded=img)
             tol = ONE_LEVEL + 1e-6 if p.blur else 0.0
             assert (ref - got).abs().max().item() <= tol, (b, v)
-    assert stats["host_decoded"] == 3  # two CMYK + the arithmetic file
+    # two CMYK + the arithmetic file (+ the progressive file off the device route)
+    assert stats["host_decoded"] == (3 if route == "device" else 4)
     n_ok = sum(cpu_ref.decode_rgb(j) is not None for j in jpegs)
     assert stats["status"][0] == n_ok and sum(n for s, n in stats["status"].items() if s > 0) == 0
     pipe.close()

@@ -118,3 +118,39 @@ def test_hand_over_replaces_only_unsupported():
             assert out[i][16:] == np.asarray(ref).tobytes() and int.from_bytes(out[i][4:8], "little") == w
     info2, _, _ = _probe(out)
     assert (info2[[0, 1], 0] == 0).all() and info2[1, 3] == 2
+
+
+def test_route_mask_policies():
+    """Coefficient-buffer images (kind 1) go to the host on "host", never on "device", and on
+    "auto" only while the batch holds at most host_max of them; unsupported images always
+    (when host_fallback); corrupt/truncated never (the device zero-fills them like the reference)."""
+    rng = np.random.default_rng(8)
+    base = encode_jpeg(textured_rgb(64, 48, rng))
+    prog = encode_jpeg(textured_rgb(64, 48, rng), progressive=True)
+    jpegs = [base, prog, _cmyk_jpeg(30, 20, rng), prog, prog[:100], b"junk"]
+    info, _, _ = _probe(jpegs)
+    m = lambda route, hmax=8, fb=True: list(fallback.route_mask(info, fb, route, hmax))  # noqa: E731
+    assert m("device") == [False, False, True, False, False, False]
+    assert m("host") == [False, True, True, True, False, False]
+    assert m("auto") == m("host") and m("auto", hmax=2) == m("host")
+    assert m("auto", hmax=1) == m("device")
+    assert m("host", fb=False) == [False, True, False, True, False, False]
+
+
+def test_hand_over_in_worker_pool_matches_serial():
+    """The spawn-context Pillow pool returns the same containers as the in-process hand-over."""
+    rng = np.random.default_rng(9)
+    prog = [encode_jpeg(textured_rgb(70 + 9 * i, 50, rng), progressive=True) for i in range(3)]
+    jpegs = [prog[0], _cmyk_jpeg(30, 20, rng), prog[1], b"\xff\xd8junk", prog[2]]
+    info, _, _ = _probe(jpegs)
+    mask = fallback.route_mask(info, True, "host", 0)
+    assert list(mask) == [True, True, True, False, True]
+    serial, n = fallback.hand_over(jpegs, info[:, 0], mask)
+    pool = fallback.HostDecoder(2)
+    try:
+        pooled, n2 = fallback.hand_over(jpegs, info[:, 0], mask, pool)
+    finally:
+        pool.close()
+    assert n == n2 == 4 and pooled == serial and pooled[3] == jpegs[3]
+    info2, _, _ = _probe(pooled)
+    assert list(info2[:, 3]) == [2, 2, 2, -1, 2]
