@@ -121,6 +121,10 @@ class HostDecoder:
             import multiprocessing as mp
             from concurrent.futures import ProcessPoolExecutor
             self._pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"))
+            # the executor starts a process per submit that finds no idle one: start them all
+            # now (each imports Pillow on its no-op decode) rather than one per later batch
+            for _ in range(self.workers):
+                self._pool.submit(decode_with_pillow, b"")
         return self._pool.submit(pillow_container, bytes(jpeg))
 
     def close(self) -> None:
