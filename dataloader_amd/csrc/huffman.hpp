@@ -23,7 +23,7 @@ namespace dino {
 // code is longer than LB.  AC tables look ahead kLookBits = 11 bits; DC tables
 // kDcLookBits = 9 (the standard DC codes are <= 9 bits for luma and only the rare
 // categories >= 10 of chroma need the slow path), which keeps an image's six tables
-// at 17.3 KiB of LDS.
+// at 17.3 KiB of LDS (32.7 KiB with the skip entries).
 constexpr int kDcLookBits = 9;
 template <int LB>
 struct HuffTableT {
@@ -35,11 +35,21 @@ struct HuffTableT {
 using HuffTable = HuffTableT<kLookBits>;
 using DcTable = HuffTableT<kDcLookBits>;
 
+// Skip entries of the state-only decodes (first decode and sync re-decodes): what a
+// step does to the decoder state without its coefficient value, indexed like `look`:
+// bits consumed (code + extra bits) | zigzag advance << 5 (DC 1; AC: r + 1, ZRL 16,
+// EOB 64), 0 when the code is longer than the lookahead.
+struct HuffSkip {
+  uint16_t ac[3][1 << kLookBits];
+  uint16_t dc[3][1 << kDcLookBits];
+};
+
 // The six tables of an image: AC tables of components 0..2, then DC tables.  Both
 // kinds share the layout up to `look`, so the slow path reads either through one type.
 struct HuffTables {
   HuffTable ac[3];
   DcTable dc[3];
+  HuffSkip skip;
 };
 static_assert(sizeof(HuffTables) % 16 == 0, "HuffTables is copied in 16-byte words");
 
@@ -97,6 +107,18 @@ DHD uint16_t huff_look_entry(const HuffTableT<LB>* t, int idx) {
   return 0;
 }
 
+// Skip entry of a decoded symbol (see HuffSkip); len 17 is libjpeg's fake zero.
+DHD uint32_t skip_from_sym(int sym, int len, bool dc) {
+  const int s = dc ? sym : sym & 15, r = dc ? 0 : sym >> 4;
+  const int zinc = dc ? 1 : (s ? r + 1 : (r == 15 ? 16 : 64));
+  return (uint32_t)(len + s) | ((uint32_t)zinc << 5);
+}
+
+// Skip entry for a lookahead entry (0 stays 0: the long-code path).
+DHD uint16_t skip_entry(uint32_t look, bool dc) {
+  return look ? (uint16_t)skip_from_sym((int)(look >> 5), (int)(look & 31u), dc) : (uint16_t)0;
+}
+
 // Bit reader over a destuffed, zero-padded big-endian byte stream.
 struct BitReader {
   const uint32_t* words;   // 4-byte aligned base of the stream (byte-swapped on read)
@@ -143,7 +165,12 @@ struct BitCursor {
 //                       (k_destuff's pad): a read past the end is clamped to the first
 //                       all-zero word, so no masking is needed on the hot path.
 // A load past the end is clamped (never out of bounds, no branch around the load).
+// (Reading the padded stream as 16-byte chunks fetched a chunk ahead was measured and
+// dropped: k_huff1 +20 %; the refill is not what the decode waits on.)
 enum : int { kSrcGlobal = 0, kSrcWin = 1, kSrcPadded = 2 };
+
+// Source of the speculative decode kernels (k_huff1/2/3) and of their emulator.
+constexpr int kHuffSrc = kSrcPadded;
 
 template <int kWin>
 DHD uint32_t src_raw(const BitReader& br, uint32_t i) {
@@ -327,7 +354,8 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
     o.value = v;
     o.zz = 0;
     z = 1;
-  } else if (v) {
+  } else if (s) {  // = (v != 0): an extended value of s >= 1 bits is never 0; the
+                   // state update then does not wait on the value (dead in the skip decodes)
     z += r;
     o.kind = 1;
     o.value = v;
@@ -350,9 +378,49 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
   return o;
 }
 
+// huff_step's effect on the state (c, z, bit position) alone, for the decodes that
+// only look for block boundaries and end states: one HuffSkip lookup gives the bits
+// and the zigzag advance, so no extra-bit value is extracted.  Same state sequence as
+// huff_step (checked by the emulator tests, which run both on the same streams).
+template <int kWin>
+DHD void skip_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
+  bc_fill<kWin>(cur, br);
+  const int comp = hi_comp(im, blk);
+  const bool dc = z == 0;
+  const uint32_t hi32 = (uint32_t)(cur.buf >> 32);
+  const uint16_t* tab = dc ? im.tabs->skip.dc[comp] : im.tabs->skip.ac[comp];
+  uint32_t e = tab[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
+  if (!e) {
+    int sym, len;
+    if (dc)
+      huff_slow(cur, im.tabs->dc + comp, &sym, &len);
+    else
+      huff_slow(cur, im.tabs->ac + comp, &sym, &len);
+    e = skip_from_sym(sym, len, dc);
+  }
+  bc_skip(cur, (int)(e & 31u));
+  z += (int32_t)(e >> 5);
+  if (z >= 64) {
+    z = 0;
+    blk = blk + 1 == im.blocks_per_mcu ? 0 : blk + 1;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Lane-level routines of the self-synchronising parallel decode (k_huffman).
 // ---------------------------------------------------------------------------
+
+#ifndef DINO_HUFF_SKIP
+#define DINO_HUFF_SKIP 1
+#endif
+// The step of the state-only decodes (skip_step; huff_step in A/B builds).
+template <int kWin>
+DHD void state_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
+  if (DINO_HUFF_SKIP)
+    skip_step<kWin>(cur, br, im, blk, z);
+  else
+    huff_step<kWin>(cur, br, im, blk, z);
+}
 
 // What a lane learns by decoding the steps that start in [st.pos, end).
 struct RangeOut {
@@ -409,7 +477,7 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
         cps[(n++) * cstride] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
       r.nblk++;
     }
-    huff_step<kWin>(cur, br, im, blk, z);
+    state_step<kWin>(cur, br, im, blk, z);
   }
   r.end.pos = cur.pos;
   r.end.c = blk;
@@ -431,17 +499,20 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
   BitCursor cur;
   bc_init<kWin>(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;
+  // the next checkpoint at or after the position, kept in registers: memory is only
+  // read when the decode passes one (every kHuffCpStride blocks), not at every block
+  Checkpoint cp = ncp > 0 ? cps[0] : Checkpoint{0xFFFFFFFFu, 0u};
   while (cur.pos < end) {
     if (z == 0) {
-      while (j < ncp && cps[j * cstride].pos < cur.pos) ++j;
-      if (j < ncp && cps[j * cstride].pos == cur.pos && (int32_t)(cps[j * cstride].cn & 15u) == blk) {
+      while (cp.pos < cur.pos) cp = ++j < ncp ? cps[j * cstride] : Checkpoint{0xFFFFFFFFu, 0u};
+      if (cp.pos == cur.pos && (int32_t)(cp.cn & 15u) == blk) {
         RangeOut r = first;
-        r.nblk = nblk + first.nblk - (int32_t)(cps[j * cstride].cn >> 4);
+        r.nblk = nblk + first.nblk - (int32_t)(cp.cn >> 4);
         return r;
       }
       nblk++;
     }
-    huff_step<kWin>(cur, br, im, blk, z);
+    state_step<kWin>(cur, br, im, blk, z);
   }
   RangeOut r;
   r.end.pos = cur.pos;

@@ -478,9 +478,12 @@ struct HuffLds {     // k_huff1
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
+// k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
+constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
+static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
 struct HuffLds3 {    // k_huff3 (no lane exchange)
   ImgDesc sd;
-  HuffTables tab;
+  alignas(16) uint8_t tab[kHuffTabBytesNoSkip];  // a HuffTables without its skip member
   int32_t img, item;
 };
 
@@ -621,6 +624,15 @@ __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict
     if (c < d.ncomp) s_tab.dc[c].look[idx] = huff_look_entry(&s_tab.dc[c], idx);
   }
   __syncthreads();
+  for (int e = t; e < 3 * (1 << kLookBits); e += kHuffThreads) {
+    const int c = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
+    if (c < d.ncomp) s_tab.skip.ac[c][idx] = skip_entry(s_tab.ac[c].look[idx], false);
+  }
+  for (int e = t; e < 3 * (1 << kDcLookBits); e += kHuffThreads) {
+    const int c = e >> kDcLookBits, idx = e & ((1 << kDcLookBits) - 1);
+    if (c < d.ncomp) s_tab.skip.dc[c][idx] = skip_entry(s_tab.dc[c].look[idx], true);
+  }
+  __syncthreads();
   uint4* dst = (uint4*)(ws + d.htab_off);
   const uint4* src = (const uint4*)&s_tab;
   for (int k = t; k < (int)(sizeof(HuffTables) / 16); k += kHuffThreads) dst[k] = src[k];
@@ -700,7 +712,8 @@ __device__ __forceinline__ bool huff_single_segment(const ImgDesc& d) {
 // Loads work item `item`'s image descriptor and tables into LDS; false past the end.
 // With skip_single, the tables of a single-segment image are not loaded (L.img = -2).
 template <typename LdsT>
-__device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_t* ws, int item, bool skip_single = false) {
+__device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_t* ws, int item, bool skip_single = false,
+                               int tab_bytes = (int)sizeof(HuffTables)) {
   if (threadIdx.x == 0) {
     L.img = huff_item_image(desc, B, item);
     if (L.img >= 0) {
@@ -713,7 +726,7 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
   if (L.img == -2) return true;
   const uint4* src = (const uint4*)(ws + L.sd.htab_off);
   uint4* dst = (uint4*)&L.tab;
-  for (int k = threadIdx.x; k < (int)(sizeof(HuffTables) / 16); k += kHuffThreads) dst[k] = src[k];
+  for (int k = threadIdx.x; k < tab_bytes / 16; k += kHuffThreads) dst[k] = src[k];
   __syncthreads();
   return true;
 }
@@ -761,7 +774,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     RangeOut myR1{};                                      // result stay in registers; only R is shared
     HUFF_PHASE(0, wall_clock64());
     if (active) {
-      myR1 = decode_range<kSrcPadded>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
+      myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
       L.R[t] = myR1;
     }
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
@@ -777,7 +790,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       __syncthreads();
       if (redo) {
         myS = want;
-        L.R[t] = decode_range_sync<kSrcPadded>(br, im, want, rend, cps, cstride, ncp, myR1);
+        L.R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1);
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
@@ -794,7 +807,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
         sink.ent = (uint32_t*)(ws + sd.coef_off);
         sink.binfo = (uint2*)(ws + sd.binfo_off);
         sink.open((int32_t)blk0);
-        decode_write<kSrcPadded>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
+        decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
                                  nbits, sink);
         sink.close();
       }
@@ -849,7 +862,7 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
         if (lr[i].pad) {
           const HState want = lr[i].W;
           lr[i].S = want;
-          lr[i].R = decode_range_sync<kSrcPadded>(br, im, want, lane_range_end(d, i, nbits),
+          lr[i].R = decode_range_sync<kHuffSrc>(br, im, want, lane_range_end(d, i, nbits),
                                              cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1);
         }
       }
@@ -875,14 +888,14 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
   HuffLds3& L = *reinterpret_cast<HuffLds3*>(smem);
   const int t = threadIdx.x;
   for (int item = blockIdx.x;; item += gridDim.x) {
-    if (!huff_load_item(L, desc, B, ws, item, true)) return;
+    if (!huff_load_item(L, desc, B, ws, item, true, kHuffTabBytesNoSkip)) return;
     if (L.img == -2) {  // decoded by k_huff1
       __syncthreads();
       continue;
     }
     const ImgDesc& sd = L.sd;
     HuffImage im;
-    hi_init(im, &L.tab, sd.mcu_comp, sd.blocks_per_mcu);
+    hi_init(im, reinterpret_cast<const HuffTables*>(L.tab), sd.mcu_comp, sd.blocks_per_mcu);
     const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
     SparseSink sink;
     sink.ent = (uint32_t*)(ws + sd.coef_off);
@@ -908,7 +921,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
       sink.open(r.blk0);
-      decode_write<kSrcPadded>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr,
+      decode_write<kHuffSrc>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr,
                                br.nbytes * 8u, sink);
       sink.close();
     }

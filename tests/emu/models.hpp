@@ -19,7 +19,7 @@ namespace dino {
 
 // ---- k_destuff (sequential statement of the same classification) ----------
 struct Destuffed {
-  std::vector<uint8_t> bytes;   // padded with zeros to a multiple of 4 + 8
+  std::vector<uint8_t> bytes;   // padded with zeros to a multiple of 16 + 64 (k_destuff's pad)
   std::vector<int32_t> rst;     // destuffed byte offset where each restart segment starts
   int32_t len = 0;
   int32_t terminated = 0;
@@ -53,8 +53,8 @@ inline Destuffed model_destuff(const uint8_t* r, int n) {
     }
   }
   d.len = (int32_t)d.bytes.size();
-  while (d.bytes.size() % 4) d.bytes.push_back(0);
-  for (int i = 0; i < 8; ++i) d.bytes.push_back(0);
+  while (d.bytes.size() % 16) d.bytes.push_back(0);
+  for (int i = 0; i < 64; ++i) d.bytes.push_back(0);
   return d;
 }
 
@@ -105,6 +105,8 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTables* tabs, H
     if (!huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &tabs->ac[c])) return false;
     for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->dc[c].look[i] = huff_look_entry(&tabs->dc[c], i);
     for (int i = 0; i < (1 << kLookBits); ++i) tabs->ac[c].look[i] = huff_look_entry(&tabs->ac[c], i);
+    for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->skip.dc[c][i] = skip_entry(tabs->dc[c].look[i], true);
+    for (int i = 0; i < (1 << kLookBits); ++i) tabs->skip.ac[c][i] = skip_entry(tabs->ac[c].look[i], false);
   }
   hi_init(im, tabs, d.mcu_comp, d.blocks_per_mcu);
   return true;
@@ -275,7 +277,7 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
       BitReader bw{win.data(), (uint32_t)win.size() * 4};
       model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, 0, sink, dcd.data(), stats);
     } else {
-      model_huffman_spec<kSrcPadded>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
+      model_huffman_spec<kHuffSrc>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
                                 stats);
     }
   }
