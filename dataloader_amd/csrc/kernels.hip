@@ -1329,22 +1329,21 @@ __device__ __forceinline__ PlaneView make_plane_view(const ImgDesc& d, const uin
   return v;
 }
 
-// 4 bytes at row[s] as one word from two aligned loads + v_alignbyte (the second
-// word may lie past the row: planes are followed by more workspace, never unmapped).
-__device__ __forceinline__ uint32_t load4(const uint8_t* row, int s) {
-  const uint32_t* w = (const uint32_t*)(row + (s & ~3));
-  return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(s & 3));
-}
-
-// 4 chroma samples [c-1, c+2] of a row.
-__device__ __forceinline__ uint32_t chroma_quad(const uint8_t* row, int c) { return load4(row, c - 1); }
+// (k_color reads 4 bytes at row[s] as two aligned words + v_alignbyte: the second word
+// may lie past the row, planes are followed by more workspace, never unmapped.)
 
 // h2v2 fancy upsampling of one chroma plane for the 4 pixels x0..x0+3 of row y,
 // given the samples [c0-1, c0+2] of the nearer row (n) and the farther row (f).
-__device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, int* out) {
+// edge: bit 0 column c0-1 is left of the plane, bits 1 / 2 columns c0+1 / c0+2 are
+// right of it; such a column is the clamp of its neighbour (jdsample.c's first and
+// last column formulas), whatever bytes were loaded for it.
+__device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, uint32_t edge, int* out) {
   int cs[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) cs[j] = 3 * (int)((n >> (8 * j)) & 255u) + (int)((f >> (8 * j)) & 255u);
+  if (edge & 1u) cs[0] = cs[1];
+  if (edge & 2u) cs[2] = cs[1];
+  if (edge & 4u) cs[3] = cs[2];
   // an even pixel x blends column x/2 with its left neighbour ((3a + b + 8) >> 4), an odd
   // one with its right neighbour ((3a + b + 7) >> 4); with cs[1] = column x0/2 the four
   // pixels use fixed columns for each parity of x0 (no dynamically indexed cs)
@@ -1362,9 +1361,10 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, int* o
 #define DINO_COLOR_WGS 32
 #endif
 constexpr int kColorWgs = DINO_COLOR_WGS;  // workgroups per image
-#ifndef DINO_COLOR_UNROLL
-#define DINO_COLOR_UNROLL 2
+#ifndef DINO_COLOR_BATCH
+#define DINO_COLOR_BATCH 1
 #endif
+constexpr int kColorBatch = DINO_COLOR_BATCH;  // quads whose loads a lane issues together (A/B: 4 and 8 slower)
 
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
 // the RGB area is padded by 16 bytes, so the last partial quad may store whole words).
@@ -1405,59 +1405,117 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
   const uint32_t pstride = (uint32_t)(qs * 4);
   const int dy = (int)(pstride / (uint32_t)W), dx = (int)(pstride - (uint32_t)dy * (uint32_t)W);
   int yq = (int)((uint32_t)(q0 * 4) / (uint32_t)W), xq = (int)((uint32_t)(q0 * 4) - (uint32_t)yq * (uint32_t)W);
-#pragma unroll DINO_COLOR_UNROLL
-  for (int64_t q = q0; q < nq; q += qs) {
-    const int64_t i0 = q * 4;
-    int y = yq, x = xq;
-    xq += dx;
-    yq += dy;
-    if (xq >= W) {
-      xq -= W;
-      ++yq;
-    }
-    union {
-      uint8_t b[12];
-      uint32_t w[3];
-    } o;
-    if (fast420 && x >= 2 && x + 3 < W && ((x + 3) >> 1) + 1 < p1.dw) {
-      const int r = y >> 1;
-      const int rf = (y & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
-      const int c0 = x >> 1;
-      const uint32_t yw = load4(p0.p + (int64_t)y * p0.pitch, x);
-      int cb[4], cr[4];
-      h2v2_quad(chroma_quad(p1.p + (int64_t)r * p1.pitch, c0), chroma_quad(p1.p + (int64_t)rf * p1.pitch, c0), x, cb);
-      h2v2_quad(chroma_quad(p2.p + (int64_t)r * p2.pitch, c0), chroma_quad(p2.p + (int64_t)rf * p2.pitch, c0), x, cr);
+  // kColorBatch quads per lane per iteration: every load of the batch is issued before
+  // any of its quads is converted (the RGB stores may alias the planes for the compiler,
+  // so it would not move the next quad's loads above this quad's stores by itself)
+  for (int64_t qb = q0; qb < nq; qb += kColorBatch * qs) {
+    int ys[kColorBatch], xs[kColorBatch];
+    bool fast[kColorBatch];
+    uint32_t yw0[kColorBatch], yw1[kColorBatch], cw[kColorBatch][8];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) ycc_to_rgb((int)((yw >> (8 * j)) & 255u), cb[j], cr[j], o.b + 3 * j);
-    } else {
+    for (int k = 0; k < kColorBatch; ++k) {
+      const int y = yq, x = xq;
+      ys[k] = y;
+      xs[k] = x;
+      xq += dx;
+      yq += dy;
+      if (xq >= W) {
+        xq -= W;
+        ++yq;
+      }
+      // every 4:2:0 quad inside one row (row edges included: the fancy upsampler's edge
+      // columns are clamps, applied to the loaded samples below) takes the vector path;
+      // a lane on the generic per-pixel path would make its whole wave run that too
+      fast[k] = fast420 && qb + k * qs < nq && x + 3 < W;
+      if (fast[k]) {  // raw words: Y at x, Cb / Cr at column x/2 - 1 of the nearer and the farther row
+        const int r = y >> 1;
+        const int rf = (y & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
+        const int cc = (x >> 1) - 1;
+        const uint32_t* yp = (const uint32_t*)(p0.p + (int64_t)y * p0.pitch + (x & ~3));
+        yw0[k] = yp[0];
+        yw1[k] = yp[1];
+        const uint32_t* cp[4] = {(const uint32_t*)(p1.p + (int64_t)r * p1.pitch + (cc & ~3)),
+                                 (const uint32_t*)(p1.p + (int64_t)rf * p1.pitch + (cc & ~3)),
+                                 (const uint32_t*)(p2.p + (int64_t)r * p2.pitch + (cc & ~3)),
+                                 (const uint32_t*)(p2.p + (int64_t)rf * p2.pitch + (cc & ~3))};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (i0 + j < npx) {
-          if (nc == 1) {
-            const uint8_t v = (uint8_t)upsample_at(p0, x, y);
-            o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = v;
-          } else {
-            const int a = upsample_at(p0, x, y), b = upsample_at(p1, x, y), c = upsample_at(p2, x, y);
-            if (ycc) {
-              ycc_to_rgb(a, b, c, o.b + 3 * j);
-            } else {
-              o.b[3 * j] = (uint8_t)a;
-              o.b[3 * j + 1] = (uint8_t)b;
-              o.b[3 * j + 2] = (uint8_t)c;
-            }
-          }
-        } else {
-          o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = 0;
-        }
-        if (++x == W) {
-          x = 0;
-          ++y;
+        for (int j = 0; j < 4; ++j) {
+          cw[k][2 * j] = cp[j][0];
+          cw[k][2 * j + 1] = cp[j][1];
         }
       }
     }
-    rgb[3 * q] = o.w[0];
-    rgb[3 * q + 1] = o.w[1];
-    rgb[3 * q + 2] = o.w[2];
+#pragma unroll
+    for (int k = 0; k < kColorBatch; ++k) {
+      const int64_t q = qb + k * qs;
+      if (q >= nq) break;
+      int y = ys[k], x = xs[k];
+      const int64_t i0 = q * 4;
+      union {
+        uint8_t b[12];
+        uint32_t w[3];
+      } o;
+      if (fast[k]) {
+        const int c0 = x >> 1;
+        const uint32_t csh = (uint32_t)((c0 - 1) & 3);
+        const uint32_t yw = __builtin_amdgcn_alignbyte(yw1[k], yw0[k], (uint32_t)(x & 3));
+        const uint32_t edge = (c0 == 0 ? 1u : 0u) | (c0 + 1 >= p1.dw ? 2u : 0u) | (c0 + 2 >= p1.dw ? 4u : 0u);
+        int cb[4], cr[4];
+        h2v2_quad(__builtin_amdgcn_alignbyte(cw[k][1], cw[k][0], csh), __builtin_amdgcn_alignbyte(cw[k][3], cw[k][2], csh),
+                  x, edge, cb);
+        h2v2_quad(__builtin_amdgcn_alignbyte(cw[k][5], cw[k][4], csh), __builtin_amdgcn_alignbyte(cw[k][7], cw[k][6], csh),
+                  x, edge, cr);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ycc_to_rgb((int)((yw >> (8 * j)) & 255u), cb[j], cr[j], o.b + 3 * j);
+      } else if (fast420) {  // a 4:2:0 quad that wraps a row: per pixel, same arithmetic
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (i0 + j < npx) {
+            const int r = y >> 1, c = x >> 1;
+            const int rn = (y & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
+            const int cn = (x & 1) ? min(c + 1, p1.dw - 1) : max(c - 1, 0);
+            const int bias = (x & 1) ? 7 : 8;
+            const int tb = pv_at(p1, c, r) * 3 + pv_at(p1, c, rn), nb = pv_at(p1, cn, r) * 3 + pv_at(p1, cn, rn);
+            const int tr = pv_at(p2, c, r) * 3 + pv_at(p2, c, rn), nr = pv_at(p2, cn, r) * 3 + pv_at(p2, cn, rn);
+            ycc_to_rgb(pv_at(p0, x, y), (tb * 3 + nb + bias) >> 4, (tr * 3 + nr + bias) >> 4, o.b + 3 * j);
+          } else {
+            o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = 0;
+          }
+          if (++x == W) {
+            x = 0;
+            ++y;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (i0 + j < npx) {
+            if (nc == 1) {
+              const uint8_t v = (uint8_t)upsample_at(p0, x, y);
+              o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = v;
+            } else {
+              const int a = upsample_at(p0, x, y), b = upsample_at(p1, x, y), c = upsample_at(p2, x, y);
+              if (ycc) {
+                ycc_to_rgb(a, b, c, o.b + 3 * j);
+              } else {
+                o.b[3 * j] = (uint8_t)a;
+                o.b[3 * j + 1] = (uint8_t)b;
+                o.b[3 * j + 2] = (uint8_t)c;
+              }
+            }
+          } else {
+            o.b[3 * j] = o.b[3 * j + 1] = o.b[3 * j + 2] = 0;
+          }
+          if (++x == W) {
+            x = 0;
+            ++y;
+          }
+        }
+      }
+      rgb[3 * q] = o.w[0];
+      rgb[3 * q + 1] = o.w[1];
+      rgb[3 * q + 2] = o.w[2];
+    }
   }
 }
 
