@@ -552,25 +552,34 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
     huff_step<kWin>(cur, br, im, blk, z);
   }
   int32_t b = first_block;
-  while (b < total_blocks && cur.pos < end) {
-    if (blk == 0 && cur.pos > avail) {  // insufficient_data before this MCU: the rest stays zero
-      for (; b < total_blocks; ++b) sink.zero(b);
-      break;
-    }
-    sink.begin(b);
-    int comp = hi_comp(im, blk);
-    for (;;) {
-      StepOut o = huff_step<kWin>(cur, br, im, blk, z);
-      if (o.kind == 0) {
-        if (pred) add3(pred, comp, o.value);
-        sink.dc((int16_t)(pred ? get3(pred, comp) : o.value));
-      } else if (o.kind == 1) {
-        sink.ac(o.zz, (int16_t)o.value);
+  if (!(b < total_blocks && cur.pos < end)) return cur.pos;
+  // one step per iteration, blocks opened and closed inside the loop: a loop per block
+  // would keep a wave in each block until its longest lane finished that block
+  bool open = false;
+  int comp = 0;
+  for (;;) {
+    if (!open) {
+      if (blk == 0 && cur.pos > avail) {  // insufficient_data before this MCU: the rest stays zero
+        for (; b < total_blocks; ++b) sink.zero(b);
+        break;
       }
-      if (o.block_done) break;
+      sink.begin(b);
+      comp = hi_comp(im, blk);
+      open = true;
     }
-    sink.end();
-    ++b;
+    const StepOut o = huff_step<kWin>(cur, br, im, blk, z);
+    if (o.kind == 0) {
+      if (pred) add3(pred, comp, o.value);
+      sink.dc((int16_t)(pred ? get3(pred, comp) : o.value));
+    } else if (o.kind == 1) {
+      sink.ac(o.zz, (int16_t)o.value);
+    }
+    if (o.block_done) {
+      sink.end();
+      ++b;
+      open = false;
+      if (!(b < total_blocks && cur.pos < end)) break;
+    }
   }
   return cur.pos;
 }

@@ -1702,6 +1702,10 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
 #define DINO_HRESIZE_MIN_ROWS 8
 #endif
 constexpr int kHresizeMinRows = DINO_HRESIZE_MIN_ROWS;  // rows per band the slice width is chosen for
+#ifndef DINO_HRESIZE_WGS
+#define DINO_HRESIZE_WGS 4
+#endif
+constexpr int kHresizeWgs = DINO_HRESIZE_WGS;  // workgroups per view (each loops over the view's tiles)
 
 // Tile shape of a view's horizontal pass: the widest slice of outputs (all of S,
 // else a multiple of 8) whose taps (16 bytes per output + 16 per output and group
@@ -2197,17 +2201,44 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
   const JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
   const int cmean = contrast_mean_from_sum(vp.lsum, N);
-  const FastDiv dtw((uint32_t)tw);
-  for (int e = threadIdx.x; e < tr * tw; e += blockDim.x) {
-    const int lr = (int)dtw.div((uint32_t)e), tc = e - lr * tw;
-    const int sr = reflect_idx(y0 - pad + lr, S), sc = reflect_idx(tc - pad, S);
-    const int64_t so = (int64_t)sr * S + sc;
-    int r = crop[so], g = crop[N + so], bb = crop[2 * N + so];
+  auto stage_px = [&](int lr, int tc, int r, int g, int bb) {
     jitter_stage1(jp, r, g, bb, p, cmean, hd);
     const int to = lr * tp + tc;
     tile[to] = (uint8_t)r;
     tile[tplane + to] = (uint8_t)g;
     tile[2 * tplane + to] = (uint8_t)bb;
+  };
+  if ((S & 3) == 0) {
+    // the band's rows four source pixels per lane (one word per plane), then the
+    // reflected halo columns: 4x fewer dependent global loads than one pixel per lane
+    const int nq = S >> 2;
+    const FastDiv dq((uint32_t)nq);
+    for (int e = threadIdx.x; e < tr * nq; e += blockDim.x) {
+      const int lr = (int)dq.div((uint32_t)e), q = e - lr * nq;
+      const int64_t so = (int64_t)reflect_idx(y0 - pad + lr, S) * S + 4 * q;
+      const uint32_t wr = *(const uint32_t*)(crop + so), wg = *(const uint32_t*)(crop + N + so),
+                     wb = *(const uint32_t*)(crop + 2 * N + so);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        stage_px(lr, pad + 4 * q + j, (int)((wr >> (8 * j)) & 255u), (int)((wg >> (8 * j)) & 255u),
+                 (int)((wb >> (8 * j)) & 255u));
+    }
+    if (pad > 0) {
+      const FastDiv dh((uint32_t)(2 * pad));
+      for (int e = threadIdx.x; e < tr * 2 * pad; e += blockDim.x) {
+        const int lr = (int)dh.div((uint32_t)e), h = e - lr * 2 * pad;
+        const int tc = h < pad ? h : S + h;  // columns [0, pad) and [S + pad, S + 2 pad)
+        const int64_t so = (int64_t)reflect_idx(y0 - pad + lr, S) * S + reflect_idx(tc - pad, S);
+        stage_px(lr, tc, crop[so], crop[N + so], crop[2 * N + so]);
+      }
+    }
+  } else {
+    const FastDiv dtw((uint32_t)tw);
+    for (int e = threadIdx.x; e < tr * tw; e += blockDim.x) {
+      const int lr = (int)dtw.div((uint32_t)e), tc = e - lr * tw;
+      const int64_t so = (int64_t)reflect_idx(y0 - pad + lr, S) * S + reflect_idx(tc - pad, S);
+      stage_px(lr, tc, crop[so], crop[N + so], crop[2 * N + so]);
+    }
   }
   __syncthreads();
   if (p.blur && threadIdx.x < ks * ks) H.k2[threadIdx.x] = H.k1[threadIdx.x / ks] * H.k1[threadIdx.x % ks];
@@ -2297,8 +2328,9 @@ __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __rest
   __syncthreads();
   const int cmean = jp.has_contrast ? contrast_mean_from_sum(wg_sum(lsum, s_part), N) : 0;
   // the ops after contrast, in place on the interior
+  const FastDiv ds((uint32_t)S);
   for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
-    const int y = e / S, x = e - y * S;
+    const int y = (int)ds.div((uint32_t)e), x = e - y * S;
     uint8_t* q = in0 + y * tp + x;
     int r = q[0], g = q[tplane], bb = q[2 * tplane];
     jitter_stage1(jp, r, g, bb, p, cmean, hd);
@@ -2309,10 +2341,20 @@ __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __rest
   if (pad > 0) {
     __syncthreads();
     // blur halo: torch's reflect padding of the jittered view
-    const int tw = S + 2 * pad, th = S + 2 * pad;
-    for (int e = threadIdx.x; e < th * tw; e += blockDim.x) {
-      const int r = e / tw, c = e - r * tw;
-      if (r >= pad && r < pad + S && c >= pad && c < pad + S) continue;
+    // over the halo only: 2 pad full rows above and below, then 2 pad columns of the interior rows
+    const int tw = S + 2 * pad, nrow = 2 * pad * tw;
+    const FastDiv dtw((uint32_t)tw), dh((uint32_t)(2 * pad));
+    for (int e = threadIdx.x; e < nrow + S * 2 * pad; e += blockDim.x) {
+      int r, c;
+      if (e < nrow) {
+        const int k = (int)dtw.div((uint32_t)e);
+        c = e - k * tw;
+        r = k < pad ? k : S + k;  // rows [0, pad) and [S + pad, S + 2 pad)
+      } else {
+        const int f = e - nrow, k = (int)dh.div((uint32_t)f), h = f - k * 2 * pad;
+        r = pad + k;
+        c = h < pad ? h : S + h;
+      }
       const int sr = reflect_idx(r - pad, S), sc = reflect_idx(c - pad, S);
       const uint8_t* src = in0 + sr * tp + sc;
       uint8_t* dst = tile + r * tp + c;
@@ -2709,7 +2751,7 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   const int kvert = v0 == 0 ? kKVertGlobal : kKVertLocal;
   TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
   TIMED(tm, kKHresize, s,
-        (k_hresize<<<dim3(16, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
+        (k_hresize<<<dim3(kHresizeWgs, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
   if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS
     const int lds = (int)sizeof(FinalLds) + vfinal_tile_bytes(S) + 3 * 256 * (int)sizeof(OutT);
     TIMED(tm, kfin, s,
