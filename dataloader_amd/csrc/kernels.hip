@@ -1928,22 +1928,28 @@ __device__ __forceinline__ uint32_t vert_apply(const ImgDesc& d, const dino_view
       if (need_v) {
         const int ymin = cvv.bounds[2 * y], ycnt = cvv.bounds[2 * y + 1];
         const int32_t* k = cvv.taps + (int64_t)y * cvv.ksize;
+        // taps outer, channels inner: one tap load serves the three planes, whose
+        // three row loads are independent (exact int32 sums: the order is free)
+        const uint8_t* q = htmp + (int64_t)ymin * S + 4 * xq;
+        int32_t a[3][4];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const uint8_t* q = htmp + c * cpl + (int64_t)ymin * S + 4 * xq;
-          int32_t a0 = 1 << (kPrecisionBits - 1), a1 = a0, a2 = a0, a3 = a0;
-#pragma unroll 4
-          for (int t = 0; t < ycnt; ++t) {  // unrolled: four row loads in flight per wait
-            const uint32_t u = *(const uint32_t*)(q + (int64_t)t * S);
-            const int32_t kk = k[t];
-            a0 += (int32_t)(u & 255u) * kk;
-            a1 += (int32_t)((u >> 8) & 255u) * kk;
-            a2 += (int32_t)((u >> 16) & 255u) * kk;
-            a3 += (int32_t)(u >> 24) * kk;
+        for (int c = 0; c < 3; ++c) a[c][0] = a[c][1] = a[c][2] = a[c][3] = 1 << (kPrecisionBits - 1);
+#pragma unroll 2
+        for (int t = 0; t < ycnt; ++t) {
+          const int32_t kk = k[t];
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const uint32_t u = *(const uint32_t*)(q + c * cpl + (int64_t)t * S);
+            a[c][0] += (int32_t)(u & 255u) * kk;
+            a[c][1] += (int32_t)((u >> 8) & 255u) * kk;
+            a[c][2] += (int32_t)((u >> 16) & 255u) * kk;
+            a[c][3] += (int32_t)(u >> 24) * kk;
           }
-          w[c] = (uint32_t)clip8_acc(a0) | ((uint32_t)clip8_acc(a1) << 8) | ((uint32_t)clip8_acc(a2) << 16) |
-                 ((uint32_t)clip8_acc(a3) << 24);
         }
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          w[c] = (uint32_t)clip8_acc(a[c][0]) | ((uint32_t)clip8_acc(a[c][1]) << 8) |
+                 ((uint32_t)clip8_acc(a[c][2]) << 16) | ((uint32_t)clip8_acc(a[c][3]) << 24);
       } else {
 #pragma unroll
         for (int c = 0; c < 3; ++c) w[c] = *(const uint32_t*)(htmp + c * cpl + (int64_t)y * S + 4 * xq);

@@ -33,6 +33,7 @@ int main(int argc, char** argv) {
   uint32_t sub = ((nbits + lanes - 1) / lanes + 31) & ~31u;
   int nl = std::min(lanes, (int)((nbits + sub - 1) / sub));
   std::vector<std::vector<Flags>> steps(nl);
+  long slow_len[18] = {0};
   long nsym = 0, nslow_ac = 0, nslow_dc = 0, ndc = 0, len_hist[18] = {0};
   for (int i = 0; i < nl; ++i) {
     uint32_t end = i == nl - 1 ? nbits : (i + 1) * sub;
@@ -49,7 +50,13 @@ int main(int argc, char** argv) {
       const uint32_t e = t->look[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
       fl.dc = dc;
       fl.boundary = dc;
-      if (!e) (dc ? fl.slow_dc : fl.slow_ac) = 1;
+      if (!e) {
+        (dc ? fl.slow_dc : fl.slow_ac) = 1;
+        int sym, len;
+        if (dc) huff_slow(cur, im.tabs->dc + comp, &sym, &len);
+        else huff_slow(cur, im.tabs->ac + comp, &sym, &len);
+        slow_len[len < 18 ? len : 17]++;
+      }
       huff_step<kSrcPadded>(cur, br, im, blk, z);
       steps[i].push_back(fl);
       ++nsym;
@@ -87,6 +94,8 @@ int main(int argc, char** argv) {
          (double)any_dc / iters, (double)all_dc / iters);
   printf("code length hist (fast path):");
   for (int l = 1; l <= 16; ++l) printf(" %d:%ld", l, len_hist[l]);
+  printf("\nslow code lengths:");
+  for (int l = 1; l <= 17; ++l) if (slow_len[l]) printf(" %d:%ld", l, slow_len[l]);
   printf("\n");
   return 0;
 }
