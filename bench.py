@@ -414,6 +414,10 @@ def main() -> None:
     import torch
     import torch.distributed as dist
 
+    # one GPU per rank; more ranks than GPUs (a rehearsal of the N-rank path on a smaller
+    # box) share them round-robin
+    ndev = max(1, torch.cuda.device_count())
+    local_rank = local_rank % ndev
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     if world > 1:

@@ -1172,6 +1172,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef DINO_IDCT_WGS
+#define DINO_IDCT_WGS 64
+#endif
+constexpr int kIdctWgs = DINO_IDCT_WGS;  // workgroups per image (grid-stride over its blocks)
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
   // (pass 2) accesses of a wave's 8 groups x 8 lanes hit 64 distinct banks
@@ -2736,7 +2740,7 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKHuff3, s, (k_huff3<<<grid3, kHuffThreads, kHuff3LdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
-  TIMED(tm, kKIdct, s, (k_idct<<<dim3(64, B), 256, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKIdct, s, (k_idct<<<dim3(kIdctWgs, B), 256, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   return hipGetLastError();
 }

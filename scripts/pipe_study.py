@@ -53,6 +53,42 @@ if __name__ == "__main__":
         torch.cuda.synchronize()
         return (time.perf_counter() - t) / steps * 1e3
 
+    # split: per slot a high-priority decode stream and a normal augment stream, so that
+    # the next batch's decode is dispatched ahead of this batch's augment workgroups
+    lo, hi = torch.cuda.Stream.priority_range()
+    orig = [e.stream for e in engs]
+    dstreams = [torch.cuda.Stream(dev, priority=hi) for _ in range(maxd)]
+    astreams = [torch.cuda.Stream(dev, priority=lo) for _ in range(maxd)]
+
+    def run_split(depth, prio=True):
+        def one(k):
+            j = k % depth
+            e = engs[j]
+            s = (k % 4) * B
+            ds = dstreams[j] if prio else orig[j]
+            as_ = astreams[j]
+            ds.wait_stream(as_)  # the ctx's workspaces: the slot's previous augment is done
+            e.stream = ds
+            e.decode(d_bytes, d_off[s:s + B + 1], B)
+            e.sample_params(cfg, 1, k, out=params[j])
+            as_.wait_stream(ds)
+            e.stream = as_
+            e.augment(cfg, params[j], views=views[j])
+        for k in range(2 * depth):
+            one(k)
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for k in range(steps):
+            one(k)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t) / steps * 1e3
+        for j, e in enumerate(engs):
+            e.stream = orig[j]
+        return ms
+
+    print("priority range", lo, hi, flush=True)
     for d in depths:
         r = {kind: round(run(kind, d), 3) for kind in ("decode", "augment", "full")}
+        r["split_prio"] = round(run_split(d, True), 3)
+        r["split_noprio"] = round(run_split(d, False), 3)
         print(f"depth {d}: ms/step {r}", flush=True)
