@@ -1173,7 +1173,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 #ifndef DINO_IDCT_WGS
-#define DINO_IDCT_WGS 64
+#define DINO_IDCT_WGS 32
 #endif
 constexpr int kIdctWgs = DINO_IDCT_WGS;  // workgroups per image (grid-stride over its blocks)
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
@@ -1362,7 +1362,7 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, uint32
 }
 
 #ifndef DINO_COLOR_WGS
-#define DINO_COLOR_WGS 32
+#define DINO_COLOR_WGS 16
 #endif
 constexpr int kColorWgs = DINO_COLOR_WGS;  // workgroups per image
 #ifndef DINO_COLOR_BATCH
@@ -1743,54 +1743,53 @@ __device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
 // source column c0; the taps' pixels start at xmin, so each group's 4 pixels are one
 // v_alignbyte of two consecutive LDS words (the upper word carried to the next
 // group).  Exact: the int32 sum equals Pillow's.
+#ifndef DINO_HRESIZE_ROWS_PER_LANE
+#define DINO_HRESIZE_ROWS_PER_LANE 2
+#endif
+constexpr int kHrRows = DINO_HRESIZE_ROWS_PER_LANE;  // rows per lane-task: the taps are read once for all of them
 __device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ rows, int pitch, int plane_bytes, int nr,
                                                  int r0, int x0, int sw, int c0, int S, const int4* __restrict__ hx,
                                                  const uint4* __restrict__ hg, uint8_t* __restrict__ tmp, int64_t cpl) {
-  // a lane computes one output column for two rows (the taps are read once for both)
-  const int npair = (nr + 1) >> 1;
-  for (int e = threadIdx.x; e < npair * sw; e += blockDim.x) {
+  // a lane computes one output column for kHrRows rows (the taps are read once for all)
+  const int ngrp = (nr + kHrRows - 1) / kHrRows;
+  for (int e = threadIdx.x; e < ngrp * sw; e += blockDim.x) {
     const int rp = e / sw, xl = e - rp * sw;
-    const int ra = 2 * rp;
-    const bool two = ra + 1 < nr;
-    const int rb = two ? ra + 1 : ra;  // odd band height: the second row repeats the first (not stored)
+    const int ra = kHrRows * rp;
     const int4 h = hx[xl];
     const int lo = h.x - c0, ng = h.y;
     const uint32_t sh = (uint32_t)(lo & 3);
-    const uint32_t* qa = (const uint32_t*)(rows + ra * pitch) + (lo >> 2);
-    const uint32_t* qb = (const uint32_t*)(rows + rb * pitch) + (lo >> 2);
     const int pw = plane_bytes >> 2;  // plane stride in words
-    int32_t acc[2][3][3];
+    const uint32_t* q[kHrRows];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < kHrRows; ++i)  // a band's last group repeats its last row (not stored)
+      q[i] = (const uint32_t*)(rows + min(ra + i, nr - 1) * pitch) + (lo >> 2);
+    int32_t acc[kHrRows][3][3];
+    uint32_t lw[kHrRows][3];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) acc[i][c][0] = acc[i][c][1] = acc[i][c][2] = 0;
-    uint32_t la[3], lb[3];
+    for (int i = 0; i < kHrRows; ++i)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      la[c] = qa[c * pw];
-      lb[c] = qb[c * pw];
-    }
+      for (int c = 0; c < 3; ++c) {
+        acc[i][c][0] = acc[i][c][1] = acc[i][c][2] = 0;
+        lw[i][c] = q[i][c * pw];
+      }
     for (int g = 0; g < ng; ++g) {
       const uint4 dg = hg[g * sw + xl];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const uint32_t ua = qa[c * pw + g + 1], ub = qb[c * pw + g + 1];
-        const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(ua, la[c], sh);
-        const int32_t pb = (int32_t)__builtin_amdgcn_alignbyte(ub, lb[c], sh);
-        acc[0][c][0] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.x, acc[0][c][0], false);
-        acc[0][c][1] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.y, acc[0][c][1], false);
-        acc[0][c][2] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.z, acc[0][c][2], false);
-        acc[1][c][0] = __builtin_amdgcn_sdot4(pb, (int32_t)dg.x, acc[1][c][0], false);
-        acc[1][c][1] = __builtin_amdgcn_sdot4(pb, (int32_t)dg.y, acc[1][c][1], false);
-        acc[1][c][2] = __builtin_amdgcn_sdot4(pb, (int32_t)dg.z, acc[1][c][2], false);
-        la[c] = ua;
-        lb[c] = ub;
-      }
+      for (int i = 0; i < kHrRows; ++i)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          const uint32_t u = q[i][c * pw + g + 1];
+          const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(u, lw[i][c], sh);
+          acc[i][c][0] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.x, acc[i][c][0], false);
+          acc[i][c][1] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.y, acc[i][c][1], false);
+          acc[i][c][2] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.z, acc[i][c][2], false);
+          lw[i][c] = u;
+        }
     }
     // int32 wrap-around is harmless: the true sum (Pillow's int32 ss) fits in int32
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (i == 1 && !two) break;
+    for (int i = 0; i < kHrRows; ++i) {
+      if (ra + i >= nr) break;
       const int64_t o = (int64_t)(r0 + ra + i) * S + x0 + xl;
 #pragma unroll
       for (int c = 0; c < 3; ++c)
