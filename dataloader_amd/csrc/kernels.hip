@@ -357,6 +357,7 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
   __shared__ int s_img;
   __shared__ int s_E;
   __shared__ uint32_t s_o0, s_r0;
+  __shared__ __attribute__((aligned(16))) uint8_t s_buf[kDestuffThreads * 16 + 16];  // a tile's output + alignment
   const int t = threadIdx.x;
   for (int item = blockIdx.x;; item += gridDim.x) {
     if (t == 0) s_img = ds_item_image(desc, B, item);
@@ -404,12 +405,19 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
         uint32_t tot;
         const uint32_t ex = block_excl_scan<kDestuffThreads>((uint32_t)__popc(ch.keep) | ((uint32_t)__popc(ch.rstm) << 16),
                                                              s_wave, &tot);
-        uint32_t o = o_run + (ex & 0xFFFFu), ro = rc_run + (ex >> 16);
-        for (uint32_t m = ch.keep | ch.rstm; m; m &= m - 1) {
-          const int j = __ffs(m) - 1;
-          if (ch.keep & (1u << j)) {
-            out[o++] = (uint8_t)((ch.wv[j >> 2] >> (8 * (j & 3))) & 255);
-          } else {
+        // the tile's kept bytes are compacted in LDS (byte j of the lane at its rank among
+        // the lane's kept bytes), then stored as aligned words: per-byte global stores in a
+        // loop over the kept bits would run 16 trips in every wave
+        const uint32_t lead = o_run & 3u, lo = lead + (ex & 0xFFFFu);
+#pragma unroll
+        for (int j = 0; j < 16; ++j)
+          if (ch.keep & (1u << j))
+            s_buf[lo + __popc(ch.keep & ((1u << j) - 1u))] = (uint8_t)((ch.wv[j >> 2] >> (8 * (j & 3))) & 255);
+        if (ch.rstm) {  // restart markers: their output offsets and sequence check
+          uint32_t ro = rc_run + (ex >> 16);
+          for (uint32_t m = ch.rstm; m; m &= m - 1) {
+            const int j = __ffs(m) - 1;
+            const uint32_t o = o_run + (ex & 0xFFFFu) + __popc(ch.keep & ((1u << j) - 1u));
             if ((int)ro < nrst_cap) rst[ro] = (int32_t)o;
             // RSTn must count 0..7 in order; otherwise libjpeg's read_restart_marker
             // resyncs (jdmarker.c jpeg_resync_to_restart), which k_prog restates
@@ -417,6 +425,22 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
             ++ro;
           }
         }
+        __syncthreads();
+        {
+          const uint32_t n = tot & 0xFFFFu, nw = (lead + n + 3) >> 2;
+          uint32_t* ow = (uint32_t*)(out + (o_run - lead));  // 4-byte aligned (ent_off is 16-aligned)
+          for (uint32_t w = t; w < nw; w += kDestuffThreads) {
+            const uint32_t b0 = 4 * w, b1 = b0 + 4;  // LDS bytes [b0, b1) = output bytes o_run - lead + b0 ...
+            const uint32_t v = *(const uint32_t*)(s_buf + b0);
+            if (b0 >= lead && b1 <= lead + n) {
+              ow[w] = v;
+            } else {  // a word shared with the previous or the next tile: its own bytes only
+              for (uint32_t k = b0; k < b1; ++k)
+                if (k >= lead && k < lead + n) out[o_run - lead + k] = (uint8_t)(v >> (8 * (k - b0)));
+            }
+          }
+        }
+        __syncthreads();
         o_run += tot & 0xFFFFu;
         rc_run += tot >> 16;
       }
