@@ -22,6 +22,6 @@ timeout -k 10 420 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/$
 timeout -k 10 300 python bench.py --mixed --no-cpu-baseline --images 8192 --unique 2048 --steps 16 \
   > gpurun_out/${TAG}_c3_bench.json 2> gpurun_out/${TAG}_c3_bench.err || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
-  python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
+  python bench.py --steps 20 --warmup 3 --no-cpu-baseline --depth 1 > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
 python scripts/show_bench.py gpurun_out/${TAG}_bench.json gpurun_out/${TAG}_c3_bench.json
 exit $rc
