@@ -35,11 +35,24 @@ namespace dino {
 // ---------------------------------------------------------------------------
 // k_parse
 // ---------------------------------------------------------------------------
-__global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets, int B,
-                        int max_dim, ImgDesc* __restrict__ desc) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B) return;
-  int64_t off = offsets[i], len = offsets[i + 1] - off;
+// One wave per image: the wave copies the file's first kParsePrefix bytes into LDS with
+// wide loads, then lane 0 walks the markers there (the walk is a chain of dependent byte
+// reads: LDS latency instead of global latency).  The parse depends on the length only
+// through bounds checks and scan_len = len - scan_off, so a walk that reaches SOS inside
+// the prefix is the walk over the whole file with scan_len corrected; one that does not
+// (a header longer than the prefix, a raw container) is redone on the global bytes.
+constexpr int kParsePrefix = 4096;
+__global__ void __launch_bounds__(64) k_parse(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
+                                              int B, int max_dim, ImgDesc* __restrict__ desc) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_head[kParsePrefix];
+  const int i = blockIdx.x;
+  const int64_t off = offsets[i], len = offsets[i + 1] - off;
+  const int64_t n = len < kParsePrefix ? len : kParsePrefix;
+  const uint8_t* src = bytes + off;
+#pragma unroll 8
+  for (int64_t k = threadIdx.x; k < n; k += 64) s_head[k] = src[k];
+  __syncthreads();
+  if (threadIdx.x != 0) return;
   ImgDesc d;
   if (len <= 0) {
     d.status = DINO_IMG_CORRUPT;
@@ -47,7 +60,11 @@ __global__ void k_parse(const uint8_t* __restrict__ bytes, const int64_t* __rest
     d.kind = 0;
     d.aug_status = 0;
   } else {
-    parse_jpeg(bytes + off, len, max_dim, &d);
+    parse_jpeg(s_head, n, max_dim, &d);
+    if (n < len) {
+      if (d.status == DINO_IMG_OK) d.scan_len = (int32_t)(len - d.scan_off);
+      else parse_jpeg(src, len, max_dim, &d);
+    }
   }
   desc[i] = d;
 }
@@ -1596,6 +1613,30 @@ __device__ bool params_valid(const dino_view_params& p, const ImgDesc& d, int S)
   return true;
 }
 
+// k_vsizes: one lane per view: validity and scratch bytes into plan[i] (htmp_off holds
+// the size and rcoef_off the offset of the coefficient tables inside it until k_vplan
+// places the view), so that the single-workgroup scan only reads packed records.
+__global__ void __launch_bounds__(256) k_vsizes(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                                int B, int nv, int n_global, int gsize, int lsize,
+                                                ViewPlan* __restrict__ plan) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * nv) return;
+  const ImgDesc& d = desc[i / nv];
+  const int S = (i % nv) < n_global ? gsize : lsize;
+  const int ok = d.status == DINO_IMG_OK && params_valid(prm[i], d, S);
+  int64_t a;
+  int32_t kh, kv;
+  view_sizes(prm[i], ok, &a, &kh, &kv);
+  ViewPlan vp;
+  vp.ok = ok;
+  vp.lsum = 0;
+  vp.kh = kh;
+  vp.kv = kv;
+  vp.htmp_off = a;
+  vp.rcoef_off = kh ? align16((int64_t)prm[i].crop_h * S * 3) : 0;
+  plan[i] = vp;
+}
+
 // Per-view scratch offsets: exclusive scan of the views' scratch sizes, or (when the
 // batch's views do not fit the augment workspace) greedy placement in batch order by
 // one lane.  A view that cannot be placed is not rendered and its image is marked
@@ -1611,14 +1652,7 @@ __global__ void __launch_bounds__(1024) k_vplan(ImgDesc* __restrict__ desc, cons
   int64_t local = 0;
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
-    if (i < N) {
-      int64_t a;
-      int32_t c, e;
-      const ImgDesc& d = desc[i / nv];
-      int S = (i % nv) < n_global ? gsize : lsize;
-      view_sizes(prm[i], d.status == DINO_IMG_OK && params_valid(prm[i], d, S), &a, &c, &e);
-      local += a;
-    }
+    if (i < N) local += plan[i].htmp_off;  // k_vsizes: the view's scratch bytes
   }
   part[t] = local;
   __syncthreads();
@@ -1633,19 +1667,11 @@ __global__ void __launch_bounds__(1024) k_vplan(ImgDesc* __restrict__ desc, cons
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
     if (i >= N) continue;
-    const ImgDesc& d = desc[i / nv];
-    int S = (i % nv) < n_global ? gsize : lsize;
-    int ok = d.status == DINO_IMG_OK && params_valid(prm[i], d, S);
-    int64_t a;
-    int32_t kh, kv;
-    view_sizes(prm[i], ok, &a, &kh, &kv);
-    ViewPlan vp;
-    vp.ok = ok && fits;
-    vp.lsum = 0;
-    vp.kh = kh;
-    vp.kv = kv;
+    ViewPlan vp = plan[i];
+    const int64_t a = vp.htmp_off;
+    vp.ok = vp.ok && fits;
     vp.htmp_off = base;
-    vp.rcoef_off = base + (kh ? align16((int64_t)prm[i].crop_h * S * 3) : 0);
+    vp.rcoef_off += base;
     plan[i] = vp;
     base += a;
   }
@@ -2751,7 +2777,7 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
   if (B <= 0) return hipSuccess;
-  TIMED(tm, kKParse, s, (k_parse<<<(B + 63) / 64, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc)));
+  TIMED(tm, kKParse, s, (k_parse<<<B, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc)));
   TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
   const int grid_ds = a.geom.grid_ds, grid1 = a.geom.grid1, grid3 = a.geom.grid3;
   TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
@@ -2812,6 +2838,8 @@ static hipError_t launch_augment_t(const AugmentArgs& a, hipStream_t s, KernelTi
 hipError_t launch_augment(const AugmentArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch, nv = a.cfg.n_global + a.cfg.n_local;
   if (B <= 0 || nv <= 0) return hipSuccess;
+  TIMED(tm, kKVplan, s, (k_vsizes<<<(B * nv + 255) / 256, 256, 0, s>>>(a.desc, a.params, B, nv, a.cfg.n_global,
+                                                                       a.cfg.global_size, a.cfg.local_size, a.plan)));
   TIMED(tm, kKVplan, s, (k_vplan<<<1, 1024, 0, s>>>(a.desc, a.params, B, nv, a.cfg.n_global, a.cfg.global_size,
                                                      a.cfg.local_size, a.aws_size, a.plan)));
   switch (a.cfg.out_dtype) {
