@@ -44,14 +44,29 @@ namespace dino {
 constexpr int kParsePrefix = 4096;
 __global__ void __launch_bounds__(64) k_parse(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
                                               int B, int max_dim, ImgDesc* __restrict__ desc) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_head[kParsePrefix];
+  __shared__ __attribute__((aligned(16))) uint8_t s_raw[kParsePrefix + 16];
   const int i = blockIdx.x;
   const int64_t off = offsets[i], len = offsets[i + 1] - off;
   const int64_t n = len < kParsePrefix ? len : kParsePrefix;
   const uint8_t* src = bytes + off;
-#pragma unroll 8
-  for (int64_t k = threadIdx.x; k < n; k += 64) s_head[k] = src[k];
+  // aligned 16-byte chunks from the chunk holding src (the copy starts `lead` bytes into
+  // s_raw); a chunk that would pass the end of the caller's buffer is copied bytewise
+  const int lead = (int)((uintptr_t)src & 15);
+  const uint4* base = (const uint4*)(src - lead);
+  const uint8_t* buf_end = bytes + offsets[B];
+  const int nchunks = (int)((lead + n + 15) >> 4);
+  for (int c = threadIdx.x; c < nchunks; c += 64) {
+    if ((const uint8_t*)(base + c + 1) <= buf_end) {
+      *(uint4*)(s_raw + 16 * c) = base[c];
+    } else {
+      for (int j = 0; j < 16; ++j) {
+        const int64_t k = 16 * (int64_t)c + j - lead;
+        if (k >= 0 && k < n) s_raw[16 * c + j] = src[k];
+      }
+    }
+  }
   __syncthreads();
+  const uint8_t* s_head = s_raw + lead;
   if (threadIdx.x != 0) return;
   ImgDesc d;
   if (len <= 0) {
@@ -2150,11 +2165,22 @@ __host__ __device__ __forceinline__ int final_tile_bytes(int S) {
   return 3 * (final_rows(S) + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
 }
 
+#ifndef DINO_BLUR_REG_KS
+#define DINO_BLUR_REG_KS 7
+#endif
+constexpr int kBlurRegKs = DINO_BLUR_REG_KS;  // blur kernels up to this size keep their weights in registers
 template <int KS, typename OutT>
 __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, int tp, int64_t tplane, int nr, int y0,
                                               int S, int ks_rt, const float* __restrict__ k2, bool solarize,
                                               const OutT* __restrict__ ntab, OutT* __restrict__ out) {
   const int ks = KS > 0 ? KS : ks_rt;
+  // the 2-D blur weights of a small kernel in registers: the tap loop then reads only
+  // the pixel rows from LDS (same products, same fma order)
+  float wreg[(KS > 0 && KS <= kBlurRegKs) ? KS * KS : 1];
+  if (KS > 0 && KS <= kBlurRegKs) {
+#pragma unroll
+    for (int k = 0; k < (KS > 0 && KS <= kBlurRegKs ? KS * KS : 0); ++k) wreg[k] = k2[k];
+  }
   const int nq = (S + 3) >> 2;
   const int64_t N = (int64_t)S * S;
   const bool vec_ok = (S & 3) == 0;
@@ -2170,7 +2196,25 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
       for (int j = 0; j < 4; ++j) val[j] = (u >> (8 * j)) & 255;
     } else {
       float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (KS > 0) {
+      if (KS > 0 && KS <= kBlurRegKs) {  // weights held in registers (loaded once per workgroup)
+        constexpr int NW = (KS + 3 + 3) / 4;
+#pragma unroll
+        for (int a = 0; a < KS; ++a) {
+          const uint32_t* row = (const uint32_t*)(pl + (y + a) * tp + x0);
+          uint32_t wv[NW];
+#pragma unroll
+          for (int q = 0; q < NW; ++q) wv[q] = row[q];
+#pragma unroll
+          for (int c = 0; c < KS; ++c) {
+            const float kk = wreg[a * KS + c];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int bi = c + j;
+              acc[j] = fmaf(kk, (float)((wv[bi >> 2] >> (8 * (bi & 3))) & 255u), acc[j]);
+            }
+          }
+        }
+      } else if (KS > 0) {
         constexpr int NW = (KS + 3 + 3) / 4;
 #pragma unroll 1
         for (int a = 0; a < KS; ++a) {
