@@ -2430,9 +2430,10 @@ __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __rest
       });
   __syncthreads();
   const int cmean = jp.has_contrast ? contrast_mean_from_sum(wg_sum(lsum, s_part), N) : 0;
-  // the ops after contrast, in place on the interior
+  // the ops after contrast, in place on the interior (none: no jitter and no grayscale)
   const FastDiv ds((uint32_t)S);
-  for (int e = threadIdx.x; e < S * S; e += blockDim.x) {
+  const bool stage1 = jp.has_contrast || jp.n_post > 0 || p.gray;
+  for (int e = threadIdx.x; stage1 && e < S * S; e += blockDim.x) {
     const int y = (int)ds.div((uint32_t)e), x = e - y * S;
     uint8_t* q = in0 + y * tp + x;
     int r = q[0], g = q[tplane], bb = q[2 * tplane];
@@ -2852,7 +2853,8 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   if (nvc <= 0) return hipSuccess;
   const int kfin = v0 == 0 ? kKFinalGlobal : kKFinalLocal;
   const int kvert = v0 == 0 ? kKVertGlobal : kKVertLocal;
-  TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), 256, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
+  const int rc_threads = S < 256 ? (S + 63) / 64 * 64 : 256;  // one lane per output column
+  TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), rc_threads, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
   TIMED(tm, kKHresize, s,
         (k_hresize<<<dim3(kHresizeWgs, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
   if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS
