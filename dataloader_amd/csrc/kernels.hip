@@ -1966,7 +1966,10 @@ struct FastDiv {
 // band of vert_rows(S) output rows; adds the band's L sum to the view's counter.
 // Fast path (planar temp rows, S % 4 == 0): a lane produces 4 adjacent pixels
 // from one 4-byte load per channel and tap and stores one word per plane.
-constexpr int kVertRows = 8;
+#ifndef DINO_VERT_ROWS
+#define DINO_VERT_ROWS 8
+#endif
+constexpr int kVertRows = DINO_VERT_ROWS;
 // rows per workgroup: 16 for the small (local) views, whose 8-row bands are short
 __host__ __device__ __forceinline__ int vert_rows(int S) { return S > 128 ? kVertRows : 2 * kVertRows; }
 
