@@ -9,10 +9,24 @@ colour jitter, grayscale, blur, solarize, normalize -> bf16 NCHW) — reference
 
 Workload (BASELINE.json configs[1]): per GPU, a 50 000-image dataset of
 synthetic textured 640x480 q85 4:2:0 JPEGs resident in HBM (``--unique``
-distinct encodes tiled to ``--images``), batch 512.  Multi-GPU: one process per
-GPU (torchrun), each rank with its own images and seed (seed + rank), no
-collective on the data path; a barrier + MAX over ranks brackets the timed
-region (weak scaling).
+distinct encodes tiled to ``--images``), batch 512.
+
+Multi-GPU (configs[3], weak scaling): one process per GPU, each rank with its
+own images and seed (seed + rank, reference config.py:204; shard ``i % world ==
+rank``, hpc_source.py:154-156), no collective on the data path.  Either the
+driver starts the ranks (torchrun: RANK/WORLD_SIZE/LOCAL_RANK in the env), or
+``bench.py --gpus N`` starts them itself, before anything touches a GPU.  Every
+rank needs a device of its own: with fewer visible GPUs than ranks the bench
+refuses, unless ``--rehearsal`` (ranks then share devices round-robin and the
+line says so: ``"rehearsal": true``, ``n_gpus`` = distinct devices).  A gloo
+barrier + MAX of the per-rank elapsed times brackets the timed region.
+
+At N = 1 the line also carries the other BASELINE configs, each timed the same
+way in this process: ``c3`` (configs[2]: mixed resolution + iBOT masks),
+``fp8`` (configs[4]: E4M3 epilogue), ``c2_dri`` (C2 with restart markers,
+SURVEY §8(d)) and ``e2e`` (configs[4]: /dev/shm tar shards through
+``MI355XBackend.build_pipeline`` + ``build_pipeline_iterator``, the drop-in
+path), plus the CPU baseline.
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """
@@ -23,6 +37,8 @@ import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -36,10 +52,12 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "images/sec decode+10-crop, device-resident (JPEG bytes in HBM), 1/2/4/8 GPU"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+VFINAL_MAX_S = 128  # kernels.hip kVFinalMaxS: views up to this size run k_vfinal (vertical pass + epilogue fused)
 
 
+# ----------------------------------------------------------------------------- synthetic data
 def _gen_one(args):
-    w, h, seed, mixed, prog = args
+    w, h, seed, mixed, prog, rst = args
     from dataloader_amd.synthetic import encode_jpeg, textured_rgb
     rng = np.random.default_rng(seed)
     if mixed:
@@ -47,16 +65,19 @@ def _gen_one(args):
         aspect = float(rng.uniform(0.75, 4.0 / 3.0))
         long_ = max(short, int(round(short * max(aspect, 1.0 / aspect))))
         w, h = (long_, short) if rng.random() < 0.5 else (short, long_)
-    return encode_jpeg(textured_rgb(w, h, rng), quality=85, progressive=prog)
+    return encode_jpeg(textured_rgb(w, h, rng), quality=85, progressive=prog, restart_mcus=rst)
 
 
-def make_unique(n: int, w: int, h: int, base_seed: int, mixed: bool, procs: int, prog_frac: float = 0.0) -> list[bytes]:
-    # 'spawn': never fork a process that may already hold a HIP context
-    # every round(1 / prog_frac)-th encode is progressive (libjpeg's simple progression)
+def make_unique(n: int, w: int, h: int, base_seed: int, mixed: bool, procs: int, prog_frac: float = 0.0,
+                restart_mcus: int = 0) -> list[bytes]:
+    """``n`` distinct textured JPEGs (every round(1 / prog_frac)-th one progressive, libjpeg's
+    simple progression; ``restart_mcus`` > 0: a DRI marker with that interval)."""
     step = int(round(1.0 / prog_frac)) if prog_frac > 0 else 0
-    jobs = [(w, h, base_seed * 100003 + k, mixed, bool(step) and k % step == step - 1) for k in range(n)]
+    jobs = [(w, h, base_seed * 100003 + k, mixed, bool(step) and k % step == step - 1, restart_mcus)
+            for k in range(n)]
     if procs <= 1:  # in-process (profiler runs: no worker processes to tear down)
         return [_gen_one(j) for j in jobs]
+    # 'spawn': never fork a process that may already hold a HIP context
     pool = get_context("spawn").Pool(procs)
     try:
         return pool.map(_gen_one, jobs, chunksize=4)
@@ -69,21 +90,21 @@ def jpeg_meta(j: bytes):
     import io
 
     from PIL import Image
-    im = Image.open(io.BytesIO(j))
-    return im.size
+    return Image.open(io.BytesIO(j)).size
 
 
-def sparse_entry_bytes(pipe, dims_420: list[bytes]) -> tuple[float, float]:
+# ----------------------------------------------------------------------------- algorithmic bytes
+def sparse_entry_bytes(pipe, jpegs: list[bytes]) -> float:
     """Mean bytes of the sparse coefficient entries k_huff1 / k_huff3 wrote per block, read
     back from the block records of the last decoded batch (dino_debug_region 2): a block
     record {first halfword, n16 | n32 << 7 | DC << 16} gives n16 halfword entries + n32
     u32 entries (+ 1 alignment halfword); 8 bytes of record per block on top."""
     eng = pipe._last.engine
     tot_e = tot_b = 0.0
-    for i in range(min(eng.last_batch, 16, len(dims_420))):
-        if b"\xff\xc2" in dims_420[i][:4096]:  # progressive (k_prog's dense buffer, not entries)
+    for i in range(min(eng.last_batch, 16, len(jpegs))):
+        if b"\xff\xc2" in jpegs[i][:4096]:  # progressive (k_prog's dense buffer, not entries)
             continue
-        w, h = jpeg_meta(dims_420[i])
+        w, h = jpeg_meta(jpegs[i])
         nblk = ((w + 15) // 16) * ((h + 15) // 16) * 6
         reg = eng.debug_region(i, 2, nblk * 256 + nblk * 8).cpu().numpy()
         y = reg[nblk * 256:nblk * 256 + nblk * 8].view(np.uint32)[1::2]
@@ -91,7 +112,7 @@ def sparse_entry_bytes(pipe, dims_420: list[bytes]) -> tuple[float, float]:
         n32 = ((y >> 7) & 0x7F).astype(np.int64)
         tot_e += float((2 * n16 + 4 * n32 + 2 * (n32 > 0)).sum())
         tot_b += nblk
-    return (tot_e / tot_b if tot_b else 0.0), 8.0
+    return tot_e / tot_b if tot_b else 0.0
 
 
 def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int, recs=None,
@@ -109,16 +130,19 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     # 4:2:0 coefficient count: luma + 2 quarter-size chroma, padded to 16x16 MCUs
     nblk = [((w + 15) // 16) * ((h + 15) // 16) * 6 for w, h in dims]
     blocks = float(np.mean(nblk))
+
     # images k_huff1 finishes itself (one 2 Mbit segment, lane ranges <= 3072 bits,
     # kernels.hip huff_single_segment); the others are written by k_huff3
-    def fused(nbytes):
-        nbits = nbytes * 8
+    def fused(j):
+        if b"\xff\xdd" in j[:2048]:  # restart intervals: k_huff3 decodes one interval per lane
+            return False
+        nbits = len(j) * 8
         if nbits > 2048 * 1024:
             return False
         n = max(1, min(256, -(-nbits // 1024)))
         sub = max(32, (-(-nbits // n) + 31) // 32 * 32)
         return sub <= 3072
-    fz = [fused(len(j)) for j in jpegs]
+    fz = [fused(j) for j in jpegs]
     blk_fused = float(np.mean([b if f else 0 for b, f in zip(nblk, fz)]))
     s_unfused = float(np.mean([len(j) if not f else 0 for j, f in zip(jpegs, fz)]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
@@ -153,9 +177,7 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     return ab
 
 
-VFINAL_MAX_S = 128  # kernels.hip kVFinalMaxS: views up to this size run k_vfinal (vertical pass + epilogue fused)
-
-
+# ----------------------------------------------------------------------------- CPU baseline
 def _measure(fn, warmup: int, iters: int, budget_s: float) -> dict:
     """scripts/benchmark.py:161-190 of the reference: warm-up, then per-iteration wall times ->
     mean/std/p50/p95 (ms).  ``iters`` is capped so that the timed part stays within ``budget_s``."""
@@ -248,7 +270,6 @@ def cpu_baseline(c2_jpegs, c1_jpegs, budget_s: float = 10.0, procs: int = 16) ->
     * best_cpu: a process pool over the box's CPU share, decoding once per image.
     Per-batch timing as reference scripts/benchmark.py:161-190 (mean/std/p50/p95)."""
     import torch
-    from multiprocessing import get_context
     torch.set_num_threads(1)
     B = 32
     workers = min(B, os.cpu_count() or 4, 16)                    # cpu.py:286
@@ -283,6 +304,205 @@ def cpu_baseline(c2_jpegs, c1_jpegs, budget_s: float = 10.0, procs: int = 16) ->
     return out
 
 
+# ----------------------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def visible_devices() -> int:
+    """GPUs this process may use.  ``torch.cuda.device_count()`` does not initialise a
+    device on this image, so the launcher may still start rank processes afterwards."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+_VIS_VARS = ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")
+
+
+def physical_device(device: int) -> str:
+    """A name of the GPU behind local device index ``device`` that is comparable across
+    ranks: the visible-devices entry when a launcher isolates ranks that way, else the index."""
+    for var in _VIS_VARS:
+        v = os.environ.get(var)
+        if v:
+            ids = [x.strip() for x in v.split(",") if x.strip()]
+            return f"{var}:{ids[device]}" if device < len(ids) else f"{var}:?{device}"
+    return str(device)
+
+
+def check_devices(world: int, devices: int, rehearsal: bool) -> None:
+    """One GPU per rank, or an explicit rehearsal (ranks share devices round-robin).  With
+    per-rank visible-device isolation each rank sees one device: the distinct-device check
+    then runs over the gathered physical names (``check_distinct``)."""
+    if devices < 1:
+        raise SystemExit(f"bench.py: no GPU visible (need {world}); nothing to measure")
+    isolated = any(os.environ.get(v) for v in _VIS_VARS) and "DINO_BENCH_LAUNCHED" not in os.environ
+    if world > devices and not rehearsal and not isolated:
+        raise SystemExit(f"bench.py: {world} ranks but only {devices} GPU(s) visible; every rank needs a GPU of "
+                         f"its own (pass --rehearsal to let ranks share devices; the line then says so)")
+
+
+def check_distinct(per_rank: list, rehearsal: bool) -> int:
+    """Distinct physical GPUs over the ranks; refuse sharing unless it is a rehearsal."""
+    names = [r["physical"] for r in per_rank]
+    distinct = len(set(names))
+    if distinct < len(names) and not rehearsal:
+        raise SystemExit(f"bench.py: {len(names)} ranks share {distinct} GPU(s) ({names}); pass --rehearsal "
+                         "to allow it (the line then says so)")
+    return distinct
+
+
+def launch_ranks(n: int, argv: list[str], devices: int, rehearsal: bool = False,
+                 cmd: list[str] | None = None, extra_env: dict | None = None) -> int:
+    """``bench.py --gpus N`` without a launcher env: start N rank processes (this script
+    again, or ``cmd``) with RANK / WORLD_SIZE / LOCAL_RANK / LOCAL_WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set, wait for all of them and return the first
+    non-zero exit code (the others are terminated).  Nothing here touches a GPU."""
+    check_devices(n, devices, rehearsal)
+    port = _free_port()
+    cmd = cmd or [sys.executable, "-u", str(Path(__file__).resolve()), *argv]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update({"RANK": str(r), "WORLD_SIZE": str(n), "LOCAL_RANK": str(r), "LOCAL_WORLD_SIZE": str(n),
+                    "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "DINO_BENCH_LAUNCHED": "1"})
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                r = p.poll()
+                if r is None:
+                    continue
+                pending.remove(p)
+                if r != 0 and rc == 0:
+                    rc = r
+                    for q in pending:  # one rank failed: the others would wait at a barrier forever
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc
+
+
+# ----------------------------------------------------------------------------- timing
+def run_leg(pipe, d_bytes, d_off, n_img: int, B: int, steps: int, warmup: int, world: int, dist,
+            maskgen=None, serial: bool = True) -> dict:
+    """Time exactly ``steps`` device-resident batches (after ``warmup``), bracketed by a
+    barrier + synchronize; then (``serial``) the same number of batches one at a time with
+    the library's HIP-event timer (a kernel's events must not also span the other slots'
+    concurrently running kernels)."""
+    import torch
+    ccfg = pipe._cfg(*pipe._sizes())
+    views = [sl.engine.alloc_views(ccfg, B) for sl in pipe._slots]  # one output set per in-flight slot
+    n_batches = max(1, n_img // B)
+
+    def step(k: int):
+        s = (k % n_batches) * B
+        pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views[k % pipe.depth])
+        if maskgen is not None:  # one mask per batch, broadcast to [B, H*W] (loader.py:585-590)
+            maskgen.generate(1).expand(B, -1)
+
+    for k in range(warmup):
+        step(k)
+    torch.cuda.synchronize()
+    st = pipe.last_status()
+    if (st != 0).any():
+        raise RuntimeError(f"decode failures in warmup batch: {np.unique(st, return_counts=True)}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(warmup + k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    out = {"dt": dt, "ktimes": {}, "t_ser": None, "last_batch": None}
+    if serial:
+        pipe.set_timing(True)
+        pipe.kernel_times()
+        t_ser = time.perf_counter()
+        for k in range(steps):
+            step(warmup + steps + k)
+            torch.cuda.synchronize()
+        out["t_ser"] = time.perf_counter() - t_ser
+        out["ktimes"] = pipe.kernel_times()
+        pipe.set_timing(False)
+        k_last = warmup + 2 * steps - 1  # the batch the last slot still holds
+        out["last_batch"] = (k_last % n_batches) * B
+    out["recs"] = pipe.last_params()
+    return out
+
+
+def load_traffic(tag: str) -> tuple[dict, str | None]:
+    """Per-launch HBM bytes per kernel from the newest committed PMC summary of this
+    workload (``profiles/r*_pmc_<tag>.json``: FETCH_SIZE and WRITE_SIZE passes of this bench
+    under rocprofv3, scripts/gpu_pmc.sh; corrections of MI355X_MICROARCH.md §HBM)."""
+    cands = sorted((ROOT / "profiles").glob(f"r*_pmc_{tag}.json"), reverse=True)
+    if tag == "c2":
+        cands.append(ROOT / "profiles" / "r02_pmc_traffic.json")
+    for f in cands:
+        if f.exists():
+            try:
+                d = json.loads(f.read_text())
+                return {k: v.get("hbm_bytes_per_launch") for k, v in d.items() if not k.startswith("_")}, f.name
+            except Exception:  # noqa: BLE001
+                pass
+    return {}, None
+
+
+def summarize(leg: dict, ab: dict, B: int, steps: int, world: int, tag: str) -> dict:
+    """value / ms per step / per-kernel times / the dominant kernel's roofline for one leg."""
+    dt = leg["dt"]
+    per_kernel = {k: {"avg_ms": (ms / n if n else 0.0), "launches": n, "total_ms": ms}
+                  for k, (ms, n) in leg["ktimes"].items()}
+    traffic, traffic_src = load_traffic(tag)
+    out = {"value": round(world * steps * B / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+           "mean_jpeg_bytes": round(ab["s_jpeg"]), "mean_pixels": round(ab["pixels"])}
+    if per_kernel:
+        dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
+        # SURVEY §8(d): algorithmic bytes per image = S_jpeg + sum over views of 3 S^2 x out bytes;
+        # one launch of any Stage-3 kernel processes the batch of B images
+        bytes_launch = ab["path"] * B
+        achieved = bytes_launch / (per_kernel[dom]["avg_ms"] * 1e-3) / 1e9
+        dom_traffic = traffic.get(dom)
+        out["roofline"] = {
+            "bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": dom_traffic, "kernel": dom,
+            "algorithmic_bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(per_kernel[dom]["avg_ms"], 4),
+            "definition": "SURVEY 8(d) bytes per image (S_jpeg + 3*sum(S_v^2)*out_bytes) x batch / dominant "
+                          "kernel's mean launch time (HIP events on its stream, serialized pass after the timed region)",
+            "traffic_source": f"profiles/{traffic_src}" if traffic_src else None}
+        roof_all = {}
+        for k, v in per_kernel.items():
+            if ab.get(k) and v["avg_ms"] > 0:
+                gbs = ab[k] * B / (v["avg_ms"] * 1e-3) / 1e9
+                roof_all[k] = {"achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 4),
+                               "avg_ms": round(v["avg_ms"], 4), "interface_bytes_per_launch": int(ab[k] * B),
+                               "traffic_bytes_per_launch": traffic.get(k)}
+        out["roofline_kernels"] = roof_all
+        out["kernels_ms_per_step"] = {k: round(v["total_ms"] / steps, 4) for k, v in per_kernel.items() if v["launches"]}
+        step_traffic = sum((traffic.get(k) or 0) * v["launches"] / max(steps, 1) for k, v in per_kernel.items()) \
+            if traffic else None
+        path_gbs = ab["path"] * B * world / (dt / steps) / 1e9
+        out["path_roofline"] = {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
+                                "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5),
+                                "pmc_traffic_bytes_per_step": int(step_traffic) if step_traffic else None,
+                                "algorithmic_bytes_per_step": int(ab["path"] * B)}
+    if leg.get("t_ser") is not None:
+        out["serialized_ms_per_step"] = round(leg["t_ser"] / steps * 1e3, 3)
+    return out
+
+
 def make_shards(jpegs, shard_size: int) -> list[bytes]:
     """WebDataset tar shards shaped like the reference fixtures (sample_%06d.jpg + .json)."""
     import io
@@ -301,17 +521,24 @@ def make_shards(jpegs, shard_size: int) -> list[bytes]:
     return shards
 
 
-def run_e2e(args, uniq, rank: int, world: int, dev, cfg, B: int) -> dict:
-    """C5 end-to-end: shards in /dev/shm (reference cache file format) -> dino_tar_index ->
-    dino_gather into pinned staging -> H2D -> Stage 3, batches in flight as the main run."""
+def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
+    """C5 end-to-end, through the drop-in path: tar shards in /dev/shm (reference cache file
+    format) -> ShardBatchFeeder (native tar index) -> ``MI355XBackend.build_pipeline`` (prefetch
+    thread: dino_gather into pinned staging + dino_probe) + ``build_pipeline_iterator``
+    (``PipelineConfig.gpu_queue`` batches in flight) -> H2D -> Stage 3; ``next()`` hands each
+    batch's views to the caller's stream as DINODataLoader consumes them (dali_node.py:110)."""
     import torch
-    import torch.distributed as dist
 
-    from dataloader_amd.pipeline import MI355XAugPipeline
-    from dataloader_amd.sharding import rank_seed
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import DinoV2AugSpec, PipelineConfig
     from dataloader_amd.tario import ShardBatchFeeder, ShmShardCache
 
-    n = (args.warmup + args.steps + 1) * B
+    pcfg = PipelineConfig(device_id=torch.cuda.current_device(), seed=1234 + rank, gpu_queue=args.gpu_queue,
+                          output_dtype=args.dtype if args.dtype != "fp8" else "bf16",
+                          dali_fp8_output=args.dtype == "fp8")
+    backend = MI355XBackend()
+    depth = backend.queue_depth(pcfg, B)
+    n = (args.warmup + args.steps + depth + 4) * B
     jpegs = [uniq[i % len(uniq)] for i in range(n)]
     shards = make_shards(jpegs, args.shard_size)
     cache = ShmShardCache(job_id=f"dino_bench_{os.getpid()}", base_dir="/dev/shm", max_gb=64.0)
@@ -321,65 +548,51 @@ def run_e2e(args, uniq, rank: int, world: int, dev, cfg, B: int) -> dict:
             cache.put(p, t)  # Stage 1 (filesystem -> /dev/shm) is outside the timed region
         del shards
         feeder = ShardBatchFeeder(cache, paths, B, nthreads=args.gather_threads)
-        pipe = MI355XAugPipeline(feeder, cfg, B, seed=rank_seed(1234, rank), out_dtype=args.dtype,
-                                 device=dev.index, max_image_dim=4096 if args.mixed else 2048, depth=args.depth)
+        spec = DinoV2AugSpec(aug_cfg=cfg)
+        pipe = backend.build_pipeline(feeder, spec, pcfg, None)
+        it = backend.build_pipeline_iterator(pipe, spec, spec.output_map, B)
         for _ in range(args.warmup):
-            pipe._enqueue_one()
-        pipe.wait()
+            out = next(it)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        feeder.index_seconds = 0.0
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            pipe._enqueue_one()
-        pipe.wait()
+            out = next(it)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
-        st = pipe.last_status()
-        if (st != 0).any():
-            raise RuntimeError(f"e2e decode failures: {np.unique(st, return_counts=True)}")
-        shards_opened = feeder._shard
+        assert len(out) == 1 and len(out[0]) == cfg.n_views
+        st = pipe.flush_stats()
+        bad = {k: v for k, v in st["status"].items() if k != 0}
+        if bad:
+            raise RuntimeError(f"e2e decode failures: {bad}")
+        res = {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
+               "e2e_ms_per_step": round(dt / args.steps * 1e3, 3),
+               "e2e_shard_prepare_ms_total": round(feeder.index_seconds * 1e3, 3),
+               "e2e_shard_wait_ms_total": round(feeder.wait_seconds * 1e3, 3),
+               "e2e_gather_threads": args.gather_threads, "e2e_batches_in_flight": pipe.depth,
+               "e2e_prefetch_ahead": pipe.prefetch_ahead,
+               "e2e_path": "/dev/shm tar shards (shard_cache file format) -> ShardBatchFeeder -> "
+                           "MI355XBackend.build_pipeline (prefetch thread: dino_gather into pinned staging, "
+                           "dino_probe) + build_pipeline_iterator -> H2D -> Stage 3"}
         feeder.close()
         pipe.close()
-        if world > 1:
-            t = torch.tensor([dt], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
-                "e2e_ms_per_step": round(dt / args.steps * 1e3, 3),
-                "e2e_shard_prepare_ms_total": round(feeder.index_seconds * 1e3, 3),
-                "e2e_shard_wait_ms_total": round(feeder.wait_seconds * 1e3, 3),
-                "e2e_shards": shards_opened, "e2e_gather_threads": args.gather_threads,
-                "e2e_path": "/dev/shm tar shards (shard_cache file format) -> dino_tar_index -> dino_gather "
-                            "(pinned) -> H2D -> Stage 3"}
+        return res
     finally:
         cache.close(remove=True)
 
 
-PMC_FILES = ("r02_pmc_traffic.json", "r01_s7_pmc_traffic.json")
-
-
-def load_traffic() -> tuple[dict, str | None]:
-    """Per-launch HBM bytes per kernel from the newest committed PMC summary (FETCH_SIZE and
-    WRITE_SIZE passes of this bench under rocprofv3, scripts/gpu_pmc.sh; corrections of
-    MI355X_MICROARCH.md §HBM): {kernel: bytes}, file name."""
-    for name in PMC_FILES:
-        f = ROOT / "profiles" / name
-        if f.exists():
-            try:
-                d = json.loads(f.read_text())
-                return {k: v.get("hbm_bytes_per_launch") for k, v in d.items() if not k.startswith("_")}, name
-            except Exception:  # noqa: BLE001
-                pass
-    return {}, None
-
-
-def main() -> None:
+# ----------------------------------------------------------------------------- main
+def build_parser() -> argparse.ArgumentParser:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); without a launcher env bench.py starts them itself")
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than GPUs (round-robin sharing; the line is marked as a rehearsal)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + rank aggregation only, no GPU work (CPU tests of the N-rank path)")
     ap.add_argument("--steps", type=int, default=98, help="timed steps (98 x 512 covers the 50k set once)")
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=512)
@@ -392,109 +605,172 @@ def main() -> None:
     ap.add_argument("--mixed", action="store_true", help="C3: short side U{224..1600} (+ iBOT masks)")
     ap.add_argument("--progressive-frac", type=float, default=0.0,
                     help="share of progressive encodes (web datasets hold some; decoded by k_prog)")
+    ap.add_argument("--restart-mcus", type=int, default=0,
+                    help="restart interval (MCUs) of the encodes: the DRI variant of SURVEY 8(d)")
     ap.add_argument("--masks", action="store_true", help="iBOT masks per batch (default with --mixed)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="time budget of each CPU-baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="N = 1: skip the c3 / fp8 / c2_dri / e2e legs (profiling runs)")
+    ap.add_argument("--extra-unique", type=int, default=1024, help="distinct encodes of the c3 / c2_dri legs")
     ap.add_argument("--h2d", action="store_true", help="also time the H2D-inclusive rate (pinned host bytes)")
     ap.add_argument("--kernel-json", default="", help="write per-kernel times here (rank 0)")
-    ap.add_argument("--e2e", action="store_true",
-                    help="C5: also time tar shards in /dev/shm -> native index -> pinned gather -> H2D -> kernels")
-    ap.add_argument("--shard-size", type=int, default=1000, help="samples per synthetic tar shard (--e2e)")
-    ap.add_argument("--gather-threads", type=int, default=8, help="dino_gather copier threads (--e2e)")
-    args = ap.parse_args()
+    ap.add_argument("--e2e", action="store_true", help="C5 end-to-end leg even with --no-extras or N > 1")
+    ap.add_argument("--gpu-queue", type=int, default=6, help="PipelineConfig.gpu_queue of the e2e leg")
+    ap.add_argument("--shard-size", type=int, default=1000, help="samples per synthetic tar shard (e2e)")
+    ap.add_argument("--gather-threads", type=int, default=8, help="dino_gather copier threads (e2e)")
+    return ap
 
+
+def _procs(args, world: int) -> int:
+    if args.procs >= 0:
+        return args.procs
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 4
+    return max(2, min(16, share // max(1, world)))
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = build_parser().parse_args(argv)
+    launched = "WORLD_SIZE" in os.environ
+    if not launched and (args.gpus or 1) > 1:
+        devices = int(os.environ.get("DINO_BENCH_DEVICES", args.gpus)) if args.dry_run else visible_devices()
+        return launch_ranks(args.gpus, argv, devices, args.rehearsal)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dry_run:
+        return dry_run(args, rank, world, local_rank)
+    return run_rank(args, rank, world, local_rank)
+
+
+def _init_group(world: int):
+    import torch.distributed as dist
+    if world > 1:
+        # barrier + MAX / gather of the per-rank times only: a CPU (gloo) group, no RCCL on this path
+        dist.init_process_group("gloo")
+    return dist
+
+
+def _rank_report(dist, world: int, rank: int, device: int, dt: float, steps: int, B: int) -> tuple[float, list]:
+    """MAX of the per-rank elapsed times and every rank's own rate (gloo)."""
+    mine = {"rank": rank, "device": device, "physical": physical_device(device),
+            "ms_per_step": round(dt / steps * 1e3, 3), "images_per_s": round(steps * B / dt, 1)}
+    if world == 1:
+        return dt, [mine]
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return max(r["ms_per_step"] for r in allr) * steps / 1e3, allr
+
+
+def dry_run(args, rank: int, world: int, local_rank: int) -> int:
+    """The N-rank plumbing without a GPU: env, gloo group, per-rank report, the rank-0 line."""
+    dist = _init_group(world)
+    devices = int(os.environ.get("DINO_BENCH_DEVICES", world))
+    check_devices(world, devices, args.rehearsal)
+    B, steps = args.batch, args.steps
+    dt = 0.001 * steps * (1 + 0.1 * rank)  # a fake, rank-dependent elapsed time
+    if world > 1:
+        dist.barrier()
+    dt_max, per_rank = _rank_report(dist, world, rank, local_rank % devices, dt, steps, B)
+    distinct = check_distinct(per_rank, args.rehearsal)
+    if rank == 0:
+        line = {"metric": METRIC, "value": round(world * steps * B / dt_max, 1), "unit": "images/s",
+                "n_gpus": distinct, "ranks": world, "steps": steps, "warmup": args.warmup,
+                "ms_per_step": round(dt_max / steps * 1e3, 3), "dry_run": True, "per_rank": per_rank,
+                "env": {"RANK": os.environ.get("RANK"), "WORLD_SIZE": os.environ.get("WORLD_SIZE"),
+                        "LOCAL_RANK": os.environ.get("LOCAL_RANK"), "MASTER_ADDR": os.environ.get("MASTER_ADDR")}}
+        if world > distinct:
+            line["rehearsal"] = True
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+def run_rank(args, rank: int, world: int, local_rank: int) -> int:
+    extras = world == 1 and not args.no_extras
+    procs = _procs(args, world)
     # synthetic data first, before anything initialises the GPU in this process
-    procs = args.procs if args.procs >= 0 else min(16, os.cpu_count() or 4)
-    uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs, args.progressive_frac)
+    uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs, args.progressive_frac,
+                       args.restart_mcus)
+    if extras:
+        print(f"bench: rank {rank}: synthesising the c3 / c2_dri sets", file=sys.stderr, flush=True)
+        uniq_c3 = make_unique(args.extra_unique, 0, 0, 11 + rank, True, procs) if not args.mixed else None
+        uniq_dri = make_unique(args.extra_unique, args.width, args.height, 21 + rank, False, procs, 0.0, 4) \
+            if not args.restart_mcus else None
 
     import torch
-    import torch.distributed as dist
-
-    # one GPU per rank; more ranks than GPUs (a rehearsal of the N-rank path on a smaller
-    # box) share them round-robin
-    ndev = max(1, torch.cuda.device_count())
-    local_rank = local_rank % ndev
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    if world > 1:
-        # barrier + MAX of the elapsed time only: a CPU (gloo) group, no RCCL on this path
-        dist.init_process_group("gloo")
+    devices = visible_devices()
+    check_devices(world, devices, args.rehearsal)
+    device = local_rank % devices  # distinct per rank unless --rehearsal
+    torch.cuda.set_device(device)
+    dev = torch.device("cuda", device)
+    dist = _init_group(world)
 
     from dataloader_amd.config import DINOAugConfig
     from dataloader_amd.engine import pack_jpegs
+    from dataloader_amd.masking import MaskingGenerator
     from dataloader_amd.pipeline import MI355XAugPipeline
     from dataloader_amd.sharding import rank_seed
 
-    n_img = args.images
-    jpegs = [uniq[i % len(uniq)] for i in range(n_img)]
-    host_buf, offsets = pack_jpegs(jpegs, pin=True)
-    d_bytes = host_buf.to(dev)
-    d_off = offsets.to(dev)
-    torch.cuda.synchronize()
-
     cfg = DINOAugConfig()
     B = args.batch
-    pipe = MI355XAugPipeline(None, cfg, B, seed=rank_seed(1234, rank), out_dtype=args.dtype, device=local_rank,
-                             max_image_dim=4096 if args.mixed else 2048, depth=args.depth,
-                             workspace_bytes=B * (40 << 20) if args.mixed else 0)
-    ccfg = pipe._cfg(cfg.global_crop_size, cfg.local_crop_size)
-    views = [sl.engine.alloc_views(ccfg, B) for sl in pipe._slots]  # one output set per in-flight slot
-    n_batches = n_img // B
-    masks_on = args.masks or args.mixed
-    maskgen = None
-    if masks_on:
-        from dataloader_amd.masking import MaskingGenerator
+    out_bytes = {"bf16": 2, "fp8": 1, "fp32": 4}[args.dtype]
+
+    def to_device(u, n_img):
+        jp = [u[i % len(u)] for i in range(n_img)]
+        hb, off = pack_jpegs(jp, pin=True)
+        return jp, hb, off, hb.to(dev), off.to(dev)
+
+    def make_maskgen():
         grid = cfg.global_crop_size // 14                     # patch 14: 16x16 at 224 (SURVEY §8a17)
-        maskgen = MaskingGenerator((grid, grid), num_masking_patches=grid * grid // 2, device=dev)
-        maskgen.seed(rank_seed(1234, rank))
+        mg = MaskingGenerator((grid, grid), num_masking_patches=grid * grid // 2, device=dev)
+        mg.seed(rank_seed(1234, rank))
+        return mg
 
-    def step(k: int):
-        s = (k % n_batches) * B
-        pipe.run_device_batch(d_bytes, d_off[s:s + B + 1], B, views=views[k % pipe.depth])
-        if maskgen is not None:  # one mask per batch, broadcast to [B, H*W] (loader.py:585-590)
-            maskgen.generate(1).expand(B, -1)
-
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    st = pipe.last_status()
-    if (st != 0).any():
-        raise RuntimeError(f"decode failures in warmup batch: {np.unique(st, return_counts=True)}")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    # per-kernel HIP-event times: a separate pass with the batches serialised, so that a
-    # kernel's events do not also span the other slot's concurrently running kernels
-    pipe.set_timing(True)
-    pipe.kernel_times()
-    t_ser = time.perf_counter()
-    for k in range(args.steps):
-        step(args.warmup + args.steps + k)
+    def leg(u, n_img, mixed: bool, dtype: str, masks: bool, tag: str, steps: int, warmup: int, serial=True):
+        jp, hb, off, d_bytes, d_off = to_device(u, n_img)
         torch.cuda.synchronize()
-    t_ser = time.perf_counter() - t_ser
-    ktimes = pipe.kernel_times()
-    pipe.set_timing(False)
-    k_last = args.warmup + 2 * args.steps - 1  # the batch the last slot still holds
-    s_last = (k_last % n_batches) * B
-    ent_b, _ = sparse_entry_bytes(pipe, jpegs[s_last:s_last + 16])
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        pipe = MI355XAugPipeline(None, cfg, B, seed=rank_seed(1234, rank), out_dtype=dtype, device=device,
+                                 max_image_dim=0, depth=args.depth,
+                                 workspace_bytes=B * (40 << 20) if mixed else 0)
+        try:
+            res = run_leg(pipe, d_bytes, d_off, n_img, B, steps, warmup, world, dist,
+                          maskgen=make_maskgen() if masks else None, serial=serial)
+            ent_b = 0.0
+            if res["last_batch"] is not None:
+                s_last = res["last_batch"]
+                ent_b = sparse_entry_bytes(pipe, jp[s_last:s_last + 16])
+            ob = {"bf16": 2, "fp8": 1, "fp32": 4}[dtype]
+            ab = algorithmic_bytes(u, cfg.global_crop_size, cfg.local_crop_size, cfg.n_global_crops,
+                                   cfg.n_local_crops, ob, recs=res["recs"], entry_bytes_per_block=ent_b or 20.0)
+            summ = summarize(res, ab, B, steps, world, tag)
+            if "path_roofline" in summ:
+                summ["path_roofline"]["sparse_entry_bytes_per_block"] = round(ent_b, 2)
+            return res, summ, (pipe, hb, off)
+        except BaseException:
+            pipe.close()
+            raise
+
+    masks_on = args.masks or args.mixed
+    main_tag = "c3" if args.mixed else ("fp8" if args.dtype == "fp8" else ("dri" if args.restart_mcus else "c2"))
+    res, summ, (pipe, host_buf, offsets) = leg(uniq, args.images, args.mixed, args.dtype, masks_on, main_tag,
+                                               args.steps, args.warmup)
+    dt, per_rank = _rank_report(dist, world, rank, device, res["dt"], args.steps, B)
+    distinct = check_distinct(per_rank, args.rehearsal)
 
     h2d_rate = None
     if args.h2d:
+        ccfg = pipe._cfg(*pipe._sizes())
+        views = [sl.engine.alloc_views(ccfg, B) for sl in pipe._slots]
+        n_batches = args.images // B
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         for k in range(args.steps):
@@ -506,78 +782,82 @@ def main() -> None:
             pipe.run_device_batch(hb, ho, B, views=views[k % pipe.depth])
         torch.cuda.synchronize()
         h2d_rate = args.steps * B / (time.perf_counter() - t1)
+    pipe.close()
+    del host_buf, offsets
+    torch.cuda.empty_cache()
 
-    e2e = run_e2e(args, uniq, rank, world, dev, cfg, B) if args.e2e else None
+    legs = {}
+    if extras:
+        n_extra = max(args.batch * (args.steps + args.warmup), 8 * B)
+        if args.dtype == "bf16" and not args.mixed and not args.restart_mcus:
+            print("bench: fp8 leg", file=sys.stderr, flush=True)
+            _, s_fp8, (p, _, _) = leg(uniq, args.images, False, "fp8", False, "fp8", args.steps, args.warmup)
+            p.close()
+            legs["fp8"] = dict(s_fp8, workload="C5 epilogue: C2 with FP8-E4M3 output (fused cast, scale 1)")
+        if uniq_c3 is not None:
+            print("bench: c3 leg", file=sys.stderr, flush=True)
+            torch.cuda.empty_cache()
+            _, s_c3, (p, _, _) = leg(uniq_c3, min(n_extra, 8192), True, args.dtype, True, "c3", args.steps,
+                                     args.warmup)
+            p.close()
+            legs["c3"] = dict(s_c3, workload=f"C3: {args.extra_unique} distinct mixed-resolution JPEGs (short side "
+                                             f"224-1600, aspect 3/4-4/3), B = {B}, iBOT masks 16x16, {args.dtype} out")
+            torch.cuda.empty_cache()
+        if uniq_dri is not None:
+            print("bench: c2_dri leg", file=sys.stderr, flush=True)
+            _, s_dri, (p, _, _) = leg(uniq_dri, n_extra, False, args.dtype, False, "dri", args.steps, args.warmup)
+            p.close()
+            legs["c2_dri"] = dict(s_dri, workload=f"C2 with restart markers every 4 MCUs (DRI), "
+                                                  f"{args.extra_unique} distinct encodes, {args.dtype} out")
+    e2e = None
+    if args.e2e or extras:
+        print("bench: e2e leg", file=sys.stderr, flush=True)
+        e2e = run_e2e(args, uniq, rank, world, cfg, B, dist)
 
-    value = world * args.steps * B / dt
-    out_bytes = {"bf16": 2, "fp8": 1, "fp32": 4}[args.dtype]
-    ab = algorithmic_bytes(uniq, cfg.global_crop_size, cfg.local_crop_size, cfg.n_global_crops,
-                           cfg.n_local_crops, out_bytes, recs=pipe.last_params(), entry_bytes_per_block=ent_b)
-    per_kernel = {k: {"avg_ms": (ms / n if n else 0.0), "launches": n, "total_ms": ms} for k, (ms, n) in ktimes.items()}
-    dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
-    traffic, traffic_src = load_traffic()
-    # algorithmic bytes per image = S_jpeg + sum over views of 3 S^2 x out bytes;
-    # one launch of any Stage-3 kernel processes the batch of B images
-    bytes_launch = ab["path"] * B
-    achieved = bytes_launch / (per_kernel[dom]["avg_ms"] * 1e-3) / 1e9
-    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": traffic.get(dom), "kernel": dom,
-            "algorithmic_bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(per_kernel[dom]["avg_ms"], 4),
-            "definition": "SURVEY 8(d) bytes per image (S_jpeg + 3*sum(S_v^2)*out_bytes) x batch / dominant kernel's "
-                          "mean launch time (HIP events on its stream, serialized pass after the timed region)",
-            "traffic_source": f"profiles/{traffic_src}" if traffic_src else None}
-    # each kernel on its own interface bytes (what it must read + write; huffman entries measured)
-    roof_all = {}
-    for k, v in per_kernel.items():
-        if ab.get(k) and v["avg_ms"] > 0:
-            gbs = ab[k] * B / (v["avg_ms"] * 1e-3) / 1e9
-            roof_all[k] = {"achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 4),
-                           "avg_ms": round(v["avg_ms"], 4), "interface_bytes_per_launch": int(ab[k] * B),
-                           "traffic_bytes_per_launch": traffic.get(k)}
-    ms_step = dt / args.steps * 1e3
-    path_gbs = ab["path"] * B * world / (dt / args.steps) / 1e9
-    step_traffic = None
-    if traffic:
-        step_traffic = sum((traffic.get(k) or 0) * v["launches"] / max(args.steps, 1) for k, v in per_kernel.items())
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        print("bench: cpu baseline", file=sys.stderr, flush=True)
         c1 = make_unique(256, 256, 256, 7, False, procs)
-        cpu = cpu_baseline(uniq, c1, args.cpu_seconds)
+        cpu = cpu_baseline(uniq if not args.mixed else uniq[:256], c1, args.cpu_seconds)
     if rank == 0:
+        ms_step = dt / args.steps * 1e3
         line = {
-            "metric": METRIC, "value": round(value, 1), "unit": "images/s", "n_gpus": world,
+            "metric": METRIC, "value": round(world * args.steps * B / dt, 1), "unit": "images/s",
+            "n_gpus": distinct, "ranks": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic",
             "config": {"workload": ("C3 mixed short side 224-1600, iBOT masks 16x16" if args.mixed else
                                     f"C2 {args.images} synthetic {args.width}x{args.height} q85 4:2:0 JPEGs "
-                                    "resident in HBM") + f", 2x224^2+8x96^2 views, {args.dtype} out",
+                                    "resident in HBM") + (f", DRI every {args.restart_mcus} MCUs" if args.restart_mcus
+                                                          else "") + f", 2x224^2+8x96^2 views, {args.dtype} out",
                        "global_batch": B * world, "batch_per_gpu": B, "parallelism": f"dp{world}",
-                       "batches_in_flight": pipe.depth, "masks": masks_on,
-                       "mean_jpeg_bytes": round(ab["s_jpeg"]), "out_dtype": args.dtype,
+                       "batches_in_flight": args.depth, "masks": masks_on,
+                       "mean_jpeg_bytes": summ["mean_jpeg_bytes"], "out_dtype": args.dtype,
                        "progressive_frac": args.progressive_frac},
-            "roofline": roof,
-            "roofline_kernels": roof_all,
-            "path_roofline": {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
-                              "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5),
-                              "pmc_traffic_bytes_per_step": int(step_traffic) if step_traffic else None,
-                              "algorithmic_bytes_per_step": int(ab["path"] * B),
-                              "sparse_entry_bytes_per_block": round(ent_b, 2)},
-            "kernels_ms_per_step": {k: round(v["total_ms"] / args.steps, 4) for k, v in per_kernel.items()},
-            "serialized_ms_per_step": round(t_ser / args.steps * 1e3, 3),
+            "per_rank": per_rank,
+            "roofline": summ.get("roofline"),
+            "roofline_kernels": summ.get("roofline_kernels"),
+            "path_roofline": summ.get("path_roofline"),
+            "kernels_ms_per_step": summ.get("kernels_ms_per_step"),
+            "serialized_ms_per_step": summ.get("serialized_ms_per_step"),
             "cpu_baseline": cpu,
         }
+        if world > distinct:
+            line["rehearsal"] = True
+            line["note"] = f"{world} ranks shared {distinct} device(s): not a scaling measurement"
+        line.update(legs)
         if h2d_rate is not None:
             line["h2d_inclusive_images_per_s"] = round(h2d_rate, 1)
         if e2e is not None:
             line["e2e"] = e2e
         print(json.dumps(line), flush=True)
         if args.kernel_json:
-            Path(args.kernel_json).write_text(json.dumps(per_kernel, indent=1))
-    pipe.close()
+            Path(args.kernel_json).write_text(json.dumps(res["ktimes"], indent=1))
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -17,8 +17,8 @@ LIB_PATH = _PKG / "libdino_ingest.so"
 
 DINO_OK = 0
 IMG_STATUS = {0: "ok", -1: "corrupt", -2: "truncated", -3: "bad-data", -4: "too-large (Pillow bomb check)",
-              1: "unsupported", 2: "multi-scan", 3: "no-space", 4: "over max_image_dim"}
-ABI_VERSION = 2
+              1: "unsupported", 2: "multi-scan", 3: "no-space", 4: "over max_image_dim (handed to Pillow)"}
+ABI_VERSION = 3
 RAW_MAGIC = 0x42475244  # "DRGB": pre-decoded RGB container (include/dino_ingest.h)
 
 _lib = None
@@ -44,11 +44,11 @@ def load() -> ctypes.CDLL:
         "dino_last_error": (ctypes.c_char_p, []),
         "dino_ctx_create": (i32, [ctypes.c_int, ctypes.POINTER(DinoLimits), ctypes.POINTER(vp)]),
         "dino_ctx_destroy": (i32, [vp]),
-        "dino_decode": (i32, [vp, vp, vp, i32, vp, vp]),
+        "dino_decode": (i32, [vp, vp, vp, vp, i32, vp, vp]),
         "dino_copy_rgb": (i32, [vp, i32, vp, vp]),
         "dino_sample_params": (i32, [vp, ctypes.POINTER(DinoAugConfig), u64, u64, vp, vp]),
         "dino_augment": (i32, [vp, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(vp), vp]),
-        "dino_run_batch": (i32, [vp, vp, vp, i32, ctypes.POINTER(DinoAugConfig), u64, u64, vp,
+        "dino_run_batch": (i32, [vp, vp, vp, vp, i32, ctypes.POINTER(DinoAugConfig), u64, u64, vp,
                                  ctypes.POINTER(vp), vp, vp]),
         "dino_masks": (i32, [i32, i32, i32, i32, i32, dbl, dbl, i32, vp, vp, vp, vp]),
         "dino_bf16_to_fp8": (i32, [vp, vp, i64, vp]),
@@ -60,9 +60,9 @@ def load() -> ctypes.CDLL:
         "dino_gather": (i32, [vp, vp, i64, vp, i64, vp, i32]),
         "dino_set_norm": (i32, [vp, vp, i32]),
         "dino_batch_info": (i32, [vp, vp, vp]),
-        "dino_probe": (i32, [vp, vp, i32, i32, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(i64),
+        "dino_probe": (i32, [vp, vp, vp, i32, i32, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(i64),
                              ctypes.POINTER(i64)]),
-        "dino_reserve": (i32, [vp, i64, i64]),
+        "dino_reserve": (i32, [vp, i64, i64, vp]),
         "dino_workspace_sizes": (i32, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "dino_masks_host": (i32, [i32, i32, i32, i32, i32, dbl, dbl, i32, vp, vp, vp]),
         "dino_resize_batch": (i32, [vp, i32, i32, vp, vp, i32, vp, vp]),

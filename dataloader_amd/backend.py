@@ -140,11 +140,41 @@ def _is_dinov2_spec(spec: Any) -> bool:
 
 
 class MI355XBackend:
-    """Backend whose Stage 3 runs as HIP kernels on an MI355X (gfx950)."""
+    """Backend whose Stage 3 runs as HIP kernels on an MI355X (gfx950).
 
-    def __init__(self, max_image_dim: int = 8192, workspace_bytes: int = 0) -> None:
+    ``max_image_dim``: 0 (default) decodes any JPEG side on the device; a positive value
+    hands larger JPEGs to Pillow.  ``max_in_flight`` caps ``PipelineConfig.gpu_queue``
+    (DALI's prefetch_queue_depth, reference pipeline.py:317 / dali_backend.py:163-164):
+    each in-flight batch owns a ctx (workspaces in HBM) and a HIP stream, and three
+    already hide the latency-bound entropy decode (DESIGN.md §5: depth 2/3/4 measured);
+    ``hbm_fraction`` further caps it so that the slots' workspaces stay a small share of
+    the device memory the training process also needs."""
+
+    # initial decode workspace per image of a backend-built slot; every batch is probed on
+    # the host first and the workspace grows (stream-ordered) to what the batch needs
+    WS_PER_IMAGE = 4 << 20
+
+    def __init__(self, max_image_dim: int = 0, workspace_bytes: int = 0, max_in_flight: int = 3,
+                 hbm_fraction: float = 0.15, host_workers: int | None = None) -> None:
         self._max_image_dim = max_image_dim
         self._workspace_bytes = workspace_bytes
+        self._max_in_flight = max(1, int(max_in_flight))
+        self._hbm_fraction = float(hbm_fraction)
+        self._host_workers = host_workers
+
+    def queue_depth(self, pipeline_cfg: Any, batch_size: int, n_views: int = 10, max_crop: int = 224) -> int:
+        """Batches in flight for ``pipeline_cfg.gpu_queue``, capped by ``max_in_flight`` and by
+        the slots' workspace footprint (decode + augment + crop planes) against the device's HBM."""
+        want = max(1, int(getattr(pipeline_cfg, "gpu_queue", 1) or 1))
+        depth = min(want, self._max_in_flight)
+        per_slot = (self._workspace_bytes or batch_size * self.WS_PER_IMAGE) + \
+            batch_size * n_views * (max_crop * 3 * 1024 + (256 << 10)) + batch_size * n_views * 3 * max_crop ** 2
+        try:
+            total = torch.cuda.get_device_properties(int(getattr(pipeline_cfg, "device_id", 0))).total_memory
+            depth = max(1, min(depth, int(total * self._hbm_fraction // max(per_slot, 1))))
+        except Exception:  # noqa: BLE001 - no device visible: the pipeline constructor reports it
+            pass
+        return depth
 
     @property
     def name(self) -> str:
@@ -199,18 +229,25 @@ class MI355XBackend:
             norm = NormTable(aug_cfg, specs)
             if hasattr(source, "register_dataset_index_callback"):
                 source.register_dataset_index_callback(norm.set_dataset_indices)
+        batch = getattr(source, "_batch_size", 1)
+        max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
+                       int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size))
         return MI355XAugPipeline(
             source=source,
             aug_cfg=aug_cfg,
-            batch_size=getattr(source, "_batch_size", 1),
+            batch_size=batch,
             resolution_src=getattr(source, "_resolution_src", None) if names is None else None,
             seed=pipeline_cfg.seed,
             out_dtype=out,
             device=pipeline_cfg.device_id,
             max_image_dim=self._max_image_dim,
-            workspace_bytes=self._workspace_bytes,
+            workspace_bytes=self._workspace_bytes or batch * self.WS_PER_IMAGE,
             norm=norm,
             view_names=names,
+            depth=self.queue_depth(pipeline_cfg, batch, aug_cfg.n_views, max_crop),
+            prefetch=1,
+            host_workers=self._host_workers,
+            start_host_pool=True,
         )
 
     def build_pipeline_iterator(self, pipeline: Any, aug_spec: Any, output_map: list[str],

@@ -23,6 +23,7 @@ using namespace dino;
 
 namespace {
 thread_local std::string g_err;
+constexpr int32_t kMaxImageDim = 65535;
 
 int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
   char buf[512];
@@ -53,6 +54,7 @@ struct dino_ctx {
   const float* d_norm = nullptr;  // per-image normalisation (dino_set_norm), nullable
   int32_t norm_n = 0;
   int32_t last_batch = -1;
+  hipStream_t ws_stream = nullptr;  // stream of the last dino_reserve (the workspaces' release order)
   LaunchGeom geom{};
   KernelTimer* timer = nullptr;
   KernelTimer* tm() { return timer && timer->enabled ? timer : nullptr; }
@@ -72,9 +74,9 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
     return fail(DINO_EINVAL, "dino_ctx_create: max_batch/max_views/max_crop_size must be > 0%s%lld");
   if (L.max_crop_size > 1024)  // k_final's LDS tile and its 32-bit index arithmetic are sized for S <= 1024
     return fail(DINO_EINVAL, "dino_ctx_create: max_crop_size %s%lld > 1024", "", L.max_crop_size);
-  if (L.max_image_dim <= 0) L.max_image_dim = 16384;
-  if (L.max_image_dim > 16384)  // pixel indices of the colour/resize kernels are 32-bit
-    return fail(DINO_EINVAL, "dino_ctx_create: max_image_dim %s%lld > 16384", "", L.max_image_dim);
+  // JPEG sides are 16-bit: 0 (or anything above) means no side limit (the bomb limit of
+  // jpeg_parse.hpp check_dims bounds every pixel index)
+  if (L.max_image_dim <= 0 || L.max_image_dim > kMaxImageDim) L.max_image_dim = kMaxImageDim;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   dino_ctx* c = new dino_ctx();
@@ -89,8 +91,12 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
   c->ws_size = L.workspace_bytes > 0 ? L.workspace_bytes : (int64_t)L.max_batch * (16ll << 20);
   c->aws_size = (int64_t)L.max_batch * L.max_views * ((int64_t)L.max_crop_size * 3 * 1024 + (256ll << 10));
   const int64_t nrec = (int64_t)L.max_batch * L.max_views;
+  // the two growable workspaces come from the stream-ordered allocator, so that dino_reserve
+  // can retire them on the ctx's stream instead of synchronising the device
   if ((e = hipMalloc(&c->d_desc, sizeof(ImgDesc) * L.max_batch)) != hipSuccess ||
-      (e = hipMalloc(&c->d_ws, c->ws_size)) != hipSuccess || (e = hipMalloc(&c->d_aws, c->aws_size)) != hipSuccess ||
+      (e = hipMallocAsync((void**)&c->d_ws, c->ws_size, nullptr)) != hipSuccess ||
+      (e = hipMallocAsync((void**)&c->d_aws, c->aws_size, nullptr)) != hipSuccess ||
+      (e = hipStreamSynchronize(nullptr)) != hipSuccess ||
       (e = hipMalloc(&c->d_plan, sizeof(ViewPlan) * nrec)) != hipSuccess ||
       (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess) {
     dino_ctx_destroy(c);
@@ -110,8 +116,10 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
 int dino_ctx_destroy(dino_ctx* c) {
   if (!c) return DINO_OK;
   (void)hipFree(c->d_desc);
-  (void)hipFree(c->d_ws);
-  (void)hipFree(c->d_aws);
+  // (callers synchronise the ctx's streams before destroying it: the null stream suffices)
+  if (c->d_ws) (void)hipFreeAsync(c->d_ws, nullptr);
+  if (c->d_aws) (void)hipFreeAsync(c->d_aws, nullptr);
+  (void)hipStreamSynchronize(nullptr);
   (void)hipFree(c->d_plan);
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_gcrop);
@@ -123,13 +131,13 @@ int dino_ctx_destroy(dino_ctx* c) {
   return DINO_OK;
 }
 
-int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch, int32_t* d_info,
-                void* stream) {
+int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
+                int32_t batch, int32_t* d_info, void* stream) {
   if (!c || !d_bytes || !d_offsets) return fail(DINO_EINVAL, "dino_decode: null argument%s%lld");
   if (batch < 0 || batch > c->lim.max_batch)
     return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
   hipStream_t s = (hipStream_t)stream;
-  DecodeArgs a{d_bytes, d_offsets, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size, c->geom};
+  DecodeArgs a{d_bytes, d_offsets, d_raw_mask, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size, c->geom};
   hipError_t e = launch_decode(a, s, c->tm());
   if (e != hipSuccess) return hip_fail(e, "dino_decode");
   if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
@@ -198,13 +206,13 @@ int dino_set_norm(dino_ctx* c, const float* d_norm, int32_t n) {
   return DINO_OK;
 }
 
-int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,
-                   const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index, dino_view_params* d_params_out,
-                   void* const* d_views, int32_t* d_info, void* stream) {
+int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
+                   int32_t batch, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
+                   dino_view_params* d_params_out, void* const* d_views, int32_t* d_info, void* stream) {
   if (!c) return fail(DINO_EINVAL, "dino_run_batch: null ctx%s%lld");
   int r = check_cfg(c, cfg);
   if (r) return r;
-  if ((r = dino_decode(c, d_bytes, d_offsets, batch, nullptr, stream))) return r;
+  if ((r = dino_decode(c, d_bytes, d_offsets, d_raw_mask, batch, nullptr, stream))) return r;
   dino_view_params* prm = d_params_out ? d_params_out : c->d_params;
   if ((r = dino_sample_params(c, cfg, seed, batch_index, prm, stream))) return r;
   if ((r = dino_augment(c, cfg, prm, d_views, stream))) return r;
@@ -235,26 +243,35 @@ int dino_batch_info(dino_ctx* c, int32_t* d_info, void* stream) {
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_batch_info");
 }
 
-int dino_reserve(dino_ctx* c, int64_t ws_bytes, int64_t aws_bytes) {
+int dino_reserve(dino_ctx* c, int64_t ws_bytes, int64_t aws_bytes, void* stream) {
   if (!c || ws_bytes < 0 || aws_bytes < 0) return fail(DINO_EINVAL, "dino_reserve: bad arguments%s%lld");
   if (ws_bytes <= c->ws_size && aws_bytes <= c->aws_size) return DINO_OK;
+  // Stream-ordered: the old buffers are released after the work already enqueued on
+  // `stream` (the only stream this ctx's batches run on) and the new ones are usable by
+  // everything enqueued after this call; no other stream of the device waits.
+  hipStream_t s = (hipStream_t)stream;
   hipError_t e = hipSetDevice(c->device);
-  if (e == hipSuccess) e = hipDeviceSynchronize();  // in-flight batches may still use the old buffers
-  if (e != hipSuccess) return hip_fail(e, "dino_reserve: synchronize");
+  if (e != hipSuccess) return hip_fail(e, "dino_reserve: hipSetDevice");
+  if (s != c->ws_stream) {  // the previous owner stream's work on the old buffers must finish first
+    if ((e = hipStreamSynchronize(c->ws_stream)) != hipSuccess) return hip_fail(e, "dino_reserve: synchronize");
+    c->ws_stream = s;
+  }
   if (ws_bytes > c->ws_size) {
     const int64_t n = ws_bytes + ws_bytes / 8;  // headroom: fewer regrowths
-    (void)hipFree(c->d_ws);
+    (void)hipFreeAsync(c->d_ws, s);
     c->d_ws = nullptr;
     c->ws_size = 0;
-    if ((e = hipMalloc(&c->d_ws, n)) != hipSuccess) return hip_fail(e, "dino_reserve: hipMalloc(workspace)");
+    if ((e = hipMallocAsync((void**)&c->d_ws, n, s)) != hipSuccess)
+      return hip_fail(e, "dino_reserve: hipMallocAsync(workspace)");
     c->ws_size = n;
   }
   if (aws_bytes > c->aws_size) {
     const int64_t n = aws_bytes + aws_bytes / 8;
-    (void)hipFree(c->d_aws);
+    (void)hipFreeAsync(c->d_aws, s);
     c->d_aws = nullptr;
     c->aws_size = 0;
-    if ((e = hipMalloc(&c->d_aws, n)) != hipSuccess) return hip_fail(e, "dino_reserve: hipMalloc(augment workspace)");
+    if ((e = hipMallocAsync((void**)&c->d_aws, n, s)) != hipSuccess)
+      return hip_fail(e, "dino_reserve: hipMallocAsync(augment workspace)");
     c->aws_size = n;
   }
   c->last_batch = -1;  // the decoded batch (if any) lived in the old workspace
@@ -268,11 +285,11 @@ int dino_workspace_sizes(dino_ctx* c, int64_t* ws_bytes, int64_t* aws_bytes) {
   return DINO_OK;
 }
 
-int dino_probe(const uint8_t* bytes, const int64_t* offsets, int32_t batch, int32_t max_image_dim,
-               const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need) {
+int dino_probe(const uint8_t* bytes, const int64_t* offsets, const uint8_t* raw_mask, int32_t batch,
+               int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need) {
   if ((!bytes && batch > 0) || !offsets || batch < 0 || !ws_need || !aws_need)
     return fail(DINO_EINVAL, "dino_probe: bad arguments%s%lld");
-  if (max_image_dim <= 0) max_image_dim = 16384;
+  if (max_image_dim <= 0 || max_image_dim > kMaxImageDim) max_image_dim = kMaxImageDim;
   int64_t ws = 0, aws = 0;
   std::vector<ScanRec> scans(kMaxScans);
   for (int32_t i = 0; i < batch; ++i) {
@@ -282,7 +299,7 @@ int dino_probe(const uint8_t* bytes, const int64_t* offsets, int32_t batch, int3
       d.status = DINO_IMG_CORRUPT;
       d.width = d.height = d.ncomp = 0;
     } else {
-      parse_jpeg(bytes + off, len, max_image_dim, &d);
+      parse_jpeg(bytes + off, len, max_image_dim, &d, raw_mask != nullptr && raw_mask[i] != 0);
       if (d.status == DINO_IMG_OK && d.kind == 1) {
         HostMarkerFinder find;
         prog_walk(bytes + off, len, &d, scans.data(), find);

@@ -33,15 +33,22 @@ DHD uint32_t rd32le(const uint8_t* p) {
 }
 
 // Size checks shared by both image kinds: Pillow refuses decompression bombs at
-// Image.open (the reference then zero-fills); images above the ctx's dimension limit
-// are left to the caller.
+// Image.open (the reference then zero-fills).  The bomb limit also bounds every pixel
+// index of the colour / resize kernels (3 x 2 x 89478485 bytes < 2^31), so any side the
+// JPEG format allows (<= 65535) decodes; a caller-chosen side limit (max_dim < 65535)
+// reports DINO_IMG_LIMIT for JPEGs, which the Python layer hands to Pillow.  Raw
+// containers (already Pillow's output) are only bound by the bomb limit.
 DHD int check_dims(ImgDesc* d, int max_dim) {
   if ((int64_t)d->width * d->height > kPilBombPixels) return (d->status = DINO_IMG_TOO_LARGE);
-  if (d->width > max_dim || d->height > max_dim) return (d->status = DINO_IMG_LIMIT);
+  if (d->kind != 2 && (d->width > max_dim || d->height > max_dim)) return (d->status = DINO_IMG_LIMIT);
   return d->status;
 }
 
-DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
+// allow_raw: the caller marked this image as a pre-decoded RGB container (raw mask of
+// dino_decode / dino_probe).  The container's magic is never trusted in user data: an
+// unmarked file that starts with it is parsed as what it is (not a JPEG -> corrupt, as
+// Pillow would raise).
+DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d, bool allow_raw = false) {
   d->status = DINO_IMG_CORRUPT;
   d->width = d->height = d->ncomp = 0;
   d->restart_interval = 0;
@@ -59,7 +66,8 @@ DHD int parse_jpeg(const uint8_t* p, int64_t len, int max_dim, ImgDesc* d) {
     for (int k = 0; k < 64; ++k) d->qt[t][k] = 0;
   bool qt_seen[4] = {false, false, false, false};
   // pre-decoded RGB container (include/dino_ingest.h DINO_RAW_MAGIC)
-  if (len >= 16 && rd32le(p) == DINO_RAW_MAGIC) {
+  if (allow_raw) {
+    if (len < 16 || rd32le(p) != DINO_RAW_MAGIC) return d->status;
     const uint32_t w = rd32le(p + 4), h = rd32le(p + 8);
     if (w < 1 || h < 1 || w > 65535 || h > 65535 || (int64_t)w * h * 3 > len - 16) return d->status;
     d->kind = 2;

@@ -43,7 +43,8 @@ namespace dino {
 // (a header longer than the prefix, a raw container) is redone on the global bytes.
 constexpr int kParsePrefix = 4096;
 __global__ void __launch_bounds__(64) k_parse(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
-                                              int B, int max_dim, ImgDesc* __restrict__ desc) {
+                                              const uint8_t* __restrict__ raw_mask, int B, int max_dim,
+                                              ImgDesc* __restrict__ desc) {
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[kParsePrefix + 16];
   const int i = blockIdx.x;
   const int64_t off = offsets[i], len = offsets[i + 1] - off;
@@ -75,10 +76,11 @@ __global__ void __launch_bounds__(64) k_parse(const uint8_t* __restrict__ bytes,
     d.kind = 0;
     d.aug_status = 0;
   } else {
-    parse_jpeg(s_head, n, max_dim, &d);
+    const bool raw = raw_mask != nullptr && raw_mask[i] != 0;
+    parse_jpeg(s_head, n, max_dim, &d, raw);
     if (n < len) {
-      if (d.status == DINO_IMG_OK) d.scan_len = (int32_t)(len - d.scan_off);
-      else parse_jpeg(src, len, max_dim, &d);
+      if (d.status == DINO_IMG_OK && !raw) d.scan_len = (int32_t)(len - d.scan_off);
+      else parse_jpeg(src, len, max_dim, &d, raw);
     }
   }
   desc[i] = d;
@@ -2825,7 +2827,7 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
   if (B <= 0) return hipSuccess;
-  TIMED(tm, kKParse, s, (k_parse<<<B, 64, 0, s>>>(a.bytes, a.offsets, B, a.max_dim, a.desc)));
+  TIMED(tm, kKParse, s, (k_parse<<<B, 64, 0, s>>>(a.bytes, a.offsets, a.raw_mask, B, a.max_dim, a.desc)));
   TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
   const int grid_ds = a.geom.grid_ds, grid1 = a.geom.grid1, grid3 = a.geom.grid3;
   TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));

@@ -23,6 +23,10 @@ def _ptr(t: torch.Tensor) -> ctypes.c_void_p:
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _optr(t: torch.Tensor | None) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+
 def _stream_handle(device: torch.device, stream: torch.cuda.Stream | None = None) -> ctypes.c_void_p:
     s = stream if stream is not None else torch.cuda.current_stream(device)
     return ctypes.c_void_p(s.cuda_stream)
@@ -45,7 +49,7 @@ class IngestEngine:
     """Owns a ``dino_ctx`` (decode + augment workspaces sized from the limits)."""
 
     def __init__(self, device: int | torch.device = 0, max_batch: int = 512, max_views: int = 10,
-                 max_crop_size: int = 224, max_image_dim: int = 8192, workspace_bytes: int = 0,
+                 max_crop_size: int = 224, max_image_dim: int = 0, workspace_bytes: int = 0,
                  stream: torch.cuda.Stream | None = None):
         self.lib = _lib.load()
         if not torch.cuda.is_available():
@@ -69,12 +73,13 @@ class IngestEngine:
 
     # ------------------------------------------------------------------ decode
     def decode(self, d_bytes: torch.Tensor, d_offsets: torch.Tensor, batch: int,
-               info: torch.Tensor | None = None) -> torch.Tensor:
+               info: torch.Tensor | None = None, raw_mask: torch.Tensor | None = None) -> torch.Tensor:
+        """``raw_mask``: device uint8[batch], 1 where the image is a raw RGB container (hand-over)."""
         if info is None:
             with self.on_stream():
                 info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
-        _lib.check(self.lib.dino_decode(self._ctx, _ptr(d_bytes), _ptr(d_offsets), batch, _ptr(info),
-                                        self._s()), "dino_decode")
+        _lib.check(self.lib.dino_decode(self._ctx, _ptr(d_bytes), _ptr(d_offsets), _optr(raw_mask), batch,
+                                        _ptr(info), self._s()), "dino_decode")
         self.last_batch = batch
         return info
 
@@ -133,7 +138,7 @@ class IngestEngine:
 
     def run_batch(self, d_bytes, d_offsets, batch: int, cfg, seed: int, batch_index: int,
                   views: list[torch.Tensor] | None = None, params_out: torch.Tensor | None = None,
-                  info: torch.Tensor | None = None):
+                  info: torch.Tensor | None = None, raw_mask: torch.Tensor | None = None):
         if views is None:
             views = self.alloc_views(cfg, batch)
         if info is None:
@@ -141,7 +146,8 @@ class IngestEngine:
                 info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
         ptrs = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
         pp = _ptr(params_out) if params_out is not None else ctypes.c_void_p(0)
-        _lib.check(self.lib.dino_run_batch(self._ctx, _ptr(d_bytes), _ptr(d_offsets), batch, ctypes.byref(cfg),
+        _lib.check(self.lib.dino_run_batch(self._ctx, _ptr(d_bytes), _ptr(d_offsets), _optr(raw_mask), batch,
+                                           ctypes.byref(cfg),
                                            seed & (2**64 - 1), batch_index, pp, ptrs, _ptr(info),
                                            self._s()), "dino_run_batch")
         self.last_batch = batch
@@ -172,13 +178,14 @@ class IngestEngine:
         return int(ws.value), int(aws.value)
 
     def reserve(self, ws_bytes: int, aws_bytes: int) -> bool:
-        """Grow the decode / augment workspaces to at least these sizes (``dino_reserve``).
-        Returns True when it had to reallocate (which synchronises the device)."""
+        """Grow the decode / augment workspaces to at least these sizes (``dino_reserve``),
+        stream-ordered on this engine's stream (no other stream of the device waits).
+        Returns True when it had to reallocate."""
         cur_ws, cur_aws = self.workspace_sizes()
         if ws_bytes <= cur_ws and aws_bytes <= cur_aws:
             return False
         with torch.cuda.device(self.device):
-            _lib.check(self.lib.dino_reserve(self._ctx, int(ws_bytes), int(aws_bytes)), "dino_reserve")
+            _lib.check(self.lib.dino_reserve(self._ctx, int(ws_bytes), int(aws_bytes), self._s()), "dino_reserve")
         return True
 
     def set_norm(self, d_norm: torch.Tensor | None) -> None:

@@ -53,13 +53,17 @@ def raw_container(rgb: np.ndarray) -> bytes:
     return struct.pack("<IIII", _lib.RAW_MAGIC, w, h, 0) + np.ascontiguousarray(rgb).tobytes()
 
 
-def probe(host_buf_ptr: int, offsets: np.ndarray, batch: int, max_image_dim: int, cfg=None):
-    """``dino_probe`` over a packed host batch -> (info[B,4] int32, ws_bytes, aws_bytes)."""
+def probe(host_buf_ptr: int, offsets: np.ndarray, batch: int, max_image_dim: int, cfg=None,
+          raw_mask: np.ndarray | None = None):
+    """``dino_probe`` over a packed host batch -> (info[B,4] int32, ws_bytes, aws_bytes).
+    ``raw_mask``: uint8[B], 1 where the image is a raw RGB container (a hand-over)."""
     lib = _lib.load()
     info = np.zeros((batch, 4), np.int32)
     ws, aws = ctypes.c_int64(0), ctypes.c_int64(0)
     offs = np.ascontiguousarray(offsets, np.int64)
-    _lib.check(lib.dino_probe(ctypes.c_void_p(host_buf_ptr), offs.ctypes.data_as(ctypes.c_void_p), batch,
+    rm = None if raw_mask is None else np.ascontiguousarray(raw_mask, np.uint8)
+    _lib.check(lib.dino_probe(ctypes.c_void_p(host_buf_ptr), offs.ctypes.data_as(ctypes.c_void_p),
+                              rm.ctypes.data_as(ctypes.c_void_p) if rm is not None else None, batch,
                               max_image_dim, ctypes.byref(cfg) if cfg is not None else None,
                               info.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ws), ctypes.byref(aws)),
                "dino_probe")
@@ -73,11 +77,13 @@ def pillow_container(jpeg) -> bytes:
 
 
 def hand_over(jpegs: list, status: np.ndarray, mask: np.ndarray | None = None,
-              pool: "HostDecoder | None" = None) -> tuple[list, int]:
-    """Replace the images the GPU decoder does not implement (``status == IMG_UNSUPPORTED``,
-    or ``mask`` when given) by Pillow-decoded raw RGB containers (zero bytes where Pillow
-    raises), in ``pool``'s worker processes when given.  Returns (new list, images handed over)."""
-    idx = np.flatnonzero(status == IMG_UNSUPPORTED if mask is None else mask)
+              pool: "HostDecoder | None" = None) -> tuple[list, int, np.ndarray]:
+    """Replace the images the GPU decoder does not decode (``status`` ``IMG_UNSUPPORTED`` or
+    ``IMG_LIMIT``, or ``mask`` when given) by Pillow-decoded raw RGB containers (zero bytes
+    where Pillow raises), in ``pool``'s worker processes when given.  Returns (new list,
+    images handed over, raw mask: uint8[B], 1 where the new entry is a container — the
+    mask dino_probe / dino_decode need to accept it)."""
+    idx = np.flatnonzero(np.isin(status, (IMG_UNSUPPORTED, IMG_LIMIT)) if mask is None else mask)
     out = list(jpegs)
     if pool is not None and len(idx) > 1:
         for i, f in zip(idx, [pool.submit(jpegs[i]) for i in idx]):
@@ -85,13 +91,22 @@ def hand_over(jpegs: list, status: np.ndarray, mask: np.ndarray | None = None,
     else:
         for i in idx:
             out[i] = pillow_container(jpegs[i])
-    return out, len(idx)
+    return out, len(idx), raw_mask_of(out, idx)
+
+
+def raw_mask_of(images: list, handed) -> np.ndarray:
+    """uint8[B]: 1 for the handed-over entries that hold a container (Pillow did not raise)."""
+    m = np.zeros(len(images), np.uint8)
+    for i in handed:
+        m[int(i)] = len(images[int(i)]) > 0
+    return m
 
 
 def route_mask(info: np.ndarray, host_fallback: bool, multiscan_route: str, host_max: int) -> np.ndarray:
     """Images of a probed batch to decode with Pillow on the host.
 
-    * ``DINO_IMG_UNSUPPORTED`` images, always (when ``host_fallback``);
+    * ``DINO_IMG_UNSUPPORTED`` images and JPEGs over a caller-chosen ``max_image_dim``
+      (``DINO_IMG_LIMIT``), always (when ``host_fallback``);
     * coefficient-buffer images (``info[:, 3] == 1``: progressive, multi-scan sequential,
       damaged restart intervals), which ``k_prog`` decodes one image per workgroup with
       every scan serial — about 100 ms of latency for a batch holding any — so that
@@ -99,7 +114,7 @@ def route_mask(info: np.ndarray, host_fallback: bool, multiscan_route: str, host
       Pillow, ``"device"`` none, ``"auto"`` all of them when the batch has at most
       ``host_max`` (the host decodes ~6 ms per 640x480 image per worker, off the
       critical path when prepared one batch ahead), else none."""
-    mask = (info[:, 0] == IMG_UNSUPPORTED) if host_fallback else np.zeros(len(info), bool)
+    mask = np.isin(info[:, 0], (IMG_UNSUPPORTED, IMG_LIMIT)) if host_fallback else np.zeros(len(info), bool)
     ms = (info[:, 0] == 0) & (info[:, 3] == 1)
     if multiscan_route == "host" or (multiscan_route == "auto" and 0 < ms.sum() <= host_max):
         mask |= ms
@@ -110,22 +125,56 @@ class HostDecoder:
     """A pool of worker processes for the Pillow hand-over.  Pillow's decode of one JPEG
     holds the GIL for most of its run (threads give no speed-up), so the workers are
     processes, started with ``spawn`` (a fork of a process that has initialised HIP is not
-    safe) and only when the first image is submitted."""
+    safe).  ``start()`` starts them eagerly (the backend-built pipeline does, so that a
+    script whose spawned children cannot start — no ``if __name__ == "__main__":`` guard
+    around the training loop — fails at construction, not at the first CMYK file
+    mid-epoch); otherwise they start with the first submitted image.  If the pool cannot
+    start or breaks, the hand-over continues in this process (same bytes, slower) with a
+    ``RuntimeWarning``."""
 
     def __init__(self, workers: int):
         self.workers = max(1, int(workers))
         self._pool = None
+        self._inline = False
 
-    def submit(self, jpeg):
-        if self._pool is None:
-            import multiprocessing as mp
-            from concurrent.futures import ProcessPoolExecutor
+    def start(self) -> None:
+        """Start the workers now and wait until each has imported Pillow."""
+        if self._pool is not None or self._inline:
+            return
+        import multiprocessing as mp
+        from concurrent.futures import ProcessPoolExecutor
+        try:
             self._pool = ProcessPoolExecutor(self.workers, mp_context=mp.get_context("spawn"))
             # the executor starts a process per submit that finds no idle one: start them all
             # now (each imports Pillow on its no-op decode) rather than one per later batch
-            for _ in range(self.workers):
-                self._pool.submit(decode_with_pillow, b"")
-        return self._pool.submit(pillow_container, bytes(jpeg))
+            warm = [self._pool.submit(decode_with_pillow, b"") for _ in range(self.workers)]
+            for f in warm:
+                f.result(timeout=120)
+        except Exception as e:  # noqa: BLE001 - BrokenProcessPool, spawn bootstrap errors, timeouts
+            self._fall_back(e)
+
+    def _fall_back(self, err: BaseException) -> None:
+        import warnings
+        warnings.warn(f"HostDecoder: the Pillow worker pool is unavailable ({type(err).__name__}: {err}); "
+                      "handing images over in-process (a spawned worker re-imports __main__: guard the "
+                      "training script with `if __name__ == '__main__':`)", RuntimeWarning, stacklevel=3)
+        if self._pool is not None:
+            self._pool.shutdown(wait=False, cancel_futures=True)
+            self._pool = None
+        self._inline = True
+
+    def submit(self, jpeg):
+        from concurrent.futures import Future
+        if self._pool is None and not self._inline:
+            self.start()
+        if not self._inline:
+            try:
+                return self._pool.submit(pillow_container, bytes(jpeg))
+            except Exception as e:  # noqa: BLE001 - the pool broke after it started
+                self._fall_back(e)
+        f = Future()
+        f.set_result(pillow_container(jpeg))
+        return f
 
     def close(self) -> None:
         if self._pool is not None:

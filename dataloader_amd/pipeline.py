@@ -25,6 +25,8 @@ have decoded but that came back zero-filled raises a ``RuntimeWarning``.
 from __future__ import annotations
 
 import os
+import queue
+import threading
 import warnings
 from collections import Counter, deque
 from typing import Any
@@ -58,34 +60,148 @@ class _Slot:
         self.inflight = None
         self.outputs: dict[str, torch.Tensor] | None = None
         self.norm: torch.Tensor | None = None         # per-image normalisation records of the batch
-        self.staging: torch.Tensor | None = None      # pinned JPEG bytes of a packed (native) source
-        self.staging_off: torch.Tensor | None = None  # pinned int64 offsets[B+1]
         self.info_host: torch.Tensor | None = None    # pinned copy of the batch's per-image status
         self.done: torch.cuda.Event | None = None     # recorded after that copy (status accounting)
         self.batch_id = -1
 
 
-class _Prepared:
-    """A pulled, probed host batch whose host-routed images are decoding in the pool."""
+class _Staging:
+    """A pinned host buffer the batch's JPEG bytes (+ int64 offsets + raw mask) are packed
+    into before the H2D copy.  Owned by the host half while it is being filled and until the
+    launch that copies it out has retired (``released`` event)."""
 
-    def __init__(self, jpegs, host_buf: torch.Tensor, offsets: np.ndarray, futures: dict):
-        self.jpegs = jpegs
-        self.host_buf = host_buf
+    def __init__(self):
+        self.buf: torch.Tensor | None = None
+        self.off: torch.Tensor | None = None
+        self.mask: torch.Tensor | None = None
+        self.released: torch.cuda.Event | None = None
+        self.busy = False
+
+    def fit(self, nbytes: int, n: int) -> None:
+        if self.buf is None or self.buf.numel() < nbytes:
+            self.buf = torch.empty(max(nbytes, 1) * 5 // 4 + 64, dtype=torch.uint8, pin_memory=True)
+        if self.off is None or self.off.numel() < n + 1:
+            self.off = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+            self.mask = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+
+
+class _StagingRing:
+    """Round-robin staging buffers shared by the host half (fills) and the launch (frees)."""
+
+    def __init__(self, n: int):
+        self._bufs = [_Staging() for _ in range(max(2, n))]
+        self._next = 0
+        self._cv = threading.Condition()
+
+    def acquire(self) -> _Staging:
+        with self._cv:
+            st = self._bufs[self._next]
+            self._next = (self._next + 1) % len(self._bufs)
+            while st.busy:  # still waiting to be launched (the ring is sized so that this is rare)
+                self._cv.wait()
+            st.busy = True
+        if st.released is not None:
+            st.released.synchronize()  # the H2D copy of its previous batch retired
+            st.released = None
+        return st
+
+    def release(self, st: _Staging, event: torch.cuda.Event | None) -> None:
+        with self._cv:
+            st.released = event
+            st.busy = False
+            self._cv.notify_all()
+
+
+class _Prepared:
+    """A pulled, packed and probed host batch whose host-routed images are decoding in the pool."""
+
+    def __init__(self, staging: _Staging, jpegs, offsets: np.ndarray, info: np.ndarray, ws: int, aws: int,
+                 sizes: tuple[int, int], futures: dict):
+        self.staging = staging
+        self.jpegs = jpegs            # the source's list (None for the native feed)
         self.offsets = offsets
+        self.info = info
+        self.ws, self.aws = ws, aws
+        self.sizes = sizes            # (G, L) the augment-workspace bound was computed for
         self.futures = futures
+
+
+_END = object()
+
+
+class _Prefetcher:
+    """The host half of the pipeline on a worker thread (DALI's prefetch queue, reference
+    pipeline.py:317 ``prefetch_queue_depth``): pull the next batch from the source, pack it
+    into pinned staging (``dino_gather``), ``dino_probe`` it and submit its Pillow
+    hand-overs, up to ``ahead`` batches ahead of the launches.  The GIL is released inside
+    the native calls, so this overlaps the launch thread and the GPU."""
+
+    def __init__(self, pipe: "MI355XAugPipeline", ahead: int):
+        self._pipe = pipe
+        self._q: queue.Queue = queue.Queue(maxsize=max(1, ahead))
+        self._stop = threading.Event()
+        self.finished = False       # the source raised StopIteration (the END marker is queued)
+        self._thread = threading.Thread(target=self._run, name="dino-prefetch", daemon=True)
+        self._thread.start()
+
+    def _put(self, item) -> bool:
+        while not self._stop.is_set():
+            try:
+                self._q.put(item, timeout=0.1)
+                return True
+            except queue.Full:
+                continue
+        return False
+
+    def _run(self) -> None:
+        try:
+            while not self._stop.is_set():
+                pb = self._pipe._prepare_next()
+                if not self._put(pb):
+                    self._pipe._ring.release(pb.staging, None)
+                    return
+        except StopIteration:
+            self.finished = True
+            self._put(_END)
+        except BaseException as e:  # noqa: BLE001 - handed to the launch thread
+            self._put(e)
+
+    def get(self) -> _Prepared:
+        item = self._q.get()
+        if item is _END:
+            raise StopIteration
+        if isinstance(item, BaseException):
+            raise item
+        return item
+
+    def close(self) -> None:
+        self._stop.set()
+        while True:  # unblock a pending put, free staging of batches never launched
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if isinstance(item, _Prepared):
+                self._pipe._ring.release(item.staging, None)
+        self._thread.join(timeout=5.0)
 
 
 class MI355XAugPipeline:
     """``depth`` > 1 keeps that many batches in flight: each slot owns a ctx and a
     HIP stream, consecutive batches alternate slots, so one batch's entropy
-    decode (latency bound) overlaps another's resize/jitter kernels."""
+    decode (latency bound) overlaps another's resize/jitter kernels.
+
+    ``prefetch`` (default: 1 when depth > 1) runs the host half — pull, pack into pinned
+    staging, probe, Pillow hand-overs — that many batches ahead on a worker thread, so the
+    calling thread only launches (H2D copy + kernels) and hands over."""
 
     def __init__(self, source: Any, aug_cfg, batch_size: int, resolution_src=None, seed: int = 0,
-                 out_dtype="bf16", device: int = 0, max_image_dim: int = 8192, workspace_bytes: int = 0,
+                 out_dtype="bf16", device: int = 0, max_image_dim: int = 0, workspace_bytes: int = 0,
                  engine: IngestEngine | None = None, depth: int = 1, norm=None,
                  view_names: list[str] | None = None, host_fallback: bool = True,
                  multiscan_route: str = "auto", host_workers: int | None = None,
-                 multiscan_host_max: int | None = None):
+                 multiscan_host_max: int | None = None, prefetch: int | None = None,
+                 start_host_pool: bool = False):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -102,6 +218,8 @@ class MI355XAugPipeline:
         self._multiscan_route = multiscan_route
         workers = int(host_workers) if host_workers else min(8, os.cpu_count() or 1)
         self._host = fallback.HostDecoder(workers)
+        if start_host_pool:
+            self._host.start()
         # "auto": the host takes a batch's coefficient-buffer images while its workers finish
         # them in about the time k_prog needs for any number of them (~100 ms vs ~6 ms/image)
         self._host_max = int(multiscan_host_max) if multiscan_host_max is not None else 8 * workers
@@ -110,6 +228,10 @@ class MI355XAugPipeline:
         self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0, "reserves": 0}
         self._pending: deque = deque()
         self.depth = max(1, int(depth))
+        self.prefetch_ahead = (1 if self.depth > 1 else 0) if prefetch is None else max(0, int(prefetch))
+        self._prefetcher: _Prefetcher | None = None
+        self._ring = _StagingRing(self.depth + self.prefetch_ahead + 2)
+        self._native = hasattr(source, "next_spans")
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
@@ -160,7 +282,8 @@ class MI355XAugPipeline:
         return self._slots[self._batch_index % self.depth]
 
     def run_device_batch(self, d_bytes: torch.Tensor, d_offsets: torch.Tensor, batch: int | None = None,
-                         views: list[torch.Tensor] | None = None) -> dict[str, torch.Tensor]:
+                         views: list[torch.Tensor] | None = None,
+                         raw_mask: torch.Tensor | None = None) -> dict[str, torch.Tensor]:
         """Stage 3 on JPEG bytes already resident in HBM (the benchmark's device-resident path).
 
         With depth > 1 the work is enqueued on the slot's stream after the caller's
@@ -171,9 +294,10 @@ class MI355XAugPipeline:
         sl = self._next_slot()
         if sl.engine.stream is not None:
             sl.engine.stream.wait_stream(torch.cuda.current_stream(self.device))
-        return self._launch(sl, d_bytes, d_offsets, batch, views)
+        return self._launch(sl, d_bytes, d_offsets, batch, views, raw_mask=raw_mask)
 
-    def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views, cfg=None, account: bool = False):
+    def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views, cfg=None, account: bool = False,
+                raw_mask: torch.Tensor | None = None):
         batch = self._batch_size if batch is None else int(batch)
         if cfg is None:
             cfg = self._cfg(*self._sizes())
@@ -188,7 +312,7 @@ class MI355XAugPipeline:
                 sl.norm = recs.to(self.device, non_blocking=True)
             eng.set_norm(sl.norm)
         views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
-                                    views=views, params_out=sl.params)
+                                    views=views, params_out=sl.params, raw_mask=raw_mask)
         sl.info = info
         sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
         if account:  # per-image status back to the host asynchronously (accounted at a later hand-over)
@@ -209,46 +333,88 @@ class MI355XAugPipeline:
         self._batch_index += 1
         return sl.outputs
 
-    # ------------------------------------------------------------------ screening
-    def _prepare(self, jpegs=None, host_buf: torch.Tensor | None = None,
-                 offsets: np.ndarray | None = None) -> "_Prepared":
-        """Pull a batch from the source (unless given), pack and ``dino_probe`` it, and start
-        the Pillow decodes of the images routed to the host (``fallback.route_mask``) in the
-        worker pool.  ``_enqueue_prepared`` waits for them and launches the batch."""
-        if jpegs is None and host_buf is None:
+    # ------------------------------------------------------------------ host half
+    def _prepare_next(self) -> _Prepared:
+        """Pull the next batch from the source, pack it into a pinned staging buffer (the
+        native feed's byte ranges or the callable source's arrays, ``dino_gather``), probe it
+        with ``dino_probe`` (status, kinds, workspace bytes for the current (G, L)) and submit
+        the Pillow decodes of the images routed to the host (``fallback.route_mask``).  Runs
+        on the prefetch thread (or inline at prefetch 0)."""
+        from .tario import gather
+        B = self._batch_size
+        if self._native:
+            items = self._source.next_spans()  # may raise StopIteration (end of epoch)
+            jpegs = None
+            need = sum(n for _, n in items)
+        else:
             jpegs = self._source()  # may raise StopIteration (end of epoch)
-            if len(jpegs) != self._batch_size:
-                raise ValueError(f"source returned {len(jpegs)} samples, expected {self._batch_size}")
-            host_buf, off_t = pack_jpegs(jpegs, pin=True)
-            offsets = off_t.numpy()
-        batch = len(offsets) - 1
-        info, _, _ = fallback.probe(host_buf.data_ptr(), offsets, batch, self._max_image_dim)
-        mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
-        idx = np.flatnonzero(mask)
-        futures = {}
-        if len(idx):
-            if jpegs is None:  # packed native feed: slice the images back out of the staging buffer
-                hb = host_buf.numpy()
-                jpegs = [hb[offsets[i]:offsets[i + 1]] for i in range(batch)]
-            futures = {int(i): self._host.submit(jpegs[i]) for i in idx}
-        return _Prepared(jpegs, host_buf, offsets, futures)
+            items = jpegs
+            need = sum(len(j) for j in jpegs)
+        if len(items) != B:
+            raise ValueError(f"source returned {len(items)} samples, expected {B}")
+        st = self._ring.acquire()
+        try:
+            st.fit(need, B)
+            off = gather(items, st.buf, getattr(self._source, "nthreads", 8))
+            st.off.numpy()[: B + 1] = off
+            sizes = self._sizes()
+            cfg = self._cfg(*sizes)
+            info, ws, aws = fallback.probe(st.buf.data_ptr(), off, B, self._max_image_dim, cfg)
+            mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
+            futures = {}
+            idx = np.flatnonzero(mask)
+            if len(idx):
+                if jpegs is None:  # packed native feed: slice the images back out of the staging buffer
+                    hb = st.buf.numpy()
+                    jpegs = [bytes(hb[off[i]:off[i + 1]]) for i in range(B)]
+                futures = {int(i): self._host.submit(jpegs[i]) for i in idx}
+            return _Prepared(st, jpegs, off, info, ws, aws, sizes, futures)
+        except BaseException:
+            self._ring.release(st, None)
+            raise
 
-    def _screen(self, sl: _Slot, pb: "_Prepared", cfg):
-        """Collect a prepared batch's host decodes (re-packing the batch if there were any)
-        and grow the slot's workspaces to ``dino_probe``'s numbers for ``cfg``.  Returns
-        the (possibly re-packed) host buffer and offsets."""
-        host_buf, offsets = pb.host_buf, pb.offsets
+    def _pull(self) -> _Prepared:
+        if self.prefetch_ahead <= 0:
+            return self._prepare_next()
+        if self._prefetcher is None:
+            self._prefetcher = _Prefetcher(self, self.prefetch_ahead)
+        return self._prefetcher.get()
+
+    def _host_result(self, f, jpeg) -> bytes:
+        try:
+            return f.result()
+        except Exception:  # noqa: BLE001 - a broken worker pool: decode here (same bytes)
+            return fallback.pillow_container(jpeg)
+
+    def _screen(self, sl: _Slot, pb: _Prepared, cfg, sizes) -> tuple[torch.Tensor, torch.Tensor, int, torch.Tensor | None]:
+        """Collect a prepared batch's host decodes (re-packing the batch into its staging if
+        there were any), re-probe only if that or the crop sizes changed what the probe saw,
+        and grow the slot's workspaces (stream-ordered).  Returns the pinned buffer, pinned
+        offsets, byte count and pinned raw mask (None when the batch has no container)."""
+        st, B = pb.staging, len(pb.offsets) - 1
+        raw = None
+        ws, aws = pb.ws, pb.aws
         if pb.futures:
+            from .tario import gather
             jpegs = list(pb.jpegs)
             for i, f in pb.futures.items():
-                jpegs[i] = f.result()
+                jpegs[i] = self._host_result(f, jpegs[i])
             self.stats["host_decoded"] += len(pb.futures)
-            host_buf, off_t = pack_jpegs(jpegs, pin=True)
-            offsets = off_t.numpy()
-        _, ws, aws = fallback.probe(host_buf.data_ptr(), offsets, len(offsets) - 1, self._max_image_dim, cfg)
+            rm = fallback.raw_mask_of(jpegs, pb.futures)
+            st.fit(sum(len(j) for j in jpegs), B)
+            off = gather(jpegs, st.buf, 8)
+            st.off.numpy()[: B + 1] = off
+            st.mask.numpy()[:B] = rm
+            raw = st.mask[:B]
+            _, ws, aws = fallback.probe(st.buf.data_ptr(), off, B, self._max_image_dim, cfg, rm)
+            nbytes = int(off[-1])
+        else:
+            nbytes = int(pb.offsets[-1])
+            if tuple(sizes) != tuple(pb.sizes):
+                _, ws, aws = fallback.probe(st.buf.data_ptr(), pb.offsets, B, self._max_image_dim, cfg)
         if sl.engine.reserve(ws, aws):
             self.stats["reserves"] += 1
-        return host_buf, offsets
+        return st.buf, st.off[: B + 1], nbytes, raw
 
     def _account(self, block: bool = False, until: _Slot | None = None) -> None:
         """Fold the per-image status of finished batches into ``stats`` (oldest first);
@@ -271,62 +437,35 @@ class MI355XAugPipeline:
                 warnings.warn(f"MI355XAugPipeline: batch {bid}: {bad.size} decodable image(s) returned zero-filled "
                               f"views ({kinds}); see MI355XAugPipeline.stats", RuntimeWarning, stacklevel=3)
 
-    def _enqueue_packed(self) -> _Slot:
-        """Native feed (``source.next_spans()``, e.g. :class:`~dataloader_amd.tario.ShardBatchFeeder`):
-        the batch's JPEG byte ranges are gathered by ``dino_gather`` straight into the
-        slot's pinned staging buffer, then one H2D copy on the slot's stream."""
-        from .tario import gather
-
-        spans = self._source.next_spans()  # may raise StopIteration (end of epoch)
-        if len(spans) != self._batch_size:
-            raise ValueError(f"source returned {len(spans)} samples, expected {self._batch_size}")
-        sl = self._next_slot()
-        if sl.event is not None:
-            sl.event.synchronize()  # the slot's previous batch (and its H2D copy) retired: staging is free
-        need = sum(n for _, n in spans)
-        if sl.staging is None or sl.staging.numel() < need:
-            sl.staging = torch.empty(max(need, 1) * 5 // 4, dtype=torch.uint8, pin_memory=True)
-        if sl.staging_off is None or sl.staging_off.numel() < len(spans) + 1:
-            sl.staging_off = torch.empty(len(spans) + 1, dtype=torch.int64, pin_memory=True)
-        off = gather(spans, sl.staging, getattr(self._source, "nthreads", 8))
-        sl.staging_off.numpy()[: len(off)] = off
-        cfg = self._cfg(*self._sizes())
-        pb = self._prepare(host_buf=sl.staging, offsets=np.asarray(off, np.int64))
-        host_buf, offsets = self._screen(sl, pb, cfg)
-        if host_buf is sl.staging:
-            host_off, nbytes = sl.staging_off[: len(off)], need
-        else:  # re-packed after a Pillow hand-over
-            host_off, nbytes = torch.from_numpy(offsets).pin_memory(), int(offsets[-1])
-        with sl.engine.on_stream():
-            d_bytes = host_buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
-            d_offsets = host_off.to(self.device, non_blocking=True)
-        self._launch(sl, d_bytes, d_offsets, len(spans), None, cfg=cfg, account=True)
-        sl.inflight = (host_buf, host_off, d_bytes, d_offsets)
-        if sl.event is None:  # depth 1 (no side stream): the staging buffer is reused next batch
-            torch.cuda.current_stream(self.device).synchronize()
-        return sl
-
     def _enqueue_one(self) -> _Slot:
-        """Pull one batch from the source and enqueue it on the next slot (H2D on that slot's stream)."""
+        """Take the next prepared batch and enqueue it on the next slot: H2D copies of the
+        staging on the slot's stream, then the kernels (``dino_run_batch``)."""
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
-        if hasattr(self._source, "next_spans"):
-            return self._enqueue_packed()
-        return self._enqueue_prepared(self._prepare())
+        return self._enqueue_prepared(self._pull())
 
-    def _enqueue_prepared(self, pb: "_Prepared") -> _Slot:
+    def _enqueue_prepared(self, pb: _Prepared) -> _Slot:
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
-        sl = self._next_slot()
-        cfg = self._cfg(*self._sizes())
-        host_buf, off_np = self._screen(sl, pb, cfg)
-        offsets = torch.from_numpy(off_np)
-        with sl.engine.on_stream():
-            d_bytes = host_buf.to(self.device, non_blocking=True)
-            d_offsets = offsets.to(self.device, non_blocking=True)
-        self._launch(sl, d_bytes, d_offsets, len(off_np) - 1, None, cfg=cfg, account=True)
-        # torch's caching host allocator keeps the pinned staging block until the copy retires
-        sl.inflight = (host_buf, d_bytes, d_offsets)
+        st = pb.staging
+        try:
+            sl = self._next_slot()
+            sizes = self._sizes()
+            cfg = self._cfg(*sizes)
+            host_buf, host_off, nbytes, raw = self._screen(sl, pb, cfg, sizes)
+            B = len(pb.offsets) - 1
+            with sl.engine.on_stream():
+                d_bytes = host_buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
+                d_offsets = host_off.to(self.device, non_blocking=True)
+                d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
+                copied = torch.cuda.Event()
+                copied.record()
+            self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw)
+            sl.inflight = (d_bytes, d_offsets, d_raw)  # device copies live until the slot's next batch
+        except BaseException:
+            self._ring.release(st, None)
+            raise
+        self._ring.release(st, copied)
         return sl
 
     def _hand_over(self, sl: _Slot) -> dict[str, torch.Tensor]:
@@ -345,6 +484,12 @@ class MI355XAugPipeline:
 
     def run_one_batch(self) -> dict[str, torch.Tensor]:
         return self._hand_over(self._enqueue_one())
+
+    def restart_epoch(self) -> None:
+        """After the source's StopIteration and its reset: let the host half pull again."""
+        if self._prefetcher is not None and self._prefetcher.finished:
+            self._prefetcher.close()
+            self._prefetcher = None
 
     def last_params(self) -> np.ndarray:
         """Records of the last batch, sample-major (``[b * n_views + v]``)."""
@@ -369,6 +514,9 @@ class MI355XAugPipeline:
         if not self._closed:
             self._closed = True
             try:
+                if self._prefetcher is not None:
+                    self._prefetcher.close()
+                    self._prefetcher = None
                 self._account(block=True)
             finally:
                 self._host.close()
@@ -385,17 +533,16 @@ class MI355XAugPipeline:
 class MI355XPipelineIterator:
     """DALIGenericIterator-shaped wrapper: ``next()`` -> ``[ {view_name: Tensor} ]``.
 
-    Keeps ``pipeline.depth`` batches in flight (DALI's prefetch queue): each
-    ``next()`` tops the queue up, then hands over the oldest batch.  With a callable
-    source one more batch is pulled and probed ahead of the queue, so that the Pillow
-    decodes of the images it routes to the host run while the GPU works."""
+    Keeps ``pipeline.depth`` batches in flight (DALI's GPU prefetch queue): each
+    ``next()`` tops the queue up, then hands over the oldest batch.  The pipeline's
+    prefetch thread prepares the host half of the next batches (pull, pack, probe, Pillow
+    hand-overs) while the GPU works."""
 
     def __init__(self, pipeline: MI355XAugPipeline, output_map: list[str], batch_size: int) -> None:
         self._pipe = pipeline
         self._output_map = list(output_map)
         self._exhausted = False
         self._queue: deque = deque()
-        self._ahead: deque = deque()  # prepared (pulled, probed, host decodes started) batches
         self._source_done = False
 
     def __iter__(self):
@@ -405,15 +552,9 @@ class MI355XPipelineIterator:
         if self._exhausted:
             raise StopIteration
         pipe = self._pipe
-        lookahead = not hasattr(pipe._source, "next_spans")
         while not self._source_done and len(self._queue) < pipe.depth:
             try:
-                if not lookahead:
-                    self._queue.append(pipe._enqueue_one())
-                    continue
-                pb = self._ahead.popleft() if self._ahead else pipe._prepare()
-                self._queue.append(pipe._enqueue_prepared(pb))
-                self._ahead.append(pipe._prepare())
+                self._queue.append(pipe._enqueue_one())
             except StopIteration:
                 self._source_done = True
         if not self._queue:
@@ -424,7 +565,8 @@ class MI355XPipelineIterator:
     def reset(self) -> None:
         self._exhausted = False
         self._source_done = False
-        self._queue.clear()  # the prepared batch (not launched yet) is the source's next one: kept
+        self._queue.clear()  # batches prepared but not launched are the source's next ones: kept
+        self._pipe.restart_epoch()
 
 
 class MI355XUserAugPipeline:
@@ -436,7 +578,7 @@ class MI355XUserAugPipeline:
     undecodable image contributes zeros of shape (3, decode_size, decode_size)."""
 
     def __init__(self, source: Any, spec, batch_size: int, out_dtype="bf16", device: int = 0,
-                 max_image_dim: int = 16384, workspace_bytes: int = 0, norm=None):
+                 max_image_dim: int = 0, workspace_bytes: int = 0, norm=None):
         self._source = source
         self._spec = spec
         self._batch_size = int(batch_size)
@@ -446,11 +588,30 @@ class MI355XUserAugPipeline:
         self._engine = IngestEngine(device, max_batch=self._batch_size, max_views=1, max_crop_size=8,
                                     max_image_dim=max_image_dim, workspace_bytes=workspace_bytes)
         self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0}
+        self._pending_status: deque = deque()
         self._closed = False
 
     @property
     def device(self) -> torch.device:
         return self._engine.device
+
+    def _fold_status(self, st: np.ndarray) -> None:
+        self.stats["batches"] += 1
+        self.stats["images"] += len(st)
+        self.stats["status"].update(int(x) for x in st)
+        if (st > 0).any():
+            warnings.warn(f"MI355XUserAugPipeline: {int((st > 0).sum())} decodable image(s) returned zeros",
+                          RuntimeWarning, stacklevel=3)
+
+    def _drain_status(self, block: bool = False) -> None:
+        while self._pending_status and (block or self._pending_status[0][1].query()):
+            host, ev = self._pending_status.popleft()
+            ev.synchronize()
+            self._fold_status(host[:, 0].numpy())
+
+    def flush_stats(self) -> dict:
+        self._drain_status(block=True)
+        return self.stats
 
     def run_one_batch(self) -> dict[str, torch.Tensor]:
         if self._closed:
@@ -460,11 +621,14 @@ class MI355XUserAugPipeline:
         assert len(jpegs) == self._batch_size
         host_buf, offsets = pack_jpegs(jpegs, pin=True)
         info, ws, _ = fallback.probe(host_buf.data_ptr(), offsets.numpy(), len(jpegs), self._max_image_dim)
-        if (info[:, 0] == fallback.IMG_UNSUPPORTED).any():
-            jpegs, n = fallback.hand_over(list(jpegs), info[:, 0])
+        raw = None
+        if np.isin(info[:, 0], (fallback.IMG_UNSUPPORTED, fallback.IMG_LIMIT)).any():
+            jpegs, n, rm = fallback.hand_over(list(jpegs), info[:, 0])
             self.stats["host_decoded"] += n
             host_buf, offsets = pack_jpegs(jpegs, pin=True)
-            info, ws, _ = fallback.probe(host_buf.data_ptr(), offsets.numpy(), len(jpegs), self._max_image_dim)
+            info, ws, _ = fallback.probe(host_buf.data_ptr(), offsets.numpy(), len(jpegs), self._max_image_dim,
+                                         raw_mask=rm)
+            raw = torch.from_numpy(rm).pin_memory()
         ds = int(self._spec.decode_size)
         shapes = {resize_shorter_size(int(w), int(h), ds) if st == 0 else (ds, ds)
                   for st, w, h, _ in info.tolist()}
@@ -481,25 +645,37 @@ class MI355XUserAugPipeline:
         eng = self._engine
         d_bytes = host_buf.to(self.device, non_blocking=True)
         d_off = offsets.to(self.device, non_blocking=True)
+        d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
         if self._norm is not None:
             self._norm_dev = torch.from_numpy(self._norm.batch_records(len(jpegs))).to(self.device)
             eng.set_norm(self._norm_dev)
-        d_info = eng.decode(d_bytes, d_off, len(jpegs))
+        d_info = eng.decode(d_bytes, d_off, len(jpegs), raw_mask=d_raw)
         out = eng.resize_batch(ow, oh, self._spec.mean, self._spec.std, self._out)
         eng.batch_info(d_info)
-        st = d_info[:, 0].cpu().numpy()
-        self.stats["batches"] += 1
-        self.stats["images"] += len(st)
-        self.stats["status"].update(int(x) for x in st)
-        if (st > 0).any():
-            warnings.warn(f"MI355XUserAugPipeline: {int((st > 0).sum())} decodable image(s) returned zeros",
-                          RuntimeWarning, stacklevel=2)
-        self._inflight = (host_buf, d_bytes, d_off)
+        self._inflight = (host_buf, d_bytes, d_off, d_raw)
+        probe_ok = info[:, 0] == 0
+        if (ow, oh) != (ds, ds) and probe_ok.any():
+            # an image that probes fine but fails on the device (damaged entropy data) is the
+            # reference's (ds, ds) zero tensor, which its torch.stack refuses next to (ow, oh):
+            # only then does the batch need its device status before returning
+            st = d_info[:, 0].cpu().numpy()
+            if ((st != 0) & probe_ok).any():
+                raise RuntimeError(f"stack expects each tensor to be equal size, got resized shapes "
+                                   f"{sorted({(ow, oh), (ds, ds)})}")
+            self._fold_status(st)
+        else:  # shapes cannot disagree: the status is read back asynchronously
+            host = torch.empty(d_info.shape, dtype=d_info.dtype, pin_memory=True)
+            host.copy_(d_info, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._pending_status.append((host, ev))
+            self._drain_status()
         return self._spec.aug_fn(out)
 
     def close(self) -> None:
         if not self._closed:
             self._closed = True
+            self._drain_status(block=True)
             self._engine.close()
 
     def __del__(self):

@@ -413,6 +413,13 @@ class ShardBatchFeeder:
         self.wait_seconds += time.perf_counter() - t0
         return res
 
+    @property
+    def _batch_size(self) -> int:
+        """The source convention backends read (reference shard_reader.py:327-329, cpu.py:671)."""
+        return self._B
+
+    _resolution_src = None  # no per-batch crop sizes: the pipeline's configured sizes apply
+
     def next_spans(self) -> list[tuple[int, int]]:
         """(address, length) of the next batch's JPEGs; StopIteration at the epoch end."""
         spans: list[tuple[int, int]] = []

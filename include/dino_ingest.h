@@ -26,10 +26,16 @@
  *    Python layer pre-screens host batches with dino_probe, grows the workspaces
  *    with dino_reserve and hands flavours it cannot decode over as pre-decoded
  *    RGB images (DINO_RAW_MAGIC below), so the product path never zero-fills an
- *    image the reference would have decoded.
+ *    image the reference would have decoded (status > 0 left after a hand-over is
+ *    counted per batch by the Python layer and raised as a RuntimeWarning).
  *  - Input images are JPEG byte strings, or pre-decoded RGB images in the raw
  *    container: 16-byte header {uint32 DINO_RAW_MAGIC, uint32 width, uint32
- *    height, uint32 0} followed by width*height*3 bytes of HWC RGB.
+ *    height, uint32 0} followed by width*height*3 bytes of HWC RGB.  A container
+ *    is only accepted where the caller marks it in the raw mask (uint8 per image,
+ *    nullable = no containers): the magic is never trusted inside user data.
+ *  - ABI 3 (from 2): raw masks on dino_decode / dino_run_batch / dino_probe, a
+ *    stream on dino_reserve (stream-ordered growth, no device-wide sync), and
+ *    max_image_dim 0 = no side limit (65535).
  */
 #ifndef DINO_INGEST_H
 #define DINO_INGEST_H
@@ -40,7 +46,7 @@
 extern "C" {
 #endif
 
-#define DINO_ABI_VERSION 2
+#define DINO_ABI_VERSION 3
 
 /* return codes */
 #define DINO_OK 0
@@ -65,7 +71,8 @@ extern "C" {
 #define DINO_IMG_MULTISCAN 2         /* (ABI v1; no longer produced: multi-scan files are decoded) */
 #define DINO_IMG_NO_SPACE 3          /* the ctx workspace could not hold the image or one of its views
                                         (dino_reserve more and run again) */
-#define DINO_IMG_LIMIT 4             /* width or height above the ctx's max_image_dim */
+#define DINO_IMG_LIMIT 4             /* JPEG width or height above a caller-chosen max_image_dim (the
+                                        default has no side limit; the Python layer hands these to Pillow) */
 
 /* raw pre-decoded RGB container ("DRGB" little-endian) */
 #define DINO_RAW_MAGIC 0x42475244u
@@ -84,7 +91,8 @@ typedef struct dino_limits {
   int32_t max_batch;           /* images per call */
   int32_t max_views;           /* views per image (n_global + n_local) */
   int32_t max_crop_size;       /* largest S of any view (<= 1024) */
-  int32_t max_image_dim;       /* largest JPEG width or height accepted (<= 16384; 0 -> 8192) */
+  int32_t max_image_dim;       /* largest JPEG width or height accepted; 0 (default) -> 65535, i.e. no
+                                  side limit (only Pillow's decompression-bomb pixel count applies) */
   int64_t workspace_bytes;     /* decode workspace (HBM); 0 -> default */
 } dino_limits;
 
@@ -141,9 +149,10 @@ int dino_ctx_destroy(dino_ctx* ctx);
 
 /* Stage 3, decode half: JPEG bytes -> RGB planes kept in the ctx workspace.
  * d_bytes: packed JPEG bytes, d_offsets: int64[batch+1] byte offsets.
+ * d_raw_mask (nullable): uint8[batch], 1 where the image is a raw RGB container.
  * d_info (nullable): int32[batch][4] = {status, width, height, components}. */
-int dino_decode(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,
-                int32_t* d_info, void* stream);
+int dino_decode(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
+                int32_t batch, int32_t* d_info, void* stream);
 
 /* Copy decoded image i (HWC uint8 RGB, pitch = width*3) to d_rgb (debug / tests). */
 int dino_copy_rgb(dino_ctx* ctx, int32_t index, uint8_t* d_rgb, void* stream);
@@ -162,8 +171,8 @@ int dino_augment(dino_ctx* ctx, const dino_aug_config* cfg, const dino_view_para
 
 /* One call = decode + sample params + augment (CPUAugPipeline.run_one_batch).
  * d_params_out (nullable) receives the sampled records. */
-int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, int32_t batch,
-                   const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
+int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
+                   int32_t batch, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
                    dino_view_params* d_params_out, void* const* views, int32_t* d_info,
                    void* stream);
 
@@ -189,14 +198,18 @@ int dino_batch_info(dino_ctx* ctx, int32_t* d_info, void* stream);
  * decode workspace bytes the batch needs; aws_need: an upper bound of the augment
  * workspace for cfg's views (0 when cfg is NULL).  Images with status > 0 are the
  * ones the caller should decode itself and pass as raw RGB (DINO_RAW_MAGIC).
+ * raw_mask (nullable, HOST): as dino_decode's.
  * Replaces nothing in the reference (its decode cannot fail for capacity). */
-int dino_probe(const uint8_t* bytes, const int64_t* offsets, int32_t batch, int32_t max_image_dim,
-               const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need);
+int dino_probe(const uint8_t* bytes, const int64_t* offsets, const uint8_t* raw_mask, int32_t batch,
+               int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need,
+               int64_t* aws_need);
 
 /* Grow the ctx's decode / augment workspaces to at least the given sizes (never
- * shrinks).  Synchronises the device first when it reallocates; the last decoded
- * batch is invalidated. */
-int dino_reserve(dino_ctx* ctx, int64_t ws_bytes, int64_t aws_bytes);
+ * shrinks), stream-ordered on `stream` (the stream the ctx's batches run on): the old
+ * buffers are released after the work already enqueued there, nothing else on the
+ * device waits (switching to another stream first synchronises the previous one).
+ * The last decoded batch is invalidated. */
+int dino_reserve(dino_ctx* ctx, int64_t ws_bytes, int64_t aws_bytes, void* stream);
 int dino_workspace_sizes(dino_ctx* ctx, int64_t* ws_bytes, int64_t* aws_bytes);
 
 /* iBOT block masks (reference MaskingGenerator.__call__, masking.py:148-172).

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), f"{name} declared in dino_ingest.h but not exported"
     assert declared == set(_lib.exported_symbols())
-    assert lib.dino_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.dino_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_ctx_create_fails_loudly_without_gpu():
@@ -43,7 +43,7 @@ def test_bad_arguments_rejected_before_any_launch():
     assert b"max_batch" in lib.dino_last_error()
     assert lib.dino_ctx_create(0, ctypes.byref(DinoLimits(4, 10, 2048, 4096, 0)), ctypes.byref(ctx)) == -1
     assert b"max_crop_size" in lib.dino_last_error()
-    assert lib.dino_decode(None, None, None, 1, None, None) == -1
+    assert lib.dino_decode(None, None, None, None, 1, None, None) == -1
     assert lib.dino_masks(0, 4, 2, 1, 2, 0.0, 1.0, 1, None, None, None, None) == -1
 
 

@@ -121,7 +121,13 @@ def test_progressive_and_raw_decode_bit_exact(gpu_device):
     jpegs = base[:1] + prog[:6] + [raw_container(raws[0])] + prog[6:] + base[1:] + [raw_container(raws[1])]
     eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
     d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    # unmarked, the containers are what Pillow sees: not a JPEG -> corrupt (no in-band magic)
     info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    is_raw = np.array([j[:4] == b"DRGB" for j in jpegs])
+    assert (info[is_raw, 0] == -1).all() and (info[~is_raw, 0] == 0).all(), info
+    assert all(cpu_ref.decode_rgb(j) is None for j in np.array(jpegs, dtype=object)[is_raw])
+    raw_mask = torch.from_numpy(is_raw.astype(np.uint8)).to(gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs), raw_mask=raw_mask).cpu().numpy()
     assert (info[:, 0] == 0).all(), info
     bad = []
     for i, j in enumerate(jpegs):

@@ -21,9 +21,9 @@ from dataloader_amd.synthetic import encode_jpeg, textured_rgb
 from oracle import cpu_ref
 
 
-def _probe(jpegs, cfg=None, max_dim=16384):
+def _probe(jpegs, cfg=None, max_dim=0, raw_mask=None):
     buf, off = pack_jpegs(jpegs, pin=False)
-    return fallback.probe(buf.data_ptr(), off.numpy(), len(jpegs), max_dim, cfg)
+    return fallback.probe(buf.data_ptr(), off.numpy(), len(jpegs), max_dim, cfg, raw_mask)
 
 
 def _cmyk_jpeg(w, h, rng):
@@ -59,7 +59,8 @@ def test_probe_classifies_like_the_reference():
         (b"", -1, None),
         (prog[: len(prog) // 2], -2, None),            # truncated progressive: Pillow raises
     ]
-    info, ws, aws = _probe([c for c, _, _ in cases])
+    rm = np.array([k == 2 for _, _, k in cases], np.uint8)
+    info, ws, aws = _probe([c for c, _, _ in cases], raw_mask=rm)
     for i, (data, want, kind) in enumerate(cases):
         assert info[i, 0] == want, (i, info[i])
         if kind is not None:
@@ -72,6 +73,10 @@ def test_probe_classifies_like_the_reference():
         else:
             assert ref is not None, i
     assert ws > 0 and aws == 0
+    # the container magic is never trusted in user data.  Unmarked, a blob that
+    # starts with it is not a JPEG, exactly as Pillow sees it (the reference zero-fills)
+    info, _, _ = _probe([raw])
+    assert info[0, 0] == -1 and cpu_ref.decode_rgb(raw) is None
 
 
 def test_probe_workspace_grows_with_images():
@@ -91,6 +96,11 @@ def test_probe_limits():
     j = encode_jpeg(textured_rgb(300, 40, rng))
     info, _, _ = _probe([j], max_dim=256)
     assert info[0, 0] == 4  # DINO_IMG_LIMIT: the caller's ceiling, not a reference failure
+    assert fallback.route_mask(info, True, "auto", 8)[0]  # ... handed to Pillow by the pipeline
+    # the default has no side limit: very wide / tall JPEGs decode on the device
+    wide = [encode_jpeg(textured_rgb(9000, 40, rng)), encode_jpeg(textured_rgb(24, 17000, rng))]
+    info, _, _ = _probe(wide)
+    assert (info[:, 0] == 0).all() and list(info[:, 1]) == [9000, 24] and list(info[:, 2]) == [40, 17000]
     # a header claiming > 2 x PIL.Image.MAX_IMAGE_PIXELS: Pillow raises DecompressionBombError
     bomb = bytearray(j)
     k = bomb.index(b"\xff\xc0")
@@ -107,7 +117,7 @@ def test_hand_over_replaces_only_unsupported():
     arith = _with_sof_byte(good, marker=0xC9)
     jpegs = [good, cmyk, arith, b"junk"]
     info, _, _ = _probe(jpegs)
-    out, n = fallback.hand_over(jpegs, info[:, 0])
+    out, n, rm = fallback.hand_over(jpegs, info[:, 0])
     assert n == 2 and out[0] is good and out[3] == b"junk"
     for i in (1, 2):
         ref = cpu_ref.decode_rgb(jpegs[i])
@@ -116,7 +126,7 @@ def test_hand_over_replaces_only_unsupported():
         else:
             w, h = ref.size
             assert out[i][16:] == np.asarray(ref).tobytes() and int.from_bytes(out[i][4:8], "little") == w
-    info2, _, _ = _probe(out)
+    info2, _, _ = _probe(out, raw_mask=rm)
     assert (info2[[0, 1], 0] == 0).all() and info2[1, 3] == 2
 
 
@@ -145,12 +155,34 @@ def test_hand_over_in_worker_pool_matches_serial():
     info, _, _ = _probe(jpegs)
     mask = fallback.route_mask(info, True, "host", 0)
     assert list(mask) == [True, True, True, False, True]
-    serial, n = fallback.hand_over(jpegs, info[:, 0], mask)
+    serial, n, rm = fallback.hand_over(jpegs, info[:, 0], mask)
     pool = fallback.HostDecoder(2)
     try:
-        pooled, n2 = fallback.hand_over(jpegs, info[:, 0], mask, pool)
+        pooled, n2, rm2 = fallback.hand_over(jpegs, info[:, 0], mask, pool)
     finally:
         pool.close()
-    assert n == n2 == 4 and pooled == serial and pooled[3] == jpegs[3]
-    info2, _, _ = _probe(pooled)
+    assert n == n2 == 4 and pooled == serial and pooled[3] == jpegs[3] and (rm == rm2).all()
+    info2, _, _ = _probe(pooled, raw_mask=rm)
     assert list(info2[:, 3]) == [2, 2, 2, -1, 2]
+
+
+def test_host_decoder_falls_back_in_process(monkeypatch):
+    """a pool that cannot start (e.g. spawned children that cannot import the
+    training script's __main__) is reported at start() and the hand-over continues in
+    this process with the same bytes."""
+    import warnings
+    rng = np.random.default_rng(10)
+    cmyk = _cmyk_jpeg(30, 20, rng)
+    dec = fallback.HostDecoder(2)
+
+    class _Broken:
+        def __init__(self, *a, **k):
+            raise OSError("cannot start workers")
+    import concurrent.futures
+    monkeypatch.setattr(concurrent.futures, "ProcessPoolExecutor", _Broken)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        dec.start()
+    assert any("in-process" in str(x.message) for x in w)
+    assert dec.submit(cmyk).result() == fallback.pillow_container(cmyk)
+    dec.close()
