@@ -63,6 +63,7 @@ def load() -> ctypes.CDLL:
         "dino_probe": (i32, [vp, vp, vp, i32, i32, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(i64),
                              ctypes.POINTER(i64)]),
         "dino_reserve": (i32, [vp, i64, i64, vp]),
+        "dino_augment_need": (i32, [vp, i32, ctypes.POINTER(DinoAugConfig), ctypes.POINTER(i64)]),
         "dino_workspace_sizes": (i32, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "dino_masks_host": (i32, [i32, i32, i32, i32, i32, dbl, dbl, i32, vp, vp, vp]),
         "dino_resize_batch": (i32, [vp, i32, i32, vp, vp, i32, vp, vp]),
@@ -86,4 +87,5 @@ def exported_symbols() -> list[str]:
             "dino_copy_rgb", "dino_sample_params", "dino_augment", "dino_run_batch", "dino_masks",
             "dino_bf16_to_fp8", "dino_debug_region", "dino_set_timing", "dino_kernel_times",
             "dino_tar_index", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
-            "dino_probe", "dino_reserve", "dino_workspace_sizes", "dino_masks_host", "dino_resize_batch"]
+            "dino_probe", "dino_reserve", "dino_workspace_sizes", "dino_masks_host", "dino_resize_batch",
+            "dino_augment_need"]

@@ -258,6 +258,7 @@ int dino_reserve(dino_ctx* c, int64_t ws_bytes, int64_t aws_bytes, void* stream)
   }
   if (ws_bytes > c->ws_size) {
     const int64_t n = ws_bytes + ws_bytes / 8;  // headroom: fewer regrowths
+    c->last_batch = -1;  // the decoded batch (if any) lived in the old workspace
     (void)hipFreeAsync(c->d_ws, s);
     c->d_ws = nullptr;
     c->ws_size = 0;
@@ -274,7 +275,19 @@ int dino_reserve(dino_ctx* c, int64_t ws_bytes, int64_t aws_bytes, void* stream)
       return hip_fail(e, "dino_reserve: hipMallocAsync(augment workspace)");
     c->aws_size = n;
   }
-  c->last_batch = -1;  // the decoded batch (if any) lived in the old workspace
+  return DINO_OK;
+}
+
+int dino_augment_need(const int32_t* info, int32_t batch, const dino_aug_config* cfg, int64_t* aws_need) {
+  if (!info || batch < 0 || !cfg || !aws_need) return fail(DINO_EINVAL, "dino_augment_need: bad arguments%s%lld");
+  int64_t aws = 0;
+  for (int32_t i = 0; i < batch; ++i) {
+    if (info[4 * i] != DINO_IMG_OK) continue;
+    for (int v = 0; v < cfg->n_global + cfg->n_local; ++v)
+      aws += view_scratch_bound(v < cfg->n_global ? cfg->global_size : cfg->local_size, info[4 * i + 1],
+                                info[4 * i + 2]);
+  }
+  *aws_need = aws;
   return DINO_OK;
 }
 

@@ -70,6 +70,16 @@ def probe(host_buf_ptr: int, offsets: np.ndarray, batch: int, max_image_dim: int
     return info, int(ws.value), int(aws.value)
 
 
+def augment_need(info: np.ndarray, cfg) -> int:
+    """``dino_augment_need``: augment-workspace bytes of a probed batch for ``cfg``'s views."""
+    lib = _lib.load()
+    inf = np.ascontiguousarray(info, np.int32)
+    aws = ctypes.c_int64(0)
+    _lib.check(lib.dino_augment_need(inf.ctypes.data_as(ctypes.c_void_p), len(inf), ctypes.byref(cfg),
+                                     ctypes.byref(aws)), "dino_augment_need")
+    return int(aws.value)
+
+
 def pillow_container(jpeg) -> bytes:
     """One hand-over: the Pillow decode as a raw container, or b"" where Pillow raises."""
     rgb = decode_with_pillow(jpeg)

@@ -24,10 +24,12 @@ have decoded but that came back zero-filled raises a ``RuntimeWarning``.
 
 from __future__ import annotations
 
+import atexit
 import os
 import queue
 import threading
 import warnings
+import weakref
 from collections import Counter, deque
 from typing import Any
 
@@ -63,6 +65,9 @@ class _Slot:
         self.info_host: torch.Tensor | None = None    # pinned copy of the batch's per-image status
         self.done: torch.cuda.Event | None = None     # recorded after that copy (status accounting)
         self.batch_id = -1
+        self.batch_index = -1                          # the batch's RNG key (seed, batch_index)
+        self.sizes: tuple[int, int] | None = None     # (G, L) the views were made at
+        self.probe: np.ndarray | None = None          # dino_probe info of the batch (host batches)
 
 
 class _Staging:
@@ -92,13 +97,21 @@ class _StagingRing:
         self._bufs = [_Staging() for _ in range(max(2, n))]
         self._next = 0
         self._cv = threading.Condition()
+        self._closed = False
+
+    def close(self) -> None:
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
 
     def acquire(self) -> _Staging:
         with self._cv:
             st = self._bufs[self._next]
             self._next = (self._next + 1) % len(self._bufs)
-            while st.busy:  # still waiting to be launched (the ring is sized so that this is rare)
+            while st.busy and not self._closed:  # still waiting to be launched (rare: the ring is sized for it)
                 self._cv.wait()
+            if self._closed:
+                raise RuntimeError("MI355XAugPipeline closed")
             st.busy = True
         if st.released is not None:
             st.released.synchronize()  # the H2D copy of its previous batch retired
@@ -127,6 +140,18 @@ class _Prepared:
 
 
 _END = object()
+# open pipelines, closed at interpreter exit before torch tears down: a prefetch thread must
+# not hold pinned tensors while the interpreter finalises them
+_LIVE: "weakref.WeakSet[MI355XAugPipeline]" = weakref.WeakSet()
+
+
+@atexit.register
+def _close_live() -> None:
+    for p in list(_LIVE):
+        try:
+            p.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 class _Prefetcher:
@@ -247,6 +272,7 @@ class MI355XAugPipeline:
             self._slots.append(_Slot(eng))
         self._last: _Slot = self._slots[0]
         self._closed = False
+        _LIVE.add(self)
 
     @property
     def engine(self) -> IngestEngine:
@@ -297,10 +323,12 @@ class MI355XAugPipeline:
         return self._launch(sl, d_bytes, d_offsets, batch, views, raw_mask=raw_mask)
 
     def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views, cfg=None, account: bool = False,
-                raw_mask: torch.Tensor | None = None):
+                raw_mask: torch.Tensor | None = None, sizes=None, probe: np.ndarray | None = None):
         batch = self._batch_size if batch is None else int(batch)
         if cfg is None:
-            cfg = self._cfg(*self._sizes())
+            sizes = self._sizes()
+            cfg = self._cfg(*sizes)
+        sl.sizes, sl.probe, sl.batch_index = sizes, probe, self._batch_index
         eng = sl.engine
         if sl.params is None or sl.params.numel() < batch * self._aug_cfg.n_views * RECORD_BYTES:
             with eng.on_stream():
@@ -406,12 +434,12 @@ class MI355XAugPipeline:
             st.off.numpy()[: B + 1] = off
             st.mask.numpy()[:B] = rm
             raw = st.mask[:B]
-            _, ws, aws = fallback.probe(st.buf.data_ptr(), off, B, self._max_image_dim, cfg, rm)
+            pb.info, ws, aws = fallback.probe(st.buf.data_ptr(), off, B, self._max_image_dim, cfg, rm)
             nbytes = int(off[-1])
         else:
             nbytes = int(pb.offsets[-1])
             if tuple(sizes) != tuple(pb.sizes):
-                _, ws, aws = fallback.probe(st.buf.data_ptr(), pb.offsets, B, self._max_image_dim, cfg)
+                aws = fallback.augment_need(pb.info, cfg)
         if sl.engine.reserve(ws, aws):
             self.stats["reserves"] += 1
         return st.buf, st.off[: B + 1], nbytes, raw
@@ -460,7 +488,8 @@ class MI355XAugPipeline:
                 d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
                 copied = torch.cuda.Event()
                 copied.record()
-            self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw)
+            self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw, sizes=sizes,
+                         probe=pb.info)
             sl.inflight = (d_bytes, d_offsets, d_raw)  # device copies live until the slot's next batch
         except BaseException:
             self._ring.release(st, None)
@@ -468,9 +497,32 @@ class MI355XAugPipeline:
         self._ring.release(st, copied)
         return sl
 
+    def _refresh(self, sl: _Slot, sizes: tuple[int, int]) -> None:
+        """The crop sizes changed (``ResolutionSource.set``, reference loader.py:280-308) after
+        this batch was launched: make its views again at the new sizes from the decoded images
+        still in the slot's workspace (same (seed, batch index) records), so that a resolution
+        change takes effect on the next batch handed over (CPUBackend semantics, cpu.py:315-317)
+        even with ``depth`` batches in flight."""
+        cfg = self._cfg(*sizes)
+        eng = sl.engine
+        if eng.reserve(0, fallback.augment_need(sl.probe, cfg)):
+            self.stats["reserves"] += 1
+        eng.sample_params(cfg, self._seed, sl.batch_index, out=sl.params)
+        views = eng.augment(cfg, sl.params)
+        eng.batch_info(sl.info)
+        sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
+        sl.sizes = sizes
+        if eng.stream is not None:
+            sl.event = torch.cuda.Event()
+            sl.event.record(eng.stream)
+
     def _hand_over(self, sl: _Slot) -> dict[str, torch.Tensor]:
         """Order the caller's stream after the slot's work and tie the outputs to it."""
         self._account()
+        if self._resolution_src is not None and sl.probe is not None:
+            sizes = self._sizes()
+            if tuple(sizes) != tuple(sl.sizes):
+                self._refresh(sl, sizes)
         if sl.event is not None:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_event(sl.event)
@@ -513,7 +565,9 @@ class MI355XAugPipeline:
     def close(self) -> None:
         if not self._closed:
             self._closed = True
+            _LIVE.discard(self)
             try:
+                self._ring.close()
                 if self._prefetcher is not None:
                     self._prefetcher.close()
                     self._prefetcher = None

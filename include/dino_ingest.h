@@ -208,8 +208,15 @@ int dino_probe(const uint8_t* bytes, const int64_t* offsets, const uint8_t* raw_
  * shrinks), stream-ordered on `stream` (the stream the ctx's batches run on): the old
  * buffers are released after the work already enqueued there, nothing else on the
  * device waits (switching to another stream first synchronises the previous one).
- * The last decoded batch is invalidated. */
+ * Growing the decode workspace invalidates the last decoded batch; growing only the
+ * augment workspace keeps it (dino_augment may run on it again, e.g. at new crop sizes). */
 int dino_reserve(dino_ctx* ctx, int64_t ws_bytes, int64_t aws_bytes, void* stream);
+
+/* Augment-workspace bound of a probed batch for cfg's views: info is dino_probe's
+ * int32[batch][4] (HOST), aws_need as dino_probe's.  Lets a caller re-augment a decoded
+ * batch at other crop sizes (a resolution change with batches in flight) after growing
+ * the augment workspace, without the batch's bytes. */
+int dino_augment_need(const int32_t* info, int32_t batch, const dino_aug_config* cfg, int64_t* aws_need);
 int dino_workspace_sizes(dino_ctx* ctx, int64_t* ws_bytes, int64_t* aws_bytes);
 
 /* iBOT block masks (reference MaskingGenerator.__call__, masking.py:148-172).
