@@ -573,6 +573,8 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
                "e2e_shard_prepare_ms_total": round(feeder.index_seconds * 1e3, 3),
                "e2e_shard_wait_ms_total": round(feeder.wait_seconds * 1e3, 3),
                "e2e_gather_threads": args.gather_threads, "e2e_batches_in_flight": pipe.depth,
+               "e2e_host_ms_per_batch": {k: round(v * 1e3 / max(1, args.warmup + args.steps), 3)
+                                         for k, v in pipe.host_seconds.items()},
                "e2e_prefetch_ahead": pipe.prefetch_ahead,
                "e2e_path": "/dev/shm tar shards (shard_cache file format) -> ShardBatchFeeder -> "
                            "MI355XBackend.build_pipeline (prefetch thread: dino_gather into pinned staging, "

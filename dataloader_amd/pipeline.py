@@ -28,6 +28,7 @@ import atexit
 import os
 import queue
 import threading
+import time
 import warnings
 import weakref
 from collections import Counter, deque
@@ -251,6 +252,9 @@ class MI355XAugPipeline:
         # per-image outcome of every batch handed over (status code -> images), images the
         # GPU decoder left to Pillow, and workspace regrowths
         self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0, "reserves": 0}
+        # host-side seconds per phase: pull / pack / probe (host half), wait (launch thread
+        # waiting for the host half), launch (H2D copies + kernel enqueue)
+        self.host_seconds = {"pull": 0.0, "pack": 0.0, "probe": 0.0, "wait": 0.0, "launch": 0.0}
         self._pending: deque = deque()
         self.depth = max(1, int(depth))
         self.prefetch_ahead = (1 if self.depth > 1 else 0) if prefetch is None else max(0, int(prefetch))
@@ -270,7 +274,8 @@ class MI355XAugPipeline:
                                    max_crop_size=max_crop, max_image_dim=max_image_dim,
                                    workspace_bytes=workspace_bytes, stream=stream)
             self._slots.append(_Slot(eng))
-        self._last: _Slot = self._slots[0]
+        self._last: _Slot = self._slots[0]          # the last launched batch
+        self._handed: _Slot | None = None            # the last batch handed over (iterator / run_one_batch)
         self._closed = False
         _LIVE.add(self)
 
@@ -358,6 +363,7 @@ class MI355XAugPipeline:
             sl.event = torch.cuda.Event()
             sl.event.record(eng.stream)
         self._last = sl
+        self._handed = None
         self._batch_index += 1
         return sl.outputs
 
@@ -370,6 +376,8 @@ class MI355XAugPipeline:
         on the prefetch thread (or inline at prefetch 0)."""
         from .tario import gather
         B = self._batch_size
+        hs = self.host_seconds
+        t0 = time.perf_counter()
         if self._native:
             items = self._source.next_spans()  # may raise StopIteration (end of epoch)
             jpegs = None
@@ -382,12 +390,17 @@ class MI355XAugPipeline:
             raise ValueError(f"source returned {len(items)} samples, expected {B}")
         st = self._ring.acquire()
         try:
+            t1 = time.perf_counter()
             st.fit(need, B)
             off = gather(items, st.buf, getattr(self._source, "nthreads", 8))
             st.off.numpy()[: B + 1] = off
+            t2 = time.perf_counter()
             sizes = self._sizes()
             cfg = self._cfg(*sizes)
             info, ws, aws = fallback.probe(st.buf.data_ptr(), off, B, self._max_image_dim, cfg)
+            hs["pull"] += t1 - t0
+            hs["pack"] += t2 - t1
+            hs["probe"] += time.perf_counter() - t2
             mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
             futures = {}
             idx = np.flatnonzero(mask)
@@ -406,7 +419,11 @@ class MI355XAugPipeline:
             return self._prepare_next()
         if self._prefetcher is None:
             self._prefetcher = _Prefetcher(self, self.prefetch_ahead)
-        return self._prefetcher.get()
+        t0 = time.perf_counter()
+        try:
+            return self._prefetcher.get()
+        finally:
+            self.host_seconds["wait"] += time.perf_counter() - t0
 
     def _host_result(self, f, jpeg) -> bytes:
         try:
@@ -476,6 +493,7 @@ class MI355XAugPipeline:
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
         st = pb.staging
+        t0 = time.perf_counter()
         try:
             sl = self._next_slot()
             sizes = self._sizes()
@@ -495,6 +513,7 @@ class MI355XAugPipeline:
             self._ring.release(st, None)
             raise
         self._ring.release(st, copied)
+        self.host_seconds["launch"] += time.perf_counter() - t0
         return sl
 
     def _refresh(self, sl: _Slot, sizes: tuple[int, int]) -> None:
@@ -528,6 +547,7 @@ class MI355XAugPipeline:
             cur.wait_event(sl.event)
             for t in sl.outputs.values():
                 t.record_stream(cur)
+        self._handed = sl
         return sl.outputs
 
     def wait(self) -> None:
@@ -543,16 +563,21 @@ class MI355XAugPipeline:
             self._prefetcher.close()
             self._prefetcher = None
 
+    def _recent(self) -> _Slot:
+        """The batch whose outputs the caller saw last: the last one handed over since the last
+        launch (the iterator keeps later batches in flight), else the last one launched."""
+        return self._handed if self._handed is not None else self._last
+
     def last_params(self) -> np.ndarray:
-        """Records of the last batch, sample-major (``[b * n_views + v]``)."""
-        sl = self._last
+        """Records of the last batch (see ``_recent``), sample-major (``[b * n_views + v]``)."""
+        sl = self._recent()
         if sl.event is not None:
             sl.event.synchronize()
         n = sl.engine.last_batch * self._aug_cfg.n_views
         return params_from_device(sl.params[: n * RECORD_BYTES])
 
     def last_status(self) -> np.ndarray:
-        sl = self._last
+        sl = self._recent()
         if sl.event is not None:
             sl.event.synchronize()
         return sl.info[:, 0].cpu().numpy() if sl.info is not None else np.zeros(0, np.int32)
