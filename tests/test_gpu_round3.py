@@ -143,8 +143,12 @@ def test_wide_and_tall_jpegs_on_device_and_over_a_limit(gpu_device):
     rng = np.random.default_rng(52)
     jpegs = [encode_jpeg(textured_rgb(9000, 400, rng)), encode_jpeg(textured_rgb(300, 9001, rng)),
              encode_jpeg(textured_rgb(20000, 64, rng)), encode_jpeg(textured_rgb(640, 480, rng))]
+    from dataloader_amd import fallback
     eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
     buf, off = pack_jpegs(jpegs, pin=False)
+    pinfo, ws, _ = fallback.probe(buf.data_ptr(), off.numpy(), len(jpegs), 0)
+    assert (pinfo[:, 0] == 0).all(), pinfo  # no side limit by default
+    eng.reserve(ws, 0)  # the bare engine's default workspace holds ~1 of these; the pipeline probes + reserves
     info = eng.decode(buf.to(gpu_device), off.to(gpu_device), len(jpegs)).cpu().numpy()
     assert (info[:, 0] == 0).all(), info
     for i, j in enumerate(jpegs):
