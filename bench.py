@@ -521,6 +521,44 @@ def make_shards(jpegs, shard_size: int) -> list[bytes]:
     return shards
 
 
+class _GilSampler:
+    """Study tool (DINO_GIL_SAMPLER=1): a thread that wakes every 0.5 ms and charges the time
+    it took to get the GIL back to the line each other thread was on when it got it (the
+    line that held the GIL, or the one that just dropped it)."""
+
+    def __init__(self):
+        import threading
+        from collections import Counter
+        self._stop = threading.Event()
+        self.hist: dict = {}
+        self._C = Counter
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self):
+        import threading
+        me = threading.get_ident()
+        names = {}
+        while not self._stop.is_set():
+            t = time.perf_counter()
+            time.sleep(0.0005)
+            late = time.perf_counter() - t - 0.0005
+            for tid, fr in sys._current_frames().items():
+                if tid == me:
+                    continue
+                if tid not in names:
+                    names[tid] = next((th.name for th in threading.enumerate() if th.ident == tid), str(tid))
+                f = fr
+                key = f"{Path(f.f_code.co_filename).name}:{f.f_lineno}:{f.f_code.co_name}"
+                h = self.hist.setdefault(names[tid], self._C())
+                h[key] += late
+
+    def stop(self) -> dict:
+        self._stop.set()
+        self._t.join()
+        return {n: [(k, round(v * 1e3, 2)) for k, v in h.most_common(8)] for n, h in self.hist.items()}
+
+
 def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
     """C5 end-to-end, through the drop-in path: tar shards in /dev/shm (reference cache file
     format) -> ShardBatchFeeder (native tar index) -> ``MI355XBackend.build_pipeline`` (prefetch
@@ -531,8 +569,10 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
 
     from dataloader_amd.backend import MI355XBackend
     from dataloader_amd.config import DinoV2AugSpec, PipelineConfig
-    from dataloader_amd.tario import ShardBatchFeeder, ShmShardCache
+    from dataloader_amd.tario import NativeShardFeed, ShardBatchFeeder, ShmShardCache
 
+    if os.environ.get("DINO_SWITCH_INTERVAL"):  # study knob: the GIL hand-off interval
+        sys.setswitchinterval(float(os.environ["DINO_SWITCH_INTERVAL"]))
     pcfg = PipelineConfig(device_id=torch.cuda.current_device(), seed=1234 + rank, gpu_queue=args.gpu_queue,
                           output_dtype=args.dtype if args.dtype != "fp8" else "bf16",
                           dali_fp8_output=args.dtype == "fp8")
@@ -547,7 +587,10 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
         for p, t in zip(paths, shards):
             cache.put(p, t)  # Stage 1 (filesystem -> /dev/shm) is outside the timed region
         del shards
-        feeder = ShardBatchFeeder(cache, paths, B, nthreads=args.gather_threads)
+        if args.e2e_feed == "native":
+            feeder = NativeShardFeed(cache, paths, B, nthreads=args.gather_threads, slots=depth + 3)
+        else:
+            feeder = ShardBatchFeeder(cache, paths, B, nthreads=args.gather_threads)
         spec = DinoV2AugSpec(aug_cfg=cfg)
         pipe = backend.build_pipeline(feeder, spec, pcfg, None)
         it = backend.build_pipeline_iterator(pipe, spec, spec.output_map, B)
@@ -556,6 +599,7 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        sampler = _GilSampler() if os.environ.get("DINO_GIL_SAMPLER") else None
         t0 = time.perf_counter()
         for _ in range(args.steps):
             out = next(it)
@@ -563,6 +607,8 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
+        if sampler is not None:
+            print(json.dumps({"gil_sampler": sampler.stop()}), file=sys.stderr, flush=True)
         assert len(out) == 1 and len(out[0]) == cfg.n_views
         st = pipe.flush_stats()
         bad = {k: v for k, v in st["status"].items() if k != 0}
@@ -570,15 +616,22 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
             raise RuntimeError(f"e2e decode failures: {bad}")
         res = {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
                "e2e_ms_per_step": round(dt / args.steps * 1e3, 3),
-               "e2e_shard_prepare_ms_total": round(feeder.index_seconds * 1e3, 3),
-               "e2e_shard_wait_ms_total": round(feeder.wait_seconds * 1e3, 3),
+               "e2e_shard_prepare_ms_total": round(getattr(feeder, "index_seconds", 0.0) * 1e3, 3),
+               "e2e_shard_wait_ms_total": round(getattr(feeder, "wait_seconds", 0.0) * 1e3, 3),
                "e2e_gather_threads": args.gather_threads, "e2e_batches_in_flight": pipe.depth,
                "e2e_host_ms_per_batch": {k: round(v * 1e3 / max(1, args.warmup + args.steps), 3)
                                          for k, v in pipe.host_seconds.items()},
                "e2e_prefetch_ahead": pipe.prefetch_ahead,
-               "e2e_path": "/dev/shm tar shards (shard_cache file format) -> ShardBatchFeeder -> "
-                           "MI355XBackend.build_pipeline (prefetch thread: dino_gather into pinned staging, "
-                           "dino_probe) + build_pipeline_iterator -> H2D -> Stage 3"}
+               "e2e_feed": args.e2e_feed,
+               "e2e_path": ("/dev/shm tar shards (shard_cache file format) -> NativeShardFeed (C++ opener + packer "
+                            "threads: mmap, pre-fault, tar index, pack + probe into pinned slots) -> "
+                            "MI355XBackend.build_pipeline + build_pipeline_iterator -> H2D -> Stage 3")
+                           if args.e2e_feed == "native" else
+                           ("/dev/shm tar shards (shard_cache file format) -> ShardBatchFeeder -> "
+                            "MI355XBackend.build_pipeline (prefetch thread: dino_gather_probe into pinned staging) "
+                            "+ build_pipeline_iterator -> H2D -> Stage 3")}
+        if hasattr(feeder, "stats"):
+            res["e2e_feed_stats"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in feeder.stats().items()}
         feeder.close()
         pipe.close()
         return res
@@ -621,7 +674,9 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--e2e", action="store_true", help="C5 end-to-end leg even with --no-extras or N > 1")
     ap.add_argument("--gpu-queue", type=int, default=6, help="PipelineConfig.gpu_queue of the e2e leg")
     ap.add_argument("--shard-size", type=int, default=1000, help="samples per synthetic tar shard (e2e)")
-    ap.add_argument("--gather-threads", type=int, default=8, help="dino_gather copier threads (e2e)")
+    ap.add_argument("--gather-threads", type=int, default=8, help="copier threads of the e2e feed")
+    ap.add_argument("--e2e-feed", default="native", choices=["native", "python"],
+                    help="e2e host half: the native shard feed (C++ threads) or the Python prefetch thread")
     return ap
 
 

@@ -18,14 +18,23 @@ LIB_PATH = _PKG / "libdino_ingest.so"
 DINO_OK = 0
 IMG_STATUS = {0: "ok", -1: "corrupt", -2: "truncated", -3: "bad-data", -4: "too-large (Pillow bomb check)",
               1: "unsupported", 2: "multi-scan", 3: "no-space", 4: "over max_image_dim (handed to Pillow)"}
-ABI_VERSION = 3
+ABI_VERSION = 4
 RAW_MAGIC = 0x42475244  # "DRGB": pre-decoded RGB container (include/dino_ingest.h)
 
 _lib = None
+FEED_END, FEED_TIMEOUT, FEED_SHARD_ERROR = 1, 2, 3
 
 
 class DinoError(RuntimeError):
     pass
+
+
+class DinoFeedBatch(ctypes.Structure):
+    """``dino_feed_batch`` (include/dino_ingest.h)."""
+
+    _fields_ = [("slot", ctypes.c_int32), ("n", ctypes.c_int32), ("nbytes", ctypes.c_int64),
+                ("host", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("info", ctypes.c_void_p),
+                ("ws_need", ctypes.c_int64), ("aws_need", ctypes.c_int64), ("seq", ctypes.c_int64)]
 
 
 def load() -> ctypes.CDLL:
@@ -45,6 +54,27 @@ def load() -> ctypes.CDLL:
         "dino_ctx_create": (i32, [ctypes.c_int, ctypes.POINTER(DinoLimits), ctypes.POINTER(vp)]),
         "dino_ctx_destroy": (i32, [vp]),
         "dino_decode": (i32, [vp, vp, vp, vp, i32, vp, vp]),
+        "dino_decode_spans": (i32, [vp, vp, vp, vp, vp, i32, vp, vp]),
+        "dino_run_batch_spans": (i32, [vp, vp, vp, vp, vp, i32, ctypes.POINTER(DinoAugConfig), u64, u64, vp,
+                                       ctypes.POINTER(vp), vp, vp]),
+        "dino_probe_spans": (i32, [vp, vp, vp, i32, i32, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(i64),
+                                   ctypes.POINTER(i64)]),
+        "dino_gather_probe": (i32, [vp, vp, i32, vp, i64, vp, i32, i32, ctypes.POINTER(DinoAugConfig), vp,
+                                    ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+        "dino_feed_create": (i32, [i32, i32, i32, i32, i32, ctypes.POINTER(DinoAugConfig), ctypes.POINTER(vp)]),
+        "dino_feed_destroy": (i32, [vp]),
+        "dino_feed_push": (i32, [vp, ctypes.c_char_p]),
+        "dino_feed_end_epoch": (i32, [vp]),
+        "dino_feed_set_cfg": (i32, [vp, ctypes.POINTER(DinoAugConfig)]),
+        "dino_feed_next": (i32, [vp, i32, ctypes.POINTER(DinoFeedBatch)]),
+        "dino_feed_copy": (i32, [vp, i32, vp, vp, vp]),
+        "dino_feed_release": (i32, [vp, i32]),
+        "dino_feed_reset": (i32, [vp]),
+        "dino_feed_stats": (i32, [vp, vp, vp]),
+        "dino_feed_last_error": (ctypes.c_char_p, []),
+        "dino_host_register": (i32, [vp, i64]),
+        "dino_host_unregister": (i32, [vp]),
+        "dino_copy_h2d": (i32, [vp, vp, i64, vp]),
         "dino_copy_rgb": (i32, [vp, i32, vp, vp]),
         "dino_sample_params": (i32, [vp, ctypes.POINTER(DinoAugConfig), u64, u64, vp, vp]),
         "dino_augment": (i32, [vp, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(vp), vp]),
@@ -88,4 +118,8 @@ def exported_symbols() -> list[str]:
             "dino_bf16_to_fp8", "dino_debug_region", "dino_set_timing", "dino_kernel_times",
             "dino_tar_index", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
             "dino_probe", "dino_reserve", "dino_workspace_sizes", "dino_masks_host", "dino_resize_batch",
-            "dino_augment_need"]
+            "dino_augment_need", "dino_decode_spans", "dino_run_batch_spans", "dino_probe_spans",
+            "dino_host_register", "dino_host_unregister", "dino_copy_h2d", "dino_gather_probe",
+            "dino_feed_create", "dino_feed_destroy", "dino_feed_push", "dino_feed_end_epoch", "dino_feed_set_cfg",
+            "dino_feed_next", "dino_feed_copy", "dino_feed_release", "dino_feed_reset", "dino_feed_stats",
+            "dino_feed_last_error"]

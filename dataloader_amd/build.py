@@ -9,7 +9,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 OUT = PKG / "libdino_ingest.so"
-SOURCES = [CSRC / "kernels.hip", CSRC / "capi.hip", CSRC / "tario.cpp"]
+SOURCES = [CSRC / "kernels.hip", CSRC / "capi.hip", CSRC / "feed.hip", CSRC / "tario.cpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-strict-aliasing",
          "-fno-gpu-flush-denormals-to-zero", "-Wall", "-Wno-unused-function", "-pthread"]
 

@@ -10,20 +10,23 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include "hostcopy.hpp"
 #include "jpeg_parse.hpp"
 #include "kernels.hpp"
 #include "mask.hpp"
 #include "plan.hpp"
+#include "probe.hpp"
 #include "progressive.hpp"
 
 using namespace dino;
 
 namespace {
 thread_local std::string g_err;
-constexpr int32_t kMaxImageDim = 65535;
 
 int fail(int code, const char* fmt, const char* a = "", long long b = 0) {
   char buf[512];
@@ -131,18 +134,24 @@ int dino_ctx_destroy(dino_ctx* c) {
   return DINO_OK;
 }
 
-int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
-                int32_t batch, int32_t* d_info, void* stream) {
+int dino_decode_spans(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const int64_t* d_lengths,
+                      const uint8_t* d_raw_mask, int32_t batch, int32_t* d_info, void* stream) {
   if (!c || !d_bytes || !d_offsets) return fail(DINO_EINVAL, "dino_decode: null argument%s%lld");
   if (batch < 0 || batch > c->lim.max_batch)
     return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
   hipStream_t s = (hipStream_t)stream;
-  DecodeArgs a{d_bytes, d_offsets, d_raw_mask, batch, c->lim.max_image_dim, c->d_desc, c->d_ws, c->ws_size, c->geom};
+  DecodeArgs a{d_bytes, d_offsets, d_lengths, d_raw_mask, batch, c->lim.max_image_dim, c->d_desc, c->d_ws,
+               c->ws_size, c->geom};
   hipError_t e = launch_decode(a, s, c->tm());
   if (e != hipSuccess) return hip_fail(e, "dino_decode");
   if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
   c->last_batch = batch;
   return DINO_OK;
+}
+
+int dino_decode(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
+                int32_t batch, int32_t* d_info, void* stream) {
+  return dino_decode_spans(c, d_bytes, d_offsets, nullptr, d_raw_mask, batch, d_info, stream);
 }
 
 int dino_copy_rgb(dino_ctx* c, int32_t index, uint8_t* d_rgb, void* stream) {
@@ -206,17 +215,25 @@ int dino_set_norm(dino_ctx* c, const float* d_norm, int32_t n) {
   return DINO_OK;
 }
 
-int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
-                   int32_t batch, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
-                   dino_view_params* d_params_out, void* const* d_views, int32_t* d_info, void* stream) {
+int dino_run_batch_spans(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const int64_t* d_lengths,
+                         const uint8_t* d_raw_mask, int32_t batch, const dino_aug_config* cfg, uint64_t seed,
+                         uint64_t batch_index, dino_view_params* d_params_out, void* const* d_views, int32_t* d_info,
+                         void* stream) {
   if (!c) return fail(DINO_EINVAL, "dino_run_batch: null ctx%s%lld");
   int r = check_cfg(c, cfg);
   if (r) return r;
-  if ((r = dino_decode(c, d_bytes, d_offsets, d_raw_mask, batch, nullptr, stream))) return r;
+  if ((r = dino_decode_spans(c, d_bytes, d_offsets, d_lengths, d_raw_mask, batch, nullptr, stream))) return r;
   dino_view_params* prm = d_params_out ? d_params_out : c->d_params;
   if ((r = dino_sample_params(c, cfg, seed, batch_index, prm, stream))) return r;
   if ((r = dino_augment(c, cfg, prm, d_views, stream))) return r;
   return d_info ? dino_batch_info(c, d_info, stream) : DINO_OK;
+}
+
+int dino_run_batch(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
+                   int32_t batch, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
+                   dino_view_params* d_params_out, void* const* d_views, int32_t* d_info, void* stream) {
+  return dino_run_batch_spans(c, d_bytes, d_offsets, nullptr, d_raw_mask, batch, cfg, seed, batch_index,
+                              d_params_out, d_views, d_info, stream);
 }
 
 int dino_resize_batch(dino_ctx* c, int32_t out_w, int32_t out_h, const float* mean, const float* stdv,
@@ -298,42 +315,129 @@ int dino_workspace_sizes(dino_ctx* c, int64_t* ws_bytes, int64_t* aws_bytes) {
   return DINO_OK;
 }
 
-int dino_probe(const uint8_t* bytes, const int64_t* offsets, const uint8_t* raw_mask, int32_t batch,
-               int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need) {
-  if ((!bytes && batch > 0) || !offsets || batch < 0 || !ws_need || !aws_need)
-    return fail(DINO_EINVAL, "dino_probe: bad arguments%s%lld");
+}  // extern "C"
+
+namespace {
+template <class Src>
+int probe_impl(Src src, const uint8_t* raw_mask, int32_t batch, int32_t max_image_dim, const dino_aug_config* cfg,
+               int32_t* info, int64_t* ws_need, int64_t* aws_need) {
   if (max_image_dim <= 0 || max_image_dim > kMaxImageDim) max_image_dim = kMaxImageDim;
   int64_t ws = 0, aws = 0;
   std::vector<ScanRec> scans(kMaxScans);
   for (int32_t i = 0; i < batch; ++i) {
-    const int64_t off = offsets[i], len = offsets[i + 1] - off;
-    ImgDesc d;
-    if (len <= 0) {
-      d.status = DINO_IMG_CORRUPT;
-      d.width = d.height = d.ncomp = 0;
-    } else {
-      parse_jpeg(bytes + off, len, max_image_dim, &d, raw_mask != nullptr && raw_mask[i] != 0);
-      if (d.status == DINO_IMG_OK && d.kind == 1) {
-        HostMarkerFinder find;
-        prog_walk(bytes + off, len, &d, scans.data(), find);
-      }
-    }
-    if (info) {
-      info[4 * i + 0] = d.status;
-      info[4 * i + 1] = d.status == DINO_IMG_OK || d.status > 0 ? d.width : 0;
-      info[4 * i + 2] = d.status == DINO_IMG_OK || d.status > 0 ? d.height : 0;
-      info[4 * i + 3] = d.status == DINO_IMG_OK ? d.kind : -1;
-    }
-    if (d.status != DINO_IMG_OK) continue;
-    ws += image_chunk_bytes(d).total();
-    if (cfg) {
-      for (int v = 0; v < cfg->n_global + cfg->n_local; ++v)
-        aws += view_scratch_bound(v < cfg->n_global ? cfg->global_size : cfg->local_size, d.width, d.height);
-    }
+    const uint8_t* p;
+    int64_t len;
+    src(i, &p, &len);
+    probe_one(p, len, raw_mask != nullptr && raw_mask[i] != 0, max_image_dim, cfg, scans.data(),
+              info ? info + 4 * i : nullptr, &ws, &aws);
   }
   *ws_need = ws;
   *aws_need = aws;
   return DINO_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int dino_probe(const uint8_t* bytes, const int64_t* offsets, const uint8_t* raw_mask, int32_t batch,
+               int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need, int64_t* aws_need) {
+  if ((!bytes && batch > 0) || !offsets || batch < 0 || !ws_need || !aws_need)
+    return fail(DINO_EINVAL, "dino_probe: bad arguments%s%lld");
+  return probe_impl(
+      [&](int32_t i, const uint8_t** p, int64_t* len) {
+        *p = bytes + offsets[i];
+        *len = offsets[i + 1] - offsets[i];
+      },
+      raw_mask, batch, max_image_dim, cfg, info, ws_need, aws_need);
+}
+
+int dino_probe_spans(const uint64_t* ptrs, const int64_t* lens, const uint8_t* raw_mask, int32_t batch,
+                     int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need,
+                     int64_t* aws_need) {
+  if (((!ptrs || !lens) && batch > 0) || batch < 0 || !ws_need || !aws_need)
+    return fail(DINO_EINVAL, "dino_probe_spans: bad arguments%s%lld");
+  return probe_impl(
+      [&](int32_t i, const uint8_t** p, int64_t* len) {
+        *p = (const uint8_t*)(uintptr_t)ptrs[i];
+        *len = lens[i];
+      },
+      raw_mask, batch, max_image_dim, cfg, info, ws_need, aws_need);
+}
+
+int dino_gather_probe(const uint64_t* src_ptrs, const int64_t* lens, int32_t n, uint8_t* dst, int64_t dst_cap,
+                      int64_t* dst_offsets, int32_t nthreads, int32_t max_image_dim, const dino_aug_config* cfg,
+                      int32_t* info, int64_t* ws_need, int64_t* aws_need) {
+  if (n < 0 || (n > 0 && (!src_ptrs || !lens || !dst)) || !dst_offsets || !ws_need || !aws_need)
+    return fail(DINO_EINVAL, "dino_gather_probe: bad arguments%s%lld");
+  if (max_image_dim <= 0 || max_image_dim > kMaxImageDim) max_image_dim = kMaxImageDim;
+  dst_offsets[0] = 0;
+  for (int32_t i = 0; i < n; ++i) {
+    if (lens[i] < 0) return fail(DINO_EINVAL, "dino_gather_probe: negative length%s%lld");
+    dst_offsets[i + 1] = dst_offsets[i] + lens[i];
+  }
+  if (dst_offsets[n] > dst_cap) return fail(DINO_ERANGE, "dino_gather_probe: destination too small%s%lld");
+  const int64_t total = dst_offsets[n];
+  int nt = nthreads > 0 ? nthreads : 1;
+  nt = (int)std::min<int64_t>(nt, std::max<int32_t>(n, 1));
+  std::vector<int64_t> ws(nt, 0), aws(nt, 0);
+  // thread k copies, then probes, images [first(k), first(k+1)): first(k) is the first image
+  // starting at or after byte k*total/nt (the header is still in cache when its parse runs)
+  auto first = [&](int k) -> int32_t {
+    if (k <= 0) return 0;
+    if (k >= nt) return n;
+    return (int32_t)(std::lower_bound(dst_offsets, dst_offsets + n, total * k / nt) - dst_offsets);
+  };
+  auto work = [&](int k) {
+    std::vector<ScanRec> scans(kMaxScans);
+    for (int32_t i = first(k), e = first(k + 1); i < e; ++i) {
+      const uint8_t* src = (const uint8_t*)(uintptr_t)src_ptrs[i];
+      if (lens[i]) stream_copy(dst + dst_offsets[i], src, lens[i]);
+      probe_one(src, lens[i], false, max_image_dim, cfg, scans.data(), info ? info + 4 * i : nullptr, &ws[k],
+                &aws[k]);
+    }
+    stream_fence();
+  };
+  if (nt == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    for (int k = 1; k < nt; ++k) th.emplace_back(work, k);
+    work(0);
+    for (auto& t : th) t.join();
+  }
+  int64_t w = 0, a = 0;
+  for (int k = 0; k < nt; ++k) {
+    w += ws[k];
+    a += aws[k];
+  }
+  *ws_need = w;
+  *aws_need = a;
+  return DINO_OK;
+}
+
+int dino_host_register(void* host, int64_t nbytes) {
+  if (!host || nbytes <= 0) return fail(DINO_EINVAL, "dino_host_register: bad arguments%s%lld");
+  // read-only page-locking first (shard mappings are PROT_READ), then the default flags
+  hipError_t e = hipHostRegister(host, (size_t)nbytes, hipHostRegisterReadOnly);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    e = hipHostRegister(host, (size_t)nbytes, hipHostRegisterDefault);
+  }
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_host_register");
+}
+
+int dino_host_unregister(void* host) {
+  if (!host) return fail(DINO_EINVAL, "dino_host_unregister: null pointer%s%lld");
+  hipError_t e = hipHostUnregister(host);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_host_unregister");
+}
+
+int dino_copy_h2d(void* d_dst, const void* host_src, int64_t nbytes, void* stream) {
+  if ((!d_dst || !host_src) && nbytes > 0) return fail(DINO_EINVAL, "dino_copy_h2d: null argument%s%lld");
+  if (nbytes <= 0) return DINO_OK;
+  hipError_t e = hipMemcpyAsync(d_dst, host_src, (size_t)nbytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_copy_h2d");
 }
 
 int dino_masks(int32_t height, int32_t width, int32_t num_masking_patches, int32_t min_num_patches,

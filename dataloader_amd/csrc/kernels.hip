@@ -43,11 +43,12 @@ namespace dino {
 // (a header longer than the prefix, a raw container) is redone on the global bytes.
 constexpr int kParsePrefix = 4096;
 __global__ void __launch_bounds__(64) k_parse(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
+                                              const int64_t* __restrict__ lengths,
                                               const uint8_t* __restrict__ raw_mask, int B, int max_dim,
                                               ImgDesc* __restrict__ desc) {
   __shared__ __attribute__((aligned(16))) uint8_t s_raw[kParsePrefix + 16];
   const int i = blockIdx.x;
-  const int64_t off = offsets[i], len = offsets[i + 1] - off;
+  const int64_t off = offsets[i], len = lengths ? lengths[i] : offsets[i + 1] - off;
   const int64_t n = len < kParsePrefix ? len : kParsePrefix;
   const uint8_t* src = bytes + off;
   // aligned 16-byte chunks from the chunk holding src (the copy starts `lead` bytes into
@@ -1050,6 +1051,7 @@ struct ProgLds {
 
 __global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict__ bytes,
                                                        const int64_t* __restrict__ offsets,
+                                                       const int64_t* __restrict__ lengths,
                                                        ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   __shared__ ProgLds L;
   const int img = blockIdx.x, t = threadIdx.x;
@@ -1057,7 +1059,7 @@ __global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict
   if (t == 0) L.d = desc[img];
   __syncthreads();
   const uint8_t* p = bytes + offsets[img];
-  const int64_t len = offsets[img + 1] - offsets[img];
+  const int64_t len = lengths ? lengths[img] : offsets[img + 1] - offsets[img];
   WaveMarkerFinder find;
   // every lane runs the walk on the LDS descriptor (identical values, identical writes)
   prog_walk(p, len, &L.d, L.scans, find);
@@ -2827,13 +2829,13 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
   if (B <= 0) return hipSuccess;
-  TIMED(tm, kKParse, s, (k_parse<<<B, 64, 0, s>>>(a.bytes, a.offsets, a.raw_mask, B, a.max_dim, a.desc)));
+  TIMED(tm, kKParse, s, (k_parse<<<B, 64, 0, s>>>(a.bytes, a.offsets, a.lengths, a.raw_mask, B, a.max_dim, a.desc)));
   TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
   const int grid_ds = a.geom.grid_ds, grid1 = a.geom.grid1, grid3 = a.geom.grid3;
   TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
-  TIMED(tm, kKProg, s, (k_prog<<<B, kProgThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));  // after k_htab's kind switch
+  TIMED(tm, kKProg, s, (k_prog<<<B, kProgThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws)));  // after k_htab's kind switch
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));

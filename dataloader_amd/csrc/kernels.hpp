@@ -68,6 +68,7 @@ hipError_t init_launch_geom(int device, LaunchGeom* g);
 struct DecodeArgs {
   const uint8_t* bytes;
   const int64_t* offsets;
+  const int64_t* lengths;   // per image byte count (nullable: offsets[i+1] - offsets[i]); spans input
   const uint8_t* raw_mask;  // per image: 1 = pre-decoded RGB container (nullable: none)
   int32_t batch;
   int32_t max_dim;

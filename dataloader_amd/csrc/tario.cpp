@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "../../include/dino_ingest.h"
+#include "hostcopy.hpp"
 
 namespace {
 
@@ -261,7 +262,8 @@ int dino_gather(const uint64_t* src_ptrs, const int64_t* lens, int64_t n, uint8_
     if (i < 0) i = 0;
     if (k > 0 && dst_offsets[i] < lo) ++i;
     for (; i < n && dst_offsets[i] < hi; ++i)
-      if (lens[i]) memcpy(dst + dst_offsets[i], (const void*)(uintptr_t)src_ptrs[i], (size_t)lens[i]);
+      if (lens[i]) dino::stream_copy(dst + dst_offsets[i], (const uint8_t*)(uintptr_t)src_ptrs[i], lens[i]);
+    dino::stream_fence();
   };
   if (nt == 1) {
     work(0);

@@ -73,15 +73,24 @@ class IngestEngine:
 
     # ------------------------------------------------------------------ decode
     def decode(self, d_bytes: torch.Tensor, d_offsets: torch.Tensor, batch: int,
-               info: torch.Tensor | None = None, raw_mask: torch.Tensor | None = None) -> torch.Tensor:
-        """``raw_mask``: device uint8[batch], 1 where the image is a raw RGB container (hand-over)."""
+               info: torch.Tensor | None = None, raw_mask: torch.Tensor | None = None,
+               lengths: torch.Tensor | None = None) -> torch.Tensor:
+        """``raw_mask``: device uint8[batch], 1 where the image is a raw RGB container (hand-over);
+        ``lengths``: device int64[batch], the spans form (``dino_decode_spans``)."""
         if info is None:
             with self.on_stream():
                 info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
-        _lib.check(self.lib.dino_decode(self._ctx, _ptr(d_bytes), _ptr(d_offsets), _optr(raw_mask), batch,
-                                        _ptr(info), self._s()), "dino_decode")
+        _lib.check(self.lib.dino_decode_spans(self._ctx, _ptr(d_bytes), _ptr(d_offsets), _optr(lengths),
+                                              _optr(raw_mask), batch, _ptr(info), self._s()), "dino_decode")
         self.last_batch = batch
         return info
+
+    def copy_from_host(self, d_dst: torch.Tensor, dst_off: int, host_addr: int, nbytes: int) -> None:
+        """Asynchronous DMA of ``nbytes`` at host address ``host_addr`` (page-locked) into
+        ``d_dst[dst_off:]`` on this engine's stream (``dino_copy_h2d``)."""
+        assert 0 <= dst_off and dst_off + nbytes <= d_dst.numel() * d_dst.element_size()
+        _lib.check(self.lib.dino_copy_h2d(ctypes.c_void_p(d_dst.data_ptr() + dst_off), ctypes.c_void_p(host_addr),
+                                          int(nbytes), self._s()), "dino_copy_h2d")
 
     def copy_rgb(self, index: int, width: int, height: int) -> torch.Tensor:
         with self.on_stream():
@@ -138,7 +147,10 @@ class IngestEngine:
 
     def run_batch(self, d_bytes, d_offsets, batch: int, cfg, seed: int, batch_index: int,
                   views: list[torch.Tensor] | None = None, params_out: torch.Tensor | None = None,
-                  info: torch.Tensor | None = None, raw_mask: torch.Tensor | None = None):
+                  info: torch.Tensor | None = None, raw_mask: torch.Tensor | None = None,
+                  lengths: torch.Tensor | None = None):
+        """``lengths`` (device int64[batch], optional): the spans form (``dino_run_batch_spans``):
+        image i is d_bytes[d_offsets[i] : d_offsets[i] + lengths[i]]."""
         if views is None:
             views = self.alloc_views(cfg, batch)
         if info is None:
@@ -146,10 +158,10 @@ class IngestEngine:
                 info = torch.empty(batch, 4, dtype=torch.int32, device=self.device)
         ptrs = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
         pp = _ptr(params_out) if params_out is not None else ctypes.c_void_p(0)
-        _lib.check(self.lib.dino_run_batch(self._ctx, _ptr(d_bytes), _ptr(d_offsets), _optr(raw_mask), batch,
-                                           ctypes.byref(cfg),
-                                           seed & (2**64 - 1), batch_index, pp, ptrs, _ptr(info),
-                                           self._s()), "dino_run_batch")
+        _lib.check(self.lib.dino_run_batch_spans(self._ctx, _ptr(d_bytes), _ptr(d_offsets), _optr(lengths),
+                                                 _optr(raw_mask), batch, ctypes.byref(cfg),
+                                                 seed & (2**64 - 1), batch_index, pp, ptrs, _ptr(info),
+                                                 self._s()), "dino_run_batch")
         self.last_batch = batch
         return views, info
 

@@ -70,6 +70,42 @@ def probe(host_buf_ptr: int, offsets: np.ndarray, batch: int, max_image_dim: int
     return info, int(ws.value), int(aws.value)
 
 
+def probe_spans(ptrs: np.ndarray, lens: np.ndarray, max_image_dim: int, cfg=None):
+    """``dino_probe_spans`` over images where they lie (absolute host addresses + lengths,
+    e.g. JPEG members of mapped shards) -> (info[B,4] int32, ws_bytes, aws_bytes)."""
+    lib = _lib.load()
+    p = np.ascontiguousarray(ptrs, np.uint64)
+    n = np.ascontiguousarray(lens, np.int64)
+    batch = len(p)
+    info = np.zeros((batch, 4), np.int32)
+    ws, aws = ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.check(lib.dino_probe_spans(p.ctypes.data_as(ctypes.c_void_p), n.ctypes.data_as(ctypes.c_void_p), None,
+                                    batch, max_image_dim, ctypes.byref(cfg) if cfg is not None else None,
+                                    info.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ws), ctypes.byref(aws)),
+               "dino_probe_spans")
+    return info, int(ws.value), int(aws.value)
+
+
+def gather_probe(ptrs: np.ndarray, lens: np.ndarray, dst, nthreads: int, max_image_dim: int, cfg=None):
+    """``dino_gather_probe``: pack the images (absolute host addresses + lengths) into the
+    pinned tensor ``dst`` and probe each right after its copy, on ``nthreads`` threads ->
+    (int64 offsets[B+1], info[B,4] int32, ws_bytes, aws_bytes)."""
+    lib = _lib.load()
+    p = np.ascontiguousarray(ptrs, np.uint64)
+    n = np.ascontiguousarray(lens, np.int64)
+    batch = len(p)
+    off = np.empty(batch + 1, np.int64)
+    info = np.zeros((batch, 4), np.int32)
+    ws, aws = ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.check(lib.dino_gather_probe(p.ctypes.data_as(ctypes.c_void_p), n.ctypes.data_as(ctypes.c_void_p), batch,
+                                     ctypes.c_void_p(dst.data_ptr()), dst.numel() * dst.element_size(),
+                                     off.ctypes.data_as(ctypes.c_void_p), int(nthreads), max_image_dim,
+                                     ctypes.byref(cfg) if cfg is not None else None,
+                                     info.ctypes.data_as(ctypes.c_void_p), ctypes.byref(ws), ctypes.byref(aws)),
+               "dino_gather_probe")
+    return off, info, int(ws.value), int(aws.value)
+
+
 def augment_need(info: np.ndarray, cfg) -> int:
     """``dino_augment_need``: augment-workspace bytes of a probed batch for ``cfg``'s views."""
     lib = _lib.load()

@@ -69,6 +69,8 @@ class _Slot:
         self.batch_index = -1                          # the batch's RNG key (seed, batch_index)
         self.sizes: tuple[int, int] | None = None     # (G, L) the views were made at
         self.probe: np.ndarray | None = None          # dino_probe info of the batch (host batches)
+        self.d_in: torch.Tensor | None = None         # HBM copy of the batch's bytes (spans / native feed)
+        self.d_off: torch.Tensor | None = None        # HBM offsets of the native feed's batch
 
 
 class _Staging:
@@ -79,15 +81,17 @@ class _Staging:
     def __init__(self):
         self.buf: torch.Tensor | None = None
         self.off: torch.Tensor | None = None
+        self.lens: torch.Tensor | None = None
         self.mask: torch.Tensor | None = None
         self.released: torch.cuda.Event | None = None
         self.busy = False
 
     def fit(self, nbytes: int, n: int) -> None:
-        if self.buf is None or self.buf.numel() < nbytes:
+        if nbytes > 0 and (self.buf is None or self.buf.numel() < nbytes):
             self.buf = torch.empty(max(nbytes, 1) * 5 // 4 + 64, dtype=torch.uint8, pin_memory=True)
         if self.off is None or self.off.numel() < n + 1:
             self.off = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+            self.lens = torch.empty(n, dtype=torch.int64, pin_memory=True)
             self.mask = torch.empty(n, dtype=torch.uint8, pin_memory=True)
 
 
@@ -130,8 +134,10 @@ class _Prepared:
     """A pulled, packed and probed host batch whose host-routed images are decoding in the pool."""
 
     def __init__(self, staging: _Staging, jpegs, offsets: np.ndarray, info: np.ndarray, ws: int, aws: int,
-                 sizes: tuple[int, int], futures: dict):
-        self.staging = staging
+                 sizes: tuple[int, int], futures: dict, spans=None, feed=None):
+        self.staging = staging        # None: no Python staging (native feed slot, or not yet needed)
+        self.spans = spans            # tario.BatchSpans: the batch stays in its page-locked shard ranges
+        self.feed = feed              # tario.FeedBatch: the batch is packed in a native feed slot
         self.jpegs = jpegs            # the source's list (None for the native feed)
         self.offsets = offsets
         self.info = info
@@ -184,7 +190,7 @@ class _Prefetcher:
             while not self._stop.is_set():
                 pb = self._pipe._prepare_next()
                 if not self._put(pb):
-                    self._pipe._ring.release(pb.staging, None)
+                    self._pipe._drop(pb)
                     return
         except StopIteration:
             self.finished = True
@@ -208,7 +214,7 @@ class _Prefetcher:
             except queue.Empty:
                 break
             if isinstance(item, _Prepared):
-                self._pipe._ring.release(item.staging, None)
+                self._pipe._drop(item)
         self._thread.join(timeout=5.0)
 
 
@@ -261,6 +267,11 @@ class MI355XAugPipeline:
         self._prefetcher: _Prefetcher | None = None
         self._ring = _StagingRing(self.depth + self.prefetch_ahead + 2)
         self._native = hasattr(source, "next_spans")
+        # the feed can hand batches over where they lie (page-locked shard ranges, DMA'd as they are)
+        self._spans_feed = hasattr(source, "next_batch_spans")
+        # the native feed (tario.NativeShardFeed): batches arrive packed + probed by C++ threads
+        self._feed = hasattr(source, "next_prepared")
+        self._held: deque = deque()   # the feed's next batch, prepared one ahead (Pillow hand-overs start early)
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
@@ -278,6 +289,10 @@ class MI355XAugPipeline:
         self._handed: _Slot | None = None            # the last batch handed over (iterator / run_one_batch)
         self._closed = False
         _LIVE.add(self)
+        if self._feed:
+            sizes = self._sizes()
+            self._feed_sizes = sizes
+            self._source.configure(max_image_dim=self._max_image_dim, cfg=self._cfg(*sizes))
 
     @property
     def engine(self) -> IngestEngine:
@@ -328,7 +343,8 @@ class MI355XAugPipeline:
         return self._launch(sl, d_bytes, d_offsets, batch, views, raw_mask=raw_mask)
 
     def _launch(self, sl: _Slot, d_bytes, d_offsets, batch, views, cfg=None, account: bool = False,
-                raw_mask: torch.Tensor | None = None, sizes=None, probe: np.ndarray | None = None):
+                raw_mask: torch.Tensor | None = None, sizes=None, probe: np.ndarray | None = None,
+                lengths: torch.Tensor | None = None):
         batch = self._batch_size if batch is None else int(batch)
         if cfg is None:
             sizes = self._sizes()
@@ -345,7 +361,7 @@ class MI355XAugPipeline:
                 sl.norm = recs.to(self.device, non_blocking=True)
             eng.set_norm(sl.norm)
         views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
-                                    views=views, params_out=sl.params, raw_mask=raw_mask)
+                                    views=views, params_out=sl.params, raw_mask=raw_mask, lengths=lengths)
         sl.info = info
         sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
         if account:  # per-image status back to the host asynchronously (accounted at a later hand-over)
@@ -369,52 +385,116 @@ class MI355XAugPipeline:
 
     # ------------------------------------------------------------------ host half
     def _prepare_next(self) -> _Prepared:
-        """Pull the next batch from the source, pack it into a pinned staging buffer (the
-        native feed's byte ranges or the callable source's arrays, ``dino_gather``), probe it
-        with ``dino_probe`` (status, kinds, workspace bytes for the current (G, L)) and submit
-        the Pillow decodes of the images routed to the host (``fallback.route_mask``).  Runs
-        on the prefetch thread (or inline at prefetch 0)."""
-        from .tario import gather
+        """Pull the next batch from the source and make it ready to launch: pack it into a
+        pinned staging buffer and probe it in one native pass (``dino_gather_probe``: the
+        copier threads parse each image's header right after copying it: status, kind,
+        workspace bytes for the current (G, L)), then submit the Pillow decodes of the images
+        routed to the host (``fallback.route_mask``).  A page-locked spans feed batch that
+        needs no hand-over is not packed at all (its shard ranges are DMA'd at launch).
+        Runs on the prefetch thread (or inline at prefetch 0)."""
+        from .tario import spans_of
         B = self._batch_size
         hs = self.host_seconds
         t0 = time.perf_counter()
-        if self._native:
-            items = self._source.next_spans()  # may raise StopIteration (end of epoch)
-            jpegs = None
-            need = sum(n for _, n in items)
+        bs = None
+        jpegs = None
+        if self._spans_feed:
+            bs = self._source.next_batch_spans()  # may raise StopIteration (end of epoch)
+            ptrs, lens = bs.ptrs, bs.lens
+        elif self._native:
+            ptrs, lens, _ = spans_of(self._source.next_spans())  # may raise StopIteration
         else:
             jpegs = self._source()  # may raise StopIteration (end of epoch)
-            items = jpegs
-            need = sum(len(j) for j in jpegs)
-        if len(items) != B:
-            raise ValueError(f"source returned {len(items)} samples, expected {B}")
-        st = self._ring.acquire()
+            ptrs, lens, _keep = spans_of(jpegs)
         try:
-            t1 = time.perf_counter()
-            st.fit(need, B)
-            off = gather(items, st.buf, getattr(self._source, "nthreads", 8))
-            st.off.numpy()[: B + 1] = off
-            t2 = time.perf_counter()
+            if len(lens) != B:
+                raise ValueError(f"source returned {len(lens)} samples, expected {B}")
             sizes = self._sizes()
             cfg = self._cfg(*sizes)
-            info, ws, aws = fallback.probe(st.buf.data_ptr(), off, B, self._max_image_dim, cfg)
-            hs["pull"] += t1 - t0
-            hs["pack"] += t2 - t1
-            hs["probe"] += time.perf_counter() - t2
-            mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
-            futures = {}
-            idx = np.flatnonzero(mask)
-            if len(idx):
-                if jpegs is None:  # packed native feed: slice the images back out of the staging buffer
-                    hb = st.buf.numpy()
-                    jpegs = [bytes(hb[off[i]:off[i + 1]]) for i in range(B)]
-                futures = {int(i): self._host.submit(jpegs[i]) for i in idx}
-            return _Prepared(st, jpegs, off, info, ws, aws, sizes, futures)
+            t1 = time.perf_counter()
+            if bs is not None and bs.registered:
+                info, ws, aws = fallback.probe_spans(ptrs, lens, self._max_image_dim, cfg)
+                if not fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max).any():
+                    st = self._ring.acquire()
+                    st.fit(0, B)
+                    st.off.numpy()[: B + 1] = bs.offsets
+                    st.lens.numpy()[:B] = lens
+                    hs["pull"] += t1 - t0
+                    hs["probe"] += time.perf_counter() - t1
+                    return _Prepared(st, None, bs.offsets, info, ws, aws, sizes, {}, spans=bs)
+            st = self._ring.acquire()
+            try:
+                st.fit(int(lens.sum()), B)
+                off, info, ws, aws = fallback.gather_probe(ptrs, lens, st.buf, getattr(self._source, "nthreads", 8),
+                                                           self._max_image_dim, cfg)
+                st.off.numpy()[: B + 1] = off
+                t2 = time.perf_counter()
+                hs["pull"] += t1 - t0
+                hs["pack"] += t2 - t1
+                if bs is not None:  # packed: the shard ranges are no longer read
+                    self._source.retire(bs, None)
+                    bs = None
+                mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
+                futures = {}
+                idx = np.flatnonzero(mask)
+                if len(idx):
+                    if jpegs is None:  # packed native feed: slice the images back out of the staging buffer
+                        hb = st.buf.numpy()
+                        jpegs = [bytes(hb[off[i]:off[i + 1]]) for i in range(B)]
+                    futures = {int(i): self._host.submit(jpegs[i]) for i in idx}
+                return _Prepared(st, jpegs, off, info, ws, aws, sizes, futures)
+            except BaseException:
+                self._ring.release(st, None)
+                raise
         except BaseException:
-            self._ring.release(st, None)
+            if bs is not None:
+                self._source.retire(bs, None)
             raise
 
+    def _drop(self, pb: _Prepared) -> None:
+        """A prepared batch that will never launch: free its staging, retire its shard ranges,
+        hand its feed slot back."""
+        if pb.staging is not None:
+            self._ring.release(pb.staging, None)
+        if pb.spans is not None:
+            self._source.retire(pb.spans, None)
+        if pb.feed is not None:
+            self._source.release(pb.feed)
+
+    def _prepare_feed(self, block: bool) -> _Prepared | None:
+        """The native feed's next batch as a ``_Prepared`` (None: not ready and ``block`` is
+        False; StopIteration at the epoch end).  Images routed to Pillow are copied out of
+        the slot and their decodes submitted; such a batch is re-packed at launch."""
+        fb = self._source.next_prepared(timeout=None if block else 0.0)
+        if fb is None:
+            return None
+        mask = fallback.route_mask(fb.info, self._host_fallback, self._multiscan_route, self._host_max)
+        if not mask.any():
+            return _Prepared(None, None, fb.offsets, fb.info, fb.ws, fb.aws, self._feed_sizes, {}, feed=fb)
+        try:
+            jpegs = fb.jpegs()
+        finally:
+            self._source.release(fb)
+        futures = {int(i): self._host.submit(jpegs[i]) for i in np.flatnonzero(mask)}
+        return _Prepared(None, jpegs, fb.offsets, fb.info, fb.ws, fb.aws, self._feed_sizes, futures)
+
+    def _pull_feed(self) -> _Prepared:
+        t0 = time.perf_counter()
+        try:
+            pb = self._held.popleft() if self._held else self._prepare_feed(block=True)
+            try:  # one batch ahead: its Pillow hand-overs (if any) run while this one is on the GPU
+                nxt = self._prepare_feed(block=False)
+                if nxt is not None:
+                    self._held.append(nxt)
+            except StopIteration:
+                pass
+            return pb
+        finally:
+            self.host_seconds["wait"] += time.perf_counter() - t0
+
     def _pull(self) -> _Prepared:
+        if self._feed:
+            return self._pull_feed()
         if self.prefetch_ahead <= 0:
             return self._prepare_next()
         if self._prefetcher is None:
@@ -436,9 +516,12 @@ class MI355XAugPipeline:
         there were any), re-probe only if that or the crop sizes changed what the probe saw,
         and grow the slot's workspaces (stream-ordered).  Returns the pinned buffer, pinned
         offsets, byte count and pinned raw mask (None when the batch has no container)."""
-        st, B = pb.staging, len(pb.offsets) - 1
+        B = len(pb.offsets) - 1
         raw = None
         ws, aws = pb.ws, pb.aws
+        if pb.futures and pb.staging is None:  # a native feed batch with hand-overs: re-packed here
+            pb.staging = self._ring.acquire()
+        st = pb.staging
         if pb.futures:
             from .tario import gather
             jpegs = list(pb.jpegs)
@@ -459,6 +542,8 @@ class MI355XAugPipeline:
                 aws = fallback.augment_need(pb.info, cfg)
         if sl.engine.reserve(ws, aws):
             self.stats["reserves"] += 1
+        if st is None:  # native feed slot: copied by dino_feed_copy
+            return None, None, nbytes, raw
         return st.buf, st.off[: B + 1], nbytes, raw
 
     def _account(self, block: bool = False, until: _Slot | None = None) -> None:
@@ -491,28 +576,63 @@ class MI355XAugPipeline:
 
     def _enqueue_prepared(self, pb: _Prepared) -> _Slot:
         if self._closed:
+            self._drop(pb)
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
         st = pb.staging
         t0 = time.perf_counter()
+        copied = None
         try:
             sl = self._next_slot()
             sizes = self._sizes()
             cfg = self._cfg(*sizes)
             host_buf, host_off, nbytes, raw = self._screen(sl, pb, cfg, sizes)
             B = len(pb.offsets) - 1
+            d_lens = None
             with sl.engine.on_stream():
-                d_bytes = host_buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
-                d_offsets = host_off.to(self.device, non_blocking=True)
+                if pb.feed is not None:  # the native feed's pinned slot: bytes + offsets in two DMAs
+                    fb, pb.feed = pb.feed, None
+                    if sl.d_in is None or sl.d_in.numel() < fb.nbytes + 64:
+                        sl.d_in = torch.empty(max(fb.nbytes, 1) * 9 // 8 + 64, dtype=torch.uint8, device=self.device)
+                    if sl.d_off is None or sl.d_off.numel() < B + 1:
+                        sl.d_off = torch.empty(B + 1, dtype=torch.int64, device=self.device)
+                    try:
+                        self._source.copy(fb, sl.d_in.data_ptr(), sl.d_off.data_ptr(), sl.engine._s().value or 0)
+                    except BaseException:
+                        self._source.release(fb)
+                        raise
+                    d_bytes, d_offsets = sl.d_in, sl.d_off[: B + 1]
+                elif pb.spans is not None:  # DMA the batch's shard ranges as they lie (no host copy)
+                    nbytes = int(pb.spans.offsets[-1])
+                    if sl.d_in is None or sl.d_in.numel() < nbytes:
+                        sl.d_in = torch.empty(max(nbytes, 1) * 9 // 8 + 64, dtype=torch.uint8, device=self.device)
+                    pos = 0
+                    for addr, n in pb.spans.parts:
+                        sl.engine.copy_from_host(sl.d_in, pos, addr, n)
+                        pos += n
+                    d_bytes = sl.d_in
+                    d_lens = st.lens[:B].to(self.device, non_blocking=True)
+                else:
+                    d_bytes = host_buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
+                if host_off is not None:
+                    d_offsets = host_off.to(self.device, non_blocking=True)
                 d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
                 copied = torch.cuda.Event()
                 copied.record()
             self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw, sizes=sizes,
-                         probe=pb.info)
-            sl.inflight = (d_bytes, d_offsets, d_raw)  # device copies live until the slot's next batch
+                         probe=pb.info, lengths=d_lens)
+            sl.inflight = (d_bytes, d_offsets, d_raw, d_lens)  # device copies live until the slot's next batch
         except BaseException:
-            self._ring.release(st, None)
+            if pb.staging is not None:
+                self._ring.release(pb.staging, copied)
+            if pb.spans is not None:
+                self._source.retire(pb.spans, copied)
+            if pb.feed is not None:
+                self._source.release(pb.feed)
             raise
-        self._ring.release(st, copied)
+        if pb.staging is not None:
+            self._ring.release(pb.staging, copied)
+        if pb.spans is not None:
+            self._source.retire(pb.spans, copied)
         self.host_seconds["launch"] += time.perf_counter() - t0
         return sl
 
@@ -559,6 +679,8 @@ class MI355XAugPipeline:
 
     def restart_epoch(self) -> None:
         """After the source's StopIteration and its reset: let the host half pull again."""
+        while self._held:  # the native feed's look-ahead batch belongs to the finished epoch
+            self._drop(self._held.popleft())
         if self._prefetcher is not None and self._prefetcher.finished:
             self._prefetcher.close()
             self._prefetcher = None
@@ -596,6 +718,8 @@ class MI355XAugPipeline:
                 if self._prefetcher is not None:
                     self._prefetcher.close()
                     self._prefetcher = None
+                while self._held:
+                    self._drop(self._held.popleft())
                 self._account(block=True)
             finally:
                 self._host.close()

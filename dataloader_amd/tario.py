@@ -18,9 +18,11 @@ This is the feed of the Stage-3 device path:
   JSON metadata, optional quality filter and shuffle buffer.  The helper itself is
   not in ``/root/reference``; its semantics here are restated from its call site
   (parity unpinned beyond the reference's fixture tars).
-* :class:`ShardBatchFeeder` — B JPEGs per batch from mapped shards packed by
-  ``dino_gather`` (threaded memcpy) into a pinned buffer + int64 offsets, the
-  layout ``dino_run_batch`` reads after one H2D copy.
+* :class:`ShardBatchFeeder` — B JPEGs per batch from mapped shards: either where
+  they lie (page-locked shard ranges DMA'd to HBM as they are, decoded through the
+  spans ABI: no host copy), or packed by ``dino_gather`` (threaded memcpy) into a
+  pinned buffer + int64 offsets, the layout ``dino_run_batch`` reads after one H2D
+  copy.
 """
 
 from __future__ import annotations
@@ -149,22 +151,35 @@ def extract_jpegs_with_meta(data, metadata_key: str | None = None, min_quality: 
     return recs
 
 
+def spans_of(srcs: Sequence) -> tuple[np.ndarray, np.ndarray, list]:
+    """(uint64 addresses, int64 lengths, keep-alive list) of a sequence of (address, length)
+    pairs or bytes-like objects."""
+    keep = []
+    n = len(srcs)
+    ptrs = np.empty(n, np.uint64)
+    lens = np.empty(n, np.int64)
+    if n and isinstance(srcs[0], tuple):
+        a = np.asarray(srcs, dtype=np.int64).reshape(n, 2)
+        ptrs[:] = a[:, 0].astype(np.uint64)
+        lens[:] = a[:, 1]
+        return ptrs, lens, keep
+    for i, s in enumerate(srcs):
+        if isinstance(s, tuple):
+            ptrs[i], lens[i] = s
+        else:
+            a, ln, k = _addr(s)
+            keep.append(k)
+            ptrs[i], lens[i] = a, ln
+    return ptrs, lens, keep
+
+
 def gather(srcs: Sequence, dst: "Any", nthreads: int = 8) -> np.ndarray:
     """Pack byte ranges back to back into ``dst`` (pinned torch uint8 tensor or ndarray).
 
     ``srcs``: sequence of (address, length) pairs or bytes-like objects.
     Returns int64 offsets[n+1] (``dino_gather``)."""
     lib = _lib.load()
-    keep = []
-    ptrs = np.empty(len(srcs), np.uint64)
-    lens = np.empty(len(srcs), np.int64)
-    for i, s in enumerate(srcs):
-        if isinstance(s, tuple):
-            ptrs[i], lens[i] = s
-        else:
-            a, n, k = _addr(s)
-            keep.append(k)
-            ptrs[i], lens[i] = a, n
+    ptrs, lens, keep = spans_of(srcs)
     off = np.empty(len(srcs) + 1, np.int64)
     if hasattr(dst, "data_ptr"):
         daddr, dcap = dst.data_ptr(), dst.numel() * dst.element_size()
@@ -172,6 +187,7 @@ def gather(srcs: Sequence, dst: "Any", nthreads: int = 8) -> np.ndarray:
         daddr, dcap, _ = _addr(dst)
     rc = lib.dino_gather(ctypes.c_void_p(ptrs.ctypes.data), ctypes.c_void_p(lens.ctypes.data), len(srcs),
                          ctypes.c_void_p(daddr), dcap, ctypes.c_void_p(off.ctypes.data), nthreads)
+    del keep
     if rc != 0:
         raise _lib.DinoError(f"dino_gather failed ({rc}): {lib.dino_tar_last_error().decode(errors='replace')}")
     return off
@@ -364,18 +380,46 @@ class ShmShardCache:
                     self._base.rmdir()
 
 
+@dataclass
+class BatchSpans:
+    """One batch as byte ranges of mapped shards (``ShardBatchFeeder.next_batch_spans``).
+
+    ``ptrs``/``lens``: each sample's JPEG member (absolute host address, length).
+    ``parts``: the contiguous shard ranges that hold the samples, in batch order
+    (address, bytes): copied to HBM as they lie, tar headers and sidecars included.
+    ``offsets``: int64[B+1], each sample's offset in the concatenated parts, and
+    [B] = their total size (the spans form of ``dino_decode_spans``).
+    ``registered``: every part lies in page-locked memory (a DMA source).
+    ``shards``: feeder shard indices of the parts (retirement bookkeeping)."""
+
+    ptrs: np.ndarray
+    lens: np.ndarray
+    parts: list
+    offsets: np.ndarray
+    registered: bool
+    shards: list
+
+
 class ShardBatchFeeder:
-    """Batches of B JPEGs from mapped shards, packed into pinned host buffers.
+    """Batches of B JPEGs from mapped shards.
 
     Shard i of the list belongs to this rank when ``i % world == rank``
-    (reference hpc_source.py:154-156).  Each shard is indexed natively once when
-    first reached; batches never straddle an epoch and the last partial batch is
-    dropped (dali_backend.py:187).  ``next_into(dst)`` packs the next batch into a
-    pinned tensor and returns the int64 offsets; ``MI355XAugPipeline`` consumes
-    ``next_spans()`` directly (gathering into its per-slot pinned staging)."""
+    (reference hpc_source.py:154-156).  Each shard is mapped, pre-faulted, indexed
+    natively and (``register``) page-locked once, on a worker thread, when first
+    reached; batches never straddle an epoch and the last partial batch is dropped
+    (dali_backend.py:187).  Two ways out:
+
+    * ``next_batch_spans()``: the batch where it lies (``BatchSpans``) — the
+      pipeline DMAs the shard ranges straight to HBM (no host copy) and decodes
+      with the spans ABI; ``retire(batch, event)`` hands back the event after which
+      the copies have read the ranges, and a consumed shard is unregistered once
+      every batch taken from it has retired;
+    * ``next_spans()`` / ``next_into(dst)``: (address, length) pairs, packed by
+      ``dino_gather`` into a pinned buffer (batches the pipeline must re-pack, e.g.
+      with Pillow hand-overs)."""
 
     def __init__(self, cache: ShmShardCache, shard_paths: Sequence[str], batch_size: int, rank: int = 0,
-                 world: int = 1, nthreads: int = 8, lookahead: int = 2) -> None:
+                 world: int = 1, nthreads: int = 8, lookahead: int = 2, register: bool = False) -> None:
         from concurrent.futures import ThreadPoolExecutor
         self._cache = cache
         self._paths = [p for i, p in enumerate(shard_paths) if i % world == rank]
@@ -384,20 +428,43 @@ class ShardBatchFeeder:
         self._shard = 0
         self._row = 0
         self._cur: tuple[np.ndarray, TarIndex] | None = None
-        self.index_seconds = 0.0   # time spent preparing shards (map + pre-fault + index), off the caller's thread
+        self.index_seconds = 0.0   # time spent preparing shards (map + pre-fault + index + register), off the caller's thread
         self.wait_seconds = 0.0    # time the caller waited for a shard to be ready
         self._lookahead = max(0, int(lookahead))
         self._pool = ThreadPoolExecutor(max_workers=max(1, self._lookahead), thread_name_prefix="shard-index") \
             if self._lookahead else None
         self._futs: dict[int, Any] = {}
+        self._register = bool(register)
+        self.register_error: str | None = None
+        self._reg_lock = threading.Lock()
+        # shard index -> {"addr", "handed", "retired", "events", "consumed"} of page-locked shards
+        self._reg: dict[int, dict] = {}
 
     def _prepare(self, k: int) -> tuple[np.ndarray, TarIndex]:
-        """Map shard k, fault its pages in and index it (a worker thread; ctypes drops the GIL)."""
+        """Map shard k, fault its pages in, index it and page-lock it (a worker thread;
+        ctypes drops the GIL)."""
         import time
         t0 = time.perf_counter()
         arr = self._cache.get_array(self._paths[k])
         prefault(arr)
         idx = index_tar(arr)
+        if self._register and arr.size:
+            with self._reg_lock:
+                ent = self._reg.get(k)
+                if ent is not None:          # still locked from an earlier epoch
+                    ent["consumed"] = False
+                    need = False
+                else:
+                    need = True
+            if need:
+                rc = _lib.load().dino_host_register(ctypes.c_void_p(arr.ctypes.data), arr.nbytes)
+                if rc == 0:
+                    with self._reg_lock:
+                        self._reg[k] = {"addr": arr.ctypes.data, "handed": 0, "retired": 0, "events": [],
+                                        "consumed": False}
+                else:  # no GPU runtime / the mapping cannot be locked: the gather path serves
+                    self._register = False
+                    self.register_error = _lib.load().dino_last_error().decode(errors="replace")
         self.index_seconds += time.perf_counter() - t0
         return arr, idx
 
@@ -420,25 +487,102 @@ class ShardBatchFeeder:
 
     _resolution_src = None  # no per-batch crop sizes: the pipeline's configured sizes apply
 
-    def next_spans(self) -> list[tuple[int, int]]:
-        """(address, length) of the next batch's JPEGs; StopIteration at the epoch end."""
-        spans: list[tuple[int, int]] = []
-        while len(spans) < self._B:
+    def _take(self) -> list[tuple[int, np.ndarray, np.ndarray]]:
+        """The next batch as (shard index, shard array, index rows) runs; StopIteration at the epoch end."""
+        runs = []
+        got = 0
+        while got < self._B:
             if self._cur is None:
                 if self._shard >= len(self._paths):
                     raise StopIteration
                 self._cur = self._open(self._shard)
                 self._row = 0
             arr, idx = self._cur
-            base = arr.ctypes.data
-            take = min(self._B - len(spans), len(idx) - self._row)
-            rows = idx.samples[self._row:self._row + take]
-            spans.extend(zip((base + rows["img_off"]).tolist(), rows["img_len"].tolist()))
+            take = min(self._B - got, len(idx) - self._row)
+            if take > 0:
+                runs.append((self._shard, arr, idx.samples[self._row:self._row + take]))
+                got += take
             self._row += take
             if self._row >= len(idx):
+                self._consumed(self._shard)
                 self._cur = None
                 self._shard += 1
+        return runs
+
+    def next_spans(self) -> list[tuple[int, int]]:
+        """(address, length) of the next batch's JPEGs; StopIteration at the epoch end."""
+        spans: list[tuple[int, int]] = []
+        for _, arr, rows in self._take():
+            spans.extend(zip((arr.ctypes.data + rows["img_off"]).tolist(), rows["img_len"].tolist()))
+        self._unregister_retired()
         return spans
+
+    def next_batch_spans(self) -> BatchSpans:
+        """The next batch where it lies (see ``BatchSpans``); StopIteration at the epoch end.
+        The caller must ``retire`` it once its copies are enqueued (or dropped)."""
+        runs = self._take()
+        ptrs = np.empty(self._B, np.uint64)
+        lens = np.empty(self._B, np.int64)
+        offs = np.empty(self._B + 1, np.int64)
+        parts, shards = [], []
+        registered = True
+        i = pos = 0
+        for k, arr, rows in runs:
+            io, il = rows["img_off"], rows["img_len"]
+            lo, hi = int(io[0]), int(io[-1] + il[-1])
+            n = len(rows)
+            ptrs[i:i + n] = arr.ctypes.data + io
+            lens[i:i + n] = il
+            offs[i:i + n] = pos + (io - lo)
+            parts.append((arr.ctypes.data + lo, hi - lo))
+            shards.append(k)
+            with self._reg_lock:
+                ent = self._reg.get(k)
+                if ent is None:
+                    registered = False
+                else:
+                    ent["handed"] += 1
+            pos += hi - lo
+            i += n
+        offs[self._B] = pos
+        self._unregister_retired()
+        return BatchSpans(ptrs, lens, parts, offs, registered, shards)
+
+    def retire(self, batch: BatchSpans, event=None) -> None:
+        """The copies out of ``batch``'s ranges are enqueued and complete with ``event``
+        (an object with ``query()`` / ``synchronize()``, e.g. a torch.cuda.Event; None: no
+        copy was made from them)."""
+        with self._reg_lock:
+            for k in batch.shards:
+                ent = self._reg.get(k)
+                if ent is not None:
+                    ent["retired"] += 1
+                    if event is not None:
+                        ent["events"].append(event)
+        self._unregister_retired()
+
+    def _consumed(self, k: int) -> None:
+        with self._reg_lock:
+            ent = self._reg.get(k)
+            if ent is not None:
+                ent["consumed"] = True
+
+    def _unregister_retired(self, block: bool = False) -> None:
+        """Unlock every consumed shard whose batches have all retired and whose copies finished."""
+        with self._reg_lock:
+            done = []
+            for k, ent in self._reg.items():
+                if not block and (not ent["consumed"] or ent["retired"] < ent["handed"]):
+                    continue
+                ev = ent["events"]
+                while ev and (block or ev[0].query()):
+                    ev.pop(0).synchronize()
+                if ev:
+                    continue
+                done.append(k)
+            for k in done:
+                ent = self._reg.pop(k)
+                _lib.load().dino_host_unregister(ctypes.c_void_p(ent["addr"]))
 
     def next_into(self, dst) -> np.ndarray:
         return gather(self.next_spans(), dst, self.nthreads)
@@ -451,6 +595,144 @@ class ShardBatchFeeder:
             self._pool.shutdown(wait=True, cancel_futures=True)
             self._pool = None
         self._futs.clear()
+        self._unregister_retired(block=True)
+
+
+class FeedBatch:
+    """A packed batch handed out by the native feed: it lives in a pinned slot until
+    ``NativeShardFeed.copy`` retires or ``release`` is called."""
+
+    __slots__ = ("slot", "n", "nbytes", "host", "offsets", "info", "ws", "aws", "seq")
+
+    def __init__(self, b) -> None:
+        self.slot, self.n, self.nbytes, self.seq = int(b.slot), int(b.n), int(b.nbytes), int(b.seq)
+        self.host = int(b.host or 0)
+        self.offsets = np.ctypeslib.as_array(ctypes.cast(b.offsets, ctypes.POINTER(ctypes.c_int64)),
+                                             (self.n + 1,)).copy()
+        self.info = np.ctypeslib.as_array(ctypes.cast(b.info, ctypes.POINTER(ctypes.c_int32)), (self.n, 4)).copy()
+        self.ws, self.aws = int(b.ws_need), int(b.aws_need)
+
+    def jpegs(self) -> list[bytes]:
+        """Copies of the batch's images (for the Pillow hand-over path)."""
+        o = self.offsets
+        return [ctypes.string_at(self.host + int(o[i]), int(o[i + 1] - o[i])) for i in range(self.n)]
+
+
+class NativeShardFeed:
+    """The node-local shard feed run natively (``dino_feed_*``, csrc/feed.hip): an opener
+    thread maps, pre-faults and indexes this rank's shard-cache files a few shards ahead;
+    a packer thread packs every batch of B samples into a pinned slot with ``nthreads``
+    copier threads and probes each image right after its copy.  No Python runs per batch
+    on the host half, so it does not wait for the GIL behind the launch thread.
+
+    Same source conventions as :class:`ShardBatchFeeder` (``_batch_size``,
+    ``_resolution_src``; shard i belongs to rank ``i % world``, reference
+    hpc_source.py:154-156; the last partial batch of an epoch is dropped,
+    dali_backend.py:187; an unreadable shard is skipped with a warning,
+    hpc_source.py:358-366).  ``MI355XAugPipeline`` consumes it through
+    ``next_prepared`` / ``copy`` / ``release``."""
+
+    def __init__(self, cache: ShmShardCache, shard_paths: Sequence[str], batch_size: int, rank: int = 0,
+                 world: int = 1, nthreads: int = 8, slots: int = 6, lookahead: int = 2) -> None:
+        self._cache = cache
+        self._paths = [p for i, p in enumerate(shard_paths) if i % world == rank]
+        self._B = int(batch_size)
+        self.nthreads = int(nthreads)
+        self._slots = max(2, int(slots))
+        self._lookahead = max(1, int(lookahead))
+        self._max_dim = 0
+        self._cfg = None
+        self._feed = ctypes.c_void_p()
+        self._started = False
+        self.shard_errors: list[str] = []
+
+    @property
+    def _batch_size(self) -> int:
+        return self._B
+
+    _resolution_src = None
+
+    def configure(self, max_image_dim: int = 0, cfg=None) -> None:
+        """Probe settings (the pipeline's ``max_image_dim`` and its view config for the
+        augment-workspace bound); the native feed starts on the first ``next_prepared``."""
+        self._max_dim = int(max_image_dim)
+        self._cfg = cfg
+        if self._feed:
+            _lib.check(_lib.load().dino_feed_set_cfg(self._feed, ctypes.byref(cfg) if cfg is not None else None),
+                       "dino_feed_set_cfg")
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != 0:
+            raise _lib.DinoError(f"{what} failed ({rc}): {_lib.load().dino_feed_last_error().decode(errors='replace')}")
+
+    def _start(self) -> None:
+        lib = _lib.load()
+        if not self._feed:
+            cfg = ctypes.byref(self._cfg) if self._cfg is not None else None
+            self._check(lib.dino_feed_create(self._B, self.nthreads, self._slots, self._lookahead, self._max_dim, cfg,
+                                             ctypes.byref(self._feed)), "dino_feed_create")
+        for p in self._paths:
+            self._check(lib.dino_feed_push(self._feed, str(self._cache._ensure(p)).encode()), "dino_feed_push")
+        self._check(lib.dino_feed_end_epoch(self._feed), "dino_feed_end_epoch")
+        self._started = True
+
+    def next_prepared(self, timeout: float | None = None) -> FeedBatch | None:
+        """The next packed batch; None when ``timeout`` (seconds) passes first; StopIteration
+        at the end of the epoch."""
+        if not self._started:
+            self._start()
+        lib = _lib.load()
+        out = _lib.DinoFeedBatch()
+        ms = -1 if timeout is None else int(timeout * 1000)
+        while True:
+            rc = lib.dino_feed_next(self._feed, ms, ctypes.byref(out))
+            if rc == _lib.FEED_SHARD_ERROR:
+                msg = lib.dino_feed_last_error().decode(errors="replace")
+                self.shard_errors.append(msg)
+                import warnings
+                warnings.warn(f"NativeShardFeed: skipped a shard: {msg}", RuntimeWarning, stacklevel=2)
+                continue
+            if rc == _lib.FEED_END:
+                raise StopIteration
+            if rc == _lib.FEED_TIMEOUT:
+                return None
+            self._check(rc, "dino_feed_next")
+            return FeedBatch(out)
+
+    def copy(self, batch: FeedBatch, d_bytes: int, d_offsets: int, stream: int) -> None:
+        """H2D copies of ``batch`` (bytes, offsets) to device addresses on ``stream`` (a hipStream_t)."""
+        self._check(_lib.load().dino_feed_copy(self._feed, batch.slot, ctypes.c_void_p(d_bytes),
+                                               ctypes.c_void_p(d_offsets), ctypes.c_void_p(stream)), "dino_feed_copy")
+
+    def release(self, batch: FeedBatch) -> None:
+        if self._feed:
+            _lib.load().dino_feed_release(self._feed, batch.slot)
+
+    def stats(self) -> dict:
+        if not self._feed:
+            return {}
+        sec = (ctypes.c_double * 4)()
+        cnt = (ctypes.c_int64 * 3)()
+        self._check(_lib.load().dino_feed_stats(self._feed, sec, cnt), "dino_feed_stats")
+        return {"open_s": sec[0], "pack_s": sec[1], "slot_wait_s": sec[2], "sample_wait_s": sec[3],
+                "batches": cnt[0], "shards_done": cnt[1], "shards_failed": cnt[2]}
+
+    def reset(self) -> None:
+        """New epoch (the pushed shards and packed batches not yet handed out are dropped)."""
+        if self._feed:
+            self._check(_lib.load().dino_feed_reset(self._feed), "dino_feed_reset")
+        self._started = False
+
+    def close(self) -> None:
+        if self._feed:
+            _lib.load().dino_feed_destroy(self._feed)
+            self._feed = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 _MADV_POPULATE_READ = 22  # Linux >= 5.14

@@ -36,6 +36,13 @@
  *  - ABI 3 (from 2): raw masks on dino_decode / dino_run_batch / dino_probe, a
  *    stream on dino_reserve (stream-ordered growth, no device-wide sync), and
  *    max_image_dim 0 = no side limit (65535).
+ *  - ABI 4 (from 3, additive): "spans" input (dino_decode_spans, dino_run_batch_spans,
+ *    dino_probe_spans) so that a batch can be copied to HBM as the contiguous byte
+ *    ranges of mapped tar shards it lies in, tar headers and sidecars included, with no
+ *    host gather; dino_host_register / dino_host_unregister / dino_copy_h2d to page-lock
+ *    those mappings and DMA from them; dino_gather_probe (pack + probe in one threaded
+ *    pass); the native shard feed dino_feed_* (the host half of a batch off the Python
+ *    interpreter).
  */
 #ifndef DINO_INGEST_H
 #define DINO_INGEST_H
@@ -46,7 +53,7 @@
 extern "C" {
 #endif
 
-#define DINO_ABI_VERSION 3
+#define DINO_ABI_VERSION 4
 
 /* return codes */
 #define DINO_OK 0
@@ -154,6 +161,14 @@ int dino_ctx_destroy(dino_ctx* ctx);
 int dino_decode(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, const uint8_t* d_raw_mask,
                 int32_t batch, int32_t* d_info, void* stream);
 
+/* Spans form of dino_decode: image i is d_bytes[d_offsets[i], d_offsets[i] + d_lengths[i])
+ * (d_lengths nullable: d_offsets[i+1] - d_offsets[i]); d_offsets[batch] is the size of the
+ * d_bytes buffer (bytes between and after images are ignored: e.g. the tar headers and
+ * sidecars of a shard range copied as a whole).  Replaces the per-sample bytes(mv)
+ * copies of reference hpc_source.py:360 / shard_reader.py:346-376 on the device feed. */
+int dino_decode_spans(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, const int64_t* d_lengths,
+                      const uint8_t* d_raw_mask, int32_t batch, int32_t* d_info, void* stream);
+
 /* Copy decoded image i (HWC uint8 RGB, pitch = width*3) to d_rgb (debug / tests). */
 int dino_copy_rgb(dino_ctx* ctx, int32_t index, uint8_t* d_rgb, void* stream);
 
@@ -175,6 +190,12 @@ int dino_run_batch(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offse
                    int32_t batch, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,
                    dino_view_params* d_params_out, void* const* views, int32_t* d_info,
                    void* stream);
+
+/* dino_run_batch on the spans form of dino_decode_spans. */
+int dino_run_batch_spans(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_offsets, const int64_t* d_lengths,
+                         const uint8_t* d_raw_mask, int32_t batch, const dino_aug_config* cfg, uint64_t seed,
+                         uint64_t batch_index, dino_view_params* d_params_out, void* const* d_views,
+                         int32_t* d_info, void* stream);
 
 /* Decode-only recipe (reference CPUUserAugPipeline.run_one_batch, cpu.py:484-500, and the
  * DALI decode-only graph, pipeline.py:693-756): every image of the last decoded batch
@@ -203,6 +224,30 @@ int dino_batch_info(dino_ctx* ctx, int32_t* d_info, void* stream);
 int dino_probe(const uint8_t* bytes, const int64_t* offsets, const uint8_t* raw_mask, int32_t batch,
                int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need,
                int64_t* aws_need);
+
+/* dino_probe over images given as absolute HOST addresses + lengths (e.g. JPEG members
+ * of mapped tar shards, as dino_gather's input), so a batch can be screened where it
+ * lies without packing it. */
+int dino_probe_spans(const uint64_t* ptrs, const int64_t* lens, const uint8_t* raw_mask, int32_t batch,
+                     int32_t max_image_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws_need,
+                     int64_t* aws_need);
+
+/* dino_gather + dino_probe in one pass: nthreads copier threads pack the images (absolute
+ * HOST addresses + lengths) into dst (streaming stores; dst_offsets[n+1] as dino_gather's)
+ * and parse each image's header right after copying it (info / ws_need / aws_need as
+ * dino_probe's, no raw containers).  The host half of a feed batch in one native call. */
+int dino_gather_probe(const uint64_t* src_ptrs, const int64_t* lens, int32_t n, uint8_t* dst, int64_t dst_cap,
+                      int64_t* dst_offsets, int32_t nthreads, int32_t max_image_dim, const dino_aug_config* cfg,
+                      int32_t* info, int64_t* ws_need, int64_t* aws_need);
+
+/* Page-lock a host range (e.g. a mapped /dev/shm shard, reference shard_cache.py:584-609)
+ * for DMA: hipHostRegister, read-only where the runtime supports it.  Unregister only
+ * after every copy from the range has retired. */
+int dino_host_register(void* host, int64_t nbytes);
+int dino_host_unregister(void* host);
+/* Asynchronous host -> device copy on `stream` (a DMA when host lies in registered or
+ * pinned memory). */
+int dino_copy_h2d(void* d_dst, const void* host_src, int64_t nbytes, void* stream);
 
 /* Grow the ctx's decode / augment workspaces to at least the given sizes (never
  * shrinks), stream-ordered on `stream` (the stream the ctx's batches run on): the old
@@ -296,6 +341,49 @@ const char* dino_tar_last_error(void);
  * assembly of shard_reader.py:346-376. */
 int dino_gather(const uint64_t* src_ptrs, const int64_t* lens, int64_t n, uint8_t* dst, int64_t dst_cap,
                 int64_t* dst_offsets, int32_t nthreads);
+
+/* ---- Native shard feed (feed.hip): the host half of a batch without Python -------
+ * An opener thread maps shard-cache files ([data_len:u64][magic:u64] + tar, reference
+ * shard_cache.py:83-85), faults them in and indexes them (dino_tar_index) a few shards
+ * ahead; a packer thread packs each batch of `batch` consecutive samples (straddling
+ * shards; the last partial batch of an epoch is dropped, dali_backend.py:187) into a
+ * pinned slot with `nthreads` copier threads, probing every image right after its copy.
+ * Replaces ShardIterator / MixingSource's per-sample extraction + bytes(mv) copies
+ * (reference hpc_source.py:329-385, :405-478) and _ReaderAdapter.__call__
+ * (shard_reader.py:346-376) for the device backend.  Shard I/O errors are reported once
+ * (DINO_FEED_SHARD_ERROR) and the shard is skipped (hpc_source.py:358-366). */
+typedef struct dino_feed dino_feed;
+typedef struct dino_feed_batch {
+  int32_t slot;                /* pass to dino_feed_copy / dino_feed_release */
+  int32_t n;                   /* images (= batch) */
+  int64_t nbytes;              /* packed bytes */
+  const uint8_t* host;         /* pinned packed bytes (valid until the slot's copy retires / release) */
+  const int64_t* offsets;      /* int64[n+1], pinned */
+  const int32_t* info;         /* int32[n][4] as dino_probe's */
+  int64_t ws_need, aws_need;   /* as dino_probe's (aws for the feed's cfg) */
+  int64_t seq;                 /* batch number since the feed was created */
+} dino_feed_batch;
+#define DINO_FEED_END 1            /* dino_feed_next: the epoch has no more batches */
+#define DINO_FEED_TIMEOUT 2        /* dino_feed_next: nothing ready within timeout_ms */
+#define DINO_FEED_SHARD_ERROR 3    /* dino_feed_next: a shard could not be read (skipped; dino_feed_last_error) */
+int dino_feed_create(int32_t batch, int32_t nthreads, int32_t nslots, int32_t lookahead, int32_t max_image_dim,
+                     const dino_aug_config* cfg, dino_feed** out);
+int dino_feed_destroy(dino_feed* feed);
+int dino_feed_push(dino_feed* feed, const char* shard_cache_path);
+int dino_feed_end_epoch(dino_feed* feed);
+int dino_feed_set_cfg(dino_feed* feed, const dino_aug_config* cfg);
+/* Next packed batch in order (blocks up to timeout_ms; < 0: forever). */
+int dino_feed_next(dino_feed* feed, int32_t timeout_ms, dino_feed_batch* out);
+/* H2D copies of a handed-out slot (bytes, offsets) on `stream`; the slot is reused after they retire. */
+int dino_feed_copy(dino_feed* feed, int32_t slot, uint8_t* d_bytes, int64_t* d_offsets, void* stream);
+/* Hand a slot back without copying it (the caller copied what it needed). */
+int dino_feed_release(dino_feed* feed, int32_t slot);
+/* New epoch: drops pushed shards and packed batches not handed out. */
+int dino_feed_reset(dino_feed* feed);
+/* seconds[4] = open+fault+index, pack+probe, waiting for a free slot, waiting for samples;
+ * counts[3] = batches packed, shards consumed, shards failed. */
+int dino_feed_stats(dino_feed* feed, double* seconds, int64_t* counts);
+const char* dino_feed_last_error(void);
 
 #ifdef __cplusplus
 }

@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), f"{name} declared in dino_ingest.h but not exported"
     assert declared == set(_lib.exported_symbols())
-    assert lib.dino_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.dino_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_ctx_create_fails_loudly_without_gpu():

@@ -229,3 +229,68 @@ def test_reserve_is_stream_ordered_with_batches_in_flight(gpu_device):
     for a, b in zip(ref, got):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_shard_spans_feed_dma_matches_packed_feed(gpu_device, tmp_path):
+    """The native shard feed (C++ threads pack + probe into pinned slots, dino_feed_copy) and
+    the /dev/shm feed handed over where it lies (page-locked shard ranges DMA'd to HBM, tar
+    headers and sidecars included, decoded through dino_run_batch_spans) gives every view
+    bit-identical to the packed feed (dino_gather into pinned staging), across shard
+    boundaries and with a CMYK sample (a Pillow hand-over: that batch takes the packing path)."""
+    import io as _io
+    import json
+    import tarfile
+
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.tario import ShardBatchFeeder, ShmShardCache
+    rng = np.random.default_rng(55)
+    uniq = [encode_jpeg(textured_rgb(200 + 8 * s, 150 + 4 * s, rng)) for s in range(5)]
+    samples = [uniq[i % 5] for i in range(60)]
+    samples[23] = _cmyk(96, 64, rng)
+    shards = []
+    for s0 in range(0, 60, 25):  # 25, 25, 10 samples: batches of 8 straddle shards
+        buf = _io.BytesIO()
+        with tarfile.open(fileobj=buf, mode="w") as tf:
+            for i in range(s0, min(60, s0 + 25)):
+                for name, data in ((f"sample_{i:06d}.jpg", samples[i]), (f"sample_{i:06d}.json", json.dumps({"i": i}).encode())):
+                    ti = tarfile.TarInfo(name)
+                    ti.size = len(data)
+                    tf.addfile(ti, _io.BytesIO(data))
+        shards.append(buf.getvalue())
+    cache = ShmShardCache(job_id="spans_gpu", base_dir=tmp_path)
+    paths = [f"/d/shard-{k}.tar" for k in range(len(shards))]
+    for p, t in zip(paths, shards):
+        cache.put(p, t)
+    spec = DinoV2AugSpec(aug_cfg=DINOAugConfig(global_crop_size=96, local_crop_size=48))
+    be = MI355XBackend(host_workers=2)
+
+    def run(register):
+        feeder = ShardBatchFeeder(cache, paths, 8, nthreads=2, register=register)
+        pipe = be.build_pipeline(feeder, spec, PipelineConfig(gpu_queue=6, seed=5), None)
+        outs = _collect(be.build_pipeline_iterator(pipe, spec, spec.output_map, 8))
+        st = pipe.flush_stats()
+        pipe.close()
+        feeder.close()
+        assert feeder.register_error is None and not feeder._reg, (feeder.register_error, feeder._reg)
+        return outs, st
+
+    def run_native():
+        from dataloader_amd.tario import NativeShardFeed
+        feed = NativeShardFeed(cache, paths, 8, nthreads=3, slots=5)
+        pipe = be.build_pipeline(feed, spec, PipelineConfig(gpu_queue=6, seed=5), None)
+        outs = _collect(be.build_pipeline_iterator(pipe, spec, spec.output_map, 8))
+        st = pipe.flush_stats()
+        pipe.close()
+        assert feed.stats()["batches"] >= 7
+        feed.close()
+        return outs, st
+
+    (ref, st0), (got, st1), (nat, st2) = run(False), run(True), run_native()
+    assert len(ref) == len(got) == len(nat) == 7
+    assert st0["host_decoded"] == st1["host_decoded"] == st2["host_decoded"] == 1
+    assert set(st1["status"]) == set(st2["status"]) == {0}
+    for k, (a, b, c) in enumerate(zip(ref, got, nat)):
+        for name in a:
+            assert torch.equal(a[name], b[name]), (k, name)
+            assert torch.equal(a[name], c[name]), (k, name, "native feed")
+    cache.close(remove=True)

@@ -236,3 +236,107 @@ def test_tar_index_forged_sizes_do_not_overflow():
         assert t.status in (tario.TAR_TRUNCATED, tario.TAR_BAD_HEADER) and len(t) == 2, field
         for r in t.samples:
             assert 0 <= r["img_off"] and r["img_off"] + r["img_len"] <= len(bad)
+
+
+def test_batch_spans_cover_the_batch_where_it_lies(tmp_path):
+    """next_batch_spans: the parts (contiguous shard ranges, tar headers and sidecars included)
+    concatenated and cut at offsets/lens give the same images as the packed feed, across shard
+    boundaries; retire() balances the bookkeeping; probe_spans == probe of the packed batch."""
+    import ctypes
+
+    from dataloader_amd import fallback
+    shards = [make_shard(n, seed=20 + k) for k, n in enumerate([7, 5, 9])]
+    cache = tario.ShmShardCache(job_id="spans", base_dir=tmp_path)
+    paths = []
+    for k, t in enumerate(shards):
+        paths.append(f"/data/shard-{k:03d}.tar")
+        cache.put(paths[-1], t)
+    expect = [img for t in shards for _, img, _ in oracle_samples(t)]
+    feeder = tario.ShardBatchFeeder(cache, paths, batch_size=4, nthreads=2, register=False)
+    got, n_parts = [], []
+    while True:
+        try:
+            bs = feeder.next_batch_spans()
+        except StopIteration:
+            break
+        assert not bs.registered and len(bs.offsets) == 5 and bs.offsets[-1] == sum(n for _, n in bs.parts)
+        flat = b"".join(ctypes.string_at(a, n) for a, n in bs.parts)
+        imgs = [flat[bs.offsets[i]:bs.offsets[i] + bs.lens[i]] for i in range(4)]
+        assert imgs == [ctypes.string_at(int(p), int(n)) for p, n in zip(bs.ptrs, bs.lens)]
+        got += imgs
+        n_parts.append(len(bs.parts))
+        info_s, ws_s, _ = fallback.probe_spans(bs.ptrs, bs.lens, 0)
+        dst = torch.empty(1 << 16, dtype=torch.uint8)
+        off = tario.gather(list(zip(bs.ptrs.tolist(), bs.lens.tolist())), dst, 1)
+        info_p, ws_p, _ = fallback.probe(dst.data_ptr(), off, 4, 0)
+        assert np.array_equal(info_s, info_p) and ws_s == ws_p
+        for nt in (1, 3):  # the fused pack + probe pass: same bytes, same probe
+            dst2 = torch.zeros(1 << 16, dtype=torch.uint8)
+            off2, info_g, ws_g, _ = fallback.gather_probe(bs.ptrs, bs.lens, dst2, nt, 0)
+            assert np.array_equal(off2, off) and np.array_equal(info_g, info_p) and ws_g == ws_p
+            assert torch.equal(dst2[:off[-1]], dst[:off[-1]])
+        feeder.retire(bs, None)
+    assert got == expect[:len(expect) // 4 * 4] and max(n_parts) == 2   # batches straddle shards
+    feeder.close()
+    cache.close(remove=True)
+
+
+@pytest.mark.parametrize("nthreads", [1, 3])
+def test_native_feed_batches_epochs_and_errors(tmp_path, nthreads):
+    """NativeShardFeed (C++ opener + packer threads; host-only slots without a GPU): the same
+    batches as the Python feeder (rank partition, batches straddling shards, last partial batch
+    dropped), each probed like dino_probe on the packed bytes; reset starts a new epoch; a
+    corrupt shard-cache file is skipped with a warning (reference hpc_source.py:358-366)."""
+    import ctypes
+
+    from dataloader_amd import fallback
+    shards = [make_shard(n, seed=30 + k) for k, n in enumerate([7, 5, 9, 6, 8])]
+    cache = tario.ShmShardCache(job_id=f"nfeed{nthreads}", base_dir=tmp_path)
+    paths = []
+    for k, t in enumerate(shards):
+        paths.append(f"/data/shard-{k:03d}.tar")
+        cache.put(paths[-1], t)
+    for world in (1, 2):
+        for rank in range(world):
+            mine = [k for k in range(5) if k % world == rank]
+            expect = [img for k in mine for _, img, _ in oracle_samples(shards[k])]
+            feed = tario.NativeShardFeed(cache, paths, 4, rank=rank, world=world, nthreads=nthreads, slots=3)
+            for epoch in range(2):
+                got = []
+                while True:
+                    try:
+                        fb = feed.next_prepared(timeout=10.0)
+                    except StopIteration:
+                        break
+                    assert fb is not None
+                    imgs = fb.jpegs()
+                    dst = torch.empty(1 << 16, dtype=torch.uint8)
+                    off = tario.gather(imgs, dst, 1)
+                    info, ws, _ = fallback.probe(dst.data_ptr(), off, 4, 0)
+                    assert np.array_equal(fb.offsets, off) and np.array_equal(fb.info, info) and fb.ws == ws
+                    got += imgs
+                    feed.release(fb)
+                assert got == expect[:len(expect) // 4 * 4], (world, rank, epoch)
+                feed.reset()
+            st = feed.stats()
+            assert st["batches"] >= 2 * (len(expect) // 4) and st["shards_failed"] == 0
+            feed.close()
+    # a shard whose cache file lost its ready magic is skipped, once, with a warning
+    bad = tario.shm_path(cache.base, paths[1])
+    raw = bytearray(bad.read_bytes())
+    raw[8:16] = b"\x00" * 8
+    bad.write_bytes(bytes(raw))
+    cache._ensure = lambda p: tario.shm_path(cache.base, p)  # the reader trusts the file as it is
+    feed = tario.NativeShardFeed(cache, paths, 4, nthreads=nthreads)
+    n = 0
+    with pytest.warns(RuntimeWarning, match="skipped a shard"):
+        while True:
+            try:
+                fb = feed.next_prepared(timeout=10.0)
+            except StopIteration:
+                break
+            n += 1
+            feed.release(fb)
+    assert n == (7 + 9 + 6 + 8) // 4 and feed.shard_errors and feed.stats()["shards_failed"] == 1
+    feed.close()
+    cache.close(remove=True)
