@@ -576,7 +576,7 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
     pcfg = PipelineConfig(device_id=torch.cuda.current_device(), seed=1234 + rank, gpu_queue=args.gpu_queue,
                           output_dtype=args.dtype if args.dtype != "fp8" else "bf16",
                           dali_fp8_output=args.dtype == "fp8")
-    backend = MI355XBackend()
+    backend = MI355XBackend(max_in_flight=args.e2e_in_flight)
     depth = backend.queue_depth(pcfg, B)
     n = (args.warmup + args.steps + depth + 4) * B
     jpegs = [uniq[i % len(uniq)] for i in range(n)]
@@ -675,6 +675,7 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--gpu-queue", type=int, default=6, help="PipelineConfig.gpu_queue of the e2e leg")
     ap.add_argument("--shard-size", type=int, default=1000, help="samples per synthetic tar shard (e2e)")
     ap.add_argument("--gather-threads", type=int, default=8, help="copier threads of the e2e feed")
+    ap.add_argument("--e2e-in-flight", type=int, default=3, help="MI355XBackend(max_in_flight) of the e2e leg")
     ap.add_argument("--e2e-feed", default="native", choices=["native", "python"],
                     help="e2e host half: the native shard feed (C++ threads) or the Python prefetch thread")
     return ap

@@ -27,6 +27,7 @@ from __future__ import annotations
 import atexit
 import os
 import queue
+import sys
 import threading
 import time
 import warnings
@@ -63,14 +64,19 @@ class _Slot:
         self.inflight = None
         self.outputs: dict[str, torch.Tensor] | None = None
         self.norm: torch.Tensor | None = None         # per-image normalisation records of the batch
-        self.info_host: torch.Tensor | None = None    # pinned copy of the batch's per-image status
-        self.done: torch.cuda.Event | None = None     # recorded after that copy (status accounting)
         self.batch_id = -1
         self.batch_index = -1                          # the batch's RNG key (seed, batch_index)
         self.sizes: tuple[int, int] | None = None     # (G, L) the views were made at
         self.probe: np.ndarray | None = None          # dino_probe info of the batch (host batches)
-        self.d_in: torch.Tensor | None = None         # HBM copy of the batch's bytes (spans / native feed)
-        self.d_off: torch.Tensor | None = None        # HBM offsets of the native feed's batch
+        self.d_in: torch.Tensor | None = None         # HBM copy of the batch's bytes (spans feed)
+        # native feed: two HBM input buffers (bytes, offsets) used alternately, so the copy of a
+        # batch runs on the copy stream while the slot's previous batch still decodes
+        self.d_ins: list = [None, None]
+        self.d_offs: list = [None, None]
+        self.buf_done: list = [None, None]            # event after the last batch that read each buffer
+        self.buf_next = 0
+        self.view_cache = None                        # (shape key, output tensors) reused once the caller drops them
+        self.consumer: torch.cuda.Stream | None = None  # the stream the last outputs were handed to
 
 
 class _Staging:
@@ -261,7 +267,8 @@ class MI355XAugPipeline:
         # host-side seconds per phase: pull / pack / probe (host half), wait (launch thread
         # waiting for the host half), launch (H2D copies + kernel enqueue)
         self.host_seconds = {"pull": 0.0, "pack": 0.0, "probe": 0.0, "wait": 0.0, "launch": 0.0}
-        self._pending: deque = deque()
+        self._pending: deque = deque()   # (pinned status copy, its event, batch id, images) per launched batch
+        self._info_pool: list = []       # pinned status buffers of accounted batches
         self.depth = max(1, int(depth))
         self.prefetch_ahead = (1 if self.depth > 1 else 0) if prefetch is None else max(0, int(prefetch))
         self._prefetcher: _Prefetcher | None = None
@@ -272,6 +279,10 @@ class MI355XAugPipeline:
         # the native feed (tario.NativeShardFeed): batches arrive packed + probed by C++ threads
         self._feed = hasattr(source, "next_prepared")
         self._held: deque = deque()   # the feed's next batch, prepared one ahead (Pillow hand-overs start early)
+        # H2D copies of the native feed's batches, off the slots' streams (DINO_COPY_STREAM=0: on them)
+        self._copy_stream = None
+        if self._feed and depth > 1 and os.environ.get("DINO_COPY_STREAM", "1") != "0":
+            self._copy_stream = torch.cuda.Stream(device=device)
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
@@ -360,21 +371,24 @@ class MI355XAugPipeline:
             with eng.on_stream():
                 sl.norm = recs.to(self.device, non_blocking=True)
             eng.set_norm(sl.norm)
+        if views is None:
+            views = self._views_for(sl, cfg, batch)
         views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
                                     views=views, params_out=sl.params, raw_mask=raw_mask, lengths=lengths)
         sl.info = info
         sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
         if account:  # per-image status back to the host asynchronously (accounted at a later hand-over)
-            if any(e[0] is sl for e in self._pending):
-                self._account(until=sl)  # the slot's previous batch (long finished) is read before its copy is reused
-            if sl.info_host is None or sl.info_host.shape[0] < batch:
-                sl.info_host = torch.empty((batch, 4), dtype=torch.int32, pin_memory=True)
+            # each pending batch owns a pinned status buffer from a small pool, so launching never
+            # waits for an earlier batch of the slot to finish
+            host = self._info_pool.pop() if self._info_pool else None
+            if host is None or host.shape[0] < batch:
+                host = torch.empty((batch, 4), dtype=torch.int32, pin_memory=True)
             with eng.on_stream():
-                sl.info_host[:batch].copy_(info, non_blocking=True)
-            sl.done = torch.cuda.Event()
-            sl.done.record(eng.stream if eng.stream is not None else torch.cuda.current_stream(self.device))
+                host[:batch].copy_(info, non_blocking=True)
+            done = torch.cuda.Event()
+            done.record(eng.stream if eng.stream is not None else torch.cuda.current_stream(self.device))
             sl.batch_id = self._batch_index
-            self._pending.append((sl, sl.batch_id, batch))
+            self._pending.append((host, done, sl.batch_id, batch))
         if eng.stream is not None:
             sl.event = torch.cuda.Event()
             sl.event.record(eng.stream)
@@ -382,6 +396,25 @@ class MI355XAugPipeline:
         self._handed = None
         self._batch_index += 1
         return sl.outputs
+
+    def _views_for(self, sl: _Slot, cfg, batch: int) -> list[torch.Tensor]:
+        """Output tensors for the slot's next batch: the slot's previous ones when nothing but
+        the slot still references them (the caller dropped that batch, as DALI's iterator
+        expects before its buffers are refilled), else new ones.  A reused set is written
+        only after the work the caller had queued on its stream by now (the caching
+        allocator's record_stream rule, applied at reuse)."""
+        key = (batch, cfg.n_global, cfg.n_local, cfg.global_size, cfg.local_size, cfg.out_dtype)
+        vc = sl.view_cache
+        # held by the cache list, the slot's outputs dict, the loop variable and getrefcount's argument
+        if vc is not None and vc[0] == key and all(sys.getrefcount(t) <= 4 for t in vc[1]):
+            if sl.consumer is not None and sl.engine.stream is not None:
+                ev = torch.cuda.Event()
+                ev.record(sl.consumer)
+                sl.engine.stream.wait_event(ev)
+            return vc[1]
+        views = sl.engine.alloc_views(cfg, batch)
+        sl.view_cache = (key, views)
+        return views
 
     # ------------------------------------------------------------------ host half
     def _prepare_next(self) -> _Prepared:
@@ -546,17 +579,16 @@ class MI355XAugPipeline:
             return None, None, nbytes, raw
         return st.buf, st.off[: B + 1], nbytes, raw
 
-    def _account(self, block: bool = False, until: _Slot | None = None) -> None:
-        """Fold the per-image status of finished batches into ``stats`` (oldest first);
-        ``until``: wait for batches up to and including that slot's pending one."""
+    def _account(self, block: bool = False) -> None:
+        """Fold the per-image status of finished batches into ``stats`` (oldest first)."""
         while self._pending:
-            sl, bid, batch = self._pending[0]
-            waiting = block or (until is not None and any(e[0] is until for e in self._pending))
-            if not waiting and not sl.done.query():
+            host, done, bid, batch = self._pending[0]
+            if not block and not done.query():
                 break
-            sl.done.synchronize()
+            done.synchronize()
             self._pending.popleft()
-            st = sl.info_host[:batch, 0].numpy()
+            st = host[:batch, 0].numpy().copy()
+            self._info_pool.append(host)
             self.stats["batches"] += 1
             self.stats["images"] += batch
             self.stats["status"].update(int(x) for x in st)
@@ -581,6 +613,7 @@ class MI355XAugPipeline:
         st = pb.staging
         t0 = time.perf_counter()
         copied = None
+        buf_j = None  # the native feed's input buffer of the slot this batch reads
         try:
             sl = self._next_slot()
             sizes = self._sizes()
@@ -591,16 +624,32 @@ class MI355XAugPipeline:
             with sl.engine.on_stream():
                 if pb.feed is not None:  # the native feed's pinned slot: bytes + offsets in two DMAs
                     fb, pb.feed = pb.feed, None
-                    if sl.d_in is None or sl.d_in.numel() < fb.nbytes + 64:
-                        sl.d_in = torch.empty(max(fb.nbytes, 1) * 9 // 8 + 64, dtype=torch.uint8, device=self.device)
-                    if sl.d_off is None or sl.d_off.numel() < B + 1:
-                        sl.d_off = torch.empty(B + 1, dtype=torch.int64, device=self.device)
+                    j = sl.buf_next
+                    sl.buf_next ^= 1
+                    if sl.d_ins[j] is None or sl.d_ins[j].numel() < fb.nbytes + 64:
+                        if sl.buf_done[j] is not None:  # the old buffer's last reader must finish first
+                            sl.buf_done[j].synchronize()
+                        sl.d_ins[j] = torch.empty(max(fb.nbytes, 1) * 9 // 8 + 64, dtype=torch.uint8,
+                                                  device=self.device)
+                    if sl.d_offs[j] is None or sl.d_offs[j].numel() < B + 1:
+                        if sl.buf_done[j] is not None:
+                            sl.buf_done[j].synchronize()
+                        sl.d_offs[j] = torch.empty(B + 1, dtype=torch.int64, device=self.device)
+                    cs = self._copy_stream if self._copy_stream is not None else sl.engine.stream
                     try:
-                        self._source.copy(fb, sl.d_in.data_ptr(), sl.d_off.data_ptr(), sl.engine._s().value or 0)
+                        if cs is not sl.engine.stream and sl.buf_done[j] is not None:
+                            cs.wait_event(sl.buf_done[j])
+                        self._source.copy(fb, sl.d_ins[j].data_ptr(), sl.d_offs[j].data_ptr(),
+                                          cs.cuda_stream if cs is not None else 0)
                     except BaseException:
                         self._source.release(fb)
                         raise
-                    d_bytes, d_offsets = sl.d_in, sl.d_off[: B + 1]
+                    if cs is not sl.engine.stream:
+                        arrived = torch.cuda.Event()
+                        arrived.record(cs)
+                        torch.cuda.current_stream(self.device).wait_event(arrived)
+                    d_bytes, d_offsets = sl.d_ins[j], sl.d_offs[j][: B + 1]
+                    buf_j = j
                 elif pb.spans is not None:  # DMA the batch's shard ranges as they lie (no host copy)
                     nbytes = int(pb.spans.offsets[-1])
                     if sl.d_in is None or sl.d_in.numel() < nbytes:
@@ -620,6 +669,8 @@ class MI355XAugPipeline:
                 copied.record()
             self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw, sizes=sizes,
                          probe=pb.info, lengths=d_lens)
+            if buf_j is not None:
+                sl.buf_done[buf_j] = sl.event
             sl.inflight = (d_bytes, d_offsets, d_raw, d_lens)  # device copies live until the slot's next batch
         except BaseException:
             if pb.staging is not None:
@@ -667,8 +718,9 @@ class MI355XAugPipeline:
             cur.wait_event(sl.event)
             for t in sl.outputs.values():
                 t.record_stream(cur)
+            sl.consumer = cur
         self._handed = sl
-        return sl.outputs
+        return dict(sl.outputs)  # the caller's own dict: its references keep the tensors from reuse
 
     def wait(self) -> None:
         """Make the caller's stream wait for the last enqueued batch."""

@@ -294,3 +294,42 @@ def test_shard_spans_feed_dma_matches_packed_feed(gpu_device, tmp_path):
             assert torch.equal(a[name], b[name]), (k, name)
             assert torch.equal(a[name], c[name]), (k, name, "native feed")
     cache.close(remove=True)
+
+
+def test_output_views_reused_only_after_the_caller_drops_them(gpu_device):
+    """A slot refills its previous output tensors only when the caller no longer references
+    them (DALI's iterator contract); batches the caller keeps are never overwritten."""
+    from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
+    rng = np.random.default_rng(56)
+    uniq = [encode_jpeg(textured_rgb(160, 120, rng)) for _ in range(6)]
+    B, nb = 4, 9
+    batches = [[uniq[(k + i) % 6] for i in range(B)] for k in range(nb)]
+    cfg = DINOAugConfig(global_crop_size=64, local_crop_size=32)
+
+    def run(keep):
+        src = _ListSource(batches)
+        pipe = MI355XAugPipeline(src, cfg, B, seed=4, depth=3)
+        it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
+        kept, snaps, ptrs = [], [], []
+        for out in it:
+            d = out[0]
+            torch.cuda.synchronize()
+            snaps.append({k: v.clone() for k, v in d.items()})
+            ptrs.append(d["view_0"].data_ptr())
+            if keep:
+                kept.append(d)
+            del out, d
+        torch.cuda.synchronize()
+        pipe.close()
+        return kept, snaps, ptrs
+
+    kept, snaps, ptrs_keep = run(True)
+    for d, s in zip(kept, snaps):
+        for k in d:
+            assert torch.equal(d[k], s[k]), k          # nothing the caller holds was refilled
+    assert len(set(ptrs_keep)) == nb
+    _, snaps2, ptrs_drop = run(False)
+    assert len(set(ptrs_drop)) < nb                    # dropped outputs are refilled in place
+    for a, b in zip(snaps, snaps2):
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
