@@ -145,15 +145,21 @@ DHD uint32_t br_peek32(const BitReader& br, uint32_t pos) {
 }
 
 // A lane's cached view of the stream: 64-bit window, left aligned, plus the next
-// stream word in flight.  The word is kept raw (as loaded) and only byte-swapped /
-// end-masked when it enters the window, so its load is waited on at the next
-// refill (~32 bits later) rather than right after it is issued.
+// kPrefetchWords stream words in flight.  The words are kept raw (as loaded) and only
+// byte-swapped / end-masked when they enter the window, so a load is waited on
+// kPrefetchWords refills (~32 bits each) after it is issued: the speculative decode
+// kernels keep one stream line per lane live, ~L2-sized in all, so a refill often comes
+// from the Infinity Cache or HBM rather than L2.
+#ifndef DINO_HUFF_PREFETCH
+#define DINO_HUFF_PREFETCH 1
+#endif
+constexpr int kPrefetchWords = DINO_HUFF_PREFETCH;
 struct BitCursor {
   uint64_t buf;        // next bits, MSB first
   int32_t nbits;       // valid bits in buf
   uint32_t pos;        // absolute bit position of the next unread bit
-  uint32_t next_word;  // index of the word held (raw) in pf
-  uint32_t pf;
+  uint32_t next_word;  // index of the word held (raw) in pf[0]
+  uint32_t pf[kPrefetchWords];
 };
 
 // Stream sources (template argument kWin of the routines below):
@@ -203,10 +209,12 @@ DHD uint32_t win_word(const BitReader& br, uint32_t i) { return src_word<kSrcWin
 template <int kWin>
 DHD void bc_fill(BitCursor& c, const BitReader& br) {
   if (c.nbits < 32) {
-    c.buf |= (uint64_t)src_cook<kWin>(br, c.pf, c.next_word) << (32 - c.nbits);
+    c.buf |= (uint64_t)src_cook<kWin>(br, c.pf[0], c.next_word) << (32 - c.nbits);
     c.nbits += 32;
+#pragma unroll
+    for (int k = 0; k + 1 < kPrefetchWords; ++k) c.pf[k] = c.pf[k + 1];
+    c.pf[kPrefetchWords - 1] = src_raw<kWin>(br, c.next_word + kPrefetchWords);
     c.next_word++;
-    c.pf = src_raw<kWin>(br, c.next_word);
   }
 }
 
@@ -217,7 +225,8 @@ DHD void bc_init(BitCursor& c, const BitReader& br, uint32_t pos) {
   c.buf = (((uint64_t)src_word<kWin>(br, w) << 32) | src_word<kWin>(br, w + 1)) << sh;
   c.nbits = 64 - (int)sh;
   c.next_word = w + 2;
-  c.pf = src_raw<kWin>(br, w + 2);
+#pragma unroll
+  for (int k = 0; k < kPrefetchWords; ++k) c.pf[k] = src_raw<kWin>(br, w + 2 + k);
 }
 
 DHD uint32_t bc_peek(const BitCursor& c, int n) { return (uint32_t)(c.buf >> (64 - n)); }

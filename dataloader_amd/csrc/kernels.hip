@@ -32,6 +32,36 @@
 
 namespace dino {
 
+// XCD-aware workgroup coordinates.  The dispatcher deals a launch's workgroups round-robin
+// over the 8 XCDs (ids equal mod 8 share an XCD and its 4 MiB L2); renumbered, each XCD owns
+// a contiguous range of the grid in (z, y, x) order, i.e. whole images, so the workgroups
+// that read one image's planes / RGB / crop rows share one L2 (cdna guide §5.5 T1, the
+// bijective form for grids not divisible by 8).  Speed only: no result depends on placement.
+#ifndef DINO_XCD_REMAP
+#define DINO_XCD_REMAP 0
+#endif
+constexpr uint32_t kXcds = 8;
+struct BlkIdx {
+  int x, y, z;
+};
+__device__ __forceinline__ BlkIdx xcd_blk() {
+  const uint32_t X = gridDim.x, Y = gridDim.y, Z = gridDim.z;
+  uint32_t L = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+  if (DINO_XCD_REMAP) {
+    const uint32_t n = X * Y * Z;
+    if (n > kXcds) {
+      const uint32_t q = n / kXcds, r = n % kXcds, xcd = L % kXcds;
+      L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / kXcds;
+    }
+  }
+  BlkIdx b;
+  b.x = (int)(L % X);
+  L /= X;
+  b.y = (int)(L % Y);
+  b.z = (int)(L / Y);
+  return b;
+}
+
 // ---------------------------------------------------------------------------
 // k_parse
 // ---------------------------------------------------------------------------
@@ -1237,11 +1267,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 #endif
 constexpr int kIdctWgs = DINO_IDCT_WGS;  // workgroups per image (grid-stride over its blocks)
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  const BlkIdx bk = xcd_blk();
   // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
   // (pass 2) accesses of a wave's 8 groups x 8 lanes hit 64 distinct banks
   __shared__ int32_t s_blk[kIdctBlocksPerWg][72];
   __shared__ uint8_t s_nat[80];
-  const ImgDesc& d = desc[blockIdx.y];
+  const ImgDesc& d = desc[bk.y];
   if (d.status != DINO_IMG_OK || d.kind == 2) return;
   // kind 1 (progressive / multi-scan): dense int16 coefficients in natural order,
   // component planes of bw x bh blocks (k_prog); kind 0: sparse entries + block records
@@ -1290,7 +1321,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   // The next block's record is loaded one iteration ahead, and its first 16 entries
   // at the end of the current iteration (once the record has arrived), so the
   // scatter at the top of an iteration normally waits on nothing.
-  int gn = blockIdx.x * kIdctBlocksPerWg + grp;
+  int gn = bk.x * kIdctBlocksPerWg + grp;
   Blk nx = locate(gn < T ? gn : 0);
   uint2 bin = make_uint2(0u, 0u);
   if (!dense && gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
@@ -1306,7 +1337,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
   __syncthreads();
-  for (int g0 = blockIdx.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
+  for (int g0 = bk.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
     const bool valid = gn < T;
     const Blk cur = nx;
     const uint2 bi = bin;
@@ -1437,13 +1468,14 @@ constexpr int kColorBatch = DINO_COLOR_BATCH;  // quads whose loads a lane issue
 // a row and other samplings use the per-pixel path (same arithmetic).
 __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
                                                const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  const ImgDesc& d = desc[blockIdx.y];
+  const BlkIdx bk = xcd_blk();
+  const ImgDesc& d = desc[bk.y];
   if (d.status != DINO_IMG_OK) return;
   if (d.kind == 2) {  // pre-decoded RGB container: copy the pixels into the workspace
-    const uint8_t* src = bytes + offsets[blockIdx.y] + d.scan_off;
+    const uint8_t* src = bytes + offsets[bk.y] + d.scan_off;
     uint32_t* dst = (uint32_t*)(ws + d.rgb_off);
     const int64_t n = (int64_t)d.width * d.height * 3, nw = (n + 3) >> 2;
-    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nw; q += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)bk.x * blockDim.x + threadIdx.x; q < nw; q += (int64_t)gridDim.x * blockDim.x) {
       uint32_t w = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
@@ -1465,7 +1497,7 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
   const int64_t nq = (npx + 3) >> 2;  // npx < 2^31 (max_image_dim <= 16384 is enforced by k_parse limits)
   // (y, x) of the lane's first quad by one division; later quads advance by the
   // grid stride (dy rows + dx pixels) without dividing again
-  const int64_t q0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, qs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t q0 = (int64_t)bk.x * blockDim.x + threadIdx.x, qs = (int64_t)gridDim.x * blockDim.x;
   const uint32_t pstride = (uint32_t)(qs * 4);
   const int dy = (int)(pstride / (uint32_t)W), dx = (int)(pstride - (uint32_t)dy * (uint32_t)W);
   int yq = (int)((uint32_t)(q0 * 4) / (uint32_t)W), xq = (int)((uint32_t)(q0 * 4) - (uint32_t)yq * (uint32_t)W);
@@ -1868,6 +1900,58 @@ __device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ row
   }
 }
 
+// The same tile with each lane's taps in registers: lane (column xl, row group rg) loads
+// its output's NG groups of tap digits once and sweeps the band's rows rg, rg + nrg, ...
+// (one LDS word per channel and group per row; the taps cost nothing per row).  NG is the
+// view's group count rounded up to 2, 4 or 8 (unrolled, predicated by the lane's own count).
+#ifndef DINO_HRESIZE_TAPREG
+#define DINO_HRESIZE_TAPREG 0
+#endif
+template <int NG>
+__device__ __forceinline__ void hresize_tile_regs(const uint8_t* __restrict__ rows, int pitch, int plane_bytes, int nr,
+                                                  int r0, int x0, int sw, int c0, int S, const int4* __restrict__ hx,
+                                                  const uint4* __restrict__ hg, uint8_t* __restrict__ tmp, int64_t cpl) {
+  const int nrg = max(1, (int)blockDim.x / sw);
+  const int e = threadIdx.x;
+  if (e >= nrg * sw) return;
+  const int rg = e / sw, xl = e - rg * sw;
+  const int4 h = hx[xl];
+  const int lo = h.x - c0, ng = h.y;
+  const uint32_t sh = (uint32_t)(lo & 3);
+  const int pw = plane_bytes >> 2;
+  uint32_t d0[NG], d1[NG], d2[NG];
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const uint4 dg = g < ng ? hg[g * sw + xl] : make_uint4(0u, 0u, 0u, 0u);
+    d0[g] = dg.x;
+    d1[g] = dg.y;
+    d2[g] = dg.z;
+  }
+  const uint32_t* q0 = (const uint32_t*)rows + (lo >> 2);
+  for (int r = rg; r < nr; r += nrg) {
+    const uint32_t* q = q0 + r * (pitch >> 2);
+    const int64_t o = (int64_t)(r0 + r) * S + x0 + xl;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const uint32_t* qc = q + c * pw;
+      int32_t a0 = 0, a1 = 0, a2 = 0;
+      uint32_t lw = qc[0];
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if (g < ng) {
+          const uint32_t u = qc[g + 1];
+          const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(u, lw, sh);
+          a0 = __builtin_amdgcn_sdot4(pa, (int32_t)d0[g], a0, false);
+          a1 = __builtin_amdgcn_sdot4(pa, (int32_t)d1[g], a1, false);
+          a2 = __builtin_amdgcn_sdot4(pa, (int32_t)d2[g], a2, false);
+          lw = u;
+        }
+      }
+      tmp[c * cpl + o] = clip8_acc((int32_t)((uint32_t)a0 + ((uint32_t)a1 << 8) + ((uint32_t)a2 << 16) + (uint32_t)h.z));
+    }
+  }
+}
+
 // Horizontal pass in tiles of (slice of outputs) x (band of rows), shaped by
 // hresize_tile: the slice's taps always come from LDS, and the band stages only the
 // source columns the slice reads [xmin(x0), xmin(x1-1) + xcnt(x1-1)), so wide crops
@@ -1875,9 +1959,10 @@ __device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ row
 __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  const ViewPlan* __restrict__ plan, int nv, int v0,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
+  const BlkIdx bk = xcd_blk();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int b = blockIdx.z;
-  const int i = b * nv + v0 + blockIdx.y;
+  const int b = bk.z;
+  const int i = b * nv + v0 + bk.y;
   const ViewPlan vp = plan[i];
   if (!vp.ok || !vp.kh) return;
   const dino_view_params p = prm[i];
@@ -1897,7 +1982,7 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   if (R < 1) {  // direct path: taps and pixels from global memory (crops too wide for LDS)
     const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
     const CoefView cv{gb, gt, kh};
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < cpl; e += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t e = (int64_t)bk.x * blockDim.x + threadIdx.x; e < cpl; e += (int64_t)gridDim.x * blockDim.x) {
       const int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
       for (int c = 0; c < 3; ++c) tmp[c * cpl + e] = hresize_at(src, cv, r, x, c);
     }
@@ -1909,7 +1994,7 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   const int plane_bytes = R * pitch;
   const int nbands = (p.crop_h + R - 1) / R;
   int cur = -1;
-  for (int u = blockIdx.x; u < nsl * nbands; u += gridDim.x) {
+  for (int u = bk.x; u < nsl * nbands; u += gridDim.x) {
     const int sl = u / nbands, band = u - sl * nbands;
     const int x0 = sl * sw, swn = min(sw, S - x0);
     const int r0 = band * R, nr = min(R, p.crop_h - r0);
@@ -1944,7 +2029,14 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
       *(uint32_t*)(dst + 2 * plane_bytes) = cb ^ 0x80808080u;
     }
     __syncthreads();
-    hresize_tile_dot(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+    if (DINO_HRESIZE_TAPREG && ng_max <= 2)
+      hresize_tile_regs<2>(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+    else if (DINO_HRESIZE_TAPREG && ng_max <= 4)
+      hresize_tile_regs<4>(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+    else if (DINO_HRESIZE_TAPREG && ng_max <= 8)
+      hresize_tile_regs<8>(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+    else
+      hresize_tile_dot(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
     __syncthreads();
   }
 }
@@ -2083,8 +2175,9 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
                                               ViewPlan* __restrict__ plan, int nv, int v0, int B,
                                               const uint8_t* __restrict__ ws, const uint8_t* __restrict__ aws,
                                               uint8_t* __restrict__ gcrop, dino_aug_config cfg, int S) {
+  const BlkIdx bk = xcd_blk();
   __shared__ uint32_t s_part[4];
-  const int b = blockIdx.z, v = v0 + blockIdx.y;
+  const int b = bk.z, v = v0 + bk.y;
   const int i = b * nv + v;
   const ViewPlan vp = plan[i];
   if (!vp.ok) return;
@@ -2092,7 +2185,7 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   const int64_t N = (int64_t)S * S;
   uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);  // (256 lanes: s_part holds 4 waves)
   const JitterPlan jp = make_jitter_plan(p);
-  const int y0 = blockIdx.x * vert_rows(S);
+  const int y0 = bk.x * vert_rows(S);
   const int nr = min(vert_rows(S), S - y0);
   const uint32_t lsum = vert_apply(
       desc[b], p, vp, ws, aws, S, y0, nr, jp, hue_delta(p.hue),
@@ -2269,14 +2362,15 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
                                                const ViewPlan* __restrict__ plan, int nv, int v0, int B,
                                                const uint8_t* __restrict__ gcrop, ViewPtrs views, dino_aug_config cfg,
                                                int S, const float* __restrict__ norm) {
+  const BlkIdx bk = xcd_blk();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
   uint8_t* tile = smem + sizeof(FinalLds);
-  const int b = blockIdx.z, v = v0 + blockIdx.y;
+  const int b = bk.z, v = v0 + bk.y;
   const int i = b * nv + v;
   const ViewPlan vp = plan[i];
   const int64_t N = (int64_t)S * S;
-  const int y0 = blockIdx.x * final_rows(S);
+  const int y0 = bk.x * final_rows(S);
   const int nr = min(final_rows(S), S - y0);
   OutT* out = (OutT*)views.p[v] + (int64_t)b * 3 * N;
   const float* nb = norm ? norm + (int64_t)b * 6 : nullptr;
@@ -2386,11 +2480,12 @@ __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __rest
                                                 const ViewPlan* __restrict__ plan, int nv, int v0, const uint8_t* __restrict__ ws,
                                                 const uint8_t* __restrict__ aws, ViewPtrs views, dino_aug_config cfg, int S,
                                                 const float* __restrict__ norm) {
+  const BlkIdx bk = xcd_blk();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint32_t s_part[kVFinalThreads / 64];
   FinalLds& H = *reinterpret_cast<FinalLds*>(smem);
   uint8_t* tile = smem + sizeof(FinalLds);
-  const int b = blockIdx.y, v = v0 + blockIdx.x;
+  const int b = bk.y, v = v0 + bk.x;
   const int i = b * nv + v;
   const ViewPlan vp = plan[i];
   const int64_t N = (int64_t)S * S;
