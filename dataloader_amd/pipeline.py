@@ -25,6 +25,7 @@ have decoded but that came back zero-filled raises a ``RuntimeWarning``.
 from __future__ import annotations
 
 import atexit
+import ctypes
 import os
 import queue
 import sys
@@ -144,6 +145,7 @@ class _Prepared:
         self.staging = staging        # None: no Python staging (native feed slot, or not yet needed)
         self.spans = spans            # tario.BatchSpans: the batch stays in its page-locked shard ranges
         self.feed = feed              # tario.FeedBatch: the batch is packed in a native feed slot
+        self.side = None              # progside.SideJob: its coefficient-buffer images, decoded ahead
         self.jpegs = jpegs            # the source's list (None for the native feed)
         self.offsets = offsets
         self.info = info
@@ -204,8 +206,11 @@ class _Prefetcher:
         except BaseException as e:  # noqa: BLE001 - handed to the launch thread
             self._put(e)
 
-    def get(self) -> _Prepared:
-        item = self._q.get()
+    def get(self, block: bool = True) -> _Prepared | None:
+        try:
+            item = self._q.get(block=block)
+        except queue.Empty:
+            return None
         if item is _END:
             raise StopIteration
         if isinstance(item, BaseException):
@@ -239,7 +244,7 @@ class MI355XAugPipeline:
                  view_names: list[str] | None = None, host_fallback: bool = True,
                  multiscan_route: str = "auto", host_workers: int | None = None,
                  multiscan_host_max: int | None = None, prefetch: int | None = None,
-                 start_host_pool: bool = False):
+                 start_host_pool: bool = False, side_ahead: int = 24):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -251,9 +256,16 @@ class MI355XAugPipeline:
         self._batch_index = 0
         self._max_image_dim = int(max_image_dim)
         self._host_fallback = bool(host_fallback)
-        if multiscan_route not in ("auto", "device", "host"):
-            raise ValueError(f"multiscan_route must be 'auto', 'device' or 'host', not {multiscan_route!r}")
+        if multiscan_route not in ("auto", "device", "host", "side"):
+            raise ValueError(f"multiscan_route must be 'auto', 'device', 'host' or 'side', not {multiscan_route!r}")
         self._multiscan_route = multiscan_route
+        # "side": coefficient-buffer images decoded on the device ahead of their batch (progside.py),
+        # side_ahead batches before it is launched
+        self._side_ahead = max(1, int(side_ahead)) if multiscan_route == "side" else 0
+        self._route = "device" if multiscan_route == "side" else multiscan_route  # what route_mask sees
+        self._side = None
+        self._ahead: deque = deque()   # prepared batches waiting for launch (side path)
+        self._source_end = False
         workers = int(host_workers) if host_workers else min(8, os.cpu_count() or 1)
         self._host = fallback.HostDecoder(workers)
         if start_host_pool:
@@ -263,7 +275,8 @@ class MI355XAugPipeline:
         self._host_max = int(multiscan_host_max) if multiscan_host_max is not None else 8 * workers
         # per-image outcome of every batch handed over (status code -> images), images the
         # GPU decoder left to Pillow, and workspace regrowths
-        self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0, "reserves": 0}
+        self.stats = {"batches": 0, "images": 0, "status": Counter(), "host_decoded": 0, "reserves": 0,
+                      "side_decoded": 0}
         # host-side seconds per phase: pull / pack / probe (host half), wait (launch thread
         # waiting for the host half), launch (H2D copies + kernel enqueue)
         self.host_seconds = {"pull": 0.0, "pack": 0.0, "probe": 0.0, "wait": 0.0, "launch": 0.0}
@@ -271,8 +284,10 @@ class MI355XAugPipeline:
         self._info_pool: list = []       # pinned status buffers of accounted batches
         self.depth = max(1, int(depth))
         self.prefetch_ahead = (1 if self.depth > 1 else 0) if prefetch is None else max(0, int(prefetch))
+        if self._side_ahead:
+            self.prefetch_ahead = max(1, self.prefetch_ahead)
         self._prefetcher: _Prefetcher | None = None
-        self._ring = _StagingRing(self.depth + self.prefetch_ahead + 2)
+        self._ring = _StagingRing(self.depth + self.prefetch_ahead + self._side_ahead + 2)
         self._native = hasattr(source, "next_spans")
         # the feed can hand batches over where they lie (page-locked shard ranges, DMA'd as they are)
         self._spans_feed = hasattr(source, "next_batch_spans")
@@ -447,7 +462,7 @@ class MI355XAugPipeline:
             t1 = time.perf_counter()
             if bs is not None and bs.registered:
                 info, ws, aws = fallback.probe_spans(ptrs, lens, self._max_image_dim, cfg)
-                if not fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max).any():
+                if not fallback.route_mask(info, self._host_fallback, self._route, self._host_max).any():
                     st = self._ring.acquire()
                     st.fit(0, B)
                     st.off.numpy()[: B + 1] = bs.offsets
@@ -467,7 +482,7 @@ class MI355XAugPipeline:
                 if bs is not None:  # packed: the shard ranges are no longer read
                     self._source.retire(bs, None)
                     bs = None
-                mask = fallback.route_mask(info, self._host_fallback, self._multiscan_route, self._host_max)
+                mask = fallback.route_mask(info, self._host_fallback, self._route, self._host_max)
                 futures = {}
                 idx = np.flatnonzero(mask)
                 if len(idx):
@@ -501,7 +516,7 @@ class MI355XAugPipeline:
         fb = self._source.next_prepared(timeout=None if block else 0.0)
         if fb is None:
             return None
-        mask = fallback.route_mask(fb.info, self._host_fallback, self._multiscan_route, self._host_max)
+        mask = fallback.route_mask(fb.info, self._host_fallback, self._route, self._host_max)
         if not mask.any():
             return _Prepared(None, None, fb.offsets, fb.info, fb.ws, fb.aws, self._feed_sizes, {}, feed=fb)
         try:
@@ -525,7 +540,61 @@ class MI355XAugPipeline:
         finally:
             self.host_seconds["wait"] += time.perf_counter() - t0
 
+    def _pull_one(self, block: bool) -> _Prepared | None:
+        """The next prepared batch from the feed or the prefetch thread (None: none ready and
+        not ``block``); StopIteration at the end of the epoch."""
+        if self._feed:
+            return self._prepare_feed(block)
+        if self._prefetcher is None:
+            self._prefetcher = _Prefetcher(self, self.prefetch_ahead)
+        return self._prefetcher.get(block)
+
+    def _side_submit(self, pb: _Prepared) -> None:
+        """Start the side decode of the batch's coefficient-buffer images (progside.py)."""
+        from . import progside
+        m = progside.side_mask(pb.info)
+        for i in pb.futures:
+            m[i] = False
+        idx = np.flatnonzero(m)
+        if not len(idx):
+            return
+        if self._side is None:
+            self._side = progside.DeviceSideDecoder(self.device, max_images=self._batch_size,
+                                                    max_image_dim=self._max_image_dim)
+        if pb.jpegs is not None:
+            imgs = {int(i): pb.jpegs[i] for i in idx}
+        elif pb.feed is not None:
+            o = pb.feed.offsets
+            imgs = {int(i): ctypes.string_at(pb.feed.host + int(o[i]), int(o[i + 1] - o[i])) for i in idx}
+        else:
+            hb, o = pb.staging.buf.numpy(), pb.offsets
+            imgs = {int(i): hb[o[i]:o[i + 1]].tobytes() for i in idx}
+        pb.side = self._side.submit(imgs)
+
+    def _pull_side(self) -> _Prepared:
+        """The side path's look-ahead: keep up to side_ahead prepared batches, each with its
+        side decode started as it arrives; hand out the oldest."""
+        t0 = time.perf_counter()
+        try:
+            while not self._source_end and len(self._ahead) < self._side_ahead:
+                try:
+                    pb = self._pull_one(block=not self._ahead)
+                except StopIteration:
+                    self._source_end = True
+                    break
+                if pb is None:
+                    break
+                self._side_submit(pb)
+                self._ahead.append(pb)
+            if not self._ahead:
+                raise StopIteration
+            return self._ahead.popleft()
+        finally:
+            self.host_seconds["wait"] += time.perf_counter() - t0
+
     def _pull(self) -> _Prepared:
+        if self._side_ahead:
+            return self._pull_side()
         if self._feed:
             return self._pull_feed()
         if self.prefetch_ahead <= 0:
@@ -665,13 +734,22 @@ class MI355XAugPipeline:
                 if host_off is not None:
                     d_offsets = host_off.to(self.device, non_blocking=True)
                 d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
+                side = None
+                if pb.side is not None:  # coefficient-buffer images decoded ahead: their containers
+                    conts = pb.side.ready()
+                    if conts:
+                        base = host_off.numpy() if host_off is not None else pb.offsets
+                        d_bytes, d_offsets, d_lens, d_raw = self._merge_side(
+                            pb.side, conts, d_bytes, int(base[-1]), base, raw, B)
+                        side = conts
+                        self.stats["side_decoded"] += len(conts)
                 copied = torch.cuda.Event()
                 copied.record()
             self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw, sizes=sizes,
                          probe=pb.info, lengths=d_lens)
             if buf_j is not None:
                 sl.buf_done[buf_j] = sl.event
-            sl.inflight = (d_bytes, d_offsets, d_raw, d_lens)  # device copies live until the slot's next batch
+            sl.inflight = (d_bytes, d_offsets, d_raw, d_lens, side)  # device copies live until the slot's next batch
         except BaseException:
             if pb.staging is not None:
                 self._ring.release(pb.staging, copied)
@@ -686,6 +764,34 @@ class MI355XAugPipeline:
             self._source.retire(pb.spans, copied)
         self.host_seconds["launch"] += time.perf_counter() - t0
         return sl
+
+    def _merge_side(self, job, conts: dict, d_bytes: torch.Tensor, nbytes: int, base_off: np.ndarray,
+                    raw: torch.Tensor | None, B: int):
+        """The batch's input with its side-decoded images swapped for their device containers
+        (spans form: the batch bytes, then the containers; those images' offsets and lengths
+        point at their containers and the raw mask marks them).  Runs on the slot's stream,
+        after the side decode (stream wait)."""
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(job.event)
+        off = np.asarray(base_off, np.int64)[: B + 1].copy()
+        lens = np.diff(off)
+        rawm = raw.cpu().numpy().astype(np.uint8) if raw is not None else np.zeros(B, np.uint8)
+        pos = (nbytes + 15) & ~15
+        total = pos + sum((int(c.numel()) + 15) & ~15 for c in conts.values())
+        merged = torch.empty(total + 64, dtype=torch.uint8, device=self.device)
+        merged[:nbytes].copy_(d_bytes[:nbytes], non_blocking=True)
+        for i, c in conts.items():
+            n = int(c.numel())
+            merged[pos:pos + n].copy_(c, non_blocking=True)
+            c.record_stream(cur)
+            off[i], lens[i], rawm[i] = pos, n, 1
+            pos += (n + 15) & ~15
+        off[B] = total
+        h_off = torch.from_numpy(off).pin_memory()
+        h_len = torch.from_numpy(lens.astype(np.int64)).pin_memory()
+        h_raw = torch.from_numpy(rawm).pin_memory()
+        return (merged, h_off.to(self.device, non_blocking=True), h_len.to(self.device, non_blocking=True),
+                h_raw.to(self.device, non_blocking=True))
 
     def _refresh(self, sl: _Slot, sizes: tuple[int, int]) -> None:
         """The crop sizes changed (``ResolutionSource.set``, reference loader.py:280-308) after
@@ -733,6 +839,9 @@ class MI355XAugPipeline:
         """After the source's StopIteration and its reset: let the host half pull again."""
         while self._held:  # the native feed's look-ahead batch belongs to the finished epoch
             self._drop(self._held.popleft())
+        while self._ahead:
+            self._drop(self._ahead.popleft())
+        self._source_end = False
         if self._prefetcher is not None and self._prefetcher.finished:
             self._prefetcher.close()
             self._prefetcher = None
@@ -772,9 +881,13 @@ class MI355XAugPipeline:
                     self._prefetcher = None
                 while self._held:
                     self._drop(self._held.popleft())
+                while self._ahead:
+                    self._drop(self._ahead.popleft())
                 self._account(block=True)
             finally:
                 self._host.close()
+                if self._side is not None:
+                    self._side.close()
                 for sl in self._slots:
                     sl.engine.close()
 

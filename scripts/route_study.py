@@ -24,7 +24,9 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--batches", type=int, default=24)
     ap.add_argument("--ks", default="0,1,4,16,64")
-    ap.add_argument("--routes", default="device,auto,host")
+    ap.add_argument("--routes", default="device,auto,host,side")
+    ap.add_argument("--side-ahead", type=int, default=24)
+    ap.add_argument("--warm", type=int, default=3, help="batches before the timed region")
     args = ap.parse_args()
     B = args.batch
     base = make_unique(B, 640, 480, 1, False, 8)
@@ -42,22 +44,25 @@ def main() -> None:
             if k == 0 and route != "auto":
                 continue
             src = iter(batches)
-            pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=1, depth=3, multiscan_route=route)
+            pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=1, depth=3, multiscan_route=route,
+                                     side_ahead=args.side_ahead)
             it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
             n = 0
             t0 = None
             for i, _ in enumerate(it):
-                if i == 3:
+                if i == args.warm:
                     torch.cuda.synchronize()
                     t0 = time.perf_counter()
-                elif i > 3:
+                elif i > args.warm:
                     n += B
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             stats = pipe.flush_stats()
             pipe.close()
             print(json.dumps({"k_progressive": k, "route": route, "batch": B, "images_per_s": round(n / dt, 1),
-                              "host_decoded": stats["host_decoded"], "status": dict(stats["status"])}), flush=True)
+                              "host_decoded": stats["host_decoded"], "side_decoded": stats.get("side_decoded"),
+                              "batches": args.batches, "warm": args.warm, "side_ahead": args.side_ahead,
+                              "status": dict(stats["status"])}), flush=True)
 
 
 if __name__ == "__main__":

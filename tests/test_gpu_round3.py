@@ -333,3 +333,41 @@ def test_output_views_reused_only_after_the_caller_drops_them(gpu_device):
     for a, b in zip(snaps, snaps2):
         for k in a:
             assert torch.equal(a[k], b[k]), k
+
+
+def test_side_route_matches_in_batch_device_route(gpu_device):
+    """multiscan_route="side": progressive / multi-scan images decoded on the device ahead of
+    their batch (progside.py) give every view bit-identical to the in-batch k_prog route
+    ("device"), with a CMYK file (Pillow hand-over) and a cut progressive file (undecodable:
+    it stays in its batch and comes back zero-filled, as the reference's) in the mix."""
+    from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
+    rng = np.random.default_rng(57)
+    uniq = [encode_jpeg(textured_rgb(240 + 8 * s, 180 + 4 * s, rng)) for s in range(5)]
+    progs = [encode_jpeg(textured_rgb(200 + 16 * s, 150 + 8 * s, rng), progressive=True) for s in range(4)]
+    cut = progs[0][: len(progs[0]) * 2 // 3]
+    B, nb = 8, 9
+    batches = [[uniq[(k + i) % 5] for i in range(B)] for k in range(nb)]
+    for k in range(nb):
+        batches[k][k % B] = progs[k % 4]
+        if k % 3 == 0:
+            batches[k][(k + 3) % B] = progs[(k + 1) % 4]
+    batches[2][5] = _cmyk(100, 80, rng)
+    batches[5][6] = cut
+    cfg = DINOAugConfig(global_crop_size=96, local_crop_size=48)
+
+    def run(route):
+        src = _ListSource(batches)
+        pipe = MI355XAugPipeline(src, cfg, B, seed=9, depth=3, multiscan_route=route, host_workers=2, side_ahead=4)
+        it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
+        outs = _collect(it)
+        st = pipe.flush_stats()
+        pipe.close()
+        return outs, st
+
+    (ref, st0), (got, st1) = run("device"), run("side")
+    assert len(ref) == len(got) == nb
+    assert st1["side_decoded"] == nb + 3 and st0["side_decoded"] == 0, (st0, st1)  # the cut file fails on the side too
+    assert st0["status"] == st1["status"] and st0["host_decoded"] == st1["host_decoded"] == 1
+    for k, (a, b) in enumerate(zip(ref, got)):
+        for name in a:
+            assert torch.equal(a[name], b[name]), (k, name)
