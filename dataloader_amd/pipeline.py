@@ -559,8 +559,7 @@ class MI355XAugPipeline:
         if not len(idx):
             return
         if self._side is None:
-            self._side = progside.DeviceSideDecoder(self.device, max_images=self._batch_size,
-                                                    max_image_dim=self._max_image_dim)
+            self._side = progside.DeviceSideDecoder(self.device, max_image_dim=self._max_image_dim)
         if pb.jpegs is not None:
             imgs = {int(i): pb.jpegs[i] for i in idx}
         elif pb.feed is not None:
@@ -569,7 +568,7 @@ class MI355XAugPipeline:
         else:
             hb, o = pb.staging.buf.numpy(), pb.offsets
             imgs = {int(i): hb[o[i]:o[i + 1]].tobytes() for i in idx}
-        pb.side = self._side.submit(imgs)
+        pb.side = self._side.add(imgs)
 
     def _pull_side(self) -> _Prepared:
         """The side path's look-ahead: keep up to side_ahead prepared batches, each with its
@@ -736,6 +735,8 @@ class MI355XAugPipeline:
                 d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
                 side = None
                 if pb.side is not None:  # coefficient-buffer images decoded ahead: their containers
+                    if pb.side.pending:  # still in the side pool: decode it now
+                        self._side.flush()
                     conts = pb.side.ready()
                     if conts:
                         base = host_off.numpy() if host_off is not None else pb.offsets

@@ -7,21 +7,23 @@ scans made non-zero), so one image takes ~15-100 ms of latency (``scripts/prog_p
 while a whole baseline batch takes ~3.4 ms.  Decoded inside its batch, a single
 progressive image stalls the pipeline (the "progressive cliff").
 
-The side path takes that latency off the batch: when a batch is prepared — many batches
-before its launch (``MI355XAugPipeline(side_ahead=N)``; the reference's own prefetch
-queue, pipeline.py:317) — its progressive images are decoded as a mini-batch by one of a
-pool of small contexts on their own HIP streams, each image's RGB copied into a device
-buffer in the raw container layout (``DINO_RAW_MAGIC`` header + HWC bytes).  At launch
-the batch's input points those images at their containers (spans ABI, raw mask) and its
-stream waits for the side decode's event, so the batch's own kernels treat them like any
-other decoded image.  Same decoder, same bytes: the views are bit-identical to the
-in-batch device route (``tests/test_gpu_round3.py``).
+The side path takes that latency off the batch.  When a batch is prepared — up to
+``side_ahead`` batches before its launch (the reference's own prefetch queue,
+pipeline.py:317) — its progressive images join a pending pool; the pool is decoded as one
+mini-batch (one ``k_prog`` wave per image, all concurrent) once it holds ``min_images``
+images or a batch that needs it is about to launch, by one of a few side contexts on
+their own HIP streams.  Each image's RGB is copied into a device buffer in the raw
+container layout (``DINO_RAW_MAGIC`` header + HWC bytes).  At launch the batch's input
+points those images at their containers (spans ABI, raw mask) and its stream waits for
+the side decode's event, so the batch's own kernels treat them like any other decoded
+image.  Same decoder, same bytes: the views are bit-identical to the in-batch device
+route (``tests/test_gpu_round3.py``).
 """
 
 from __future__ import annotations
 
+import ctypes
 import struct
-from collections import deque
 
 import numpy as np
 import torch
@@ -31,24 +33,27 @@ from .engine import IngestEngine, pack_jpegs
 
 
 class SideJob:
-    """One mini-batch on the side path: device containers by batch index, ready after ``event``."""
+    """One batch's share of the side path: device containers by batch index, ready after
+    ``event`` (None until the pool holding its images is launched)."""
 
-    __slots__ = ("containers", "event", "engine", "status", "order")
+    __slots__ = ("containers", "event", "status", "rows", "pending")
 
-    def __init__(self, containers: dict, event: torch.cuda.Event, engine, status: torch.Tensor, order: list):
-        self.containers = containers
-        self.event = event
-        self.engine = engine
-        self.status = status      # pinned int32[n][4]: the side decode's per-image outcome
-        self.order = order        # batch index of each mini-batch row
+    def __init__(self):
+        self.containers: dict = {}
+        self.event: torch.cuda.Event | None = None
+        self.status: torch.Tensor | None = None   # pinned int32[n][4] of the mini-batch
+        self.rows: dict = {}                      # batch index -> mini-batch row
+        self.pending = True
 
     def ready(self) -> dict:
-        """The containers of images the side decode finished (waits for it; normally long done).
-        An image the device decoder failed on is left out: its batch decodes it again and
-        reaches the same outcome (zero-filled views where Pillow raises)."""
+        """The containers of images the side decode finished (waits for it; normally long
+        done).  An image the device decoder failed on is left out: its batch decodes it
+        again and reaches the same outcome (zero-filled views where Pillow raises)."""
+        if self.event is None:
+            return {}
         self.event.synchronize()
         st = self.status.numpy()[:, 0]
-        return {i: c for i, c in self.containers.items() if st[self.order.index(i)] == 0}
+        return {i: c for i, c in self.containers.items() if st[self.rows[i]] == 0}
 
 
 class _SideEngine:
@@ -56,27 +61,47 @@ class _SideEngine:
         self.stream = torch.cuda.Stream(device=device)
         self.eng = IngestEngine(device, max_batch=max_images, max_views=1, max_crop_size=8,
                                 max_image_dim=max_image_dim, workspace_bytes=64 << 20, stream=self.stream)
-        self.max_images = max_images
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
-        self.keep = None                             # host / device inputs of the job in flight
+        self.keep = None                             # host / device inputs of the mini-batch in flight
 
     def idle(self) -> bool:
         return self.last is None or self.last.query()
 
 
 class DeviceSideDecoder:
-    """A pool of ``engines`` side contexts (created on demand up to the cap); ``submit``
-    blocks only when every context still has a job in flight (backpressure)."""
+    """Pending pool + ``engines`` side contexts (created on demand).  ``add`` queues a
+    batch's images and launches the pool once it holds ``min_images``; ``flush`` launches
+    it now (a batch holding pending images is about to launch).  A launch waits only when
+    every context still has a mini-batch in flight (backpressure)."""
 
-    def __init__(self, device: torch.device, max_images: int = 64, engines: int = 48, max_image_dim: int = 0):
+    def __init__(self, device: torch.device, max_images: int = 512, min_images: int | None = None,
+                 engines: int | None = None, max_image_dim: int = 0):
+        import os
+        # measured (scripts/route_study.py, 16 progressive per 256-image batch): pools of 16 images on
+        # 2 contexts 25.7k img/s; 1 image on 8: 18.8k; >= 32 images per launch: 2.4k (a long k_prog
+        # launch holds the hardware queue it shares with a slot's stream)
+        min_images = int(os.environ.get("DINO_SIDE_MIN", 16)) if min_images is None else min_images
+        engines = int(os.environ.get("DINO_SIDE_ENGINES", 2)) if engines is None else engines
         self.device = device
         self.max_images = int(max_images)
+        self.min_images = max(1, min(int(min_images), self.max_images))
         self.cap = max(1, int(engines))
         self.max_image_dim = int(max_image_dim)
         self._engines: list[_SideEngine] = []
         self._rr = 0
-        self.jobs = 0
+        self._pool: list = []   # (job, batch index, JPEG bytes)
+        self.launches = 0
         self.images = 0
+
+    def add(self, imgs: dict) -> SideJob | None:
+        if not imgs:
+            return None
+        job = SideJob()
+        for i in sorted(imgs):
+            self._pool.append((job, int(i), imgs[i]))
+        if len(self._pool) >= self.min_images:
+            self.flush()
+        return job
 
     def _engine(self) -> _SideEngine:
         for e in self._engines:
@@ -91,20 +116,19 @@ class DeviceSideDecoder:
         e.last.synchronize()
         return e
 
-    def submit(self, jpegs: dict) -> SideJob | None:
-        """Decode ``{batch index: JPEG bytes}`` (at most ``max_images``) on a side context;
-        images the decoder fails on are left out (their batch decodes them itself and
-        reaches the same failure)."""
-        idx = sorted(jpegs)[: self.max_images]
-        if not idx:
-            return None
+    def flush(self) -> None:
+        """Decode the pending pool now (in mini-batches of at most ``max_images``)."""
+        while self._pool:
+            part, self._pool = self._pool[: self.max_images], self._pool[self.max_images:]
+            self._launch(part)
+
+    def _launch(self, part: list) -> None:
         se = self._engine()
-        items = [jpegs[i] for i in idx]
+        eng = se.eng
+        items = [j for _, _, j in part]
         hb, off = pack_jpegs(items, pin=True)
         info, ws, _ = fallback.probe(hb.data_ptr(), off.numpy(), len(items), self.max_image_dim)
-        eng = se.eng
         eng.reserve(ws, 0)
-        conts = {}
         heads = []
         with eng.on_stream():
             d_bytes = hb.to(self.device, non_blocking=True)
@@ -112,7 +136,8 @@ class DeviceSideDecoder:
             d_info = eng.decode(d_bytes, d_off, len(items))
             status = torch.empty((len(items), 4), dtype=torch.int32, pin_memory=True)
             status.copy_(d_info, non_blocking=True)
-            for k, i in enumerate(idx):
+            for k, (job, i, _) in enumerate(part):
+                job.rows[i] = k
                 st, w, h = int(info[k, 0]), int(info[k, 1]), int(info[k, 2])
                 if st != 0 or int(info[k, 3]) == 2:
                     continue
@@ -121,28 +146,25 @@ class DeviceSideDecoder:
                                        dtype=torch.uint8).pin_memory()
                 heads.append(hdr)
                 c[:16].copy_(hdr, non_blocking=True)
-                _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, _rgb_ptr(c), eng._s()), "dino_copy_rgb")
-                conts[i] = c
+                _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(c.data_ptr() + 16), eng._s()),
+                           "dino_copy_rgb")
+                job.containers[i] = c
             ev = torch.cuda.Event()
             ev.record(se.stream)
-        # decode failures found on the device (the probe passed): that image stays in its batch
+        for job, _, _ in part:
+            job.event, job.status, job.pending = ev, status, False
         se.last = ev
         se.keep = (hb, off, d_bytes, d_off, heads)
-        self.jobs += 1
-        self.images += len(conts)
-        return SideJob(conts, ev, se, status, idx) if conts else None
+        self.launches += 1
+        self.images += len(part)
 
     def close(self) -> None:
+        self._pool.clear()
         for e in self._engines:
             if e.last is not None:
                 e.last.synchronize()
             e.eng.close()
         self._engines.clear()
-
-
-def _rgb_ptr(c: torch.Tensor):
-    import ctypes
-    return ctypes.c_void_p(c.data_ptr() + 16)
 
 
 def side_mask(info: np.ndarray) -> np.ndarray:
