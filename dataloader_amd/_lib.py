@@ -75,6 +75,8 @@ def load() -> ctypes.CDLL:
         "dino_host_register": (i32, [vp, i64]),
         "dino_host_unregister": (i32, [vp]),
         "dino_copy_h2d": (i32, [vp, vp, i64, vp]),
+        "dino_stream_create": (i32, [i32, i32, ctypes.POINTER(vp)]),
+        "dino_stream_destroy": (i32, [vp]),
         "dino_copy_rgb": (i32, [vp, i32, vp, vp]),
         "dino_sample_params": (i32, [vp, ctypes.POINTER(DinoAugConfig), u64, u64, vp, vp]),
         "dino_augment": (i32, [vp, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(vp), vp]),
@@ -122,4 +124,4 @@ def exported_symbols() -> list[str]:
             "dino_host_register", "dino_host_unregister", "dino_copy_h2d", "dino_gather_probe",
             "dino_feed_create", "dino_feed_destroy", "dino_feed_push", "dino_feed_end_epoch", "dino_feed_set_cfg",
             "dino_feed_next", "dino_feed_copy", "dino_feed_release", "dino_feed_reset", "dino_feed_stats",
-            "dino_feed_last_error"]
+            "dino_feed_last_error", "dino_stream_create", "dino_stream_destroy"]

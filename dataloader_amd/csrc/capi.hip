@@ -15,6 +15,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_ext.h>
+
 #include "hostcopy.hpp"
 #include "jpeg_parse.hpp"
 #include "kernels.hpp"
@@ -54,6 +56,7 @@ struct dino_ctx {
   ViewPlan* d_plan = nullptr;
   dino_view_params* d_params = nullptr;
   uint8_t* d_gcrop = nullptr;
+  PCtl* d_pctl = nullptr;         // the batch's coefficient-buffer registry (k_plan / k_pwalk / k_pscan)
   const float* d_norm = nullptr;  // per-image normalisation (dino_set_norm), nullable
   int32_t norm_n = 0;
   int32_t last_batch = -1;
@@ -101,7 +104,8 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
       (e = hipMallocAsync((void**)&c->d_aws, c->aws_size, nullptr)) != hipSuccess ||
       (e = hipStreamSynchronize(nullptr)) != hipSuccess ||
       (e = hipMalloc(&c->d_plan, sizeof(ViewPlan) * nrec)) != hipSuccess ||
-      (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess) {
+      (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess ||
+      (e = hipMalloc((void**)&c->d_pctl, pctl_bytes(L.max_batch))) != hipSuccess) {
     dino_ctx_destroy(c);
     return hip_fail(e, "dino_ctx_create: hipMalloc");
   }
@@ -126,6 +130,7 @@ int dino_ctx_destroy(dino_ctx* c) {
   (void)hipFree(c->d_plan);
   (void)hipFree(c->d_params);
   (void)hipFree(c->d_gcrop);
+  (void)hipFree(c->d_pctl);
   if (c->timer) {
     c->timer->destroy();
     delete c->timer;
@@ -141,7 +146,7 @@ int dino_decode_spans(dino_ctx* c, const uint8_t* d_bytes, const int64_t* d_offs
     return fail(DINO_EINVAL, "dino_decode: batch %s%lld exceeds ctx max_batch", "", batch);
   hipStream_t s = (hipStream_t)stream;
   DecodeArgs a{d_bytes, d_offsets, d_lengths, d_raw_mask, batch, c->lim.max_image_dim, c->d_desc, c->d_ws,
-               c->ws_size, c->geom};
+               c->ws_size, c->geom, c->d_pctl};
   hipError_t e = launch_decode(a, s, c->tm());
   if (e != hipSuccess) return hip_fail(e, "dino_decode");
   if (d_info && (e = launch_info(c->d_desc, batch, d_info, s)) != hipSuccess) return hip_fail(e, "dino_decode(info)");
@@ -414,6 +419,33 @@ int dino_gather_probe(const uint64_t* src_ptrs, const int64_t* lens, int32_t n, 
   *ws_need = w;
   *aws_need = a;
   return DINO_OK;
+}
+
+int dino_stream_create(int device, int32_t cu_count, void** stream) {
+  if (!stream) return fail(DINO_EINVAL, "dino_stream_create: null argument%s%lld");
+  *stream = nullptr;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  int n = 0;
+  if ((e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
+    return hip_fail(e, "dino_stream_create");
+  const int k = cu_count <= 0 || cu_count >= n ? n : cu_count;
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int i = 0; i < k; ++i) {
+    const int cu = (int)((int64_t)i * n / k);
+    mask[cu >> 5] |= 1u << (cu & 31);
+  }
+  hipStream_t s = nullptr;
+  if ((e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data())) != hipSuccess)
+    return hip_fail(e, "hipExtStreamCreateWithCUMask");
+  *stream = (void*)s;
+  return DINO_OK;
+}
+
+int dino_stream_destroy(void* stream) {
+  if (!stream) return DINO_OK;
+  hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "hipStreamDestroy");
 }
 
 int dino_host_register(void* host, int64_t nbytes) {

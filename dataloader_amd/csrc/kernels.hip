@@ -25,6 +25,7 @@
 #include "mask.hpp"
 #include "plan.hpp"
 #include "progressive.hpp"
+#include "pscan.hpp"
 #include "sampler.hpp"
 
 #include <stdio.h>
@@ -147,10 +148,16 @@ __device__ void plan_place(ImgDesc& d, const ChunkSizes& z, int64_t base, int64_
 // that an image that does not fit leaves its bytes to the later ones: only images
 // that cannot be placed get DINO_IMG_NO_SPACE (the host probe, dino_probe, sizes
 // the workspace so that this does not happen on the product path).
-__global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size) {
+__global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B, int64_t ws_size,
+                                              PCtl* __restrict__ pctl) {
   __shared__ int64_t part[1024];
   __shared__ int32_t dpart[1024];
   const int t = threadIdx.x;
+  if (t == 0) {  // the batch's coefficient-buffer registry (k_pwalk, k_pscan)
+    pctl->ticket = 0;
+    pctl->nprog = 0;
+    pctl->max_scans = 0;
+  }
   const int per = (B + 1023) / 1024;
   int64_t local = 0;
   int32_t dlocal = 0;
@@ -1019,19 +1026,22 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
 }
 
 // ---------------------------------------------------------------------------
-// k_prog: progressive and multi-scan images (kind 1), one wave per image
-// (progressive.hpp).  The wave walks the marker segments together, zeroes the
-// dense coefficient buffer, then decodes scan i on lane i, one dependency level at
-// a time; the Huffman tables of a level's scans are built into an LDS pool (in
-// chunks when a level needs more tables than the pool holds).
+// Coefficient-buffer images (kind 1: progressive, multi-scan sequential, restart
+// images with missing / out-of-sequence markers), pscan.hpp:
+//   k_pwalk  one workgroup per image: the marker walk (wave 0), the scan list in
+//            dependency-level order, every decoder table the scans use (global
+//            PTab, read through the scalar cache), the zeroed coefficient buffer,
+//            and the image's registration in the batch's PCtl
+//   k_pscan  persistent waves taking scan tickets; one wave decodes one scan, its
+//            serial part wave-uniform (scalar ALU + scalar cache), its coefficient
+//            stores lane-parallel; a scan waits for the previous level's scans of
+//            its image (only ever scans with earlier tickets: no deadlock)
 // ---------------------------------------------------------------------------
-constexpr int kProgThreads = 64;
-constexpr int kProgPool = 16;
 #ifdef DINO_PROG_PHASES
-// per image (first kProgPhaseImgs of the batch) and scan: start, end (wall_clock64) and
-// the scan's level / band / approximation (instrumented builds only)
+// per image (first kProgPhaseImgs of the batch) and scan (level order): start, end
+// (wall_clock64) and the scan's level / band / approximation (instrumented builds only)
 constexpr int kProgPhaseImgs = 64;
-__device__ uint64_t g_prog_phase[kProgPhaseImgs][kProgThreads][3];
+__device__ uint64_t g_prog_phase[kProgPhaseImgs][64][3];
 hipError_t copy_prog_phases(uint64_t* host) {
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return e;
@@ -1065,126 +1075,552 @@ struct WaveMarkerFinder {
   }
 };
 
-struct ProgLds {
+constexpr int kPWalkThreads = 256;
+struct PWalkLds {
   ImgDesc d;
   ScanRec scans[kMaxScans];
-  ProgTable pool[kProgPool];
-  uint8_t nat[80];                     // jpeg_natural_order (+ safety entries), read per coefficient
-  __attribute__((aligned(16))) uint8_t ring[kProgThreads][64];  // each lane's staged raw bytes (RawBits)
-  __attribute__((aligned(16))) int16_t blk[kProgThreads][64];    // each lane's AC-refinement block
-  int32_t slot_off[kProgPool];         // BITS offset of the table in each pool slot
-  int32_t slot_dc[kProgPool];
-  int8_t tslot[kMaxScans][8];          // pool slot of each scan table (dc 0..3, ac 4..7), -1 none
-  int32_t ready[kMaxScans];
-  int32_t nslots, next, bad;
+  uint64_t ts[kMaxScans];
+  int32_t slot_off[kPMaxTabs];
+  uint8_t slot_dc[kPMaxTabs];
+  ProgTable tab[kPMaxTabs];
+  int32_t ntab, bad;
 };
 
-__global__ void __launch_bounds__(kProgThreads) k_prog(const uint8_t* __restrict__ bytes,
-                                                       const int64_t* __restrict__ offsets,
-                                                       const int64_t* __restrict__ lengths,
-                                                       ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  __shared__ ProgLds L;
+__global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restrict__ bytes,
+                                                         const int64_t* __restrict__ offsets,
+                                                         const int64_t* __restrict__ lengths,
+                                                         ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
+                                                         PCtl* __restrict__ pctl) {
+  __shared__ PWalkLds L;
   const int img = blockIdx.x, t = threadIdx.x;
   if (desc[img].status != DINO_IMG_OK || desc[img].kind != 1) return;
-  if (t == 0) L.d = desc[img];
-  __syncthreads();
   const uint8_t* p = bytes + offsets[img];
   const int64_t len = lengths ? lengths[img] : offsets[img + 1] - offsets[img];
-  WaveMarkerFinder find;
-  // every lane runs the walk on the LDS descriptor (identical values, identical writes)
-  prog_walk(p, len, &L.d, L.scans, find);
+  if (t == 0) L.d = desc[img];
+  __syncthreads();
+  if (t < 64) {  // wave 0: every lane runs the walk on the LDS descriptor (identical values, identical writes)
+    WaveMarkerFinder find;
+    prog_walk(p, len, &L.d, L.scans, find);
+  }
   __syncthreads();
   const ImgDesc& dl = L.d;
-  if (dl.status != DINO_IMG_OK) {
-    if (t == 0) desc[img].status = dl.status;
+  uint8_t* region = ws + dl.htab_off;
+  if (t == 0 && dl.status == DINO_IMG_OK) {
+    // the region k_plan placed (kind 1: kPRegionBytes; a restart image switched by k_htab: its table area)
+    L.ntab = prog_table_slots(L.scans, dl.n_scans, L.slot_off, L.slot_dc, L.ts,
+                              ptab_capacity(dl.hlane_off - dl.htab_off));
+    L.bad = 0;
+  }
+  __syncthreads();
+  if (dl.status != DINO_IMG_OK || L.ntab < 0) {
+    if (t == 0) desc[img].status = dl.status != DINO_IMG_OK ? dl.status : DINO_IMG_UNSUPPORTED;
     return;
   }
-  const int n = dl.n_scans;
-  // zero the dense coefficient buffer (libjpeg's pre-zeroed coefficient arrays)
+  const int n = dl.n_scans, ntab = L.ntab;
+  if (t < ntab && !huff_build_derived(p + L.slot_off[t], L.slot_dc[t] != 0, &L.tab[t])) atomicOr(&L.bad, 1);
+  __syncthreads();
+  if (L.bad) {  // JERR_BAD_HUFF_TABLE (libjpeg raises when the scan using it starts: the image fails either way)
+    if (t == 0) desc[img].status = DINO_IMG_CORRUPT;
+    return;
+  }
+  PTab* tabs = (PTab*)(region + kPTabOff);
+  for (int e = t; e < ntab << kPLookBits; e += kPWalkThreads)
+    tabs[e >> kPLookBits].look[e & ((1 << kPLookBits) - 1)] = ptab_look_entry(&L.tab[e >> kPLookBits], e & ((1 << kPLookBits) - 1));
+  if (t < ntab) ptab_fill_derived(&L.tab[t], &tabs[t]);
+  PHdr* hd = (PHdr*)region;
+  PScan* ps = (PScan*)(region + kPScanOff);
+  if (t < n) {
+    PScan o;
+    o.sr = L.scans[t];
+    o.tslots = L.ts[t];
+    ps[prog_level_rank(L.scans, n, t)] = o;
+  }
+  int nlev = 0;
+  for (int i = 0; i < n; ++i) nlev = L.scans[i].level + 1 > nlev ? L.scans[i].level + 1 : nlev;
+  if (t < kMaxScans) {
+    int c = 0;
+    for (int i = 0; i < n; ++i) c += L.scans[i].level == t;
+    hd->cnt[t] = c;
+    hd->done[t] = 0;
+  }
+  if (t == 0) {
+    hd->n_scans = n;
+    hd->n_levels = nlev;
+  }
+  // libjpeg's zeroed coefficient arrays
   {
     uint4* c4 = (uint4*)(ws + dl.coef_off);
     const int64_t nq = dl.coef_bytes >> 4;
-    for (int64_t q = t; q < nq; q += kProgThreads) c4[q] = make_uint4(0u, 0u, 0u, 0u);
-  }
-  int maxlv = 0;
-  for (int i = 0; i < n; ++i) maxlv = L.scans[i].level > maxlv ? L.scans[i].level : maxlv;
-  if (t == 0) L.bad = 0;
-  if (t < kMaxScans) L.ready[t] = 0;
-  for (int k = t; k < 80; k += kProgThreads) L.nat[k] = kNaturalOrder[k];
-  __syncthreads();
-  int16_t* coef = (int16_t*)(ws + dl.coef_off);
-  for (int lv = 0; lv <= maxlv; ++lv) {
-    int first = 0;
-    for (;;) {
-      if (t == 0) {  // assign pool slots to the next scans of this level that fit
-        int used = 0, i = first;
-        for (; i < n; ++i) {
-          const ScanRec& sr = L.scans[i];
-          if (sr.level != lv) continue;
-          int need = 0;
-          for (int k = 0; k < 4; ++k) need += (sr.dc_tab[k] >= 0) + (sr.ac_tab[k] >= 0);
-          if (used + need > kProgPool) break;
-          for (int k = 0; k < 4; ++k) {
-            L.tslot[i][k] = -1;
-            L.tslot[i][4 + k] = -1;
-            if (sr.dc_tab[k] >= 0) {
-              L.slot_off[used] = sr.dc_tab[k];
-              L.slot_dc[used] = 1;
-              L.tslot[i][k] = (int8_t)used++;
-            }
-            if (sr.ac_tab[k] >= 0) {
-              L.slot_off[used] = sr.ac_tab[k];
-              L.slot_dc[used] = 0;
-              L.tslot[i][4 + k] = (int8_t)used++;
-            }
-          }
-          L.ready[i] = 1;
-        }
-        L.nslots = used;
-        L.next = i;
-      }
-      __syncthreads();
-      const int nslots = L.nslots;
-      if (t < nslots && !huff_build_derived(p + L.slot_off[t], L.slot_dc[t] != 0, &L.pool[t])) atomicOr(&L.bad, 1);
-      __syncthreads();
-      if (L.bad) break;
-      for (int e = t; e < nslots * (1 << kProgLookBits); e += kProgThreads) {
-        const int sl = e >> kProgLookBits, ix = e & ((1 << kProgLookBits) - 1);
-        L.pool[sl].look[ix] = huff_look_entry(&L.pool[sl], ix);
-      }
-      __syncthreads();
-      if (t < n && L.ready[t]) {
-        const ScanRec sr = L.scans[t];
-        ScanTables tb;
-        LdsTable pool = (LdsTable)&L.pool[0];
-        for (int k = 0; k < 4; ++k) {
-          tb.dc[k] = pool + (L.tslot[t][k] >= 0 ? L.tslot[t][k] : 0);
-          tb.ac[k] = pool + (L.tslot[t][4 + k] >= 0 ? L.tslot[t][4 + k] : 0);
-        }
-#ifdef DINO_PROG_PHASES
-        const uint64_t t0 = wall_clock64();
-#endif
-        prog_decode_scan(p, len, dl, sr, tb, coef, (const DINO_LDS uint8_t*)L.nat, (DINO_LDS uint8_t*)L.ring[t],
-                         bytes + offsets[gridDim.x], (DINO_LDS int16_t*)L.blk[t]);
-#ifdef DINO_PROG_PHASES
-        if (img < kProgPhaseImgs) {
-          g_prog_phase[img][t][0] = t0;
-          g_prog_phase[img][t][1] = wall_clock64();
-          g_prog_phase[img][t][2] = (uint64_t)sr.level | ((uint64_t)sr.ss << 8) | ((uint64_t)sr.se << 16) |
-                                    ((uint64_t)sr.ah << 24) | ((uint64_t)sr.al << 28) | ((uint64_t)sr.ns << 32);
-        }
-#endif
-        L.ready[t] = 0;
-      }
-      __syncthreads();  // (workgroup scope: this level's coefficient stores are visible to the next)
-      first = L.next;
-      if (first >= n) break;
-    }
-    if (L.bad) break;
+    for (int64_t q = t; q < nq; q += kPWalkThreads) c4[q] = make_uint4(0u, 0u, 0u, 0u);
   }
   if (t == 0) {
     desc[img].n_scans = n;
-    if (L.bad) desc[img].status = DINO_IMG_CORRUPT;  // JERR_BAD_HUFF_TABLE
+    const uint32_t k = atomicAdd(&pctl->nprog, 1u);
+    pctl->pimg[k] = img;
+    atomicMax(&pctl->max_scans, (uint32_t)n);
+  }
+}
+
+// Lane-conditional stores of the scan waves go to this dummy slot instead of branching
+// around the store: a divergent branch inside the decode loops makes the compiler's
+// uniformity analysis treat the loops' scalar state (bit position, EOB run, masks) as
+// divergent at the join, which moves the whole serial decode from SGPRs to VGPRs
+// (measured: 250 instructions per symbol instead of ~50).
+__device__ uint32_t g_pscan_dummy[64 * 4];
+__device__ __forceinline__ int16_t* pick16(bool c, int16_t* p, int lane) {
+  return c ? p : (int16_t*)&g_pscan_dummy[lane];
+}
+
+// The lanes' half of a scan (see pscan.hpp): pending (element, value) stores in lane
+// registers, and for AC refinement the 16-block groups of coefficients (lane k holds
+// zigzag coefficient k of each block of the group).
+struct WaveCoefSink {
+  int16_t* coef;
+  DINO_LDS int16_t* stage;  // [16][64]: the staged group's coefficients
+  int lane, natk;
+  int32_t n;                // pending entries (uniform)
+  int32_t eidx, eval;       // lane n's entry: element, value (| 1 << 16: OR into the coefficient)
+  // AC refinement
+  int64_t plane;
+  int32_t bw, mcx, nblk;
+  int32_t grp, nxgrp, g;
+  int32_t cbx, cby;         // block (x, y) of the next rnz
+  int64_t cur;              // element of the current block
+  uint32_t mlo, mhi;        // lane j: zigzag non-zero mask of block j of the staged group
+  int32_t nx[16];           // the next group's coefficients (prefetched)
+
+  __device__ __forceinline__ void flush() {  // (branch-free: see g_pscan_dummy)
+    const bool act = lane < n, isor = (eval & 0x10000) != 0;
+    uint32_t* w = (act & isor) ? (uint32_t*)(coef + (eidx & ~1)) : &g_pscan_dummy[64 + lane];
+    __hip_atomic_fetch_or(w, isor ? (uint32_t)(eval & 0xFFFF) << (16 * (eidx & 1)) : 0u, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    *pick16(act & !isor, coef + eidx, lane) = (int16_t)eval;
+    n = 0;
+  }
+  __device__ __forceinline__ void put(int64_t e, int32_t v) {
+    eidx = lane == n ? (int32_t)e : eidx;
+    eval = lane == n ? v : eval;
+    if (++n == 64) flush();
+  }
+  __device__ __forceinline__ void set(int64_t e, int32_t v) { put(e, v & 0xFFFF); }
+  __device__ __forceinline__ void orw(int64_t e, int32_t v) { put(e, (v & 0xFFFF) | 0x10000); }
+
+  __device__ __forceinline__ void load_group(int32_t G) {
+    const int32_t m0 = G * 16;
+    int32_t by = m0 / mcx, bx = m0 - by * mcx;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int64_t e = plane + ((int64_t)by * bw + bx) * 64;
+      nx[j] = m0 + j < nblk ? (int32_t)coef[e + natk] : 0;
+      if (++bx == mcx) {
+        bx = 0;
+        ++by;
+      }
+    }
+    nxgrp = G;
+  }
+  __device__ __forceinline__ void rbegin(int64_t pl, int32_t w, int32_t mcus_x, int32_t mcus_y) {
+    plane = pl;
+    bw = w;
+    mcx = mcus_x;
+    nblk = mcus_x * mcus_y;
+    grp = -1;
+    cbx = cby = 0;
+    load_group(0);
+  }
+  // rnz is called for m = 0, 1, 2, ... in order
+  __device__ __forceinline__ uint64_t rnz(int64_t m) {
+    const int32_t G = (int32_t)(m >> 4);
+    if (G != grp) {
+      if (nxgrp != G) load_group(G);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        stage[j * 64 + lane] = (int16_t)nx[j];
+        const uint64_t b = __ballot(nx[j] != 0);
+        mlo = lane == j ? (uint32_t)b : mlo;
+        mhi = lane == j ? (uint32_t)(b >> 32) : mhi;
+      }
+      grp = G;
+      if ((G + 1) * 16 < nblk) load_group(G + 1);  // prefetched while this group decodes
+    }
+    g = (int32_t)(m & 15);
+    cur = plane + ((int64_t)cby * bw + cbx) * 64;
+    if (++cbx == mcx) {
+      cbx = 0;
+      ++cby;
+    }
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)mhi, g) << 32 |
+           (uint32_t)__builtin_amdgcn_readlane((int32_t)mlo, g);
+  }
+  __device__ __forceinline__ void rapply(uint64_t corr, uint64_t nzn, uint64_t neg, int al) {
+    const bool c = (corr >> lane) & 1u, nw = (nzn >> lane) & 1u;
+    const int16_t v = stage[g * 64 + lane];
+    const int16_t x = ac_refine_value(v, c, nw, (neg >> lane) & 1u, al);
+    *pick16(x != v, coef + cur + natk, lane) = x;  // (branch-free: see g_pscan_dummy)
+  }
+};
+
+// The scan's decoder tables in VGPRs: 8 table positions (DC of scan component k < 4,
+// AC k - 4) x 512 lookahead entries of 16 bits; entry i of position k is half (i & 1) of
+// lane ((k * 512 + i) >> 1) & 63 of register (k * 512 + i) >> 7.  A lookup is one
+// indexed register move + one readlane: no memory access on the decode chain.  Codes
+// longer than the lookahead search the PTab (scalar cache).  Lane k also holds
+// jpeg_natural_order[k].
+typedef uint32_t u32x32 __attribute__((ext_vector_type(32)));
+struct VTab {
+  u32x32 v;
+  const DINO_CONST PTab* tabs;
+  uint64_t ts;
+  uint32_t natv;
+  __device__ __forceinline__ void load(const PTab* tb, uint64_t slots, int lane) {
+    tabs = (const DINO_CONST PTab*)tb;
+    ts = slots;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int s = pbyte64(slots, k);
+      const uint32_t* src = (const uint32_t*)tb[s < 0xFF ? s : 0].look;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * k + j] = s < 0xFF ? src[64 * j + lane] : 0u;
+    }
+    natv = kNaturalOrder[lane];
+  }
+  __device__ __forceinline__ void lookup(int k, uint32_t p, int* sym, int* len) const {
+    // (uniform, but the compiler may compute it on the VALU: without the readfirstlane the
+    // indexed move would become a waterfall loop)
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)((uint32_t)k * 512u + (p >> (32 - kPLookBits))));
+    const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int32_t)v[h >> 7], (h >> 1) & 63);
+    const uint32_t e = (h & 1) ? x >> 16 : x & 0xFFFFu;
+    if (e) {
+      *sym = (int)(e >> 4);
+      *len = (int)(e & 15u);
+    } else {
+      ptab_slow(tabs + pbyte64(ts, k), p, sym, len);
+    }
+  }
+  __device__ __forceinline__ int nat(int k) const { return __builtin_amdgcn_readlane((int32_t)natv, k < 64 ? k : 63); }
+};
+
+// The destuffed scan as a bit string, read through two 256-byte windows of lane
+// registers (A: dwords 64 wa .. 64 wa + 63, B: the next 64, loaded when A is entered, so
+// the load has a whole window of decoding to land).  Bytes past the data read as zeros.
+struct CleanReader {
+  const uint32_t* src;  // destuffed bytes (4-byte aligned; the last dword zero padded)
+  uint32_t nw;          // dwords holding data
+  uint32_t pos, nbits;  // bits consumed, data bits
+  int32_t wa;
+  uint32_t A, B;
+  int lane;
+  __device__ __forceinline__ uint32_t loadw(int32_t gi) const {
+    const uint32_t w = (uint32_t)gi * 64u + (uint32_t)lane;
+    const uint32_t x = src[w < nw ? w : 0u];  // (always loaded: no branch, see g_pscan_dummy)
+    return w < nw ? __builtin_bswap32(x) : 0u;
+  }
+  __device__ __forceinline__ void init(const uint32_t* s, uint32_t nbytes, int ln) {
+    src = s;
+    nw = (nbytes + 3) >> 2;
+    nbits = nbytes * 8;
+    pos = 0;
+    lane = ln;
+    wa = 0;
+    A = loadw(0);
+    B = loadw(1);
+  }
+  __device__ __forceinline__ uint32_t peek() const {
+    const uint32_t ps = pos;
+    const int32_t wu = wa;
+    const uint32_t w = ps >> 5, sh = ps & 31;
+    // dwords w and w + 1: both in A, or w in A and w + 1 the first of B (w < 64 (wa + 1))
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)A, w & 63);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)((int32_t)((w + 1) >> 6) == wu ? A : B), (w + 1) & 63);
+    const uint64_t x = (uint64_t)hi << 32 | lo;
+    return (uint32_t)((x << sh) >> 32);
+  }
+  __device__ __forceinline__ void skip(int n) {
+    pos += (uint32_t)n;
+    if ((int32_t)(pos >> 11) > wa) {
+      A = B;
+      ++wa;
+      B = loadw(wa + 1);
+    }
+  }
+  __device__ __forceinline__ bool insuff() const { return pos > nbits; }
+  __device__ __forceinline__ void restart(int*) {}
+};
+
+// Destuff [from, ...) of the image into dst (4-byte aligned) with host_destuff's rule,
+// 256 bytes per step (one aligned dword per lane, neighbours by shuffles); returns the
+// data bytes.  The bytes after them up to the next dword boundary are zeroed.
+__device__ __forceinline__ uint32_t wave_destuff(const uint8_t* img, int64_t len, int64_t from, uint8_t* dst, int lane) {
+  const uintptr_t beg = (uintptr_t)(img + from), end = (uintptr_t)(img + len);
+  uint32_t out = 0, carry = 0;  // carry: the byte before this step's first dword
+  const uint64_t lt = lane ? ~0ull >> (64 - lane) : 0ull;  // lanes below this one
+  for (uintptr_t c = beg & ~(uintptr_t)3; c < end; c += 256) {
+    const uintptr_t wa = c + 4u * (uint32_t)lane;
+    // (loads clamped to the first word instead of branched around: see g_pscan_dummy)
+    const uintptr_t w0 = beg & ~(uintptr_t)3;
+    const uint32_t wl = *(const uint32_t*)(wa < end ? wa : w0);
+    const uint32_t w = wa < end ? wl : 0u;
+    // (every lane runs both shuffles: a lane reading an inactive lane would get nothing)
+    const uint32_t dn = (uint32_t)__shfl_down((int)w, 1);
+    const uint32_t up = (uint32_t)__shfl_up((int)w, 1);
+    const bool nxt = (lane == 63) & (wa + 4 < end);
+    const uint32_t wl4 = *(const uint32_t*)(nxt ? wa + 4 : w0);
+    const uint32_t wn = lane == 63 ? (nxt ? wl4 : 0u) : dn;
+    const uint32_t wp = lane ? up : carry << 24;
+    uint32_t keep = 0, term = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uintptr_t a = wa + i;
+      const uint32_t b = (w >> (8 * i)) & 255u;
+      const uint32_t nx = i < 3 ? (w >> (8 * i + 8)) & 255u : wn & 255u;
+      const uint32_t pv = i > 0 ? (w >> (8 * i - 8)) & 255u : wp >> 24;
+      const bool valid = (a >= beg) & (a < end), nxv = a + 1 < end, pvv = a > beg;
+      // (bitwise, branch-free: see g_pscan_dummy)
+      const bool isff = b == 0xFFu;
+      const bool kff = isff & nxv & (nx == 0u);
+      const bool tff = isff & !kff & (!nxv | (nx != 0xFFu));
+      const bool knon = !isff & !((b == 0u) & pvv & (pv == 0xFFu));
+      keep |= (uint32_t)(valid & (kff | knon)) << i;
+      term |= (uint32_t)(valid & tff) << i;
+    }
+    const uint64_t tl = __ballot(term != 0);
+    if (tl) {
+      const int f = __ffsll((long long)tl) - 1;
+      const int fi = __shfl(term ? __builtin_ctz(term) : 0, f);
+      keep = lane > f ? 0u : (lane == f ? keep & ((1u << fi) - 1u) : keep);
+    }
+    const uint32_t cnt = __builtin_popcount(keep);
+    const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
+    uint32_t o = out + (uint32_t)(__builtin_popcountll(b0 & lt) + 2 * __builtin_popcountll(b1 & lt) +
+                                  4 * __builtin_popcountll(b2 & lt));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // (branch-free: kept bytes to dst, the others to the dummy slot)
+      const bool k = (keep >> i) & 1u;
+      *(k ? dst + o : (uint8_t*)&g_pscan_dummy[128 + lane]) = (uint8_t)(w >> (8 * i));
+      o += k;
+    }
+    out += (uint32_t)(__builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2));
+    if (tl) break;
+    carry = (uint32_t)__builtin_amdgcn_readlane((int32_t)w, 63) >> 24;
+  }
+  *((uint32_t)lane < ((4u - (out & 3u)) & 3u) ? dst + out + lane : (uint8_t*)&g_pscan_dummy[128 + lane]) = 0;
+  __threadfence();  // this wave reads the bytes back (CleanReader)
+  return out;
+}
+
+// Specialised loops for the AC scans of progressive files (the bulk of their symbols:
+// ~85 % of a libjpeg-default progressive 640x480 file, profiles/r03_prog_phases_*):
+// one component, the AC table at table position 4, the destuffed reader, no restart
+// intervals.  A wave issues at most one instruction per cycle and a dependent chain
+// far fewer, so these loops keep the per-symbol path short: the bit-mask searches of
+// the refinement (the run's stop position, the correction bits) are one lane-parallel
+// rank (v_mbcnt) + ballot each instead of a loop over bits, and the AC-first values
+// collect in lane k = zigzag k of the block (one masked store per block).
+__device__ __forceinline__ uint32_t lane_rank(uint64_t mask) {  // set bits of mask below this lane
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+__device__ __forceinline__ uint64_t ubal(bool b) { return __ballot(b); }
+
+// Correction bits (one per set bit of c, increasing k, MSB first), read as a bit mask.
+__device__ __forceinline__ uint64_t fast_corrections(CleanReader& r, uint64_t c, int lane) {
+  int n = __builtin_popcountll(c);
+  if (!n) return 0;
+  const uint32_t rank = lane_rank(c);
+  const bool in = (c >> lane) & 1u;
+  uint64_t corr = 0;
+  int base = 0;
+  while (n > 0) {
+    const int take = n > 32 ? 32 : n;
+    const uint32_t bits = r.peek();
+    const int32_t q = (int32_t)rank - base;
+    // (bitwise &: a short-circuit && on lane values is a divergent branch, see g_pscan_dummy)
+    corr |= ubal(in & (q >= 0) & (q < take) & (((bits >> ((31 - q) & 31)) & 1u) != 0u));
+    r.skip(take);
+    base += take;
+    n -= take;
+  }
+  return corr;
+}
+
+// decode_mcu_AC_refine over the whole scan (see r_refine_block for the bookkeeping).
+__device__ __forceinline__ void fast_ac_refine(CleanReader& r, const VTab& t, const ScanRec& sr, int64_t plane, int32_t bw,
+                               int32_t mcx, int32_t mcy, WaveCoefSink& sink, int lane) {
+  const int ss = sr.ss, se = sr.se, al = sr.al;
+  const uint64_t band = (uint64_t)low_bits(se + 1) & ~(uint64_t)low_bits(ss);
+  int32_t eobrun = 0;
+  sink.rbegin(plane, bw, mcx, mcy);
+  const int32_t nblk = mcx * mcy;
+  for (int32_t m = 0; m < nblk; ++m) {
+    const uint64_t nzz = sink.rnz(m) & band;
+    if (r.insuff()) continue;
+    uint64_t corr = 0, nzn = 0, neg = 0;
+    int k = ss;
+    if (eobrun == 0) {
+      while (k <= se) {
+        const uint32_t p = r.peek();
+        int sym, len;
+        t.lookup(4, p, &sym, &len);
+        const int rr = sym >> 4, s = sym & 15;
+        bool negative = false;
+        if (s) {
+          negative = ((p << len) >> 31) == 0u;
+          r.skip(len + 1);
+        } else if (rr != 15) {
+          eobrun = (1 << rr) + (int32_t)peek_extra(p, len, rr);
+          r.skip(len + rr);
+          break;
+        } else {
+          r.skip(len);
+        }
+        // stop: the (rr+1)-th position at or after k that was zero before the scan
+        const uint64_t z = ~nzz & band & ~(uint64_t)low_bits(k);
+        const uint64_t hit = ubal((((z >> lane) & 1u) != 0u) & (lane_rank(z) == (uint32_t)rr));
+        const int stop = hit ? __builtin_ctzll(hit) : se + 1;
+        corr |= fast_corrections(r, nzz & (uint64_t)low_bits(stop) & ~(uint64_t)low_bits(k), lane);
+        k = stop;
+        if (s) {
+          const uint64_t bit = k < 64 ? 1ull << k : 1ull << 63;
+          nzn |= bit;
+          if (negative) neg |= bit;
+          else neg &= ~bit;
+        }
+        ++k;
+      }
+    }
+    if (eobrun > 0) {
+      if (k <= se) corr |= fast_corrections(r, nzz & ~(uint64_t)low_bits(k), lane);
+      --eobrun;
+    }
+    sink.rapply(corr, nzn, neg, al);
+  }
+}
+
+// decode_mcu_AC_first over the whole scan: values gather in lane k (zigzag k) of the
+// block and leave with one masked store.
+__device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, const ScanRec& sr, int16_t* coef, int64_t plane,
+                              int32_t bw, int32_t mcx, int32_t mcy, int lane, int natk) {
+  const int ss = sr.ss, se = sr.se, al = sr.al;
+  int32_t eobrun = 0;
+  int32_t bx = 0;
+  int64_t rowe = plane;  // element of block (0, by)
+  for (int32_t by = 0; by < mcy; ++by, rowe += (int64_t)bw * 64) {
+    for (bx = 0; bx < mcx; ++bx) {
+      if (eobrun > 0) {
+        --eobrun;
+        continue;
+      }
+      if (r.insuff()) continue;
+      int32_t val = 0;
+      uint64_t have = 0;
+      for (int k = ss; k <= se; k++) {
+        const uint32_t p = r.peek();
+        int sym, len;
+        t.lookup(4, p, &sym, &len);
+        const int rr = sym >> 4, s = sym & 15;
+        if (s) {
+          k += rr;
+          const int v = huff_extend((int)peek_extra(p, len, s), s);
+          r.skip(len + s);
+          const int kk = k < 64 ? k : 63;  // (libjpeg's safety entries map k > 63 to 63)
+          val = lane == kk ? (int32_t)((uint32_t)v << al) : val;
+          have |= 1ull << kk;
+        } else if (rr == 15) {
+          r.skip(len);
+          k += 15;
+        } else {
+          eobrun = (1 << rr) + (int32_t)peek_extra(p, len, rr) - 1;
+          r.skip(len + rr);
+          break;
+        }
+      }
+      *pick16((have >> lane) & 1u, coef + rowe + (int64_t)bx * 64 + natk, lane) = (int16_t)val;
+    }
+  }
+}
+
+constexpr int kPScanThreads = 64;
+__global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restrict__ bytes,
+                                                         const int64_t* __restrict__ offsets,
+                                                         const int64_t* __restrict__ lengths,
+                                                         const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
+                                                         PCtl* __restrict__ pctl) {
+  __shared__ int16_t s_stage[16 * 64];
+  const int lane = threadIdx.x;
+  const DINO_CONST PCtl* cc = (const DINO_CONST PCtl*)pctl;
+  const uint32_t nprog = cc->nprog;
+  const uint32_t total = nprog * cc->max_scans;
+  const DINO_CONST int64_t* offs = (const DINO_CONST int64_t*)offsets;
+  const DINO_CONST int64_t* lens = (const DINO_CONST int64_t*)lengths;
+  for (;;) {
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(&pctl->ticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)__shfl(tk, 0));
+    if (tk >= total) break;
+    const uint32_t j = tk / nprog;
+    const int img = cc->pimg[tk - j * nprog];
+    const DINO_CONST ImgDesc* d = (const DINO_CONST ImgDesc*)(desc + img);
+    uint8_t* region = ws + d->htab_off;
+    const DINO_CONST PHdr* hd = (const DINO_CONST PHdr*)region;
+    if ((int)j >= hd->n_scans) continue;
+    const DINO_CONST PScan* ps = (const DINO_CONST PScan*)(region + kPScanOff) + j;
+    const ScanRec sr = ps->sr;
+    const int64_t off = offs[img];
+    const int64_t len = lengths ? lens[img] : offs[img + 1] - off;
+    const uint8_t* p = bytes + off;
+    // the scan's bytes destuffed and its tables in registers before waiting for its level
+    VTab tb;
+    tb.load((const PTab*)(region + kPTabOff), ps->tslots, lane);
+    uint32_t* clean = (uint32_t*)(ws + d->ent_off + ((sr.data_off - d->scan_off + 3) & ~3));
+    const uint32_t dlen = sr.restart_interval == 0 ? wave_destuff(p, len, sr.data_off, (uint8_t*)clean, lane) : 0u;
+    if (sr.level > 0) {  // the previous level's scans of this image (earlier tickets, running or done)
+      int32_t* dn = &((PHdr*)region)->done[sr.level - 1];
+      const int32_t need = hd->cnt[sr.level - 1];
+      for (;;) {
+        const int32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(dn, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT));
+        if (v >= need) break;
+        __builtin_amdgcn_s_sleep(4);
+      }
+    }
+#ifdef DINO_PROG_PHASES
+    const uint64_t t0 = wall_clock64();
+#endif
+    WaveCoefSink sink;
+    sink.coef = (int16_t*)(ws + d->coef_off);
+    sink.stage = (DINO_LDS int16_t*)s_stage;
+    sink.lane = lane;
+    sink.natk = kNaturalOrder[lane];
+    sink.n = 0;
+    sink.eidx = sink.eval = 0;
+    sink.mlo = sink.mhi = 0;
+    sink.grp = sink.nxgrp = -1;
+    const bool prog = d->progressive != 0;
+    if (sr.restart_interval == 0) {
+      CleanReader r;
+      r.init(clean, dlen, lane);
+      if (prog && sr.ss > 0) {  // AC scans: one component (start_pass_phuff_decoder)
+        const int ci = sr.comp[0];
+        const int64_t plane = d->comp[ci].coef_off / 2;
+        const int32_t bw = d->comp[ci].bw, mcx = ceil_div(d->comp[ci].dw, 8), mcy = ceil_div(d->comp[ci].dh, 8);
+        if (sr.ah > 0) fast_ac_refine(r, tb, sr, plane, bw, mcx, mcy, sink, lane);
+        else fast_ac_first(r, tb, sr, sink.coef, plane, bw, mcx, mcy, lane, sink.natk);
+      } else {
+        pscan_decode(r, tb, d, sr, prog, sink);
+      }
+    } else {
+      RawReader r;
+      pb_init(r.b, (uintptr_t)p, len, sr.data_off);
+      pscan_decode(r, tb, d, sr, prog, sink);
+    }
+#ifdef DINO_PROG_PHASES
+    if (img < kProgPhaseImgs && lane == 0) {
+      g_prog_phase[img][j][0] = t0;
+      g_prog_phase[img][j][1] = wall_clock64();
+      g_prog_phase[img][j][2] = (uint64_t)sr.level | ((uint64_t)sr.ss << 8) | ((uint64_t)sr.se << 16) |
+                                ((uint64_t)sr.ah << 24) | ((uint64_t)sr.al << 28) | ((uint64_t)sr.ns << 32);
+    }
+#endif
+    __threadfence();  // this scan's coefficient stores before its completion count
+    if (lane == 0) __hip_atomic_fetch_add(&((PHdr*)region)->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2877,7 +3313,7 @@ static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_d
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
                                                        "k_vert_local", "k_dcscan", "k_htab", "k_hseg", "k_huff2",
-                                                       "k_huff3", "k_prog"};
+                                                       "k_huff3", "k_prog", "k_pwalk"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -2918,6 +3354,7 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
   g->grid_ds = 4 * cus;
   g->grid3 = persistent_grid(reinterpret_cast<const void*>(&k_huff3), kHuff3LdsBytes, cus);
   g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
+  g->grid_ps = 4 * cus;  // scan waves: a batch's level-0 scans all start at once
   return hipSuccess;
 }
 
@@ -2925,12 +3362,14 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   const int B = a.batch;
   if (B <= 0) return hipSuccess;
   TIMED(tm, kKParse, s, (k_parse<<<B, 64, 0, s>>>(a.bytes, a.offsets, a.lengths, a.raw_mask, B, a.max_dim, a.desc)));
-  TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size)));
+  TIMED(tm, kKPlan, s, (k_plan<<<1, 1024, 0, s>>>(a.desc, B, a.ws_size, a.pctl)));
   const int grid_ds = a.geom.grid_ds, grid1 = a.geom.grid1, grid3 = a.geom.grid3;
   TIMED(tm, kKDestuff, s, (k_destuff_count<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
-  TIMED(tm, kKProg, s, (k_prog<<<B, kProgThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws)));  // after k_htab's kind switch
+  // after k_htab's kind switch
+  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
+  TIMED(tm, kKProg, s, (k_pscan<<<a.geom.grid_ps, kPScanThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));

@@ -38,7 +38,7 @@ struct ViewPlan {
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuff1, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
   kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKProg,
-  kKNumKernels
+  kKPwalk, kKNumKernels
 };
 
 struct KernelTimer {
@@ -62,7 +62,17 @@ struct LaunchGeom {
   int32_t grid_ds;   // persistent destuff grid
   int32_t grid1;     // persistent k_huff1 grid (occupancy x CUs)
   int32_t grid3;     // persistent k_huff3 grid
+  int32_t grid_ps;   // persistent k_pscan grid (waves)
 };
+
+// Coefficient-buffer images of a batch (k_plan zeroes, k_pwalk registers, k_pscan
+// takes tickets): ticket t = scan t / nprog of image pimg[t % nprog] (each image's scans
+// in dependency-level order, so a scan only ever waits for scans with earlier tickets).
+struct PCtl {
+  uint32_t ticket, nprog, max_scans, pad;
+  int32_t pimg[1];  // [max_batch]
+};
+DHD int64_t pctl_bytes(int max_batch) { return 16 + 4 * (int64_t)(max_batch > 0 ? max_batch : 1); }
 hipError_t init_launch_geom(int device, LaunchGeom* g);
 
 struct DecodeArgs {
@@ -76,6 +86,7 @@ struct DecodeArgs {
   uint8_t* ws;
   int64_t ws_size;
   LaunchGeom geom;
+  PCtl* pctl;
 };
 
 // Output pointers travel as a kernel argument (no host->device copy whose source

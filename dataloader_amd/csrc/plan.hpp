@@ -5,6 +5,7 @@
 
 #include "kernels.hpp"
 #include "progressive.hpp"
+#include "pscan.hpp"
 #include "resize.hpp"
 
 namespace dino {
@@ -60,7 +61,9 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
   z.plane = align16(p);
   if (d.kind == 1) {
+    z.ent = align16((int64_t)d.scan_len + 64);  // each scan's destuffed bytes (k_pscan)
     z.coef = align16(d.coef_bytes);
+    z.htab = kPRegionBytes;  // scan list + decoder tables (k_pwalk -> k_pscan)
     return z;
   }
   z.ent = align16((int64_t)d.scan_len + 64);
@@ -74,6 +77,10 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   z.dspart = 16 * (int64_t)ds_parts(d);
   return z;
 }
+
+// A restart image that k_htab moves to the coefficient-buffer path keeps its baseline
+// table area: its one scan needs at most 4 DC + 4 AC tables there.
+static_assert(((int64_t)sizeof(HuffTables) - kPTabOff) / (int64_t)sizeof(PTab) >= 8, "switched restart images");
 
 // Horizontal taps in the signed-dot4 layout (k_hresize): per output x an int4
 // {xmin, groups, corr, 0}, then groups of 4 taps as signed base-256 digit planes.

@@ -21,7 +21,13 @@ inline void probe_one(const uint8_t* p, int64_t len, bool raw, int32_t max_image
     parse_jpeg(p, len, max_image_dim, &d, raw);
     if (d.status == DINO_IMG_OK && d.kind == 1) {
       HostMarkerFinder find;
-      prog_walk(p, len, &d, scans, find);
+      if (prog_walk(p, len, &d, scans, find) == DINO_IMG_OK) {
+        // k_pwalk's table slots: more distinct tables than the region holds -> Pillow
+        int32_t slot_off[kPMaxTabs];
+        uint8_t slot_dc[kPMaxTabs];
+        uint64_t ts[kMaxScans];
+        if (prog_table_slots(scans, d.n_scans, slot_off, slot_dc, ts, kPMaxTabs) < 0) d.status = DINO_IMG_UNSUPPORTED;
+      }
     }
   }
   if (info_row) {

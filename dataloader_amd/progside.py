@@ -56,9 +56,36 @@ class SideJob:
         return {i: c for i, c in self.containers.items() if st[self.rows[i]] == 0}
 
 
+# Dedicated-queue streams are kept for the life of the process and reused by later side
+# contexts: tensors allocated on a stream keep a reference to it in torch's caching
+# allocator, so destroying one under torch is unsafe (measured: a segfault at close).
+_FREE_STREAMS: dict = {}
+
+
+def _take_stream(device: int, cu_count: int):
+    free = _FREE_STREAMS.setdefault((device, cu_count), [])
+    if free:
+        return free.pop()
+    h = ctypes.c_void_p()
+    _lib.check(_lib.load().dino_stream_create(device, cu_count, ctypes.byref(h)), "dino_stream_create")
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device))
+
+
 class _SideEngine:
-    def __init__(self, device: torch.device, max_images: int, max_image_dim: int):
-        self.stream = torch.cuda.Stream(device=device)
+    """One side context on a stream with its own hardware queue (``dino_stream_create``):
+    a side decode runs for milliseconds, and on a queue shared with a batch stream the
+    batch's kernels would wait behind it (measured: pools of >= 32 images on shared
+    queues fell to 2.4k img/s, profiles/r03_route_study.jsonl).  ``cu_count`` > 0 confines
+    the side decode to that many CUs."""
+
+    def __init__(self, device: torch.device, max_images: int, max_image_dim: int, cu_count: int = 0,
+                 dedicated: bool = True):
+        self._key = None
+        if dedicated:
+            self._key = (device.index or 0, int(cu_count))
+            self.stream = _take_stream(*self._key)
+        else:
+            self.stream = torch.cuda.Stream(device=device)
         self.eng = IngestEngine(device, max_batch=max_images, max_views=1, max_crop_size=8,
                                 max_image_dim=max_image_dim, workspace_bytes=64 << 20, stream=self.stream)
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
@@ -66,6 +93,15 @@ class _SideEngine:
 
     def idle(self) -> bool:
         return self.last is None or self.last.query()
+
+    def close(self) -> None:
+        if self.last is not None:
+            self.last.synchronize()
+        self.eng.close()
+        if self._key is not None:
+            self.stream.synchronize()
+            _FREE_STREAMS.setdefault(self._key, []).append(self.stream)
+            self._key = None
 
 
 class DeviceSideDecoder:
@@ -82,6 +118,10 @@ class DeviceSideDecoder:
         # launch holds the hardware queue it shares with a slot's stream)
         min_images = int(os.environ.get("DINO_SIDE_MIN", 16)) if min_images is None else min_images
         engines = int(os.environ.get("DINO_SIDE_ENGINES", 2)) if engines is None else engines
+        self.cu_count = int(os.environ.get("DINO_SIDE_CUS", 0))
+        self.timing = os.environ.get("DINO_SIDE_TIMING", "0") == "1"  # per-launch GPU spans (analysis)
+        self.spans: list = []
+        self.dedicated = os.environ.get("DINO_SIDE_DEDICATED", "1") != "0"
         self.device = device
         self.max_images = int(max_images)
         self.min_images = max(1, min(int(min_images), self.max_images))
@@ -108,7 +148,7 @@ class DeviceSideDecoder:
             if e.idle():
                 return e
         if len(self._engines) < self.cap:
-            e = _SideEngine(self.device, self.max_images, self.max_image_dim)
+            e = _SideEngine(self.device, self.max_images, self.max_image_dim, self.cu_count, self.dedicated)
             self._engines.append(e)
             return e
         e = self._engines[self._rr % len(self._engines)]
@@ -131,6 +171,9 @@ class DeviceSideDecoder:
         eng.reserve(ws, 0)
         heads = []
         with eng.on_stream():
+            if self.timing:
+                t0 = torch.cuda.Event(enable_timing=True)
+                t0.record(se.stream)
             d_bytes = hb.to(self.device, non_blocking=True)
             d_off = off.to(self.device, non_blocking=True)
             d_info = eng.decode(d_bytes, d_off, len(items))
@@ -149,8 +192,10 @@ class DeviceSideDecoder:
                 _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(c.data_ptr() + 16), eng._s()),
                            "dino_copy_rgb")
                 job.containers[i] = c
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(enable_timing=self.timing)
             ev.record(se.stream)
+            if self.timing:
+                self.spans.append((t0, ev, len(part)))
         for job, _, _ in part:
             job.event, job.status, job.pending = ev, status, False
         se.last = ev
@@ -158,12 +203,21 @@ class DeviceSideDecoder:
         self.launches += 1
         self.images += len(part)
 
+    def launch_ms(self) -> list:
+        """(GPU ms, images) of every timed launch (DINO_SIDE_TIMING=1)."""
+        out = []
+        for a, b, n in self.spans:
+            b.synchronize()
+            out.append((round(a.elapsed_time(b), 2), n))
+        return out
+
     def close(self) -> None:
+        if self.timing:
+            import sys
+            print("side launches (ms, images):", self.launch_ms(), file=sys.stderr)
         self._pool.clear()
         for e in self._engines:
-            if e.last is not None:
-                e.last.synchronize()
-            e.eng.close()
+            e.close()
         self._engines.clear()
 
 

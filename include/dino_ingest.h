@@ -249,6 +249,13 @@ int dino_host_unregister(void* host);
  * pinned memory). */
 int dino_copy_h2d(void* d_dst, const void* host_src, int64_t nbytes, void* stream);
 
+/* A stream on its own hardware queue (a CU-masked stream: the runtime never shares
+ * its queue with other streams), for work that must not queue behind, or hold up,
+ * the batch streams: the progressive side decode (dataloader_amd/progside.py).
+ * cu_count <= 0 or >= the device's CUs: every CU; else cu_count CUs spread evenly. */
+int dino_stream_create(int device, int32_t cu_count, void** stream);
+int dino_stream_destroy(void* stream);
+
 /* Grow the ctx's decode / augment workspaces to at least the given sizes (never
  * shrinks), stream-ordered on `stream` (the stream the ctx's batches run on): the old
  * buffers are released after the work already enqueued there, nothing else on the

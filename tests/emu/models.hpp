@@ -14,6 +14,7 @@
 #include "../../dataloader_amd/csrc/idct.hpp"
 #include "../../dataloader_amd/csrc/jpeg_parse.hpp"
 #include "../../dataloader_amd/csrc/progressive.hpp"
+#include "../../dataloader_amd/csrc/pscan.hpp"
 
 namespace dino {
 
@@ -184,30 +185,41 @@ struct StageCapture {
 
 inline int model_idct_color(const ImgDesc& d, const std::vector<int16_t>& coef, uint8_t* out_rgb, StageCapture* cap);
 
-// k_prog: the marker walk, then every scan in file order (the kernel's level order
-// gives the same coefficients: scans of one level touch disjoint coefficients).
+// k_pwalk + k_pscan: the marker walk, the table slots, then every scan in file order
+// (the kernels' level order gives the same coefficients: scans of one level touch
+// disjoint coefficients), each through pscan_decode with plain-memory stores.
 inline int host_model_decode_multiscan(const uint8_t* p, int64_t len, ImgDesc& d, uint8_t* out_rgb, int32_t* stats,
                                        StageCapture* cap) {
   std::vector<ScanRec> scans(kMaxScans);
   HostMarkerFinder find;
   if (prog_walk(p, len, &d, scans.data(), find) != DINO_IMG_OK) return d.status;
+  std::vector<int32_t> slot_off(kPMaxTabs);
+  std::vector<uint8_t> slot_dc(kPMaxTabs);
+  std::vector<uint64_t> ts(kMaxScans);
+  const int ntab = prog_table_slots(scans.data(), d.n_scans, slot_off.data(), slot_dc.data(), ts.data(), kPMaxTabs);
+  if (ntab < 0) return DINO_IMG_UNSUPPORTED;
+  std::vector<PTab> tabs(ntab > 0 ? ntab : 1);
+  for (int s = 0; s < ntab; ++s) {
+    ProgTable t;
+    if (!huff_build_derived(p + slot_off[s], slot_dc[s] != 0, &t)) return DINO_IMG_CORRUPT;
+    ptab_fill_derived(&t, &tabs[s]);
+    for (int i = 0; i < (1 << kPLookBits); ++i) tabs[s].look[i] = ptab_look_entry(&t, i);
+  }
   std::vector<int16_t> coef(d.coef_bytes / 2, 0);
-  std::vector<ProgTable> tabs(8);
+  std::vector<uint8_t> clean(len + 16, 0);
   for (int i = 0; i < d.n_scans; ++i) {
     const ScanRec& sr = scans[i];
-    ScanTables tb;
-    for (int k = 0; k < 4; ++k) {
-      tb.dc[k] = tb.ac[k] = &tabs[0];
-      if (sr.dc_tab[k] >= 0) {
-        if (!prog_build_table(p + sr.dc_tab[k], true, &tabs[k])) return DINO_IMG_CORRUPT;
-        tb.dc[k] = &tabs[k];
-      }
-      if (sr.ac_tab[k] >= 0) {
-        if (!prog_build_table(p + sr.ac_tab[k], false, &tabs[4 + k])) return DINO_IMG_CORRUPT;
-        tb.ac[k] = &tabs[4 + k];
-      }
+    HostCoefSink sink{coef.data()};
+    const HostTabs tb{tabs.data(), ts[i]};
+    if (sr.restart_interval == 0) {  // k_pscan's destuffed reader
+      HostClean r{clean.data(), host_destuff(p, len, sr.data_off, clean.data())};
+      pscan_decode(r, tb, &d, sr, d.progressive != 0, sink);
+      std::fill(clean.begin(), clean.end(), 0);
+    } else {
+      RawReader r;
+      pb_init(r.b, (uintptr_t)p, len, sr.data_off);
+      pscan_decode(r, tb, &d, sr, d.progressive != 0, sink);
     }
-    prog_decode_scan(p, len, d, sr, tb, coef.data(), kNaturalOrder);
   }
   if (stats) {
     stats[0] = d.n_scans;
