@@ -1166,10 +1166,21 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
 // uniformity analysis treat the loops' scalar state (bit position, EOB run, masks) as
 // divergent at the join, which moves the whole serial decode from SGPRs to VGPRs
 // (measured: 250 instructions per symbol instead of ~50).
-__device__ uint32_t g_pscan_dummy[64 * 4];
-__device__ __forceinline__ int16_t* pick16(bool c, int16_t* p, int lane) {
-  return c ? p : (int16_t*)&g_pscan_dummy[lane];
+// Stores go through buffer resources whose range check drops the disabled lanes' stores
+// (offset kNoStore is out of range): no branch, and no lane writes anything it should not
+// (a shared dummy address would be written by every wave at once).  The OR entries of the
+// DC refinement (atomics) keep a dummy word, one per lane and wave slot.
+constexpr uint32_t kNoStore = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t store_rsrc(void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7FFFFFFF, 0x00020000);
 }
+__device__ __forceinline__ void store16_if(__amdgpu_buffer_rsrc_t r, bool c, int64_t elem, int16_t v) {
+  __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, r, c ? (int)(uint32_t)(elem * 2) : (int)kNoStore, 0, 0);
+}
+__device__ __forceinline__ void store8_if(__amdgpu_buffer_rsrc_t r, bool c, uint32_t off, uint8_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8(v, r, c ? (int)off : (int)kNoStore, 0, 0);
+}
+__device__ uint32_t g_pscan_dummy[1024 * 64];
 
 // The lanes' half of a scan (see pscan.hpp): pending (element, value) stores in lane
 // registers, and for AC refinement the 16-block groups of coefficients (lane k holds
@@ -1191,10 +1202,10 @@ struct WaveCoefSink {
 
   __device__ __forceinline__ void flush() {  // (branch-free: see g_pscan_dummy)
     const bool act = lane < n, isor = (eval & 0x10000) != 0;
-    uint32_t* w = (act & isor) ? (uint32_t*)(coef + (eidx & ~1)) : &g_pscan_dummy[64 + lane];
+    uint32_t* w = (act & isor) ? (uint32_t*)(coef + (eidx & ~1)) : &g_pscan_dummy[(blockIdx.x & 1023) * 64 + lane];
     __hip_atomic_fetch_or(w, isor ? (uint32_t)(eval & 0xFFFF) << (16 * (eidx & 1)) : 0u, __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
-    *pick16(act & !isor, coef + eidx, lane) = (int16_t)eval;
+    store16_if(store_rsrc(coef), act & !isor, eidx, (int16_t)eval);
     n = 0;
   }
   __device__ __forceinline__ void put(int64_t e, int32_t v) {
@@ -1256,7 +1267,7 @@ struct WaveCoefSink {
     const bool c = (corr >> lane) & 1u, nw = (nzn >> lane) & 1u;
     const int16_t v = stage[g * 64 + lane];
     const int16_t x = ac_refine_value(v, c, nw, (neg >> lane) & 1u, al);
-    *pick16(x != v, coef + cur + natk, lane) = x;  // (branch-free: see g_pscan_dummy)
+    store16_if(store_rsrc(coef), x != v, cur + natk, x);  // (branch-free: see g_pscan_dummy)
   }
 };
 
@@ -1272,6 +1283,7 @@ struct VTab {
   const DINO_CONST PTab* tabs;
   uint64_t ts;
   uint32_t natv;
+  uint32_t hv4, mv4;  // AC table (position 4): huffval dwords; lanes 0-6 maxcode[10..16], 8-14 valoffset[10..16]
   __device__ __forceinline__ void load(const PTab* tb, uint64_t slots, int lane) {
     tabs = (const DINO_CONST PTab*)tb;
     ts = slots;
@@ -1283,6 +1295,11 @@ struct VTab {
       for (int j = 0; j < 4; ++j) v[4 * k + j] = s < 0xFF ? src[64 * j + lane] : 0u;
     }
     natv = kNaturalOrder[lane];
+    const int s4 = pbyte64(slots, 4);
+    const PTab* t4 = tb + (s4 < 0xFF ? s4 : 0);
+    hv4 = t4->huffval[lane];
+    const int q = lane & 7;
+    mv4 = q < 7 && lane < 16 ? (uint32_t)(lane < 8 ? t4->maxcode[kPLookBits + 1 + q] : t4->valoffset[kPLookBits + 1 + q]) : 0u;
   }
   __device__ __forceinline__ void lookup(int k, uint32_t p, int* sym, int* len) const {
     // (uniform, but the compiler may compute it on the VALU: without the readfirstlane the
@@ -1293,6 +1310,19 @@ struct VTab {
     if (e) {
       *sym = (int)(e >> 4);
       *len = (int)(e & 15u);
+    } else if (k == 4) {  // the AC table's long codes from lane registers (no scalar-cache round trip)
+      const uint32_t p17 = p >> 15;
+      int l = 17, off = 0;
+#pragma unroll
+      for (int q = 16 - kPLookBits - 1; q >= 0; --q) {
+        if ((int32_t)(p17 >> (17 - (kPLookBits + 1 + q))) <= __builtin_amdgcn_readlane((int32_t)mv4, q)) {
+          l = kPLookBits + 1 + q;
+          off = __builtin_amdgcn_readlane((int32_t)mv4, 8 + q);
+        }
+      }
+      *len = l;
+      const int ix = ((int)(p17 >> (17 - (l > 16 ? 16 : l))) + off) & 255;
+      *sym = l > 16 ? 0 : (int)(((uint32_t)__builtin_amdgcn_readlane((int32_t)hv4, ix >> 2) >> (8 * (ix & 3))) & 0xFFu);
     } else {
       ptab_slow(tabs + pbyte64(ts, k), p, sym, len);
     }
@@ -1308,13 +1338,16 @@ struct CleanReader {
   uint32_t nw;          // dwords holding data
   uint32_t pos, nbits;  // bits consumed, data bits
   int32_t wa;
-  uint32_t A, B;
+  uint32_t A, B, Braw;  // Braw: the next-but-one window as loaded (swapped when it becomes B)
   int lane;
-  __device__ __forceinline__ uint32_t loadw(int32_t gi) const {
+  __device__ __forceinline__ uint32_t rawload(int32_t gi) const {
     const uint32_t w = (uint32_t)gi * 64u + (uint32_t)lane;
-    const uint32_t x = src[w < nw ? w : 0u];  // (always loaded: no branch, see g_pscan_dummy)
-    return w < nw ? __builtin_bswap32(x) : 0u;
+    return src[w < nw ? w : 0u];  // (always loaded: no branch, see g_pscan_dummy)
   }
+  __device__ __forceinline__ uint32_t swapw(int32_t gi, uint32_t x) const {
+    return (uint32_t)gi * 64u + (uint32_t)lane < nw ? __builtin_bswap32(x) : 0u;
+  }
+  __device__ __forceinline__ uint32_t loadw(int32_t gi) const { return swapw(gi, rawload(gi)); }
   __device__ __forceinline__ void init(const uint32_t* s, uint32_t nbytes, int ln) {
     src = s;
     nw = (nbytes + 3) >> 2;
@@ -1324,6 +1357,7 @@ struct CleanReader {
     wa = 0;
     A = loadw(0);
     B = loadw(1);
+    Braw = rawload(2);
   }
   __device__ __forceinline__ uint32_t peek() const {
     const uint32_t ps = pos;
@@ -1337,10 +1371,11 @@ struct CleanReader {
   }
   __device__ __forceinline__ void skip(int n) {
     pos += (uint32_t)n;
-    if ((int32_t)(pos >> 11) > wa) {
+    if ((int32_t)(pos >> 11) > wa) {  // the load of the new B was issued a window ago: no wait here
       A = B;
       ++wa;
-      B = loadw(wa + 1);
+      B = swapw(wa + 1, Braw);
+      Braw = rawload(wa + 2);
     }
   }
   __device__ __forceinline__ bool insuff() const { return pos > nbits; }
@@ -1353,6 +1388,7 @@ struct CleanReader {
 __device__ __forceinline__ uint32_t wave_destuff(const uint8_t* img, int64_t len, int64_t from, uint8_t* dst, int lane) {
   const uintptr_t beg = (uintptr_t)(img + from), end = (uintptr_t)(img + len);
   uint32_t out = 0, carry = 0;  // carry: the byte before this step's first dword
+  const __amdgpu_buffer_rsrc_t dr = store_rsrc(dst);
   const uint64_t lt = lane ? ~0ull >> (64 - lane) : 0ull;  // lanes below this one
   for (uintptr_t c = beg & ~(uintptr_t)3; c < end; c += 256) {
     const uintptr_t wa = c + 4u * (uint32_t)lane;
@@ -1394,16 +1430,16 @@ __device__ __forceinline__ uint32_t wave_destuff(const uint8_t* img, int64_t len
     uint32_t o = out + (uint32_t)(__builtin_popcountll(b0 & lt) + 2 * __builtin_popcountll(b1 & lt) +
                                   4 * __builtin_popcountll(b2 & lt));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {  // (branch-free: kept bytes to dst, the others to the dummy slot)
+    for (int i = 0; i < 4; ++i) {  // (branch-free: see g_pscan_dummy)
       const bool k = (keep >> i) & 1u;
-      *(k ? dst + o : (uint8_t*)&g_pscan_dummy[128 + lane]) = (uint8_t)(w >> (8 * i));
+      store8_if(dr, k, o, (uint8_t)(w >> (8 * i)));
       o += k;
     }
     out += (uint32_t)(__builtin_popcountll(b0) + 2 * __builtin_popcountll(b1) + 4 * __builtin_popcountll(b2));
     if (tl) break;
     carry = (uint32_t)__builtin_amdgcn_readlane((int32_t)w, 63) >> 24;
   }
-  *((uint32_t)lane < ((4u - (out & 3u)) & 3u) ? dst + out + lane : (uint8_t*)&g_pscan_dummy[128 + lane]) = 0;
+  store8_if(dr, (uint32_t)lane < ((4u - (out & 3u)) & 3u), out + lane, 0);
   __threadfence();  // this wave reads the bytes back (CleanReader)
   return out;
 }
@@ -1500,6 +1536,7 @@ __device__ __forceinline__ void fast_ac_refine(CleanReader& r, const VTab& t, co
 __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, const ScanRec& sr, int16_t* coef, int64_t plane,
                               int32_t bw, int32_t mcx, int32_t mcy, int lane, int natk) {
   const int ss = sr.ss, se = sr.se, al = sr.al;
+  const __amdgpu_buffer_rsrc_t cr = store_rsrc(coef);
   int32_t eobrun = 0;
   int32_t bx = 0;
   int64_t rowe = plane;  // element of block (0, by)
@@ -1533,7 +1570,7 @@ __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, con
           break;
         }
       }
-      *pick16((have >> lane) & 1u, coef + rowe + (int64_t)bx * 64 + natk, lane) = (int16_t)val;
+      store16_if(cr, (have >> lane) & 1u, rowe + (int64_t)bx * 64 + natk, (int16_t)val);
     }
   }
 }
@@ -3354,7 +3391,12 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
   g->grid_ds = 4 * cus;
   g->grid3 = persistent_grid(reinterpret_cast<const void*>(&k_huff3), kHuff3LdsBytes, cus);
   g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
-  g->grid_ps = 4 * cus;  // scan waves: a batch's level-0 scans all start at once
+  // scan waves: one per CU by default.  A scan's serial decode runs on the CU's one scalar
+  // unit, which the CU's waves share: two scan waves on a CU each run at about half speed
+  // (DINO_PSCAN_PER_CU: waves per CU, measured in profiles/r03_prog_*).
+  const char* pc = getenv("DINO_PSCAN_PER_CU");
+  const int per_cu = pc && atoi(pc) > 0 ? atoi(pc) : 1;
+  g->grid_ps = per_cu * cus;
   return hipSuccess;
 }
 
