@@ -2270,6 +2270,32 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
   }
 }
 
+#ifndef DINO_HRESIZE_MFMA
+#define DINO_HRESIZE_MFMA 0
+#endif
+#ifndef DINO_HRESIZE_MFMA_STEPS
+#define DINO_HRESIZE_MFMA_STEPS 2
+#endif
+#ifndef DINO_HRESIZE_MFMA_PITCH
+#define DINO_HRESIZE_MFMA_PITCH 320
+#endif
+constexpr int kHrMfmaMaxSteps = DINO_HRESIZE_MFMA_STEPS;  // 64-column K steps per 16-column block
+constexpr int kHrMfmaMaxK = 64 * kHrMfmaMaxSteps;
+constexpr int kHrMfmaMaxPitch = DINO_HRESIZE_MFMA_PITCH;  // bytes per staged row (views needing more: v_dot4 kernel)
+constexpr int kHrMfmaLds = 2 * 3 * 16 * kHrMfmaMaxPitch;  // 2 band buffers x 3 planes x 16 rows
+constexpr int kHrMfmaPre = 4;                        // staging items per thread loaded a band ahead
+typedef int32_t hr_v4i __attribute__((ext_vector_type(4)));
+
+// Conservative per-view test from the view geometry alone (both kernels evaluate it):
+// a 16-column block spans <= 15 cw / S + 1 + kh source columns, + 15 for its 16-byte
+// aligned start; a 64-column group <= 63 cw / S + 1 + kh, + 15 + 64 of read slack.
+__host__ __device__ __forceinline__ bool hresize_mfma_ok(int S, int cw, int kh) {
+  if (!DINO_HRESIZE_MFMA || kh <= 0) return false;
+  const int64_t blk = (15ll * cw + S - 1) / S + 1 + kh + 15;
+  const int64_t grp = (63ll * cw + S - 1) / S + 1 + kh + 15 + 64;
+  return blk <= kHrMfmaMaxK && ((grp + 15) & ~15ll) <= kHrMfmaMaxPitch;
+}
+
 // Horizontal pass.  A workgroup owns bands of R source rows of one view.  The
 // crop's pixels for those rows are staged in LDS as RGBX words (each lane turns
 // 12 source bytes = 4 pixels into one 16-byte LDS store); the view's taps are
@@ -2284,6 +2310,10 @@ constexpr int kHresizeMinRows = DINO_HRESIZE_MIN_ROWS;  // rows per band the sli
 #define DINO_HRESIZE_WGS 4
 #endif
 constexpr int kHresizeWgs = DINO_HRESIZE_WGS;  // workgroups per view (each loops over the view's tiles)
+#ifndef DINO_HRESIZE_PREFETCH
+#define DINO_HRESIZE_PREFETCH 0
+#endif
+constexpr int kHrPre = DINO_HRESIZE_PREFETCH;  // staging items per thread loaded one tile ahead (0: none)
 
 // Tile shape of a view's horizontal pass: the widest slice of outputs (all of S,
 // else a multiple of 8) whose taps (16 bytes per output + 16 per output and group
@@ -2441,6 +2471,7 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   const dino_view_params p = prm[i];
   const ImgDesc& d = desc[b];
   const int S = p.out_size, W = d.width, cw = p.crop_w, kh = vp.kh;
+  if (hresize_mfma_ok(S, cw, kh)) return;  // k_hresize_mfma's view
   const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);
   const int32_t* gt = gb + 4 * S;
   const int4* ghx = (const int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
@@ -2466,50 +2497,281 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   uint8_t* rows = smem + 16 * sw * (1 + ng_max);
   const int plane_bytes = R * pitch;
   const int nbands = (p.crop_h + R - 1) / R;
-  int cur = -1;
-  for (int u = bk.x; u < nsl * nbands; u += gridDim.x) {
-    const int sl = u / nbands, band = u - sl * nbands;
-    const int x0 = sl * sw, swn = min(sw, S - x0);
-    const int r0 = band * R, nr = min(R, p.crop_h - r0);
-    if (sl != cur) {  // taps of the slice -> LDS
-      __syncthreads();
-      for (int k = threadIdx.x; k < swn; k += blockDim.x) lx[k] = ghx[x0 + k];
-      for (int k = threadIdx.x; k < swn * ng_max; k += blockDim.x) {
-        const int g = k / swn, xl = k - g * swn;
-        lg[g * swn + xl] = ghg[(int64_t)g * S + x0 + xl];
+  const int ntiles = nsl * nbands;
+  // Tile u: slice sl (outputs [x0, x0 + swn)), band of rows [r0, r0 + nr), source columns
+  // staged from c0 in ngroups groups of 4 pixels.
+  struct Tile {
+    int sl, x0, swn, r0, nr, c0, ngroups;
+  };
+  auto tile_of = [&](int u) {
+    Tile T;
+    T.sl = u / nbands;
+    const int band = u - T.sl * nbands;
+    T.x0 = T.sl * sw;
+    T.swn = min(sw, S - T.x0);
+    T.r0 = band * R;
+    T.nr = min(R, p.crop_h - T.r0);
+    T.c0 = ghx[T.x0].x & ~3;  // first source column staged (4-aligned within the crop)
+    const int c1 = min(cw, ghx[T.x0 + T.swn - 1].x + gb[2 * (T.x0 + T.swn - 1) + 1]);
+    T.ngroups = (c1 - T.c0 + 3) >> 2;
+    return T;
+  };
+  // staging item e of tile T: row e / ngroups, group e % ngroups (12 source bytes = 4 pixels)
+  auto item_src = [&](const Tile& T, int e, int* r, int* g) {
+    *r = e / T.ngroups;
+    *g = e - *r * T.ngroups;
+    return rgb + ((int64_t)(p.crop_top + T.r0 + *r) * W + p.crop_left + T.c0) * 3 + 12 * *g;
+  };
+  auto stage_put = [&](int r, int g, const uint8_t* src, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
+    const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);  // R0 G0 B0 R1
+    const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);  // G1 B1 R2 G2
+    const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);  // B2 R3 G3 B3
+    // de-interleave 4 pixels into one word per channel (v_perm byte selects), sign bit flipped
+    const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
+    const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
+    const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
+    uint8_t* dst = rows + r * pitch + 4 * g;
+    *(uint32_t*)dst = cr ^ 0x80808080u;
+    *(uint32_t*)(dst + plane_bytes) = cg ^ 0x80808080u;
+    *(uint32_t*)(dst + 2 * plane_bytes) = cb ^ 0x80808080u;
+  };
+  // The first kHrPre staging items of each thread are loaded one tile ahead (during the
+  // previous tile's dot products), the rest when the tile starts.
+  uint32_t pf[kHrPre > 0 ? kHrPre : 1][4];
+  auto prefetch = [&](const Tile& T) {
+#pragma unroll
+    for (int j = 0; j < kHrPre; ++j) {
+      const int e = (int)threadIdx.x + j * (int)blockDim.x;
+      if (e < T.nr * T.ngroups) {
+        int r, g;
+        const uint8_t* src = item_src(T, e, &r, &g);
+        const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
+        pf[j][0] = a0[0];
+        pf[j][1] = a0[1];
+        pf[j][2] = a0[2];
+        pf[j][3] = a0[3];
       }
-      cur = sl;
     }
-    const int c0 = ghx[x0].x & ~3;  // first source column staged (4-aligned within the crop)
-    const int c1 = min(cw, ghx[x0 + swn - 1].x + gb[2 * (x0 + swn - 1) + 1]);
-    const int ngroups = (c1 - c0 + 3) >> 2;
-    for (int e = threadIdx.x; e < nr * ngroups; e += blockDim.x) {
-      const int r = e / ngroups, g = e - r * ngroups;
-      const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left + c0) * 3 + 12 * g;
+  };
+  int cur = -1;
+  if (kHrPre && (int)bk.x < ntiles) prefetch(tile_of(bk.x));
+  for (int u = bk.x; u < ntiles; u += gridDim.x) {
+    const Tile T = tile_of(u);
+    if (T.sl != cur) {  // taps of the slice -> LDS (the previous tile ended with a barrier)
+      for (int k = threadIdx.x; k < T.swn; k += blockDim.x) lx[k] = ghx[T.x0 + k];
+      for (int k = threadIdx.x; k < T.swn * ng_max; k += blockDim.x) {
+        const int g = k / T.swn, xl = k - g * T.swn;
+        lg[g * T.swn + xl] = ghg[(int64_t)g * S + T.x0 + xl];
+      }
+      cur = T.sl;
+    }
+    const int nitems = T.nr * T.ngroups;
+#pragma unroll
+    for (int j = 0; j < kHrPre; ++j) {
+      const int e = (int)threadIdx.x + j * (int)blockDim.x;
+      if (e < nitems) {
+        int r, g;
+        const uint8_t* src = item_src(T, e, &r, &g);
+        stage_put(r, g, src, pf[j][0], pf[j][1], pf[j][2], pf[j][3]);
+      }
+    }
+    for (int e = (int)threadIdx.x + kHrPre * (int)blockDim.x; e < nitems; e += blockDim.x) {
+      int r, g;
+      const uint8_t* src = item_src(T, e, &r, &g);
       const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
-      const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
-      const uint32_t w0 = a0[0], w1 = a0[1], w2 = a0[2], w3 = a0[3];
-      const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);  // R0 G0 B0 R1
-      const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);  // G1 B1 R2 G2
-      const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);  // B2 R3 G3 B3
-      // de-interleave 4 pixels into one word per channel (v_perm byte selects), sign bit flipped
-      const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
-      const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
-      const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
-      uint8_t* dst = rows + r * pitch + 4 * g;
-      *(uint32_t*)dst = cr ^ 0x80808080u;
-      *(uint32_t*)(dst + plane_bytes) = cg ^ 0x80808080u;
-      *(uint32_t*)(dst + 2 * plane_bytes) = cb ^ 0x80808080u;
+      stage_put(r, g, src, a0[0], a0[1], a0[2], a0[3]);
     }
     __syncthreads();
+    if (kHrPre && u + (int)gridDim.x < ntiles) prefetch(tile_of(u + gridDim.x));
     if (DINO_HRESIZE_TAPREG && ng_max <= 2)
-      hresize_tile_regs<2>(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+      hresize_tile_regs<2>(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
     else if (DINO_HRESIZE_TAPREG && ng_max <= 4)
-      hresize_tile_regs<4>(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+      hresize_tile_regs<4>(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
     else if (DINO_HRESIZE_TAPREG && ng_max <= 8)
-      hresize_tile_regs<8>(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+      hresize_tile_regs<8>(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
     else
-      hresize_tile_dot(rows, pitch, plane_bytes, nr, r0, x0, swn, c0, S, lx, lg, tmp, cpl);
+      hresize_tile_dot(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
+    __syncthreads();
+  }
+}
+
+// Horizontal pass on the matrix cores (round 3).  The horizontal resample of a band of
+// 16 crop rows to 16 output columns is a product of the rows' pixels (16 x K source
+// columns) with a banded weight matrix (K x 16: column x holds its taps at source columns
+// [xmin(x), xmin(x) + cnt(x)), zero elsewhere).  Same exact integer sums as the v_dot4
+// path: pixels sign-flipped to int8 (p - 128), taps as three signed base-256 digit
+// planes, one v_mfma_i32_16x16x64_i8 per channel, digit and 64-column step; the digit
+// sums recombine to Pillow's int32 sum (+ the 128 x sum-of-taps correction).
+// A workgroup owns 64 output columns of one view (4 waves x 16 columns); each wave
+// builds its weight fragments once (global taps -> registers) and sweeps the crop's
+// rows in bands of 16 that the workgroup stages in LDS as planar sign-flipped rows
+// (16-byte aligned, so each A fragment is one ds_read_b128).  Views whose 16-column
+// blocks need more than kHrMfmaMaxK source columns, or whose 64-column span does not fit
+// the staging budget, keep the v_dot4 kernel (hresize_mfma_ok decides for both).
+__global__ void __launch_bounds__(256) k_hresize_mfma(const ImgDesc* __restrict__ desc,
+                                                      const dino_view_params* __restrict__ prm,
+                                                      const ViewPlan* __restrict__ plan, int nv, int v0,
+                                                      const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int b = blockIdx.z;
+  const int i = b * nv + v0 + blockIdx.y;
+  const ViewPlan vp = plan[i];
+  if (!vp.ok || !vp.kh) return;
+  const dino_view_params p = prm[i];
+  const int S = p.out_size, cw = p.crop_w, kh = vp.kh;
+  if (!hresize_mfma_ok(S, cw, kh)) return;
+  const int xg0 = 64 * (int)blockIdx.x;
+  if (xg0 >= S) return;
+  const ImgDesc& d = desc[b];
+  const int W = d.width;
+  const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);  // [S][2]: xmin, cnt
+  const int32_t* gt = gb + 4 * S;                            // [S][kh] taps
+  const int4* ghx = (const int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
+  const uint8_t* rgb = ws + d.rgb_off;
+  uint8_t* tmp = aws + vp.htmp_off;
+  const int64_t cpl = (int64_t)p.crop_h * S;
+  const int ncols = min(64, S - xg0);
+  const int c0 = gb[2 * xg0] & ~15;  // staged source columns [c0, c1), 16-aligned start
+  const int c1 = min(cw, gb[2 * (xg0 + ncols - 1)] + gb[2 * (xg0 + ncols - 1) + 1]);
+  const int pitch = ((c1 - c0 + 15) & ~15) + 64;  // + the read slack of the last K step
+  const int plane = 16 * pitch;
+  const int ngroups = (c1 - c0 + 3) >> 2;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int xb = xg0 + 16 * w;  // this wave's 16 output columns
+  const bool wact = xb < xg0 + ncols;
+  const int ncw = wact ? min(16, S - xb) : 0;
+  const int kb = wact ? (gb[2 * xb] & ~15) : c0;
+  const int nk = wact ? (gb[2 * (xb + ncw - 1)] + gb[2 * (xb + ncw - 1) + 1] - kb + 63) >> 6 : 0;
+  // weight fragments: lane (column xb + (lane & 15), k quarter lane >> 4) holds, per K step
+  // s and digit, the 16 digits of source columns kb + 64 s + 16 (lane >> 4) + j
+  hr_v4i bw[kHrMfmaMaxSteps][3];
+  const int xo = xb + (lane & 15);
+  const bool cval = wact && (lane & 15) < ncw;
+  const int xm = cval ? gb[2 * xo] : 0, cnt = cval ? gb[2 * xo + 1] : 0;
+  const int32_t corr = cval ? ghx[xo].z : 0;
+#pragma unroll
+  for (int s = 0; s < kHrMfmaMaxSteps; ++s) {
+    uint32_t dg[3][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+    if (s < nk) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int t = kb + 64 * s + 16 * (lane >> 4) + j - xm;
+        const int32_t kt = t >= 0 && t < cnt ? gt[(int64_t)xo * kh + t] : 0;
+        const int32_t d0 = (int32_t)(int8_t)(uint8_t)(kt & 0xFF);
+        const int32_t r1 = (kt - d0) >> 8;
+        const int32_t d1 = (int32_t)(int8_t)(uint8_t)(r1 & 0xFF);
+        const int32_t d2 = (r1 - d1) >> 8;
+        dg[0][j >> 2] |= (uint32_t)(uint8_t)d0 << (8 * (j & 3));
+        dg[1][j >> 2] |= (uint32_t)(uint8_t)d1 << (8 * (j & 3));
+        dg[2][j >> 2] |= (uint32_t)(uint8_t)d2 << (8 * (j & 3));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      bw[s][q][0] = (int32_t)dg[q][0];
+      bw[s][q][1] = (int32_t)dg[q][1];
+      bw[s][q][2] = (int32_t)dg[q][2];
+      bw[s][q][3] = (int32_t)dg[q][3];
+    }
+  }
+  const int arow = lane & 15, acol = kb - c0 + 16 * (lane >> 4);
+  const int nbands = (p.crop_h + 15) >> 4;
+  // staging item e of band r0: row e / ngroups, group e % ngroups (12 source bytes = 4 pixels)
+  auto src_of = [&](int r0, int e, int* r, int* g) {
+    *r = e / ngroups;
+    *g = e - *r * ngroups;
+    return rgb + ((int64_t)(p.crop_top + r0 + *r) * W + p.crop_left + c0) * 3 + 12 * *g;
+  };
+  auto put = [&](uint8_t* buf, int r, int g, const uint8_t* src, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
+    const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
+    const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
+    const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);
+    const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
+    const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
+    const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
+    uint8_t* dst = buf + r * pitch + 4 * g;
+    *(uint32_t*)dst = cr ^ 0x80808080u;
+    *(uint32_t*)(dst + plane) = cg ^ 0x80808080u;
+    *(uint32_t*)(dst + 2 * plane) = cb ^ 0x80808080u;
+  };
+  // band k is staged in buffer k & 1: the first kHrMfmaPre items of each thread are loaded
+  // while the previous band's MFMAs run, the rest when the band is stored
+  uint32_t pf[kHrMfmaPre][4];
+  auto prefetch = [&](int r0) {
+    const int n = min(16, p.crop_h - r0) * ngroups;
+#pragma unroll
+    for (int j = 0; j < kHrMfmaPre; ++j) {
+      const int e = (int)threadIdx.x + j * (int)blockDim.x;
+      if (e < n) {
+        int r, g;
+        const uint32_t* a0 = (const uint32_t*)((uintptr_t)src_of(r0, e, &r, &g) & ~(uintptr_t)3);
+        pf[j][0] = a0[0];
+        pf[j][1] = a0[1];
+        pf[j][2] = a0[2];
+        pf[j][3] = a0[3];
+      }
+    }
+  };
+  auto store = [&](int r0, uint8_t* buf) {
+    const int n = min(16, p.crop_h - r0) * ngroups;
+#pragma unroll
+    for (int j = 0; j < kHrMfmaPre; ++j) {
+      const int e = (int)threadIdx.x + j * (int)blockDim.x;
+      if (e < n) {
+        int r, g;
+        const uint8_t* src = src_of(r0, e, &r, &g);
+        put(buf, r, g, src, pf[j][0], pf[j][1], pf[j][2], pf[j][3]);
+      }
+    }
+    for (int e = (int)threadIdx.x + kHrMfmaPre * (int)blockDim.x; e < n; e += blockDim.x) {
+      int r, g;
+      const uint8_t* src = src_of(r0, e, &r, &g);
+      const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
+      put(buf, r, g, src, a0[0], a0[1], a0[2], a0[3]);
+    }
+  };
+  prefetch(0);
+  store(0, smem);
+  __syncthreads();
+  for (int k = 0; k < nbands; ++k) {
+    const int r0 = 16 * k, nr = min(16, p.crop_h - r0);
+    uint8_t* cur = smem + (k & 1) * 3 * plane;
+    if (k + 1 < nbands) prefetch(r0 + 16);  // lands during this band's MFMAs
+    if (wact) {
+      hr_v4i acc[3][3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) acc[c][q] = hr_v4i{0, 0, 0, 0};
+      const uint8_t* rowp = cur + (arow < nr ? arow : nr - 1) * pitch + acol;  // (rows >= nr: not stored)
+#pragma unroll
+      for (int s = 0; s < kHrMfmaMaxSteps; ++s) {
+        if (s < nk) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            const hr_v4i a = *(const hr_v4i*)(rowp + c * plane + 64 * s);
+#pragma unroll
+            for (int q = 0; q < 3; ++q) acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bw[s][q], acc[c][q], 0, 0, 0);
+          }
+        }
+      }
+      if (cval) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int r = r0 + 4 * (lane >> 4) + kk;  // C/D: column lane & 15, row 4 (lane >> 4) + kk
+          if (r >= r0 + nr) break;
+          const int64_t o = (int64_t)r * S + xo;
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            tmp[c * cpl + o] = clip8_acc((int32_t)((uint32_t)acc[c][0][kk] + ((uint32_t)acc[c][1][kk] << 8) +
+                                                   ((uint32_t)acc[c][2][kk] << 16) + (uint32_t)corr));
+        }
+      }
+    }
+    // band k + 1 into the other buffer (band k - 1's readers passed the last barrier)
+    if (k + 1 < nbands) store(r0 + 16, smem + ((k + 1) & 1) * 3 * plane);
     __syncthreads();
   }
 }
@@ -3390,6 +3652,9 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
     return e;
   g->grid_ds = 4 * cus;
   g->grid3 = persistent_grid(reinterpret_cast<const void*>(&k_huff3), kHuff3LdsBytes, cus);
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hresize_mfma), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kHrMfmaLds)) != hipSuccess)
+    return e;
   g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
   // scan waves: one per CU by default.  A scan's serial decode runs on the CU's one scalar
   // unit, which the CU's waves share: two scan waves on a CU each run at about half speed
@@ -3438,6 +3703,10 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   const int kvert = v0 == 0 ? kKVertGlobal : kKVertLocal;
   const int rc_threads = S < 256 ? (S + 63) / 64 * 64 : 256;  // one lane per output column
   TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), rc_threads, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
+  if (DINO_HRESIZE_MFMA)
+    TIMED(tm, kKHresize, s,
+          (k_hresize_mfma<<<dim3((S + 63) / 64, nvc, B), 256, kHrMfmaLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
+                                                                                 a.aws)));
   TIMED(tm, kKHresize, s,
         (k_hresize<<<dim3(kHresizeWgs, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
   if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS
