@@ -1133,6 +1133,8 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
     PScan o;
     o.sr = L.scans[t];
     o.tslots = L.ts[t];
+    o.pipe = prog_pipelined(L.scans, n, t, dl.progressive != 0, &o.deps) ? 1 : 0;
+    o.pad = 0;
     ps[prog_level_rank(L.scans, n, t)] = o;
   }
   int nlev = 0;
@@ -1142,6 +1144,7 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
     for (int i = 0; i < n; ++i) c += L.scans[i].level == t;
     hd->cnt[t] = c;
     hd->done[t] = 0;
+    hd->prog[t] = 0;
   }
   if (t == 0) {
     hd->n_scans = n;
@@ -1478,15 +1481,50 @@ __device__ __forceinline__ uint64_t fast_corrections(CleanReader& r, uint64_t c,
   return corr;
 }
 
+// Block pipelining between the AC scans of one component (prog_pipelined): a scan
+// publishes how many of its blocks are stored every kPipeBlocks blocks (release: the
+// wave's stores are complete and written back first), and a scan that reads what
+// earlier scans wrote waits, before it loads a group of coefficients, until every one of
+// them has published past that group (acquire).  Its dependencies hold earlier tickets,
+// so they are running or done.
+constexpr int kPipeBlocks = 128;
+struct ScanPipe {
+  int32_t* prog;      // PHdr::prog
+  int32_t self;       // this scan's sorted index (publishes prog[self])
+  uint64_t deps;      // sorted indices of the scans it follows (0xFF: none)
+  int32_t avail;      // blocks every dependency has published (as last seen)
+  __device__ __forceinline__ void publish(int32_t nb) {
+    __hip_atomic_store(&prog[self], nb, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ void need(int32_t nb) {  // wait until every dependency passed block nb
+    while (avail < nb) {
+      int32_t m = 0x7FFFFFFF;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int dj = pbyte64(deps, k);
+        if (dj != 0xFF) {
+          const int32_t v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&prog[dj], __ATOMIC_ACQUIRE,
+                                                                             __HIP_MEMORY_SCOPE_AGENT));
+          m = v < m ? v : m;
+        }
+      }
+      avail = m;
+      if (avail < nb) __builtin_amdgcn_s_sleep(8);
+    }
+  }
+};
+
 // decode_mcu_AC_refine over the whole scan (see r_refine_block for the bookkeeping).
 __device__ __forceinline__ void fast_ac_refine(CleanReader& r, const VTab& t, const ScanRec& sr, int64_t plane, int32_t bw,
-                               int32_t mcx, int32_t mcy, WaveCoefSink& sink, int lane) {
+                               int32_t mcx, int32_t mcy, WaveCoefSink& sink, int lane, ScanPipe& pp) {
   const int ss = sr.ss, se = sr.se, al = sr.al;
   const uint64_t band = (uint64_t)low_bits(se + 1) & ~(uint64_t)low_bits(ss);
   int32_t eobrun = 0;
-  sink.rbegin(plane, bw, mcx, mcy);
   const int32_t nblk = mcx * mcy;
+  pp.need(min(32, nblk));  // rbegin loads the first group, rnz the next one ahead
+  sink.rbegin(plane, bw, mcx, mcy);
   for (int32_t m = 0; m < nblk; ++m) {
+    if ((m & 15) == 0) pp.need(min(m + 32, nblk));
     const uint64_t nzz = sink.rnz(m) & band;
     if (r.insuff()) continue;
     uint64_t corr = 0, nzn = 0, neg = 0;
@@ -1528,13 +1566,15 @@ __device__ __forceinline__ void fast_ac_refine(CleanReader& r, const VTab& t, co
       --eobrun;
     }
     sink.rapply(corr, nzn, neg, al);
+    if (((m + 1) & (kPipeBlocks - 1)) == 0) pp.publish(m + 1);
   }
+  pp.publish(nblk);
 }
 
 // decode_mcu_AC_first over the whole scan: values gather in lane k (zigzag k) of the
 // block and leave with one masked store.
 __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, const ScanRec& sr, int16_t* coef, int64_t plane,
-                              int32_t bw, int32_t mcx, int32_t mcy, int lane, int natk) {
+                              int32_t bw, int32_t mcx, int32_t mcy, int lane, int natk, ScanPipe& pp) {
   const int ss = sr.ss, se = sr.se, al = sr.al;
   const __amdgpu_buffer_rsrc_t cr = store_rsrc(coef);
   int32_t eobrun = 0;
@@ -1572,7 +1612,10 @@ __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, con
       }
       store16_if(cr, (have >> lane) & 1u, rowe + (int64_t)bx * 64 + natk, (int16_t)val);
     }
+    const int32_t done = (by + 1) * mcx;  // (published when it crosses a multiple of kPipeBlocks)
+    if (done / kPipeBlocks != (done - mcx) / kPipeBlocks) pp.publish(done);
   }
+  pp.publish(mcx * mcy);
 }
 
 constexpr int kPScanThreads = 64;
@@ -1609,7 +1652,8 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
     tb.load((const PTab*)(region + kPTabOff), ps->tslots, lane);
     uint32_t* clean = (uint32_t*)(ws + d->ent_off + ((sr.data_off - d->scan_off + 3) & ~3));
     const uint32_t dlen = sr.restart_interval == 0 ? wave_destuff(p, len, sr.data_off, (uint8_t*)clean, lane) : 0u;
-    if (sr.level > 0) {  // the previous level's scans of this image (earlier tickets, running or done)
+    const bool pipe = ps->pipe != 0;
+    if (sr.level > 0 && !pipe) {  // the previous level's scans of this image (earlier tickets, running or done)
       int32_t* dn = &((PHdr*)region)->done[sr.level - 1];
       const int32_t need = hd->cnt[sr.level - 1];
       for (;;) {
@@ -1638,8 +1682,9 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
         const int ci = sr.comp[0];
         const int64_t plane = d->comp[ci].coef_off / 2;
         const int32_t bw = d->comp[ci].bw, mcx = ceil_div(d->comp[ci].dw, 8), mcy = ceil_div(d->comp[ci].dh, 8);
-        if (sr.ah > 0) fast_ac_refine(r, tb, sr, plane, bw, mcx, mcy, sink, lane);
-        else fast_ac_first(r, tb, sr, sink.coef, plane, bw, mcx, mcy, lane, sink.natk);
+        ScanPipe pp{&((PHdr*)region)->prog[0], (int32_t)j, pipe ? ps->deps : ~0ull, pipe ? 0 : 0x7FFFFFFF};
+        if (sr.ah > 0) fast_ac_refine(r, tb, sr, plane, bw, mcx, mcy, sink, lane, pp);
+        else fast_ac_first(r, tb, sr, sink.coef, plane, bw, mcx, mcy, lane, sink.natk, pp);
       } else {
         pscan_decode(r, tb, d, sr, prog, sink);
       }

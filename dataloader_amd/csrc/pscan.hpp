@@ -105,18 +105,62 @@ DHD void ptab_slow(const DINO_CONST PTab* t, uint32_t p, int* sym, int* len) {
 // Per-image scan list (k_pwalk -> k_pscan), in the image's htab region:
 //   PHdr | PScan[kMaxScans] (sorted by dependency level, stable) | PTab[ntab]
 // ---------------------------------------------------------------------------
+// Dependency-level order of the scans (stable): rank of scan i.
+DHD int prog_level_rank(const ScanRec* scans, int n, int i) {
+  int r = 0;
+  for (int j = 0; j < n; ++j)
+    r += scans[j].level < scans[i].level || (scans[j].level == scans[i].level && j < i);
+  return r;
+}
+
 struct PScan {
   ScanRec sr;
   uint64_t tslots;  // byte k: table slot of DC table k (k < 4) / AC table k - 4; 0xFF none
+  uint64_t deps;    // pipelined scans: byte k = sorted index of an earlier scan it reads after, 0xFF none
+  int32_t pipe;     // 1: follows its dependencies block by block (prog_pipelined), 0: waits for its level
+  int32_t pad;
 };
-static_assert(sizeof(PScan) == 96, "PScan layout");
+static_assert(sizeof(PScan) == 112, "PScan layout");
 struct PHdr {
   int32_t n_scans, n_levels;
   int32_t cnt[kMaxScans];   // scans per level
   int32_t done[kMaxScans];  // scans of each level completed (k_pscan)
+  int32_t prog[kMaxScans];  // blocks each scan (sorted index) has finished and published
   int32_t pad[14];
 };
-static_assert(sizeof(PHdr) == 576, "PHdr layout");
+static_assert(sizeof(PHdr) == 832, "PHdr layout");
+
+// Scans whose coefficient sets intersect (a shared component and overlapping bands).
+DHD bool scans_overlap(const ScanRec& a, const ScanRec& b) {
+  if (a.se < b.ss || b.se < a.ss) return false;
+  for (int i = 0; i < a.ns && i < 4; ++i)
+    for (int j = 0; j < b.ns && j < 4; ++j)
+      if (a.comp[i] == b.comp[j]) return true;
+  return false;
+}
+// A scan k_pscan decodes on its block-streaming AC path (one component, destuffed reader).
+DHD bool scan_streams(const ScanRec& a, bool progressive) {
+  return progressive && a.ss > 0 && a.ns == 1 && a.restart_interval == 0;
+}
+// Block pipelining: scan i may follow the earlier scans that wrote its coefficients block by
+// block (instead of waiting for their whole level) when it and all of them stream the same
+// component's blocks in the same raster order.  deps: their sorted indices (rank).
+DHD bool prog_pipelined(const ScanRec* scans, int n, int i, bool progressive, uint64_t* deps) {
+  *deps = ~0ull;
+  if (!scan_streams(scans[i], progressive)) return false;
+  int nd = 0;
+  for (int j = 0; j < i; ++j) {
+    if (!scans_overlap(scans[j], scans[i])) continue;
+    if (nd == 8 || !scan_streams(scans[j], progressive) || scans[j].comp[0] != scans[i].comp[0]) {
+      *deps = ~0ull;
+      return false;
+    }
+    const uint64_t r = (uint64_t)prog_level_rank(scans, n, j);
+    *deps = (*deps & ~(0xFFull << (8 * nd))) | (r << (8 * nd));
+    ++nd;
+  }
+  return true;
+}
 constexpr int64_t kPScanOff = sizeof(PHdr);
 constexpr int64_t kPTabOff = kPScanOff + (int64_t)kMaxScans * sizeof(PScan);
 constexpr int kPMaxTabs = 32;  // distinct DHT tables an image's scans may use (more: host decode)
@@ -151,13 +195,6 @@ DHD int prog_table_slots(const ScanRec* scans, int n, int32_t* slot_off, uint8_t
   return ns;
 }
 
-// Dependency-level order of the scans (stable): rank of scan i.
-DHD int prog_level_rank(const ScanRec* scans, int n, int i) {
-  int r = 0;
-  for (int j = 0; j < n; ++j)
-    r += scans[j].level < scans[i].level || (scans[j].level == scans[i].level && j < i);
-  return r;
-}
 
 // ---------------------------------------------------------------------------
 // Scalar bit reader over the raw (stuffed) scan bytes: RawBits' semantics, bytes

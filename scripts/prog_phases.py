@@ -60,6 +60,10 @@ def main():
     for level in range(int(lv[:n].max()) + 1):
         idx = [i for i in range(n) if lv[i] == level]
         print(f"  level {level}: max scan {dur[:, idx].max():8.1f} us")
+    # per image: first scan start -> last scan end (the scans' critical path, with pipelining)
+    st, en = ph[:, :n, 0].astype(np.int64), ph[:, :n, 1].astype(np.int64)
+    span = (en.max(axis=1) - st.min(axis=1)) / 100.0
+    print(f"  image makespan (first scan start -> last scan end): mean {span.mean():8.1f} us, max {span.max():8.1f} us")
     eng.close()
 
 
