@@ -1205,7 +1205,7 @@ struct WaveCoefSink {
 
   __device__ __forceinline__ void flush() {  // (branch-free: see g_pscan_dummy)
     const bool act = lane < n, isor = (eval & 0x10000) != 0;
-    uint32_t* w = (act & isor) ? (uint32_t*)(coef + (eidx & ~1)) : &g_pscan_dummy[(blockIdx.x & 1023) * 64 + lane];
+    uint32_t* w = (act & isor) ? (uint32_t*)(coef + (eidx & ~1)) : &g_pscan_dummy[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & 1023) * 64 + lane];
     __hip_atomic_fetch_or(w, isor ? (uint32_t)(eval & 0xFFFF) << (16 * (eidx & 1)) : 0u, __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
     store16_if(store_rsrc(coef), act & !isor, eidx, (int16_t)eval);
@@ -1633,14 +1633,19 @@ __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, con
   pp.publish(mcx * mcy);
 }
 
-constexpr int kPScanThreads = 64;
+// Scan waves per workgroup: each wave takes its own tickets; the waves of one workgroup
+// sit on different SIMDs of the CU (DINO_PSCAN_WAVES, measured in profiles/r03_prog_*).
+#ifndef DINO_PSCAN_WAVES
+#define DINO_PSCAN_WAVES 4
+#endif
+constexpr int kPScanThreads = 64 * DINO_PSCAN_WAVES;
 __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restrict__ bytes,
                                                          const int64_t* __restrict__ offsets,
                                                          const int64_t* __restrict__ lengths,
                                                          const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
                                                          PCtl* __restrict__ pctl) {
-  __shared__ int16_t s_stage[16 * 64];
-  const int lane = threadIdx.x;
+  __shared__ int16_t s_stage[DINO_PSCAN_WAVES][16 * 64];
+  const int lane = threadIdx.x & 63;
   const DINO_CONST PCtl* cc = (const DINO_CONST PCtl*)pctl;
   const uint32_t nprog = cc->nprog;
   const uint32_t total = nprog * cc->max_scans;
@@ -1682,7 +1687,7 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
 #endif
     WaveCoefSink sink;
     sink.coef = (int16_t*)(ws + d->coef_off);
-    sink.stage = (DINO_LDS int16_t*)s_stage;
+    sink.stage = (DINO_LDS int16_t*)s_stage[threadIdx.x >> 6];
     sink.lane = lane;
     sink.natk = kNaturalOrder[lane];
     sink.n = 0;

@@ -14,7 +14,7 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
-LIB = ROOT / "build" / "lib_progph.so"
+LIB = Path(os.environ.get("DINO_PROGPH_LIB", str(ROOT / "build" / "lib_progph.so")))
 
 
 def main():
