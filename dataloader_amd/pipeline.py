@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import atexit
 import ctypes
+import itertools
 import os
 import queue
 import sys
@@ -244,7 +245,7 @@ class MI355XAugPipeline:
                  view_names: list[str] | None = None, host_fallback: bool = True,
                  multiscan_route: str = "auto", host_workers: int | None = None,
                  multiscan_host_max: int | None = None, prefetch: int | None = None,
-                 start_host_pool: bool = False, side_ahead: int = 24):
+                 start_host_pool: bool = False, side_ahead: int = 64):
         self._source = source
         self._aug_cfg = aug_cfg
         self._batch_size = int(batch_size)
@@ -546,7 +547,10 @@ class MI355XAugPipeline:
         if self._feed:
             return self._prepare_feed(block)
         if self._prefetcher is None:
-            self._prefetcher = _Prefetcher(self, self.prefetch_ahead)
+            # the side path's look-ahead fills from this queue: sized to it, so that the host
+            # half runs side_ahead batches ahead (a queue of prefetch_ahead would keep the
+            # look-ahead at that depth and each batch would wait for its own side decode)
+            self._prefetcher = _Prefetcher(self, self.prefetch_ahead + self._side_ahead)
         return self._prefetcher.get(block)
 
     def _side_submit(self, pb: _Prepared) -> None:
@@ -587,6 +591,14 @@ class MI355XAugPipeline:
                 self._ahead.append(pb)
             if not self._ahead:
                 raise StopIteration
+            # the pool launches when it holds min_images, or once its oldest batch is within
+            # half the look-ahead of its own launch (a decode then has those batches' time to
+            # finish; flushing at launch would make the batch wait for it)
+            urgent = min(len(self._ahead), max(1, self._side_ahead // 2))
+            if self._side is not None and any(pb.side is not None and pb.side.pending
+                                              for pb in itertools.islice(self._ahead, urgent)):
+                self._side.flush()
+                self.stats["side_urgent"] = self.stats.get("side_urgent", 0) + 1
             return self._ahead.popleft()
         finally:
             self.host_seconds["wait"] += time.perf_counter() - t0

@@ -113,10 +113,12 @@ class DeviceSideDecoder:
     def __init__(self, device: torch.device, max_images: int = 512, min_images: int | None = None,
                  engines: int | None = None, max_image_dim: int = 0):
         import os
-        # measured (scripts/route_study.py, 16 progressive per 256-image batch): pools of 16 images on
-        # 2 contexts 25.7k img/s; 1 image on 8: 18.8k; >= 32 images per launch: 2.4k (a long k_prog
-        # launch holds the hardware queue it shares with a slot's stream)
-        min_images = int(os.environ.get("DINO_SIDE_MIN", 16)) if min_images is None else min_images
+        # measured (scripts/route_study.py, 16 progressive per 256-image batch, dedicated queues,
+        # look-ahead 64, profiles/r03_side_pools.jsonl): pools of 16 images on 2 contexts 11.2k img/s,
+        # 64: 37.7k, 128: 53.2k, 256: 66.5k, 512: 74.3k.  One k_pscan launch of N progressive images
+        # takes ~30 ms up to N = 64 and 45 ms at N = 512 (scripts/prog_scale.py), so the pool waits
+        # for max_images, or until its oldest batch is half the look-ahead from its launch (pipeline.py)
+        min_images = int(os.environ.get("DINO_SIDE_MIN", max_images)) if min_images is None else min_images
         engines = int(os.environ.get("DINO_SIDE_ENGINES", 2)) if engines is None else engines
         self.cu_count = int(os.environ.get("DINO_SIDE_CUS", 0))
         self.timing = os.environ.get("DINO_SIDE_TIMING", "0") == "1"  # per-launch GPU spans (analysis)

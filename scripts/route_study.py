@@ -60,7 +60,7 @@ def main() -> None:
             stats = pipe.flush_stats()
             pipe.close()
             print(json.dumps({"k_progressive": k, "route": route, "batch": B, "images_per_s": round(n / dt, 1),
-                              "host_decoded": stats["host_decoded"], "side_decoded": stats.get("side_decoded"),
+                              "host_decoded": stats["host_decoded"], "side_decoded": stats.get("side_decoded"), "side_urgent": stats.get("side_urgent"),
                               "batches": args.batches, "warm": args.warm, "side_ahead": args.side_ahead,
                               "status": dict(stats["status"])}), flush=True)
 
