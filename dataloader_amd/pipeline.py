@@ -147,6 +147,7 @@ class _Prepared:
         self.spans = spans            # tario.BatchSpans: the batch stays in its page-locked shard ranges
         self.feed = feed              # tario.FeedBatch: the batch is packed in a native feed slot
         self.side = None              # progside.SideJob: its coefficient-buffer images, decoded ahead
+        self.side_submitted = False   # _side_submit ran (on the prefetch thread, or at the pull)
         self.jpegs = jpegs            # the source's list (None for the native feed)
         self.offsets = offsets
         self.info = info
@@ -556,6 +557,9 @@ class MI355XAugPipeline:
     def _side_submit(self, pb: _Prepared) -> None:
         """Start the side decode of the batch's coefficient-buffer images (progside.py)."""
         from . import progside
+        if pb.side_submitted:
+            return
+        pb.side_submitted = True
         m = progside.side_mask(pb.info)
         for i in pb.futures:
             m[i] = False

@@ -23,7 +23,7 @@ route (``tests/test_gpu_round3.py``).
 from __future__ import annotations
 
 import ctypes
-import struct
+import threading
 
 import numpy as np
 import torch
@@ -134,15 +134,18 @@ class DeviceSideDecoder:
         self._pool: list = []   # (job, batch index, JPEG bytes)
         self.launches = 0
         self.images = 0
+        # add (the prefetch thread) and flush (also the launch thread, for a batch about to launch)
+        self._lock = threading.RLock()
 
     def add(self, imgs: dict) -> SideJob | None:
         if not imgs:
             return None
         job = SideJob()
-        for i in sorted(imgs):
-            self._pool.append((job, int(i), imgs[i]))
-        if len(self._pool) >= self.min_images:
-            self.flush()
+        with self._lock:
+            for i in sorted(imgs):
+                self._pool.append((job, int(i), imgs[i]))
+            if len(self._pool) >= self.min_images:
+                self.flush()
         return job
 
     def _engine(self) -> _SideEngine:
@@ -160,9 +163,10 @@ class DeviceSideDecoder:
 
     def flush(self) -> None:
         """Decode the pending pool now (in mini-batches of at most ``max_images``)."""
-        while self._pool:
-            part, self._pool = self._pool[: self.max_images], self._pool[self.max_images:]
-            self._launch(part)
+        with self._lock, torch.cuda.device(self.device):
+            while self._pool:
+                part, self._pool = self._pool[: self.max_images], self._pool[self.max_images:]
+                self._launch(part)
 
     def _launch(self, part: list) -> None:
         se = self._engine()
@@ -181,19 +185,30 @@ class DeviceSideDecoder:
             d_info = eng.decode(d_bytes, d_off, len(items))
             status = torch.empty((len(items), 4), dtype=torch.int32, pin_memory=True)
             status.copy_(d_info, non_blocking=True)
+            # every decoded image's container is a 16-byte aligned slice of one device buffer;
+            # the headers go over in one copy and one scatter (per-image pinned headers and
+            # copies cost the launch thread ~10 us each)
             for k, (job, i, _) in enumerate(part):
                 job.rows[i] = k
-                st, w, h = int(info[k, 0]), int(info[k, 1]), int(info[k, 2])
-                if st != 0 or int(info[k, 3]) == 2:
-                    continue
-                c = torch.empty(16 + w * h * 3, dtype=torch.uint8, device=self.device)
-                hdr = torch.frombuffer(bytearray(struct.pack("<IIII", _lib.RAW_MAGIC, w, h, 0)),
-                                       dtype=torch.uint8).pin_memory()
-                heads.append(hdr)
-                c[:16].copy_(hdr, non_blocking=True)
-                _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(c.data_ptr() + 16), eng._s()),
-                           "dino_copy_rgb")
-                job.containers[i] = c
+            keep = [(k, job, i, int(info[k, 1]), int(info[k, 2])) for k, (job, i, _) in enumerate(part)
+                    if int(info[k, 0]) == 0 and int(info[k, 3]) != 2]
+            if keep:
+                start = np.zeros(len(keep) + 1, np.int64)
+                start[1:] = np.cumsum([(16 + w * h * 3 + 15) & ~15 for _, _, _, w, h in keep])
+                big = torch.empty(int(start[-1]), dtype=torch.uint8, device=self.device)
+                hdr = np.zeros((len(keep), 4), np.uint32)
+                hdr[:, 0] = _lib.RAW_MAGIC
+                hdr[:, 1] = [w for _, _, _, w, _ in keep]
+                hdr[:, 2] = [h for _, _, _, _, h in keep]
+                h_hdr = torch.from_numpy(hdr.view(np.uint8).reshape(-1)).pin_memory()
+                h_pos = torch.from_numpy((start[:-1, None] + np.arange(16)).reshape(-1)).pin_memory()
+                heads.extend((h_hdr, h_pos))
+                big[h_pos.to(self.device, non_blocking=True)] = h_hdr.to(self.device, non_blocking=True)
+                for (k, job, i, w, h), o in zip(keep, start[:-1]):
+                    o = int(o)
+                    _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(big.data_ptr() + o + 16), eng._s()),
+                               "dino_copy_rgb")
+                    job.containers[i] = big[o:o + 16 + w * h * 3]
             ev = torch.cuda.Event(enable_timing=self.timing)
             ev.record(se.stream)
             if self.timing:
@@ -217,10 +232,11 @@ class DeviceSideDecoder:
         if self.timing:
             import sys
             print("side launches (ms, images):", self.launch_ms(), file=sys.stderr)
-        self._pool.clear()
-        for e in self._engines:
-            e.close()
-        self._engines.clear()
+        with self._lock:
+            self._pool.clear()
+            for e in self._engines:
+                e.close()
+            self._engines.clear()
 
 
 def side_mask(info: np.ndarray) -> np.ndarray:
