@@ -755,11 +755,13 @@ class MI355XAugPipeline:
                         self._side.flush()
                     conts = pb.side.ready()
                     if conts:
+                        tm = time.perf_counter()
                         base = host_off.numpy() if host_off is not None else pb.offsets
                         d_bytes, d_offsets, d_lens, d_raw = self._merge_side(
                             pb.side, conts, d_bytes, int(base[-1]), base, raw, B)
                         side = conts
                         self.stats["side_decoded"] += len(conts)
+                        self.host_seconds["merge"] = self.host_seconds.get("merge", 0.0) + time.perf_counter() - tm
                 copied = torch.cuda.Event()
                 copied.record()
             self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw, sizes=sizes,

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import time
 
 import numpy as np
 import torch
@@ -134,6 +135,8 @@ class DeviceSideDecoder:
         self._pool: list = []   # (job, batch index, JPEG bytes)
         self.launches = 0
         self.images = 0
+        self.host_seconds = 0.0   # spent in _launch (pack, probe, launches; waits for a free context)
+        self.phase_seconds = {"engine": 0.0, "pack": 0.0, "probe": 0.0, "decode": 0.0, "containers": 0.0}
         # add (the prefetch thread) and flush (also the launch thread, for a batch about to launch)
         self._lock = threading.RLock()
 
@@ -169,11 +172,19 @@ class DeviceSideDecoder:
                 self._launch(part)
 
     def _launch(self, part: list) -> None:
+        t_start = time.perf_counter()
+        ph = self.phase_seconds
         se = self._engine()
+        t1 = time.perf_counter()
+        ph["engine"] += t1 - t_start
         eng = se.eng
         items = [j for _, _, j in part]
         hb, off = pack_jpegs(items, pin=True)
+        t2 = time.perf_counter()
+        ph["pack"] += t2 - t1
         info, ws, _ = fallback.probe(hb.data_ptr(), off.numpy(), len(items), self.max_image_dim)
+        t3 = time.perf_counter()
+        ph["probe"] += t3 - t2
         eng.reserve(ws, 0)
         heads = []
         with eng.on_stream():
@@ -188,6 +199,8 @@ class DeviceSideDecoder:
             # every decoded image's container is a 16-byte aligned slice of one device buffer;
             # the headers go over in one copy and one scatter (per-image pinned headers and
             # copies cost the launch thread ~10 us each)
+            t4 = time.perf_counter()
+            ph["decode"] += t4 - t3
             for k, (job, i, _) in enumerate(part):
                 job.rows[i] = k
             keep = [(k, job, i, int(info[k, 1]), int(info[k, 2])) for k, (job, i, _) in enumerate(part)
@@ -209,6 +222,7 @@ class DeviceSideDecoder:
                     _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(big.data_ptr() + o + 16), eng._s()),
                                "dino_copy_rgb")
                     job.containers[i] = big[o:o + 16 + w * h * 3]
+            ph["containers"] += time.perf_counter() - t4
             ev = torch.cuda.Event(enable_timing=self.timing)
             ev.record(se.stream)
             if self.timing:
@@ -219,6 +233,7 @@ class DeviceSideDecoder:
         se.keep = (hb, off, d_bytes, d_off, heads)
         self.launches += 1
         self.images += len(part)
+        self.host_seconds += time.perf_counter() - t_start
 
     def launch_ms(self) -> list:
         """(GPU ms, images) of every timed launch (DINO_SIDE_TIMING=1)."""

@@ -57,11 +57,17 @@ def main() -> None:
                     n += B
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
+            hs = {k: round(v * 1e3 / max(1, args.batches), 3) for k, v in pipe.host_seconds.items()}
+            side = getattr(pipe, "_side", None)
             stats = pipe.flush_stats()
             pipe.close()
             print(json.dumps({"k_progressive": k, "route": route, "batch": B, "images_per_s": round(n / dt, 1),
                               "host_decoded": stats["host_decoded"], "side_decoded": stats.get("side_decoded"), "side_urgent": stats.get("side_urgent"),
                               "batches": args.batches, "warm": args.warm, "side_ahead": args.side_ahead,
+                              "host_ms_per_batch": hs,
+                              "side_launches": getattr(side, "launches", None),
+                              "side_phase_ms_per_batch": {k: round(v * 1e3 / args.batches, 3) for k, v in side.phase_seconds.items()} if side else None,
+                              "side_host_ms_per_batch": round(side.host_seconds * 1e3 / args.batches, 3) if side else None,
                               "status": dict(stats["status"])}), flush=True)
 
 
