@@ -41,7 +41,7 @@ def main() -> None:
                 j[(t * B) // max(k, 1) + b % max(1, B // max(k, 1))] = prog[(b * k + t) % len(prog)]
             batches.append(j)
         for route in args.routes.split(","):
-            if k == 0 and route != "auto":
+            if k == 0 and route not in ("auto", "side"):
                 continue
             src = iter(batches)
             pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=1, depth=3, multiscan_route=route,
