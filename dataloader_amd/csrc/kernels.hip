@@ -1480,6 +1480,18 @@ __device__ __forceinline__ uint64_t fast_corrections(CleanReader& r, uint64_t c,
   }
   return corr;
 }
+// The same when the caller already holds the next pav bits (pw, MSB first): no new peek
+// when they suffice (a refinement symbol's code + sign leave >= 14 of its 32-bit peek).
+__device__ __forceinline__ uint64_t fast_corrections_p(CleanReader& r, uint64_t c, int lane, uint32_t pw, int pav) {
+  const int n = __builtin_popcountll(c);
+  if (!n) return 0;
+  if (n > pav) return fast_corrections(r, c, lane);
+  const uint32_t rank = lane_rank(c);  // < n <= 32 on the lanes of c
+  const uint64_t corr = ubal((((c >> lane) & 1u) != 0u) & (((pw >> ((31 - rank) & 31)) & 1u) != 0u));
+  r.skip(n);
+  return corr;
+}
+
 // Block pipelining between the AC scans of one component (prog_pipelined): a scan
 // publishes how many of its blocks are stored every kPipeBlocks blocks (release: the
 // wave's stores are complete and written back first), and a scan that reads what
@@ -1546,23 +1558,14 @@ __device__ __forceinline__ void fast_ac_refine(CleanReader& r, const VTab& t, co
         } else {
           used = len;
         }
+        r.skip(used);
         // stop: the (rr+1)-th position at or after k that was zero before the scan (rr = 0: the first)
         const uint64_t z = ~nzz & band & ~(uint64_t)low_bits(k);
         uint64_t hit = z;
         if (rr) hit = ubal((((z >> lane) & 1u) != 0u) & (lane_rank(z) == (uint32_t)rr));
         const int stop = hit ? __builtin_ctzll(hit) : se + 1;
-        // the correction bits follow the symbol: from the same peek when they fit (one skip
-        // for both; code + sign leave >= 15 of its 32 bits), else read after it
-        const uint64_t cm = nzz & (uint64_t)low_bits(stop) & ~(uint64_t)low_bits(k);
-        const int nc = __builtin_popcountll(cm);
-        if (nc <= 32 - used) {
-          const uint32_t pw = p << used;  // (used <= 17)
-          corr |= ubal((((cm >> lane) & 1u) != 0u) & (((pw >> ((31 - lane_rank(cm)) & 31)) & 1u) != 0u));
-          r.skip(used + nc);
-        } else {
-          r.skip(used);
-          corr |= fast_corrections(r, cm, lane);
-        }
+        corr |= fast_corrections_p(r, nzz & (uint64_t)low_bits(stop) & ~(uint64_t)low_bits(k), lane,
+                                   used < 32 ? p << used : 0u, 32 - used);
         k = stop;
         if (s) {
           const uint64_t bit = k < 64 ? 1ull << k : 1ull << 63;
