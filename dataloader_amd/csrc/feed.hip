@@ -22,8 +22,10 @@
 // took 0.9 ms per 512-image batch alone and 16 ms next to a Python-busy thread).
 #include <errno.h>
 #include <fcntl.h>
+#include <poll.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/inotify.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -34,6 +36,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -76,6 +79,79 @@ struct Shard {
     if (map) munmap(map, map_len);
   }
 };
+
+// The reference's _is_ready (shard_cache.py:331-340): the file exists and its header carries
+// the ready magic (written last by the node master, then tmp -> rename, :689-703).
+bool shard_ready(const std::string& path) {
+  const int fd = open(path.c_str(), O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return false;
+  uint64_t hdr[2] = {0, 0};
+  const ssize_t n = pread(fd, hdr, sizeof hdr, 0);
+  close(fd);
+  return n == (ssize_t)sizeof hdr && hdr[1] == kShardMagic;
+}
+
+// A non-master rank's wait for the node master's write (reference _inotify_wait,
+// shard_cache.py:373-449): check, watch the cache directory for IN_CLOSE_WRITE | IN_MOVED_TO,
+// check again (the rename may land between the check and the watch), then wake on events
+// until the file is ready or the timeout passes; stat-polls every 50 ms where inotify is
+// unavailable.  Wakes at least every 100 ms to observe `cancelled` (feed reset / destroy).
+// "" when ready, else the reason.
+std::string wait_shard(const std::string& path, int32_t timeout_ms, const std::function<bool()>& cancelled) {
+  if (shard_ready(path)) return "";
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  const size_t slash = path.rfind('/');
+  const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : path.substr(0, slash));
+  int ifd = inotify_init1(IN_NONBLOCK | IN_CLOEXEC);
+  int wd = ifd >= 0 ? inotify_add_watch(ifd, dir.c_str(), IN_CLOSE_WRITE | IN_MOVED_TO) : -1;
+  std::string err;
+  for (;;) {
+    if (shard_ready(path)) break;
+    if (cancelled()) {
+      err = "shard " + path + ": wait cancelled";
+      break;
+    }
+    const auto left = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now());
+    if (left.count() <= 0) {
+      char t[64];
+      snprintf(t, sizeof t, "%.0f", timeout_ms / 1000.0);
+      err = std::string("Timed out (") + t + "s) waiting for shard: " + path;
+      break;
+    }
+    if (wd >= 0) {
+      struct pollfd pf = {ifd, POLLIN, 0};
+      if (poll(&pf, 1, (int)std::min<int64_t>(left.count(), 100)) > 0) {
+        char buf[4096];
+        while (read(ifd, buf, sizeof buf) > 0) {
+        }
+      }
+    } else {
+      usleep((useconds_t)std::min<int64_t>(left.count(), 50) * 1000);
+    }
+  }
+  if (wd >= 0) inotify_rm_watch(ifd, wd);
+  if (ifd >= 0) close(ifd);
+  return err;
+}
+
+// Seeded in-shard sample order (the shuffle buffer of the extraction step, reference
+// hpc_source.py:461-467 -> _extract_jpegs_with_meta(shuffle_buffer=512, rng)): Fisher-Yates
+// over the shard's samples, keyed by (seed, epoch, shard path) with splitmix64.
+uint64_t splitmix64(uint64_t& x) {
+  uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+void shuffle_samples(std::vector<dino_tar_sample>& v, uint64_t seed, uint64_t epoch, const std::string& path) {
+  uint64_t h = 1469598103934665603ull;  // FNV-1a of the path
+  for (unsigned char c : path) h = (h ^ c) * 1099511628211ull;
+  uint64_t st = seed ^ (epoch * 0xD1B54A32D192ED03ull) ^ h;
+  for (size_t i = v.size(); i > 1; --i) {
+    const size_t j = (size_t)(splitmix64(st) % i);
+    std::swap(v[i - 1], v[j]);
+  }
+}
 
 // Opens, pre-faults and indexes one shard-cache file; "" on success, else the reason.
 std::string open_shard(Shard& s) {
@@ -236,6 +312,10 @@ struct dino_feed {
   int32_t batch = 0, max_dim = 0, lookahead = 2;
   dino_aug_config cfg{};
   bool have_cfg = false;
+  int32_t wait_ms = 0;                 // > 0: wait that long for a shard the node master has not written yet
+  bool shuffle = false;                // seeded in-shard sample order
+  uint64_t shuffle_seed = 0;
+  uint64_t epoch = 0;                  // epochs since create (the shuffle key)
   std::unique_ptr<CopyPool> pool;
   std::vector<Slot> slots;
   std::mutex m;
@@ -268,9 +348,19 @@ void dino_feed::opener_loop() {
     pending.pop_front();
     ++opening;
     const int64_t gen = generation;
+    const int32_t wait = wait_ms;
+    const bool shuf = shuffle;
+    const uint64_t seed = shuffle_seed, ep = epoch;
     lk.unlock();
     const double t0 = now_s();
-    std::string err = open_shard(*sh);
+    std::string err;
+    if (wait > 0)
+      err = wait_shard(sh->path, wait, [&] {
+        std::lock_guard<std::mutex> g(m);
+        return stop || gen != generation;
+      });
+    if (err.empty()) err = open_shard(*sh);
+    if (err.empty() && shuf) shuffle_samples(sh->samples, seed, ep, sh->path);
     const double dt = now_s() - t0;
     lk.lock();
     --opening;
@@ -491,6 +581,21 @@ int dino_feed_set_cfg(dino_feed* f, const dino_aug_config* cfg) {
   return DINO_OK;
 }
 
+int dino_feed_set_shard_wait(dino_feed* f, int32_t timeout_ms) {
+  if (!f) return feed_fail(DINO_EINVAL, "dino_feed_set_shard_wait: null feed");
+  std::lock_guard<std::mutex> g(f->m);
+  f->wait_ms = std::max(0, timeout_ms);
+  return DINO_OK;
+}
+
+int dino_feed_set_shuffle(dino_feed* f, int32_t enable, uint64_t seed) {
+  if (!f) return feed_fail(DINO_EINVAL, "dino_feed_set_shuffle: null feed");
+  std::lock_guard<std::mutex> g(f->m);
+  f->shuffle = enable != 0;
+  f->shuffle_seed = seed;
+  return DINO_OK;
+}
+
 int dino_feed_next(dino_feed* f, int32_t timeout_ms, dino_feed_batch* out) {
   if (!f || !out) return feed_fail(DINO_EINVAL, "dino_feed_next: bad arguments");
   std::unique_lock<std::mutex> lk(f->m);
@@ -571,6 +676,7 @@ int dino_feed_reset(dino_feed* f) {
   {
     std::lock_guard<std::mutex> g(f->m);
     ++f->generation;
+    ++f->epoch;
     f->pending.clear();
     f->opened.clear();
     f->epoch_end = f->epoch_done = false;

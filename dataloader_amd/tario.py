@@ -246,12 +246,55 @@ def write_shm_shard(shm: Path, data) -> None:
 
 
 def is_ready(shm: Path) -> bool:
+    """The file exists and carries the ready magic (reference ``_is_ready``, shard_cache.py:331-340)."""
     try:
         with open(shm, "rb") as f:
             hdr = f.read(HDR_SIZE)
         return len(hdr) == HDR_SIZE and struct.unpack(HDR_FMT, hdr)[1] == READY_MAGIC
     except OSError:
         return False
+
+
+_IN_CLOSE_WRITE, _IN_MOVED_TO, _IN_NONBLOCK, _IN_CLOEXEC = 0x8, 0x80, 0o4000, 0o2000000
+
+
+def wait_ready(shm: Path, timeout_s: float) -> None:
+    """Block until the node master has written ``shm`` (reference ``_inotify_wait``,
+    shard_cache.py:373-449): check, watch the cache directory for ``IN_CLOSE_WRITE |
+    IN_MOVED_TO``, check again (closes the race with a rename between the first check and
+    the watch), then wake on events; stat-polls every 50 ms where inotify is unavailable.
+    Raises ``TimeoutError`` after ``timeout_s`` seconds, as the reference does."""
+    import select
+    import time
+    shm = Path(shm)
+    if is_ready(shm):
+        return
+    deadline = time.monotonic() + timeout_s
+    ifd = wd = -1
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        ifd = libc.inotify_init1(_IN_NONBLOCK | _IN_CLOEXEC)
+        if ifd >= 0:
+            wd = libc.inotify_add_watch(ifd, str(shm.parent).encode(), _IN_CLOSE_WRITE | _IN_MOVED_TO)
+    except (OSError, AttributeError):
+        ifd = wd = -1
+    try:
+        while not is_ready(shm):
+            left = deadline - time.monotonic()
+            if left <= 0:
+                raise TimeoutError(f"Timed out ({timeout_s:.0f}s) waiting for shard: {shm}")
+            if wd >= 0:
+                r, _, _ = select.select([ifd], [], [], min(left, 1.0))
+                if r:
+                    with contextlib.suppress(OSError):
+                        os.read(ifd, 4096)
+            else:
+                time.sleep(min(left, 0.05))
+    finally:
+        if wd >= 0:
+            libc.inotify_rm_watch(ifd, wd)
+        if ifd >= 0:
+            os.close(ifd)
 
 
 class ShmShardCache:
@@ -263,10 +306,12 @@ class ShmShardCache:
     """
 
     def __init__(self, job_id: str = "dino", node_master: bool = True, max_gb: float = 128.0,
-                 base_dir: str | os.PathLike = "/dev/shm", max_mapped: int = 256) -> None:
+                 base_dir: str | os.PathLike = "/dev/shm", max_mapped: int = 256,
+                 shard_timeout_s: float = 300.0) -> None:
         self._base = Path(base_dir) / job_id
         self._base.mkdir(parents=True, exist_ok=True)
         self._node_master = node_master
+        self.shard_timeout_s = float(shard_timeout_s)  # how long a non-master rank waits for a shard (reference :507)
         self._max_bytes = int(max_gb * (1 << 30))
         self._lru: OrderedDict[str, int] = OrderedDict()
         self._total = 0
@@ -281,12 +326,24 @@ class ShmShardCache:
     def _path(self, shard_path: str) -> Path:
         return shm_path(self._base, shard_path)
 
+    @property
+    def node_master(self) -> bool:
+        return self._node_master
+
+    def path_of(self, shard_path: str) -> Path:
+        """The cache file of ``shard_path`` (it may not be written yet)."""
+        return self._path(shard_path)
+
     def _ensure(self, shard_path: str) -> Path:
+        """The ready cache file of ``shard_path``: the node master loads a missing shard; any
+        other rank waits for the master's write (reference get_view, shard_cache.py:588-603)
+        and raises ``TimeoutError`` after ``shard_timeout_s``."""
         shm = self._path(shard_path)
         if is_ready(shm):
             return shm
         if not self._node_master:
-            raise FileNotFoundError(f"shard {shard_path} not in the node cache ({shm})")
+            wait_ready(shm, self.shard_timeout_s)
+            return shm
         with open(shard_path, "rb") as f:
             data = f.read()
         self.put(shard_path, data)
@@ -633,9 +690,16 @@ class NativeShardFeed:
     ``next_prepared`` / ``copy`` / ``release``."""
 
     def __init__(self, cache: ShmShardCache, shard_paths: Sequence[str], batch_size: int, rank: int = 0,
-                 world: int = 1, nthreads: int = 8, slots: int = 6, lookahead: int = 2) -> None:
+                 world: int = 1, nthreads: int = 8, slots: int = 6, lookahead: int = 2,
+                 shuffle: bool = False, seed: int = 0) -> None:
         self._cache = cache
         self._paths = [p for i, p in enumerate(shard_paths) if i % world == rank]
+        # shuffle: the reference's per-epoch shard order (ShardIterator._make_shard_cycle,
+        # hpc_source.py:205, 263, 488-500: numpy default_rng(seed + rank [+ epoch * 997]).shuffle)
+        # and a seeded in-shard sample order (the extraction shuffle buffer, :461-467)
+        self._shuffle = bool(shuffle)
+        self._seed = int(seed) + int(rank)
+        self.epoch = 0
         self._B = int(batch_size)
         self.nthreads = int(nthreads)
         self._slots = max(2, int(slots))
@@ -665,14 +729,28 @@ class NativeShardFeed:
         if rc != 0:
             raise _lib.DinoError(f"{what} failed ({rc}): {_lib.load().dino_feed_last_error().decode(errors='replace')}")
 
+    def epoch_order(self, epoch: int | None = None) -> list[str]:
+        """This rank's shard order for ``epoch`` (the reference's shard cycle)."""
+        paths = list(self._paths)
+        if self._shuffle:
+            e = self.epoch if epoch is None else int(epoch)
+            np.random.default_rng(self._seed + e * 997).shuffle(paths)
+        return paths
+
     def _start(self) -> None:
         lib = _lib.load()
         if not self._feed:
             cfg = ctypes.byref(self._cfg) if self._cfg is not None else None
             self._check(lib.dino_feed_create(self._B, self.nthreads, self._slots, self._lookahead, self._max_dim, cfg,
                                              ctypes.byref(self._feed)), "dino_feed_create")
-        for p in self._paths:
-            self._check(lib.dino_feed_push(self._feed, str(self._cache._ensure(p)).encode()), "dino_feed_push")
+            if not self._cache.node_master:  # the opener waits for the node master's writes
+                self._check(lib.dino_feed_set_shard_wait(self._feed, int(self._cache.shard_timeout_s * 1000)),
+                            "dino_feed_set_shard_wait")
+            self._check(lib.dino_feed_set_shuffle(self._feed, int(self._shuffle), self._seed & (2**64 - 1)),
+                        "dino_feed_set_shuffle")
+        for p in self.epoch_order():
+            shm = self._cache._ensure(p) if self._cache.node_master else self._cache.path_of(p)
+            self._check(lib.dino_feed_push(self._feed, str(shm).encode()), "dino_feed_push")
         self._check(lib.dino_feed_end_epoch(self._feed), "dino_feed_end_epoch")
         self._started = True
 
@@ -717,10 +795,12 @@ class NativeShardFeed:
         return {"open_s": sec[0], "pack_s": sec[1], "slot_wait_s": sec[2], "sample_wait_s": sec[3],
                 "batches": cnt[0], "shards_done": cnt[1], "shards_failed": cnt[2]}
 
-    def reset(self) -> None:
-        """New epoch (the pushed shards and packed batches not yet handed out are dropped)."""
+    def reset(self, epoch: int | None = None) -> None:
+        """New epoch (the pushed shards and packed batches not yet handed out are dropped);
+        ``epoch`` defaults to the next one (reference ShardIterator.reset_epoch, :242-273)."""
         if self._feed:
             self._check(_lib.load().dino_feed_reset(self._feed), "dino_feed_reset")
+        self.epoch = self.epoch + 1 if epoch is None else int(epoch)
         self._started = False
 
     def close(self) -> None:

@@ -379,6 +379,15 @@ int dino_feed_destroy(dino_feed* feed);
 int dino_feed_push(dino_feed* feed, const char* shard_cache_path);
 int dino_feed_end_epoch(dino_feed* feed);
 int dino_feed_set_cfg(dino_feed* feed, const dino_aug_config* cfg);
+/* Non-master ranks: wait up to timeout_ms for a pushed shard-cache file the node master has
+ * not written yet (reference NodeSharedShardCache.get_view -> _inotify_wait,
+ * shard_cache.py:596-603, :373-449: inotify on the cache directory, stat-poll fallback);
+ * a shard still missing then is reported as DINO_FEED_SHARD_ERROR ("Timed out ...") and
+ * skipped (hpc_source.py:358-366).  0 (default): a shard must be ready when opened. */
+int dino_feed_set_shard_wait(dino_feed* feed, int32_t timeout_ms);
+/* enable != 0: each shard's samples are taken in a seeded random order keyed by (seed, epoch,
+ * shard path) (the extraction step's shuffle buffer, hpc_source.py:461-467). */
+int dino_feed_set_shuffle(dino_feed* feed, int32_t enable, uint64_t seed);
 /* Next packed batch in order (blocks up to timeout_ms; < 0: forever). */
 int dino_feed_next(dino_feed* feed, int32_t timeout_ms, dino_feed_batch* out);
 /* H2D copies of a handed-out slot (bytes, offsets) on `stream`; the slot is reused after they retire. */

@@ -165,14 +165,16 @@ def test_shm_cache_format_and_views(tmp_path):
     arr = cache.get_array(str(src))
     assert arr.tobytes() == tar and len(tario.index_tar(arr)) == 5
     assert cache.get(str(src)) == tar and 0 < cache.utilisation < 1
-    # a reader that is not the node master fails on a missing shard; a corrupt magic is refused
-    other = tario.ShmShardCache(job_id="job", base_dir=tmp_path, node_master=False)
-    with pytest.raises(FileNotFoundError):
+    # a reader that is not the node master waits for the master's write and times out on a
+    # missing shard; a corrupt magic is "not ready" (reference _is_ready / _inotify_wait)
+    other = tario.ShmShardCache(job_id="job", base_dir=tmp_path, node_master=False, shard_timeout_s=0.2)
+    with pytest.raises(TimeoutError, match="waiting for shard"):
         other.get(str(tmp_path / "missing.tar"))
     bad = tmp_path / "job" / hashlib.sha1(b"bad").hexdigest()[:16]
     bad.write_bytes(struct.pack("QQ", 3, 0xDEADBEEFCAFEF00D - 1) + b"abc")
-    with pytest.raises(FileNotFoundError):
+    with pytest.raises(TimeoutError):
         other.get("bad")                                        # not ready: the magic is the ready flag
+    assert other.get(str(src)) == tar                           # written by the master: no wait
     cache.close(remove=True)
     assert not shm.exists()
 
@@ -339,4 +341,142 @@ def test_native_feed_batches_epochs_and_errors(tmp_path, nthreads):
             feed.release(fb)
     assert n == (7 + 9 + 6 + 8) // 4 and feed.shard_errors and feed.stats()["shards_failed"] == 1
     feed.close()
+    cache.close(remove=True)
+
+
+def _feed_reader(base, job, paths, rank, world, timeout_s, q):
+    """A non-master rank (spawned process): drive NativeShardFeed over the node cache while the
+    master is still writing it; report the bytes of every batch."""
+    from dataloader_amd import tario as t
+    cache = t.ShmShardCache(job_id=job, base_dir=base, node_master=False, shard_timeout_s=timeout_s)
+    feed = t.NativeShardFeed(cache, paths, 4, rank=rank, world=world, nthreads=2, slots=3)
+    out = []
+    try:
+        while True:
+            try:
+                fb = feed.next_prepared(timeout=60.0)
+            except StopIteration:
+                break
+            if fb is None:
+                out = "stalled"
+                break
+            out.append(b"".join(fb.jpegs()))
+            feed.release(fb)
+        q.put((rank, out, list(feed.shard_errors)))
+    finally:
+        feed.close()
+        cache.close()
+
+
+def _expected_batches(tmp_path, shards, paths, rank, world):
+    """Batches of a pre-written cache (the master's view), the bar for the waiting readers."""
+    cache = tario.ShmShardCache(job_id="prewritten", base_dir=tmp_path)
+    for p, t in zip(paths, shards):
+        cache.put(p, t)
+    feed = tario.NativeShardFeed(cache, paths, 4, rank=rank, world=world, nthreads=2, slots=3)
+    out = []
+    while True:
+        try:
+            fb = feed.next_prepared(timeout=10.0)
+        except StopIteration:
+            break
+        out.append(b"".join(fb.jpegs()))
+        feed.release(fb)
+    feed.close()
+    cache.close(remove=True)
+    return out
+
+
+def test_non_master_ranks_wait_for_the_node_master(tmp_path):
+    """Row f2 (reference shard_cache.py:588-603, :373-449, master = local rank 0, loader.py:467):
+    two non-master processes drive the native feed over a node cache that the master (this
+    process) writes shard by shard with a delay; each gets every batch bit-identical to a
+    pre-written cache.  A shard the master never writes times out and is skipped with a warning
+    (hpc_source.py:358-366)."""
+    import multiprocessing as mp
+    import time
+    shards = [make_shard(n, seed=60 + k) for k, n in enumerate([9, 6, 8, 7])]
+    paths = [f"/lustre/ds/shard-{k:03d}.tar" for k in range(4)]
+    expect = {r: _expected_batches(tmp_path, shards, paths, r, 2) for r in range(2)}
+    master = tario.ShmShardCache(job_id="live", base_dir=tmp_path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_feed_reader, args=(tmp_path, "live", paths, r, 2, 60.0, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    try:
+        time.sleep(1.0)                                  # readers are up and waiting on the first shards
+        for p, t in zip(paths, shards):
+            master.put(p, t)
+            time.sleep(0.3)
+        got = {}
+        for _ in procs:
+            r, batches, errs = q.get(timeout=120)
+            got[r] = (batches, errs)
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+    for r in range(2):
+        batches, errs = got[r]
+        assert errs == [] and batches == expect[r] and len(batches) > 0, r
+    # a shard the master never writes: the waiting reader times out on it, skips it, goes on
+    reader = tario.ShmShardCache(job_id="live", base_dir=tmp_path, node_master=False, shard_timeout_s=0.5)
+    feed = tario.NativeShardFeed(reader, paths[:2] + ["/lustre/ds/never.tar"] + paths[2:], 4, nthreads=2)
+    n = 0
+    with pytest.warns(RuntimeWarning, match="Timed out"):
+        while True:
+            try:
+                fb = feed.next_prepared(timeout=30.0)
+            except StopIteration:
+                break
+            n += 1
+            feed.release(fb)
+    assert n == sum(len(oracle_samples(t)) for t in shards) // 4 and len(feed.shard_errors) == 1
+    feed.close()
+    with pytest.raises(TimeoutError):
+        with reader.get_view("/lustre/ds/never.tar"):
+            pass
+    master.close(remove=True)
+
+
+def test_native_feed_shuffle_orders(tmp_path):
+    """shuffle=True: the reference's per-epoch shard order (numpy default_rng(seed + rank +
+    epoch * 997).shuffle, hpc_source.py:263, 488-500) and a seeded in-shard order; the same
+    samples per epoch, a different order per epoch, the same order for the same (seed, epoch)."""
+    shards = [make_shard(n, seed=80 + k) for k, n in enumerate([8, 8, 8, 8, 8])]
+    cache = tario.ShmShardCache(job_id="shuf", base_dir=tmp_path)
+    paths = [f"/d/s{k}.tar" for k in range(5)]
+    for p, t in zip(paths, shards):
+        cache.put(p, t)
+
+    def epoch_imgs(feed):
+        got = []
+        while True:
+            try:
+                fb = feed.next_prepared(timeout=10.0)
+            except StopIteration:
+                break
+            got += fb.jpegs()
+            feed.release(fb)
+        return got
+
+    f1 = tario.NativeShardFeed(cache, paths, 4, nthreads=2, shuffle=True, seed=5)
+    f2 = tario.NativeShardFeed(cache, paths, 4, nthreads=2, shuffle=True, seed=5)
+    order = list(paths)
+    np.random.default_rng(5).shuffle(order)
+    assert f1.epoch_order() == order
+    e0 = epoch_imgs(f1)
+    f1.reset()
+    e1 = epoch_imgs(f1)
+    assert e0 == epoch_imgs(f2)                          # deterministic
+    allimgs = sorted(img for t in shards for _, img, _ in oracle_samples(t))
+    assert sorted(e0) == sorted(e1) == allimgs and e0 != e1
+    plain = [img for p in order for _, img, _ in oracle_samples(shards[paths.index(p)])]
+    assert e0 != plain                                   # samples shuffled inside each shard
+    first = {img for _, img, _ in oracle_samples(shards[paths.index(order[0])])}
+    assert set(e0[:8]) == first                          # ... but shard by shard
+    for f in (f1, f2):
+        f.close()
     cache.close(remove=True)
