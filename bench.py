@@ -410,18 +410,30 @@ def run_leg(pipe, d_bytes, d_off, n_img: int, B: int, steps: int, warmup: int, w
         if maskgen is not None:  # one mask per batch, broadcast to [B, H*W] (loader.py:585-590)
             maskgen.generate(1).expand(B, -1)
 
+    # every batch's per-image status ([B, 4] int32 from the batch's own kernels) goes to a pinned
+    # row asynchronously on the batch's stream, inside the timed region (an 8 KiB copy per
+    # batch); all of them are checked afterwards: a timed batch with a zero-filled image
+    # (anything but the reference's own corrupt -> zeros, cpu.py:250-253, none of which the
+    # synthetic sets hold) fails the leg instead of raising its rate unseen
+    n_rows = warmup + 2 * steps
+    status = torch.zeros((n_rows, B, 4), dtype=torch.int32, pin_memory=True)
+
+    def record_status(k: int):
+        sl = pipe._last
+        with sl.engine.on_stream():
+            status[k].copy_(sl.info, non_blocking=True)
+
     for k in range(warmup):
         step(k)
+        record_status(k)
     torch.cuda.synchronize()
-    st = pipe.last_status()
-    if (st != 0).any():
-        raise RuntimeError(f"decode failures in warmup batch: {np.unique(st, return_counts=True)}")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
         step(warmup + k)
+        record_status(warmup + k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -433,12 +445,22 @@ def run_leg(pipe, d_bytes, d_off, n_img: int, B: int, steps: int, warmup: int, w
         t_ser = time.perf_counter()
         for k in range(steps):
             step(warmup + steps + k)
+            record_status(warmup + steps + k)
             torch.cuda.synchronize()
         out["t_ser"] = time.perf_counter() - t_ser
         out["ktimes"] = pipe.kernel_times()
         pipe.set_timing(False)
         k_last = warmup + 2 * steps - 1  # the batch the last slot still holds
         out["last_batch"] = (k_last % n_batches) * B
+    rows = warmup + steps * (2 if serial else 1)
+    st = status[:rows, :, 0].numpy()
+    if (st != 0).any():
+        codes, counts = np.unique(st[st != 0], return_counts=True)
+        bad_rows = sorted(set(np.nonzero(st)[0].tolist()))
+        raise RuntimeError(f"bench: {int((st != 0).sum())} image(s) not decoded in batches {bad_rows[:8]} "
+                           f"(status codes {dict(zip(codes.tolist(), counts.tolist()))})")
+    out["statuses_checked"] = int(steps * B)            # the timed batches' images, all status 0
+    out["statuses_checked_total"] = int(rows * B)        # + warm-up + serialized pass
     out["recs"] = pipe.last_params()
     return out
 
@@ -467,7 +489,8 @@ def summarize(leg: dict, ab: dict, B: int, steps: int, world: int, tag: str) -> 
                   for k, (ms, n) in leg["ktimes"].items()}
     traffic, traffic_src = load_traffic(tag)
     out = {"value": round(world * steps * B / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
-           "mean_jpeg_bytes": round(ab["s_jpeg"]), "mean_pixels": round(ab["pixels"])}
+           "mean_jpeg_bytes": round(ab["s_jpeg"]), "mean_pixels": round(ab["pixels"]),
+           "statuses_checked": leg.get("statuses_checked"), "statuses_checked_total": leg.get("statuses_checked_total")}
     if per_kernel:
         dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
         # algorithmic bytes per image = S_jpeg + sum over views of 3 S^2 x out bytes;
@@ -615,6 +638,7 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
         if bad:
             raise RuntimeError(f"e2e decode failures: {bad}")
         res = {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
+               "statuses_checked": int(st["images"]), "batches_accounted": int(st["batches"]),
                "e2e_ms_per_step": round(dt / args.steps * 1e3, 3),
                "e2e_shard_prepare_ms_total": round(getattr(feeder, "index_seconds", 0.0) * 1e3, 3),
                "e2e_shard_wait_ms_total": round(getattr(feeder, "wait_seconds", 0.0) * 1e3, 3),
@@ -637,6 +661,88 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
         return res
     finally:
         cache.close(remove=True)
+
+
+class _ProgMixSource:
+    """A callable source with the reference's conventions (``_batch_size``, ``_resolution_src``;
+    _ReaderAdapter.__call__, shard_reader.py:346-376): batch k holds the C2 images with one
+    image in every ``1 / prog_frac`` replaced by a progressive encode (a different set each batch)."""
+
+    def __init__(self, base, prog, B: int, prog_frac: float, n_batches: int):
+        self._base, self._prog, self._B = base, prog, B
+        self._every = max(1, int(round(1.0 / prog_frac)))
+        self._n = n_batches
+        self._k = 0
+        self._batch_size = B
+        self._resolution_src = None
+        self.progressive_pulled = 0
+
+    def __call__(self):
+        if self._k >= self._n:
+            raise StopIteration
+        k, B = self._k, self._B
+        self._k += 1
+        out = [self._base[(k * B + i) % len(self._base)] for i in range(B)]
+        t = 0
+        for i in range(k % self._every, B, self._every):
+            out[i] = self._prog[(k * 61 + t) % len(self._prog)]
+            t += 1
+        self.progressive_pulled += t
+        return out
+
+
+def run_prog_leg(args, uniq, uniq_prog, rank: int, world: int, cfg, B: int, dist) -> dict:
+    """Progressive mix through the drop-in path: ``MI355XBackend.build_pipeline``
+    + ``build_pipeline_iterator`` with the backend's default routing, on C2 batches in which one
+    image in 16 is a progressive JPEG (16 per 256; web datasets hold such files, the GPU peer
+    decodes them on the device, reference pipeline.py:429-434).  Host-fed (the source returns
+    JPEG byte lists, as _ReaderAdapter does); the warm-up fills the side look-ahead first."""
+    import torch
+
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import DinoV2AugSpec, PipelineConfig
+
+    pcfg = PipelineConfig(device_id=torch.cuda.current_device(), seed=4321 + rank, gpu_queue=args.gpu_queue)
+    backend = MI355XBackend()
+    warm = max(args.warmup, 2 * int(getattr(pcfg, "cpu_queue", 16)))
+    steps = max(args.steps, 64)
+    src = _ProgMixSource(uniq, uniq_prog, B, args.prog_mix, warm + steps + 64)
+    spec = DinoV2AugSpec(aug_cfg=cfg)
+    pipe = backend.build_pipeline(src, spec, pcfg, None)
+    it = backend.build_pipeline_iterator(pipe, spec, spec.output_map, B)
+    try:
+        for _ in range(warm):
+            out = next(it)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = next(it)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        assert len(out) == 1 and len(out[0]) == cfg.n_views
+        st = pipe.flush_stats()
+        bad = {k: v for k, v in st["status"].items() if k != 0}
+        if bad:
+            raise RuntimeError(f"c2_prog decode failures: {bad}")
+        handed = warm + steps
+        prog_handed = sum(len(range(k % src._every, B, src._every)) for k in range(handed))
+        return {"value": round(world * steps * B / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+                "steps": steps, "warmup": warm, "progressive_per_batch": len(range(0, B, src._every)),
+                "progressive_frac": round(1.0 / src._every, 5),
+                "route": pipe._multiscan_route, "side_ahead": pipe._side_ahead, "batches_in_flight": pipe.depth,
+                "statuses_checked": int(st["images"]), "batches_accounted": int(st["batches"]),
+                "side_decoded": int(st["side_decoded"]), "host_decoded": int(st["host_decoded"]),
+                "progressive_handed_over": prog_handed,
+                "host_ms_per_batch": {k: round(v * 1e3 / max(1, handed), 3) for k, v in pipe.host_seconds.items()},
+                "workload": f"C2 (640x480 q85, B = {B}) with one image in {src._every} a progressive encode "
+                            f"({len(uniq_prog)} distinct), host-fed through MI355XBackend.build_pipeline "
+                            "(default route) + build_pipeline_iterator"}
+    finally:
+        pipe.close()
 
 
 # ----------------------------------------------------------------------------- main
@@ -678,6 +784,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--e2e-in-flight", type=int, default=3, help="MI355XBackend(max_in_flight) of the e2e leg")
     ap.add_argument("--e2e-feed", default="native", choices=["native", "python"],
                     help="e2e host half: the native shard feed (C++ threads) or the Python prefetch thread")
+    ap.add_argument("--prog-mix", type=float, default=1.0 / 16,
+                    help="c2_prog leg: share of progressive images per batch (0: skip the leg)")
     return ap
 
 
@@ -763,6 +871,8 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
         uniq_c3 = make_unique(args.extra_unique, 0, 0, 11 + rank, True, procs) if not args.mixed else None
         uniq_dri = make_unique(args.extra_unique, args.width, args.height, 21 + rank, False, procs, 0.0, 4) \
             if not args.restart_mcus else None
+        uniq_prog = make_unique(64, args.width, args.height, 31 + rank, False, procs, 1.0) \
+            if args.prog_mix > 0 and not args.mixed else None
 
     import torch
     devices = visible_devices()
@@ -867,6 +977,11 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
             p.close()
             legs["c2_dri"] = dict(s_dri, workload=f"C2 with restart markers every 4 MCUs (DRI), "
                                                   f"{args.extra_unique} distinct encodes, {args.dtype} out")
+        if uniq_prog is not None:
+            print("bench: c2_prog leg", file=sys.stderr, flush=True)
+            torch.cuda.empty_cache()
+            legs["c2_prog"] = run_prog_leg(args, uniq, uniq_prog, rank, world, cfg, B, dist)
+            legs["c2_prog"]["vs_c2"] = round(legs["c2_prog"]["value"] / (world * args.steps * B / dt), 4)
     e2e = None
     if args.e2e or extras:
         print("bench: e2e leg", file=sys.stderr, flush=True)
@@ -898,6 +1013,7 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
             "roofline_kernels": summ.get("roofline_kernels"),
             "path_roofline": summ.get("path_roofline"),
             "kernels_ms_per_step": summ.get("kernels_ms_per_step"),
+            "statuses_checked": summ.get("statuses_checked"),
             "serialized_ms_per_step": summ.get("serialized_ms_per_step"),
             "cpu_baseline": cpu,
         }

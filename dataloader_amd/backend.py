@@ -155,12 +155,32 @@ class MI355XBackend:
     WS_PER_IMAGE = 4 << 20
 
     def __init__(self, max_image_dim: int = 0, workspace_bytes: int = 0, max_in_flight: int = 3,
-                 hbm_fraction: float = 0.15, host_workers: int | None = None) -> None:
+                 hbm_fraction: float = 0.15, host_workers: int | None = None, multiscan_route: str = "side",
+                 side_ahead: int | None = None) -> None:
         self._max_image_dim = max_image_dim
         self._workspace_bytes = workspace_bytes
         self._max_in_flight = max(1, int(max_in_flight))
         self._hbm_fraction = float(hbm_fraction)
         self._host_workers = host_workers
+        # progressive / multi-scan JPEGs: decoded on the device ahead of their batch ("side",
+        # default; the GPU peer decodes every flavour on the device, reference pipeline.py:429-434);
+        # Pillow only for what the device decoder does not implement (MI355XAugPipeline)
+        self._multiscan_route = multiscan_route
+        self._side_ahead = side_ahead  # None: PipelineConfig.cpu_queue (see side_look_ahead)
+
+    def side_look_ahead(self, pipeline_cfg: Any, source: Any, depth: int) -> int:
+        """Batches the side route pulls ahead of their launch: DALI's CPU prefetch queue
+        (``PipelineConfig.cpu_queue``, 16 by default, reference config.py:166, pipeline.py:317
+        fills it by calling the source ahead), capped so that everything pulled and not yet
+        handed over (look-ahead + prefetch queue + batches in flight) fits the source's
+        metadata FIFO (``_ReaderAdapter._meta_queue``, 64 slots, shard_reader.py:98, 357-375:
+        an overflow raises)."""
+        want = self._side_ahead if self._side_ahead is not None else int(getattr(pipeline_cfg, "cpu_queue", 16) or 16)
+        mq = getattr(source, "_meta_queue", None)
+        cap = getattr(mq, "maxsize", 0) or 0
+        if cap > 0:
+            want = min(want, cap - depth - 6)  # 4 in the prefetch queue, 1 being prepared, 1 spare
+        return max(1, int(want))
 
     def queue_depth(self, pipeline_cfg: Any, batch_size: int, n_views: int = 10, max_crop: int = 224) -> int:
         """Batches in flight for ``pipeline_cfg.gpu_queue``, capped by ``max_in_flight`` and by
@@ -232,6 +252,7 @@ class MI355XBackend:
         batch = getattr(source, "_batch_size", 1)
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size))
+        depth = self.queue_depth(pipeline_cfg, batch, aug_cfg.n_views, max_crop)
         return MI355XAugPipeline(
             source=source,
             aug_cfg=aug_cfg,
@@ -244,10 +265,12 @@ class MI355XBackend:
             workspace_bytes=self._workspace_bytes or batch * self.WS_PER_IMAGE,
             norm=norm,
             view_names=names,
-            depth=self.queue_depth(pipeline_cfg, batch, aug_cfg.n_views, max_crop),
+            depth=depth,
             prefetch=1,
             host_workers=self._host_workers,
             start_host_pool=True,
+            multiscan_route=self._multiscan_route,
+            side_ahead=self.side_look_ahead(pipeline_cfg, source, depth),
         )
 
     def build_pipeline_iterator(self, pipeline: Any, aug_spec: Any, output_map: list[str],

@@ -85,12 +85,14 @@ class IngestEngine:
         self.last_batch = batch
         return info
 
-    def copy_from_host(self, d_dst: torch.Tensor, dst_off: int, host_addr: int, nbytes: int) -> None:
+    def copy_from_host(self, d_dst: torch.Tensor, dst_off: int, host_addr: int, nbytes: int,
+                       stream: torch.cuda.Stream | None = None) -> None:
         """Asynchronous DMA of ``nbytes`` at host address ``host_addr`` (page-locked) into
-        ``d_dst[dst_off:]`` on this engine's stream (``dino_copy_h2d``)."""
+        ``d_dst[dst_off:]`` on ``stream`` (default: this engine's stream; ``dino_copy_h2d``)."""
         assert 0 <= dst_off and dst_off + nbytes <= d_dst.numel() * d_dst.element_size()
+        s = ctypes.c_void_p(stream.cuda_stream) if stream is not None else self._s()
         _lib.check(self.lib.dino_copy_h2d(ctypes.c_void_p(d_dst.data_ptr() + dst_off), ctypes.c_void_p(host_addr),
-                                          int(nbytes), self._s()), "dino_copy_h2d")
+                                          int(nbytes), s), "dino_copy_h2d")
 
     def copy_rgb(self, index: int, width: int, height: int) -> torch.Tensor:
         with self.on_stream():

@@ -55,6 +55,19 @@ def _out_code(out_dtype) -> int:
     return _DTYPES.get(out_dtype, OUT_BF16)
 
 
+def _unshared(t: torch.Tensor) -> bool:
+    """Nothing outside the pipeline holds ``t`` or its memory: the tensor object is referenced
+    only by the slot's view cache list, its outputs dict and the caller's loop variable (plus
+    the call's argument, this parameter and getrefcount's own), and its storage only by ``t``
+    (a view, slice or chunk the caller kept shares the storage and raises its use count)."""
+    if sys.getrefcount(t) > 6:
+        return False
+    use_count = getattr(torch._C, "_storage_Use_Count", None)
+    if use_count is None:  # no way to see views: never reuse
+        return False
+    return use_count(t.untyped_storage()._cdata) <= 2  # t + the temporary storage object
+
+
 class _Slot:
     """One in-flight batch: an engine (ctx + stream) and the batch's small buffers."""
 
@@ -154,6 +167,11 @@ class _Prepared:
         self.ws, self.aws = ws, aws
         self.sizes = sizes            # (G, L) the augment-workspace bound was computed for
         self.futures = futures
+        # side look-ahead: the batch's input copied to HBM when it entered the look-ahead (its
+        # pinned staging / feed slot / shard ranges are free again); ready after `copied`
+        self.dev = None               # (d_bytes, d_offsets, d_lens or None)
+        self.lens = None              # host image lengths of a spans batch staged on the device
+        self.copied: torch.cuda.Event | None = None
 
 
 _END = object()
@@ -289,7 +307,8 @@ class MI355XAugPipeline:
         if self._side_ahead:
             self.prefetch_ahead = max(1, self.prefetch_ahead)
         self._prefetcher: _Prefetcher | None = None
-        self._ring = _StagingRing(self.depth + self.prefetch_ahead + self._side_ahead + 2)
+        # the side look-ahead holds its batches in HBM (``_stage_on_device``), not in staging
+        self._ring = _StagingRing(self.depth + self.prefetch_ahead + (4 if self._side_ahead else 0) + 2)
         self._native = hasattr(source, "next_spans")
         # the feed can hand batches over where they lie (page-locked shard ranges, DMA'd as they are)
         self._spans_feed = hasattr(source, "next_batch_spans")
@@ -298,7 +317,7 @@ class MI355XAugPipeline:
         self._held: deque = deque()   # the feed's next batch, prepared one ahead (Pillow hand-overs start early)
         # H2D copies of the native feed's batches, off the slots' streams (DINO_COPY_STREAM=0: on them)
         self._copy_stream = None
-        if self._feed and depth > 1 and os.environ.get("DINO_COPY_STREAM", "1") != "0":
+        if (self._feed and depth > 1 and os.environ.get("DINO_COPY_STREAM", "1") != "0") or self._side_ahead:
             self._copy_stream = torch.cuda.Stream(device=device)
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
@@ -422,8 +441,7 @@ class MI355XAugPipeline:
         allocator's record_stream rule, applied at reuse)."""
         key = (batch, cfg.n_global, cfg.n_local, cfg.global_size, cfg.local_size, cfg.out_dtype)
         vc = sl.view_cache
-        # held by the cache list, the slot's outputs dict, the loop variable and getrefcount's argument
-        if vc is not None and vc[0] == key and all(sys.getrefcount(t) <= 4 for t in vc[1]):
+        if vc is not None and vc[0] == key and all(_unshared(t) for t in vc[1]):
             if sl.consumer is not None and sl.engine.stream is not None:
                 ev = torch.cuda.Event()
                 ev.record(sl.consumer)
@@ -548,10 +566,11 @@ class MI355XAugPipeline:
         if self._feed:
             return self._prepare_feed(block)
         if self._prefetcher is None:
-            # the side path's look-ahead fills from this queue: sized to it, so that the host
-            # half runs side_ahead batches ahead (a queue of prefetch_ahead would keep the
-            # look-ahead at that depth and each batch would wait for its own side decode)
-            self._prefetcher = _Prefetcher(self, self.prefetch_ahead + self._side_ahead)
+            # the side path's look-ahead fills from this queue, which _pull_side drains at every
+            # launch: a queue longer than prefetch_ahead lets the look-ahead grow by up to 4
+            # batches per launch (a queue of 1 would keep it where it starts) without pulling
+            # many more batches from the source than the look-ahead holds
+            self._prefetcher = _Prefetcher(self, self.prefetch_ahead + min(self._side_ahead, 4))
         return self._prefetcher.get(block)
 
     def _side_submit(self, pb: _Prepared) -> None:
@@ -573,10 +592,62 @@ class MI355XAugPipeline:
         elif pb.feed is not None:
             o = pb.feed.offsets
             imgs = {int(i): ctypes.string_at(pb.feed.host + int(o[i]), int(o[i + 1] - o[i])) for i in idx}
+        elif pb.spans is not None:  # a batch left where it lies (page-locked shard ranges): never packed
+            imgs = {int(i): ctypes.string_at(int(pb.spans.ptrs[i]), int(pb.spans.lens[i])) for i in idx}
         else:
             hb, o = pb.staging.buf.numpy(), pb.offsets
             imgs = {int(i): hb[o[i]:o[i + 1]].tobytes() for i in idx}
         pb.side = self._side.add(imgs)
+
+    def _stage_on_device(self, pb: _Prepared) -> None:
+        """Copy a batch that joins the side look-ahead to HBM now, on the copy stream, and free
+        its host buffer (pinned staging, native feed slot, page-locked shard ranges) once the
+        copy retires: the look-ahead is up to ``side_ahead`` batches deep, and holding them in
+        host buffers would take that many pinned batches.  A batch waiting for Pillow
+        hand-overs stays on the host (it is re-packed at launch)."""
+        if pb.futures or pb.dev is not None:
+            return
+        cs = self._copy_stream
+        B = len(pb.offsets) - 1
+        d_lens = None
+        with torch.cuda.stream(cs):
+            if pb.feed is not None:
+                fb = pb.feed
+                d_bytes = torch.empty(max(fb.nbytes, 1) + 64, dtype=torch.uint8, device=self.device)
+                d_off = torch.empty(B + 1, dtype=torch.int64, device=self.device)
+                try:
+                    self._source.copy(fb, d_bytes.data_ptr(), d_off.data_ptr(), cs.cuda_stream)
+                except BaseException:
+                    self._source.release(fb)
+                    raise
+                finally:
+                    pb.feed = None  # the slot returns to the packer when this copy retires
+            elif pb.spans is not None:
+                nbytes = int(pb.spans.offsets[-1])
+                d_bytes = torch.empty(max(nbytes, 1) + 64, dtype=torch.uint8, device=self.device)
+                pos = 0
+                eng = self._slots[0].engine
+                for addr, n in pb.spans.parts:
+                    eng.copy_from_host(d_bytes, pos, addr, n, stream=cs)
+                    pos += n
+                d_off = pb.staging.off[: B + 1].to(self.device, non_blocking=True)
+                d_lens = pb.staging.lens[:B].to(self.device, non_blocking=True)
+            else:
+                st = pb.staging
+                nbytes = int(pb.offsets[-1])
+                d_bytes = st.buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
+                d_off = st.off[: B + 1].to(self.device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        if pb.spans is not None:
+            pb.lens = np.asarray(pb.spans.lens, np.int64).copy()
+            self._source.retire(pb.spans, ev)
+            pb.spans = None
+        if pb.staging is not None:
+            self._ring.release(pb.staging, ev)
+            pb.staging = None
+        pb.dev = (d_bytes, d_off, d_lens)
+        pb.copied = ev
 
     def _pull_side(self) -> _Prepared:
         """The side path's look-ahead: keep up to side_ahead prepared batches, each with its
@@ -592,6 +663,7 @@ class MI355XAugPipeline:
                 if pb is None:
                     break
                 self._side_submit(pb)
+                self._stage_on_device(pb)
                 self._ahead.append(pb)
             if not self._ahead:
                 raise StopIteration
@@ -706,7 +778,14 @@ class MI355XAugPipeline:
             B = len(pb.offsets) - 1
             d_lens = None
             with sl.engine.on_stream():
-                if pb.feed is not None:  # the native feed's pinned slot: bytes + offsets in two DMAs
+                if pb.dev is not None:  # copied to HBM when it joined the side look-ahead
+                    cur = torch.cuda.current_stream(self.device)
+                    cur.wait_event(pb.copied)
+                    d_bytes, d_offsets, d_lens = pb.dev
+                    for t in pb.dev:
+                        if t is not None:
+                            t.record_stream(cur)
+                elif pb.feed is not None:  # the native feed's pinned slot: bytes + offsets in two DMAs
                     fb, pb.feed = pb.feed, None
                     j = sl.buf_next
                     sl.buf_next ^= 1
@@ -746,7 +825,7 @@ class MI355XAugPipeline:
                     d_lens = st.lens[:B].to(self.device, non_blocking=True)
                 else:
                     d_bytes = host_buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
-                if host_off is not None:
+                if host_off is not None and pb.dev is None:
                     d_offsets = host_off.to(self.device, non_blocking=True)
                 d_raw = raw.to(self.device, non_blocking=True) if raw is not None else None
                 side = None
@@ -757,8 +836,12 @@ class MI355XAugPipeline:
                     if conts:
                         tm = time.perf_counter()
                         base = host_off.numpy() if host_off is not None else pb.offsets
+                        # image lengths: the spans form's own (its offsets point into shard
+                        # ranges, the gaps hold tar headers and sidecars); packed: the gaps
+                        base_lens = pb.spans.lens if pb.spans is not None else \
+                            pb.lens if pb.lens is not None else np.diff(base[: B + 1])
                         d_bytes, d_offsets, d_lens, d_raw = self._merge_side(
-                            pb.side, conts, d_bytes, int(base[-1]), base, raw, B)
+                            pb.side, conts, d_bytes, int(base[B]), base, base_lens, raw, B)
                         side = conts
                         self.stats["side_decoded"] += len(conts)
                         self.host_seconds["merge"] = self.host_seconds.get("merge", 0.0) + time.perf_counter() - tm
@@ -785,7 +868,7 @@ class MI355XAugPipeline:
         return sl
 
     def _merge_side(self, job, conts: dict, d_bytes: torch.Tensor, nbytes: int, base_off: np.ndarray,
-                    raw: torch.Tensor | None, B: int):
+                    base_lens: np.ndarray, raw: torch.Tensor | None, B: int):
         """The batch's input with its side-decoded images swapped for their device containers
         (spans form: the batch bytes, then the containers; those images' offsets and lengths
         point at their containers and the raw mask marks them).  Runs on the slot's stream,
@@ -793,7 +876,7 @@ class MI355XAugPipeline:
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(job.event)
         off = np.asarray(base_off, np.int64)[: B + 1].copy()
-        lens = np.diff(off)
+        lens = np.asarray(base_lens, np.int64)[:B].copy()
         rawm = raw.cpu().numpy().astype(np.uint8) if raw is not None else np.zeros(B, np.uint8)
         pos = (nbytes + 15) & ~15
         total = pos + sum((int(c.numel()) + 15) & ~15 for c in conts.values())

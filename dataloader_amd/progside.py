@@ -57,19 +57,32 @@ class SideJob:
         return {i: c for i, c in self.containers.items() if st[self.rows[i]] == 0}
 
 
-# Dedicated-queue streams are kept for the life of the process and reused by later side
-# contexts: tensors allocated on a stream keep a reference to it in torch's caching
-# allocator, so destroying one under torch is unsafe (measured: a segfault at close).
-_FREE_STREAMS: dict = {}
+class _RawStream:
+    """A HIP stream torch never sees: only the library's launches run on it (``cuda_stream`` is
+    all ``IngestEngine`` reads).  torch must not record anything on it (an ExternalStream
+    would let the caching allocators record free-time events on it, so destroying it
+    would leave them a dangling stream: the segfault at close, gpurun_out/ss2.err)."""
+
+    __slots__ = ("cuda_stream", "device")
+
+    def __init__(self, handle: int, device: int):
+        self.cuda_stream = handle
+        self.device = device
 
 
-def _take_stream(device: int, cu_count: int):
-    free = _FREE_STREAMS.setdefault((device, cu_count), [])
-    if free:
-        return free.pop()
+_LIVE_STREAMS = {"created": 0, "destroyed": 0}
+
+
+def live_streams() -> int:
+    """Dedicated side streams created and not yet destroyed (0 once every side decoder closed)."""
+    return _LIVE_STREAMS["created"] - _LIVE_STREAMS["destroyed"]
+
+
+def _create_stream(device: int, cu_count: int) -> _RawStream:
     h = ctypes.c_void_p()
     _lib.check(_lib.load().dino_stream_create(device, cu_count, ctypes.byref(h)), "dino_stream_create")
-    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device))
+    _LIVE_STREAMS["created"] += 1
+    return _RawStream(h.value, device)
 
 
 class _SideEngine:
@@ -77,18 +90,20 @@ class _SideEngine:
     a side decode runs for milliseconds, and on a queue shared with a batch stream the
     batch's kernels would wait behind it (measured: pools of >= 32 images on shared
     queues fell to 2.4k img/s, profiles/r03_route_study.jsonl).  ``cu_count`` > 0 confines
-    the side decode to that many CUs."""
+    the side decode to that many CUs.
+
+    Only the library's kernels run on the dedicated stream: every torch allocation, copy
+    and scatter of a side launch runs on this context's torch stream ``copy``, ordered with
+    the dedicated stream by events both ways, so the stream is destroyed at ``close``.
+    Consecutive launches of a context are ordered by the dedicated stream itself."""
 
     def __init__(self, device: torch.device, max_images: int, max_image_dim: int, cu_count: int = 0,
                  dedicated: bool = True):
-        self._key = None
-        if dedicated:
-            self._key = (device.index or 0, int(cu_count))
-            self.stream = _take_stream(*self._key)
-        else:
-            self.stream = torch.cuda.Stream(device=device)
+        self.raw = _create_stream(device.index or 0, int(cu_count)) if dedicated else None
+        self.stream = self.raw if dedicated else torch.cuda.Stream(device=device)
         self.eng = IngestEngine(device, max_batch=max_images, max_views=1, max_crop_size=8,
                                 max_image_dim=max_image_dim, workspace_bytes=64 << 20, stream=self.stream)
+        self.copy = torch.cuda.Stream(device=device)  # this context's torch stream (allocations, copies)
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
         self.keep = None                             # host / device inputs of the mini-batch in flight
 
@@ -98,11 +113,12 @@ class _SideEngine:
     def close(self) -> None:
         if self.last is not None:
             self.last.synchronize()
+        self.keep = None
         self.eng.close()
-        if self._key is not None:
-            self.stream.synchronize()
-            _FREE_STREAMS.setdefault(self._key, []).append(self.stream)
-            self._key = None
+        if self.raw is not None:
+            _lib.check(_lib.load().dino_stream_destroy(ctypes.c_void_p(self.raw.cuda_stream)), "dino_stream_destroy")
+            _LIVE_STREAMS["destroyed"] += 1
+            self.raw = None
 
 
 class DeviceSideDecoder:
@@ -187,24 +203,24 @@ class DeviceSideDecoder:
         ph["probe"] += t3 - t2
         eng.reserve(ws, 0)
         heads = []
-        with eng.on_stream():
+        cs = se.copy
+        es = torch.cuda.ExternalStream(se.stream.cuda_stream, device=self.device) if se.raw is not None \
+            else se.stream  # (only to enqueue event waits / records: torch never allocates on it)
+        for k, (job, i, _) in enumerate(part):
+            job.rows[i] = k
+        keep = [(k, job, i, int(info[k, 1]), int(info[k, 2])) for k, (job, i, _) in enumerate(part)
+                if int(info[k, 0]) == 0 and int(info[k, 3]) != 2]
+        with torch.cuda.stream(cs):
             if self.timing:
                 t0 = torch.cuda.Event(enable_timing=True)
-                t0.record(se.stream)
+                t0.record(es)
             d_bytes = hb.to(self.device, non_blocking=True)
             d_off = off.to(self.device, non_blocking=True)
-            d_info = eng.decode(d_bytes, d_off, len(items))
-            status = torch.empty((len(items), 4), dtype=torch.int32, pin_memory=True)
-            status.copy_(d_info, non_blocking=True)
+            d_info = torch.empty((len(items), 4), dtype=torch.int32, device=self.device)
             # every decoded image's container is a 16-byte aligned slice of one device buffer;
             # the headers go over in one copy and one scatter (per-image pinned headers and
             # copies cost the launch thread ~10 us each)
-            t4 = time.perf_counter()
-            ph["decode"] += t4 - t3
-            for k, (job, i, _) in enumerate(part):
-                job.rows[i] = k
-            keep = [(k, job, i, int(info[k, 1]), int(info[k, 2])) for k, (job, i, _) in enumerate(part)
-                    if int(info[k, 0]) == 0 and int(info[k, 3]) != 2]
+            big = None
             if keep:
                 start = np.zeros(len(keep) + 1, np.int64)
                 start[1:] = np.cumsum([(16 + w * h * 3 + 15) & ~15 for _, _, _, w, h in keep])
@@ -217,14 +233,27 @@ class DeviceSideDecoder:
                 h_pos = torch.from_numpy((start[:-1, None] + np.arange(16)).reshape(-1)).pin_memory()
                 heads.extend((h_hdr, h_pos))
                 big[h_pos.to(self.device, non_blocking=True)] = h_hdr.to(self.device, non_blocking=True)
-                for (k, job, i, w, h), o in zip(keep, start[:-1]):
-                    o = int(o)
-                    _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(big.data_ptr() + o + 16), eng._s()),
-                               "dino_copy_rgb")
-                    job.containers[i] = big[o:o + 16 + w * h * 3]
+            # the library's kernels on the dedicated stream, after the inputs (and after any
+            # earlier use of the memory the allocator just handed out, on this torch stream)
+            ready = torch.cuda.Event()
+            ready.record(cs)
+            es.wait_event(ready)
+            eng.decode(d_bytes, d_off, len(items), info=d_info)
+            t4 = time.perf_counter()
+            ph["decode"] += t4 - t3
+            for (k, job, i, w, h), o in zip(keep, start[:-1] if keep else []):
+                o = int(o)
+                _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(big.data_ptr() + o + 16), eng._s()),
+                           "dino_copy_rgb")
+                job.containers[i] = big[o:o + 16 + w * h * 3]
+            done = torch.cuda.Event()
+            done.record(es)
+            cs.wait_event(done)  # back on the torch stream: status copy, consumers wait for ev
+            status = torch.empty((len(items), 4), dtype=torch.int32, pin_memory=True)
+            status.copy_(d_info, non_blocking=True)
             ph["containers"] += time.perf_counter() - t4
             ev = torch.cuda.Event(enable_timing=self.timing)
-            ev.record(se.stream)
+            ev.record(cs)
             if self.timing:
                 self.spans.append((t0, ev, len(part)))
         for job, _, _ in part:

@@ -116,3 +116,75 @@ def test_masking_generator_validation_matches_reference():
     MaskingGenerator(8, num_masking_patches=0)  # min > max allowed when target == 0
     g = MaskingGenerator((10, 16))
     assert g.get_shape() == (10, 16) and g.num_masking_patches == 80 and "10x16" in repr(g)
+
+
+def _doc_blocks(lang: str) -> list[str]:
+    import re
+    text = (ROOT / "INTEGRATION.md").read_text()
+    return re.findall(r"```" + lang + r"\n(.*?)```", text, flags=re.S)
+
+
+def _header_params() -> dict[str, int]:
+    """Parameter count of every function the header declares."""
+    import re
+    hdr = (ROOT / "include" / "dino_ingest.h").read_text()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(dino_\w+)\s*\(([^;{]*?)\)\s*;", hdr, flags=re.S):
+        args = m.group(2).strip()
+        out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1
+    return out
+
+
+def test_integration_c_examples_compile_against_the_header(tmp_path):
+    """VERDICT r3 #8: every C example of INTEGRATION.md compiles against include/dino_ingest.h."""
+    import subprocess
+    blocks = _doc_blocks("c")
+    assert len(blocks) >= 2
+    for k, code in enumerate(blocks):
+        src = tmp_path / f"example_{k}.c"
+        src.write_text(code)
+        r = subprocess.run(["gcc", "-fsyntax-only", "-std=c11", "-Wall", "-Werror", "-I", str(ROOT / "include"),
+                            str(src)], capture_output=True, text=True)
+        assert r.returncode == 0, f"INTEGRATION.md C block {k}:\n{r.stderr}"
+
+
+def test_integration_ctypes_argtypes_match_header_and_binding():
+    """Every ``lib.<fn>.argtypes = [...]`` of INTEGRATION.md has the header's parameter count and
+    _lib.py's, and _lib.py binds every header function with the header's count."""
+    import re
+
+    from dataloader_amd import _lib
+    lib = _lib.load()
+    params = _header_params()
+    for name in _lib.exported_symbols():
+        assert name in params, name
+        assert len(getattr(lib, name).argtypes) == params[name], (name, getattr(lib, name).argtypes, params[name])
+    seen = 0
+    for code in _doc_blocks("python"):
+        for m in re.finditer(r"lib\.(dino_\w+)\.argtypes\s*=\s*\[(.*?)\]\n", code, flags=re.S):
+            items = [x for x in re.split(r",(?![^()]*\))", m.group(2).replace("\n", " ")) if x.strip()]
+            assert len(items) == params[m.group(1)], (m.group(1), len(items), params[m.group(1)])
+            seen += 1
+    assert seen >= 3
+
+
+def test_backend_side_look_ahead_fits_the_metadata_fifo():
+    """The side route pulls PipelineConfig.cpu_queue batches ahead (DALI's CPU prefetch queue,
+    reference config.py:166), never more than the source's metadata FIFO holds
+    (_ReaderAdapter._meta_queue, 64 slots, shard_reader.py:98, 357-375: an overflow raises)."""
+    import queue
+
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import PipelineConfig
+
+    class Src:
+        def __init__(self, n):
+            self._meta_queue = queue.Queue(maxsize=n)
+
+    be = MI355XBackend()
+    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 16
+    assert be.side_look_ahead(PipelineConfig(), object(), 3) == 16
+    assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 6
+    assert be.side_look_ahead(PipelineConfig(cpu_queue=40), Src(64), 3) == 40
+    assert MI355XBackend(side_ahead=8).side_look_ahead(PipelineConfig(), Src(64), 3) == 8

@@ -56,7 +56,8 @@ def _collect(it):
 def test_backend_queue_depth_matches_serial(gpu_device):
     """gpu_queue = 6 -> 3 batches in flight + the prefetch thread; every view of every batch
     equals the gpu_queue = 1 pipeline's (same seed, same batch indices), with a progressive
-    file (Pillow on the thread, "auto") and a CMYK file (hand-over) in some batches."""
+    file (the device side route, the backend default since round 4) and a CMYK file (Pillow
+    hand-over on the thread) in some batches."""
     from dataloader_amd.backend import MI355XBackend
     rng = np.random.default_rng(50)
     uniq = [encode_jpeg(textured_rgb(300 + 12 * s, 220 + 6 * s, rng)) for s in range(6)]
@@ -80,7 +81,8 @@ def test_backend_queue_depth_matches_serial(gpu_device):
 
     (ref, st1), (got, st3) = run(1), run(6)
     assert len(ref) == len(got) == nb
-    assert st1["host_decoded"] == st3["host_decoded"] == 3 and set(st3["status"]) == {0}
+    assert st1["host_decoded"] == st3["host_decoded"] == 1 and set(st3["status"]) == {0}
+    assert st1["side_decoded"] == st3["side_decoded"] == 2
     for k, (a, b) in enumerate(zip(ref, got)):
         for name in a:
             assert torch.equal(a[name], b[name]), (k, name)
