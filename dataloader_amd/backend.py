@@ -166,16 +166,23 @@ class MI355XBackend:
         # default; the GPU peer decodes every flavour on the device, reference pipeline.py:429-434);
         # Pillow only for what the device decoder does not implement (MI355XAugPipeline)
         self._multiscan_route = multiscan_route
-        self._side_ahead = side_ahead  # None: PipelineConfig.cpu_queue (see side_look_ahead)
+        self._side_ahead = side_ahead  # None: SIDE_AHEAD (see side_look_ahead)
+
+    # side look-ahead in batches (measured, scripts/route_study.py, B = 512 with 32 progressive:
+    # 16 -> 84.8k img/s, 48 -> 92.2-94.9k; profiles/r04_side_ahead.jsonl): a side decode pool
+    # takes ~45 ms, about 13 batch launches, so the look-ahead must cover several of them
+    SIDE_AHEAD = 48
 
     def side_look_ahead(self, pipeline_cfg: Any, source: Any, depth: int) -> int:
-        """Batches the side route pulls ahead of their launch: DALI's CPU prefetch queue
-        (``PipelineConfig.cpu_queue``, 16 by default, reference config.py:166, pipeline.py:317
-        fills it by calling the source ahead), capped so that everything pulled and not yet
-        handed over (look-ahead + prefetch queue + batches in flight) fits the source's
-        metadata FIFO (``_ReaderAdapter._meta_queue``, 64 slots, shard_reader.py:98, 357-375:
-        an overflow raises)."""
-        want = self._side_ahead if self._side_ahead is not None else int(getattr(pipeline_cfg, "cpu_queue", 16) or 16)
+        """Batches the side route pulls ahead of their launch (DALI's CPU prefetch queue plays
+        this role for the reference's GPU peer: ``PipelineConfig.cpu_queue`` batches pulled
+        ahead, reference config.py:166, pipeline.py:317): ``max(cpu_queue, SIDE_AHEAD)``, capped
+        so that everything pulled and not yet handed over (look-ahead + prefetch queue + batches
+        in flight) fits the source's metadata FIFO (``_ReaderAdapter._meta_queue``, 64 slots,
+        shard_reader.py:98, 357-375: an overflow raises).  The look-ahead's batches wait in HBM
+        (MI355XAugPipeline._stage_on_device): 48 C2 batches take ~2 GB of the 288."""
+        want = self._side_ahead if self._side_ahead is not None else \
+            max(self.SIDE_AHEAD, int(getattr(pipeline_cfg, "cpu_queue", 16) or 16))
         mq = getattr(source, "_meta_queue", None)
         cap = getattr(mq, "maxsize", 0) or 0
         if cap > 0:

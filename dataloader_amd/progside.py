@@ -135,6 +135,7 @@ class DeviceSideDecoder:
         # 64: 37.7k, 128: 53.2k, 256: 66.5k, 512: 74.3k.  One k_pscan launch of N progressive images
         # takes ~30 ms up to N = 64 and 45 ms at N = 512 (scripts/prog_scale.py), so the pool waits
         # for max_images, or until its oldest batch is half the look-ahead from its launch (pipeline.py)
+        max_images = int(os.environ.get("DINO_SIDE_MAX", max_images))
         min_images = int(os.environ.get("DINO_SIDE_MIN", max_images)) if min_images is None else min_images
         engines = int(os.environ.get("DINO_SIDE_ENGINES", 2)) if engines is None else engines
         self.cu_count = int(os.environ.get("DINO_SIDE_CUS", 0))

@@ -170,8 +170,8 @@ def test_integration_ctypes_argtypes_match_header_and_binding():
 
 
 def test_backend_side_look_ahead_fits_the_metadata_fifo():
-    """The side route pulls PipelineConfig.cpu_queue batches ahead (DALI's CPU prefetch queue,
-    reference config.py:166), never more than the source's metadata FIFO holds
+    """The side route pulls max(PipelineConfig.cpu_queue, 48) batches ahead (DALI's CPU prefetch
+    queue, reference config.py:166), never more than the source's metadata FIFO holds
     (_ReaderAdapter._meta_queue, 64 slots, shard_reader.py:98, 357-375: an overflow raises)."""
     import queue
 
@@ -183,8 +183,9 @@ def test_backend_side_look_ahead_fits_the_metadata_fifo():
             self._meta_queue = queue.Queue(maxsize=n)
 
     be = MI355XBackend()
-    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 16
-    assert be.side_look_ahead(PipelineConfig(), object(), 3) == 16
+    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 48
+    assert be.side_look_ahead(PipelineConfig(), object(), 3) == 48
     assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 6
-    assert be.side_look_ahead(PipelineConfig(cpu_queue=40), Src(64), 3) == 40
+    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), Src(64), 3) == 64 - 3 - 6
+    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), object(), 3) == 60
     assert MI355XBackend(side_ahead=8).side_look_ahead(PipelineConfig(), Src(64), 3) == 8
