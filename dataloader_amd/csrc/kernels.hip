@@ -45,7 +45,17 @@ constexpr uint32_t kXcds = 8;
 struct BlkIdx {
   int x, y, z;
 };
+// Issue priority of the batch kernels' waves (s_setprio): above the progressive side
+// decode's scan waves (k_pscan keeps the default 0), so that a SIMD running both issues the
+// batch's instruction first when both are ready (A/B: DINO_MAIN_PRIO).
+#ifndef DINO_MAIN_PRIO
+#define DINO_MAIN_PRIO 3
+#endif
+__device__ __forceinline__ void main_prio() {
+  if (DINO_MAIN_PRIO > 0) __builtin_amdgcn_s_setprio(DINO_MAIN_PRIO);
+}
 __device__ __forceinline__ BlkIdx xcd_blk() {
+  main_prio();
   const uint32_t X = gridDim.x, Y = gridDim.y, Z = gridDim.z;
   uint32_t L = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
   if (DINO_XCD_REMAP) {
@@ -369,6 +379,7 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_count(const uint8_t
                                                                    const int64_t* __restrict__ offsets, int B,
                                                                    const ImgDesc* __restrict__ desc,
                                                                    uint8_t* __restrict__ ws) {
+  main_prio();
   __shared__ uint32_t s_wave[kDestuffThreads / 64];
   __shared__ int s_img;
   __shared__ int s_term;
@@ -425,6 +436,7 @@ __global__ void __launch_bounds__(kDestuffThreads) k_destuff_write(const uint8_t
                                                                    const int64_t* __restrict__ offsets, int B,
                                                                    ImgDesc* __restrict__ desc,
                                                                    uint8_t* __restrict__ ws) {
+  main_prio();
   __shared__ uint32_t s_wave[kDestuffThreads / 64];
   __shared__ int s_img;
   __shared__ int s_E;
@@ -681,6 +693,7 @@ __device__ __forceinline__ uint32_t lane_write_end(const ImgDesc& d, int i) {
 __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict__ bytes,
                                                        const int64_t* __restrict__ offsets,
                                                        ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  main_prio();
   __shared__ HuffTables s_tab;
   __shared__ int32_t s_bad;
   ImgDesc& d = desc[blockIdx.x];
@@ -844,6 +857,7 @@ __device__ uint64_t g_huff_phase[kPhaseItems][5];
 
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
+  main_prio();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   const int t = threadIdx.x;
@@ -925,6 +939,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
 constexpr int kHuff2Threads = 256;
 
 __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  main_prio();
   __shared__ HuffTables s_tab;
   __shared__ uint32_t s_wave[kHuff2Threads / 64];
   const ImgDesc& d = desc[blockIdx.x];
@@ -980,6 +995,7 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
 
 __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
+  main_prio();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   HuffLds3& L = *reinterpret_cast<HuffLds3*>(smem);
   const int t = threadIdx.x;
@@ -1735,6 +1751,7 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
 constexpr int kDcScanThreads = 256;
 
 __global__ void __launch_bounds__(kDcScanThreads) k_dcscan(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  main_prio();
   constexpr int K = 8;  // blocks per lane per tile: a wave covers 512 consecutive blocks
   __shared__ uint32_t s_wave[kDcScanThreads / 64];
   const ImgDesc& d = desc[blockIdx.x];
@@ -2328,6 +2345,8 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
         }
         hg[(int64_t)g * S + x] = make_uint4(dp[0], dp[1], dp[2], 0u);
       }
+      // k_hresize runs the view's ng_max groups for every output: zero taps past this one's
+      for (int g = ng; g < (vp.kh + 3) / 4; ++g) hg[(int64_t)g * S + x] = make_uint4(0u, 0u, 0u, 0u);
       hx[x] = make_int4(hb[2 * x], ng, 128 * ksum + (1 << (kPrecisionBits - 1)), 0);
     }
     if (vp.kv)
@@ -2385,137 +2404,100 @@ constexpr int kHrPre = DINO_HRESIZE_PREFETCH;  // staging items per thread loade
 // of 4 taps) and kHresizeMinRows staged rows fit kHresizeLds; then as many rows per
 // band as fit (<= 16).  R = 0: even 8 outputs do not fit (direct path).
 struct HrTile {
-  int sw, pitch, R;
+  int sw, pitch, R, R3p;
 };
 __device__ __forceinline__ int hresize_pitch(int S, int cw, int kh, int sw) {
   // widest source span of a slice (+ 4 for the word alignment of its first column)
   const int span = min(cw, (int)(((int64_t)sw * cw + S - 1) / S) + kh + 2) + 4;
   return ((span + 3) & ~3) + 8;  // + slack for the last group's upper word
 }
+// LDS bytes of a band of R rows: (pitch / 4) source words x (3 R + 2) row-channel words,
+// plus room for the over-read of the last output's zero-tap groups (ng_max words).
+__device__ __forceinline__ int hresize_rows_bytes(int pitch, int R, int ng_max) {
+  return (pitch / 4 + ng_max + 1) * (3 * R + 2) * 4;
+}
 __device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
-  const int tap_bytes = 16 * (1 + (kh + 3) / 4);
-  HrTile t{0, 0, 0};
+  const int ng_max = (kh + 3) / 4;
+  const int tap_bytes = 16 * (1 + (ng_max | 1));
+  HrTile t{0, 0, 0, 0};
   int sw = S;
-  while (tap_bytes * sw + kHresizeMinRows * 3 * hresize_pitch(S, cw, kh, sw) > kHresizeLds) {
+  while (tap_bytes * sw + hresize_rows_bytes(hresize_pitch(S, cw, kh, sw), kHresizeMinRows, ng_max) > kHresizeLds) {
     sw = sw == S ? ((S - 1) & ~7) : sw - 8;
     if (sw < 8) return t;
   }
   t.sw = sw;
   t.pitch = hresize_pitch(S, cw, kh, sw);
-  t.R = min(16, (kHresizeLds - tap_bytes * sw) / (3 * t.pitch));
+  int R = 16;
+  while (R > kHresizeMinRows && tap_bytes * sw + hresize_rows_bytes(t.pitch, R, ng_max) > kHresizeLds) R -= 2;
+  t.R = R;
+  t.R3p = 3 * R + 2;
   return t;
 }
 
-// One tile: nr staged rows x the outputs [x0, x0 + sw) of a slice.  Lane (r, x)
-// accumulates three signed-dot4 digit products per channel and group of 4 taps.
-// Rows are staged planar with the sign bit flipped (p - 128 as int8), starting at
-// source column c0; the taps' pixels start at xmin, so each group's 4 pixels are one
-// v_alignbyte of two consecutive LDS words (the upper word carried to the next
-// group).  Exact: the int32 sum equals Pillow's.
-#ifndef DINO_HRESIZE_ROWS_PER_LANE
-#define DINO_HRESIZE_ROWS_PER_LANE 2
-#endif
-constexpr int kHrRows = DINO_HRESIZE_ROWS_PER_LANE;  // rows per lane-task: the taps are read once for all of them
-__device__ __forceinline__ void hresize_tile_dot(const uint8_t* __restrict__ rows, int pitch, int plane_bytes, int nr,
-                                                 int r0, int x0, int sw, int c0, int S, const int4* __restrict__ hx,
+// One tile: nr staged rows x the outputs [x0, x0 + sw) of a slice.  Lane (row pair, x)
+// accumulates three signed-dot4 digit products per row, channel and group of 4 taps.
+// Rows are staged with the sign bit flipped (p - 128 as int8) from source column c0,
+// word-interleaved: word (gw, r, c) = 4 pixels gw of row r, channel c at gw * R3p + 3 r + c
+// (R3p = 3 R + 2: even, so a row pair's six words are one 8-byte-aligned run: three
+// ds_read_b64 per group and one address for all of them).  The taps' pixels start at xmin,
+// so each group's 4 pixels are one v_alignbyte of a word and the next group's (carried).
+// The group loop runs the view's ng_max groups for every lane (taps past an output's own
+// count are zero digits, k_rcoeffs), a wave-uniform trip count the compiler unrolls for
+// NG <= 8.  Exact: the int32 sum equals Pillow's.
+template <int NG>
+__device__ __forceinline__ void hresize_tile_dot(const uint32_t* __restrict__ rows, int R3p, int nr, int r0, int x0,
+                                                 int sw, int c0, int S, int ng, int ngp, const int4* __restrict__ hx,
                                                  const uint4* __restrict__ hg, uint8_t* __restrict__ tmp, int64_t cpl) {
-  // a lane computes one output column for kHrRows rows (the taps are read once for all)
-  const int ngrp = (nr + kHrRows - 1) / kHrRows;
-  for (int e = threadIdx.x; e < ngrp * sw; e += blockDim.x) {
-    const int rp = e / sw, xl = e - rp * sw;
-    const int ra = kHrRows * rp;
+  if (NG) ng = NG;
+  const int npair = (nr + 1) >> 1;
+  const int qs = R3p >> 1;  // uint2 stride per source group
+  // lane task (row pair rp, output xl), advanced by the block size without dividing again
+  const int dq = (int)blockDim.x / sw, dr = (int)blockDim.x - dq * sw;
+  int rp = (int)threadIdx.x / sw, xl = (int)threadIdx.x - rp * sw;
+  for (; rp < npair; rp += dq, xl += dr, (xl >= sw ? (xl -= sw, ++rp) : 0)) {
+    const int ra = 2 * rp;  // rows ra, ra + 1 (a band's odd last row pairs with an unstored row: not written)
     const int4 h = hx[xl];
-    const int lo = h.x - c0, ng = h.y;
+    const int lo = h.x - c0;
     const uint32_t sh = (uint32_t)(lo & 3);
-    const int pw = plane_bytes >> 2;  // plane stride in words
-    const uint32_t* q[kHrRows];
+    const uint2* q = (const uint2*)(rows + __umul24((uint32_t)(lo >> 2), (uint32_t)R3p) + 3 * ra);
+    uint32_t lw[6];
+    {
+      const uint2 a0 = q[0], a1 = q[1], a2 = q[2];
+      lw[0] = a0.x, lw[1] = a0.y, lw[2] = a1.x, lw[3] = a1.y, lw[4] = a2.x, lw[5] = a2.y;
+    }
+    int32_t acc[6][3];  // digit 0 starts at the rounding + sign-flip correction h.z
 #pragma unroll
-    for (int i = 0; i < kHrRows; ++i)  // a band's last group repeats its last row (not stored)
-      q[i] = (const uint32_t*)(rows + min(ra + i, nr - 1) * pitch) + (lo >> 2);
-    int32_t acc[kHrRows][3][3];
-    uint32_t lw[kHrRows][3];
+    for (int k = 0; k < 6; ++k) acc[k][0] = h.z, acc[k][1] = acc[k][2] = 0;
+    const uint4* dgp = hg + xl * ngp;  // this output's taps: ngp consecutive groups (immediate offsets)
 #pragma unroll
-    for (int i = 0; i < kHrRows; ++i)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        acc[i][c][0] = acc[i][c][1] = acc[i][c][2] = 0;
-        lw[i][c] = q[i][c * pw];
-      }
     for (int g = 0; g < ng; ++g) {
-      const uint4 dg = hg[g * sw + xl];
+      const uint4 dg = dgp[g];
+      const uint2* qn = q + (g + 1) * qs;
+      const uint2 b0 = qn[0], b1 = qn[1], b2 = qn[2];
+      const uint32_t uw[6] = {b0.x, b0.y, b1.x, b1.y, b2.x, b2.y};
 #pragma unroll
-      for (int i = 0; i < kHrRows; ++i)
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const uint32_t u = q[i][c * pw + g + 1];
-          const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(u, lw[i][c], sh);
-          acc[i][c][0] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.x, acc[i][c][0], false);
-          acc[i][c][1] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.y, acc[i][c][1], false);
-          acc[i][c][2] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.z, acc[i][c][2], false);
-          lw[i][c] = u;
-        }
+      for (int k = 0; k < 6; ++k) {
+        const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(uw[k], lw[k], sh);
+        acc[k][0] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.x, acc[k][0], false);
+        acc[k][1] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.y, acc[k][1], false);
+        acc[k][2] = __builtin_amdgcn_sdot4(pa, (int32_t)dg.z, acc[k][2], false);
+        lw[k] = uw[k];
+      }
     }
     // int32 wrap-around is harmless: the true sum (Pillow's int32 ss) fits in int32
+    // (clip8_acc as one med3: the sum is < 2^30 unless it clips to 255, and <= 0 clips to 0;
+    // 32-bit offsets: a view's planes hold < 3 x 2^20 x 1024 bytes)
+    const uint32_t ob = (uint32_t)((r0 + ra) * S + x0 + xl);
 #pragma unroll
-    for (int i = 0; i < kHrRows; ++i) {
+    for (int i = 0; i < 2; ++i) {
       if (ra + i >= nr) break;
-      const int64_t o = (int64_t)(r0 + ra + i) * S + x0 + xl;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        tmp[c * cpl + o] = clip8_acc((int32_t)((uint32_t)acc[i][c][0] + ((uint32_t)acc[i][c][1] << 8) +
-                                               ((uint32_t)acc[i][c][2] << 16) + (uint32_t)h.z));
-    }
-  }
-}
-
-// The same tile with each lane's taps in registers: lane (column xl, row group rg) loads
-// its output's NG groups of tap digits once and sweeps the band's rows rg, rg + nrg, ...
-// (one LDS word per channel and group per row; the taps cost nothing per row).  NG is the
-// view's group count rounded up to 2, 4 or 8 (unrolled, predicated by the lane's own count).
-#ifndef DINO_HRESIZE_TAPREG
-#define DINO_HRESIZE_TAPREG 0
-#endif
-template <int NG>
-__device__ __forceinline__ void hresize_tile_regs(const uint8_t* __restrict__ rows, int pitch, int plane_bytes, int nr,
-                                                  int r0, int x0, int sw, int c0, int S, const int4* __restrict__ hx,
-                                                  const uint4* __restrict__ hg, uint8_t* __restrict__ tmp, int64_t cpl) {
-  const int nrg = max(1, (int)blockDim.x / sw);
-  const int e = threadIdx.x;
-  if (e >= nrg * sw) return;
-  const int rg = e / sw, xl = e - rg * sw;
-  const int4 h = hx[xl];
-  const int lo = h.x - c0, ng = h.y;
-  const uint32_t sh = (uint32_t)(lo & 3);
-  const int pw = plane_bytes >> 2;
-  uint32_t d0[NG], d1[NG], d2[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const uint4 dg = g < ng ? hg[g * sw + xl] : make_uint4(0u, 0u, 0u, 0u);
-    d0[g] = dg.x;
-    d1[g] = dg.y;
-    d2[g] = dg.z;
-  }
-  const uint32_t* q0 = (const uint32_t*)rows + (lo >> 2);
-  for (int r = rg; r < nr; r += nrg) {
-    const uint32_t* q = q0 + r * (pitch >> 2);
-    const int64_t o = (int64_t)(r0 + r) * S + x0 + xl;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const uint32_t* qc = q + c * pw;
-      int32_t a0 = 0, a1 = 0, a2 = 0;
-      uint32_t lw = qc[0];
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        if (g < ng) {
-          const uint32_t u = qc[g + 1];
-          const int32_t pa = (int32_t)__builtin_amdgcn_alignbyte(u, lw, sh);
-          a0 = __builtin_amdgcn_sdot4(pa, (int32_t)d0[g], a0, false);
-          a1 = __builtin_amdgcn_sdot4(pa, (int32_t)d1[g], a1, false);
-          a2 = __builtin_amdgcn_sdot4(pa, (int32_t)d2[g], a2, false);
-          lw = u;
-        }
+      for (int c = 0; c < 3; ++c) {
+        const int k = 3 * i + c;
+        const uint32_t so = (uint32_t)__builtin_amdgcn_readfirstlane((int)((uint32_t)(i * S) + (uint32_t)c * (uint32_t)cpl));
+        const int32_t sum = (int32_t)((uint32_t)acc[k][0] + ((uint32_t)acc[k][1] << 8) + ((uint32_t)acc[k][2] << 16));
+        tmp[ob + so] = (uint8_t)min(max(sum >> kPrecisionBits, 0), 255);
       }
-      tmp[c * cpl + o] = clip8_acc((int32_t)((uint32_t)a0 + ((uint32_t)a1 << 8) + ((uint32_t)a2 << 16) + (uint32_t)h.z));
     }
   }
 }
@@ -2545,8 +2527,9 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
   uint8_t* tmp = aws + vp.htmp_off;
   const int64_t cpl = (int64_t)p.crop_h * S;
   const int ng_max = (kh + 3) / 4;
+  const int ngp = ng_max | 1;  // tap groups per output in LDS: odd, so 16 lanes' b128 reads hit distinct banks
   const HrTile tl = hresize_tile(S, cw, kh);
-  const int sw = tl.sw, pitch = tl.pitch, R = tl.R;
+  const int sw = tl.sw, pitch = tl.pitch, R = tl.R, R3p = tl.R3p;
   const int nsl = sw > 0 ? (S + sw - 1) / sw : 0;
   if (R < 1) {  // direct path: taps and pixels from global memory (crops too wide for LDS)
     const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
@@ -2557,10 +2540,11 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
     }
     return;
   }
-  int4* lx = (int4*)smem;
+  // LDS: the staged rows first (an edge output's zero-tap over-read stays inside the rows'
+  // pad), then the slice's taps
+  uint32_t* rows = (uint32_t*)smem;
+  int4* lx = (int4*)(smem + ((hresize_rows_bytes(pitch, R, ng_max) + 15) & ~15));
   uint4* lg = (uint4*)(lx + sw);
-  uint8_t* rows = smem + 16 * sw * (1 + ng_max);
-  const int plane_bytes = R * pitch;
   const int nbands = (p.crop_h + R - 1) / R;
   const int ntiles = nsl * nbands;
   // Tile u: slice sl (outputs [x0, x0 + swn)), band of rows [r0, r0 + nr), source columns
@@ -2596,10 +2580,10 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
     const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
     const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
     const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
-    uint8_t* dst = rows + r * pitch + 4 * g;
-    *(uint32_t*)dst = cr ^ 0x80808080u;
-    *(uint32_t*)(dst + plane_bytes) = cg ^ 0x80808080u;
-    *(uint32_t*)(dst + 2 * plane_bytes) = cb ^ 0x80808080u;
+    uint32_t* dst = rows + g * R3p + 3 * r;
+    dst[0] = cr ^ 0x80808080u;
+    dst[1] = cg ^ 0x80808080u;
+    dst[2] = cb ^ 0x80808080u;
   };
   // The first kHrPre staging items of each thread are loaded one tile ahead (during the
   // previous tile's dot products), the rest when the tile starts.
@@ -2627,7 +2611,7 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
       for (int k = threadIdx.x; k < T.swn; k += blockDim.x) lx[k] = ghx[T.x0 + k];
       for (int k = threadIdx.x; k < T.swn * ng_max; k += blockDim.x) {
         const int g = k / T.swn, xl = k - g * T.swn;
-        lg[g * T.swn + xl] = ghg[(int64_t)g * S + T.x0 + xl];
+        lg[xl * ngp + g] = ghg[(int64_t)g * S + T.x0 + xl];
       }
       cur = T.sl;
     }
@@ -2649,14 +2633,23 @@ __global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ des
     }
     __syncthreads();
     if (kHrPre && u + (int)gridDim.x < ntiles) prefetch(tile_of(u + gridDim.x));
-    if (DINO_HRESIZE_TAPREG && ng_max <= 2)
-      hresize_tile_regs<2>(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
-    else if (DINO_HRESIZE_TAPREG && ng_max <= 4)
-      hresize_tile_regs<4>(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
-    else if (DINO_HRESIZE_TAPREG && ng_max <= 8)
-      hresize_tile_regs<8>(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
-    else
-      hresize_tile_dot(rows, pitch, plane_bytes, T.nr, T.r0, T.x0, T.swn, T.c0, S, lx, lg, tmp, cpl);
+    switch (ng_max) {
+#define DINO_HR_CASE(N) \
+  case N: \
+    hresize_tile_dot<N>(rows, R3p, T.nr, T.r0, T.x0, T.swn, T.c0, S, ng_max, ngp, lx, lg, tmp, cpl); \
+    break;
+      DINO_HR_CASE(1)
+      DINO_HR_CASE(2)
+      DINO_HR_CASE(3)
+      DINO_HR_CASE(4)
+      DINO_HR_CASE(5)
+      DINO_HR_CASE(6)
+      DINO_HR_CASE(7)
+      DINO_HR_CASE(8)
+#undef DINO_HR_CASE
+      default:
+        hresize_tile_dot<0>(rows, R3p, T.nr, T.r0, T.x0, T.swn, T.c0, S, ng_max, ngp, lx, lg, tmp, cpl);
+    }
     __syncthreads();
   }
 }
