@@ -1091,6 +1091,36 @@ struct WaveMarkerFinder {
   }
 };
 
+// Lane-mode AC refinement (k_prefine): the AC refinement scans of a component leave k_pscan
+// (which only destuffs them) for k_prefine, one lane per (image, component), when every
+// refinement scan of the component is a single-component scan without restart intervals
+// and no scan other than a refinement follows one it overlaps (nothing k_pscan decodes
+// reads their coefficients).  The components that may go to lane mode (bit c) come from the
+// environment (DINO_PREFINE_COMPS, read per ctx; default 0: none).  Measured and not the
+// default (profiles/r04_prefine_*): a lane decodes a scan ~3.5x slower than a scan wave
+// (its serial chain is a divergent VALU chain with LDS lookups, ~2 900 cycles per symbol
+// against ~840), so lane mode cuts the side decode's issue slots to ~1/64 of a wave per scan
+// but a 64-image pool takes 225 ms (all components) or 43 ms (chroma only) instead of 31 ms,
+// and the side route measured 36k / 96k img/s against 101k in wave mode.
+__device__ __forceinline__ bool scan_is_ac_refine(const ScanRec& a, bool prog) { return prog && a.ss > 0 && a.ah > 0; }
+__device__ int prog_lane_refine(const ScanRec* scans, int n, bool prog) {
+  if (!prog) return 0;
+  int mask = 0, bad = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!scan_is_ac_refine(scans[i], prog)) continue;
+    const int c = scans[i].comp[0] & 3;
+    mask |= 1 << c;
+    if (scans[i].ns != 1 || scans[i].restart_interval != 0) bad |= 1 << c;
+    for (int j = i + 1; j < n; ++j)
+      if (!scan_is_ac_refine(scans[j], prog) && scans_overlap(scans[i], scans[j])) bad |= 1 << c;
+  }
+  return mask & ~bad;
+}
+// The scan goes to k_prefine (the component bit of PHdr::pad[0]).
+__device__ __forceinline__ bool scan_lane_refine(int lanemask, const ScanRec& a, bool prog) {
+  return scan_is_ac_refine(a, prog) && ((lanemask >> (a.comp[0] & 3)) & 1);
+}
+
 constexpr int kPWalkThreads = 256;
 struct PWalkLds {
   ImgDesc d;
@@ -1106,7 +1136,7 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
                                                          const int64_t* __restrict__ offsets,
                                                          const int64_t* __restrict__ lengths,
                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
-                                                         PCtl* __restrict__ pctl) {
+                                                         PCtl* __restrict__ pctl, int prefine) {
   __shared__ PWalkLds L;
   const int img = blockIdx.x, t = threadIdx.x;
   if (desc[img].status != DINO_IMG_OK || desc[img].kind != 1) return;
@@ -1165,6 +1195,7 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
   if (t == 0) {
     hd->n_scans = n;
     hd->n_levels = nlev;
+    hd->pad[0] = prog_lane_refine(L.scans, n, dl.progressive != 0) & prefine;
   }
   // libjpeg's zeroed coefficient arrays
   {
@@ -1688,6 +1719,17 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
     tb.load((const PTab*)(region + kPTabOff), ps->tslots, lane);
     uint32_t* clean = (uint32_t*)(ws + d->ent_off + ((sr.data_off - d->scan_off + 3) & ~3));
     const uint32_t dlen = sr.restart_interval == 0 ? wave_destuff(p, len, sr.data_off, (uint8_t*)clean, lane) : 0u;
+    if (scan_lane_refine(hd->pad[0], sr, d->progressive != 0)) {
+      // decoded by k_prefine (lane mode): its destuffed length for the lane's reader, and its
+      // completion for the level count (no scan k_pscan decodes depends on it)
+      if (lane == 0) ((PScan*)(region + kPScanOff) + j)->pad = (int32_t)dlen;
+      __threadfence();
+      if (lane == 0) {
+        __hip_atomic_store(&((PHdr*)region)->prog[j], 0x7FFFFFFF, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&((PHdr*)region)->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;
+    }
     const bool pipe = ps->pipe != 0;
     if (sr.level > 0 && !pipe) {  // the previous level's scans of this image (earlier tickets, running or done)
       int32_t* dn = &((PHdr*)region)->done[sr.level - 1];
@@ -1739,6 +1781,210 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
 #endif
     __threadfence();  // this scan's coefficient stores before its completion count
     if (lane == 0) __hip_atomic_fetch_add(&((PHdr*)region)->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_prefine: the AC refinement scans of the images k_pwalk marked (prog_lane_refine), one
+// lane per (image, component): the lane decodes the component's refinement scans in scan
+// order over the component's blocks (decode_mcu_AC_refine, r_refine_block), its own stream
+// and its own table, with no other lane of the wave involved.  A wave thus advances 64
+// scans per instruction instead of one (k_pscan runs one scan per wave, its serial chain on
+// the scalar unit): a refinement scan costs ~1/64 of a wave's issue slots, so the side
+// decode leaves the batch kernels their issue slots, at the price of a longer latency per
+// scan (the side look-ahead covers it).
+//   per lane: the scan's 9-bit lookahead (1 KiB) and the block being refined (128 B) in
+//   LDS; the block's coefficients loaded one block ahead (8 x 16 B), its zigzag non-zero
+//   mask from those registers; changed coefficients stored one by one.
+// ---------------------------------------------------------------------------
+constexpr int kPrefineLds = 64 * (1024 + 64 + 256) + 64 * 128 + 80;
+
+// Per-lane bit reader over a destuffed scan (4-byte aligned, zero padded to a dword; bits
+// past the data read as zeros, libjpeg's fill): a 64-bit window kept >= 33 bits full from a
+// staged 16-byte chunk, the next chunk's load in flight a whole chunk ahead (on gfx9 a load's
+// wait also waits for every store issued before it: the refinement stores blocks, so a
+// refill loaded just before its use would wait for those stores).
+struct LaneClean {
+  const uint32_t* src;
+  uint32_t nw, nbits, pos, next;  // nw: dwords holding data; next: index of the chunk in flight
+  uint64_t buf;
+  int32_t nb, cw;                  // valid window bits; words of `cur` not yet consumed
+  uint4 cur, fly;
+  __device__ __forceinline__ uint4 ldq(uint32_t q) const {  // chunk q: 4 dword loads, clamped
+    const uint32_t w = 4u * q;
+    return make_uint4(src[w < nw ? w : 0u], src[w + 1 < nw ? w + 1 : 0u], src[w + 2 < nw ? w + 2 : 0u],
+                      src[w + 3 < nw ? w + 3 : 0u]);
+  }
+  __device__ __forceinline__ uint32_t take() {  // the next big-endian word of the stream (0 past the data)
+    if (cw == 0) {
+      cur = fly;
+      ++next;
+      fly = ldq(next);
+      cw = 4;
+    }
+    const uint32_t x = cw == 4 ? cur.x : (cw == 3 ? cur.y : (cw == 2 ? cur.z : cur.w));
+    const uint32_t wi = 4u * (next - 1u) + (uint32_t)(4 - cw);
+    --cw;
+    return wi < nw ? __builtin_bswap32(x) : 0u;
+  }
+  __device__ __forceinline__ void fill() {
+    while (nb <= 32) {
+      buf |= (uint64_t)take() << (32 - nb);
+      nb += 32;
+    }
+  }
+  __device__ __forceinline__ void init(const uint32_t* s, uint32_t nbytes) {
+    src = s;
+    nw = (nbytes + 3) >> 2;
+    nbits = nbytes * 8u;
+    pos = 0;
+    next = 0;
+    fly = ldq(0);
+    cw = 0;
+    buf = 0;
+    nb = 0;
+    fill();
+  }
+  __device__ __forceinline__ uint32_t peek() const { return (uint32_t)(buf >> 32); }
+  __device__ __forceinline__ void skip(int n) {
+    buf <<= n;
+    nb -= n;
+    pos += (uint32_t)n;
+    fill();
+  }
+  __device__ __forceinline__ bool insuff() const { return pos > nbits; }
+};
+
+// A lane's decoder table in LDS: the 9-bit lookahead and the long-code search data (a
+// lane reading the PTab in global memory for a long code would stall its whole wave).
+constexpr int kLaneTabBytes = 1024 + 64 + 256;
+struct LaneTab {
+  const DINO_LDS uint16_t* look;
+  const DINO_LDS int32_t* mv;    // maxcode[10..16], valoffset[10..16] (16 words)
+  const DINO_LDS uint8_t* hv;    // huffval[256]
+  __device__ __forceinline__ void lookup(int, uint32_t p, int* sym, int* len) const {
+    const uint32_t e = look[p >> (32 - kPLookBits)];
+    if (e) {
+      *sym = (int)(e >> 4);
+      *len = (int)(e & 15u);
+      return;
+    }
+    const uint32_t p17 = p >> 15;
+    int l = 17, off = 0;
+    for (int q = 16 - kPLookBits - 1; q >= 0; --q) {  // the shortest matching length wins
+      if ((int32_t)(p17 >> (17 - (kPLookBits + 1 + q))) <= mv[q]) {
+        l = kPLookBits + 1 + q;
+        off = mv[8 + q];
+      }
+    }
+    *len = l;
+    *sym = l > 16 ? 0 : (int)hv[((int)(p17 >> (17 - (l > 16 ? 16 : l))) + off) & 255];  // (l 17: JWRN_HUFF_BAD_CODE)
+  }
+};
+
+__global__ void __launch_bounds__(64) k_prefine(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
+                                                const PCtl* __restrict__ pctl, int maxb) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x;
+  DINO_LDS uint8_t* nat = (DINO_LDS uint8_t*)(smem + 64 * kLaneTabBytes + 64 * 128);
+  for (int q = lane; q < 80; q += 64) nat[q] = kNaturalOrder[q];
+  __syncthreads();
+  const int g = blockIdx.x * 64 + lane;
+  const int c = g / maxb, k = g - c * maxb;
+  if (c >= 3 || k >= (int)pctl->nprog) return;
+  const int img = pctl->pimg[k];
+  const ImgDesc& d = desc[img];
+  if (d.status != DINO_IMG_OK || d.kind != 1 || c >= d.ncomp) return;
+  uint8_t* region = ws + d.htab_off;
+  const PHdr* hd = (const PHdr*)region;
+  if (!((hd->pad[0] >> c) & 1)) return;
+  DINO_LDS uint8_t* ltab = (DINO_LDS uint8_t*)smem + lane * kLaneTabBytes;
+  DINO_LDS int16_t* blk = (DINO_LDS int16_t*)(smem + 64 * kLaneTabBytes) + lane * 64;
+  int16_t* coef = (int16_t*)(ws + d.coef_off);
+  const CompDesc& cd = d.comp[c];
+  const int64_t plane = cd.coef_off / 2;
+  const int32_t bw = cd.bw, mcx = ceil_div(cd.dw, 8), mcy = ceil_div(cd.dh, 8);
+  const int64_t nmcu = (int64_t)mcx * mcy;
+  const int n = hd->n_scans;
+  for (int j = 0; j < n; ++j) {
+    const PScan ps = ((const PScan*)(region + kPScanOff))[j];
+    const ScanRec& sr = ps.sr;
+    if (!(sr.ss > 0 && sr.ah > 0 && sr.comp[0] == c)) continue;
+    const PTab* tab = (const PTab*)(region + kPTabOff) + pbyte64(ps.tslots, 4);
+    {  // lookahead, maxcode / valoffset of lengths 10..16, huffval -> the lane's LDS table
+      const uint4* src = (const uint4*)tab->look;
+      DINO_LDS uint4* dst = (DINO_LDS uint4*)ltab;
+#pragma unroll 4
+      for (int q = 0; q < (1 << kPLookBits) * 2 / 16; ++q) dst[q] = src[q];
+      DINO_LDS int32_t* mv = (DINO_LDS int32_t*)(ltab + 1024);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        mv[q] = q < 7 ? tab->maxcode[kPLookBits + 1 + q] : 0;
+        mv[8 + q] = q < 7 ? tab->valoffset[kPLookBits + 1 + q] : 0;
+      }
+      const uint4* hs = (const uint4*)tab->huffval;
+      DINO_LDS uint4* hd4 = (DINO_LDS uint4*)(ltab + 1024 + 64);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) hd4[q] = hs[q];
+    }
+    LaneTab lt{(const DINO_LDS uint16_t*)ltab, (const DINO_LDS int32_t*)(ltab + 1024),
+               (const DINO_LDS uint8_t*)(ltab + 1024 + 64)};
+    LaneClean r;
+    r.init((const uint32_t*)(ws + d.ent_off + ((sr.data_off - d.scan_off + 3) & ~3)), (uint32_t)ps.pad);
+    const int ss = sr.ss, se = sr.se, al = sr.al;
+    int32_t eobrun = 0;
+    uint4 nxt[8];
+    {
+      const uint4* b4 = (const uint4*)(coef + plane);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
+    }
+    int32_t bx = 0, by = 0;
+    for (int64_t m = 0; m < nmcu; ++m) {
+      const int64_t e0 = plane + ((int64_t)by * bw + bx) * 64;
+      uint64_t nzz = 0;
+      {
+        uint32_t w[32];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          ((DINO_LDS uint4*)blk)[q] = nxt[q];
+          w[4 * q] = nxt[q].x;
+          w[4 * q + 1] = nxt[q].y;
+          w[4 * q + 2] = nxt[q].z;
+          w[4 * q + 3] = nxt[q].w;
+        }
+#pragma unroll
+        for (int kk = 1; kk < 64; ++kk) {  // constant indices: registers only
+          const int pos = kNaturalOrder[kk];
+          nzz |= (uint64_t)(((w[pos >> 1] >> (16 * (pos & 1))) & 0xFFFFu) != 0) << kk;
+        }
+      }
+      if (++bx == mcx) {
+        bx = 0;
+        ++by;
+      }
+      if (m + 1 < nmcu) {  // the next block's coefficients load while this one decodes
+        const uint4* b4 = (const uint4*)(coef + plane + ((int64_t)by * bw + bx) * 64);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
+      }
+      if (r.insuff()) continue;
+      uint64_t corr, nzn, neg;
+      r_refine_block(r, lt, ss, se, nzz, &eobrun, &corr, &nzn, &neg);
+      bool changed = false;
+      for (uint64_t mm = corr | nzn; mm; mm &= mm - 1) {
+        const int kk = __builtin_ctzll(mm);
+        const int pos = nat[kk];
+        const int16_t v = ac_refine_value(blk[pos], (corr >> kk) & 1u, (nzn >> kk) & 1u, (neg >> kk) & 1u, al);
+        changed |= v != blk[pos];
+        blk[pos] = v;
+      }
+      if (changed) {  // the refined block back as eight 16-byte stores
+        uint4* b4 = (uint4*)(coef + e0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) b4[q] = ((const DINO_LDS uint4*)blk)[q];
+      }
+    }
   }
 }
 
@@ -3713,6 +3959,9 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
   if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hresize_mfma), hipFuncAttributeMaxDynamicSharedMemorySize,
                                kHrMfmaLds)) != hipSuccess)
     return e;
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_prefine), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kPrefineLds)) != hipSuccess)
+    return e;
   g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
   // scan waves: one per CU by default.  A scan's serial decode runs on the CU's one scalar
   // unit, which the CU's waves share: two scan waves on a CU each run at about half speed
@@ -3720,6 +3969,8 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
   const char* pc = getenv("DINO_PSCAN_PER_CU");
   const int per_cu = pc && atoi(pc) > 0 ? atoi(pc) : 1;
   g->grid_ps = per_cu * cus;
+  const char* pf = getenv("DINO_PREFINE_COMPS");
+  g->prefine = pf ? (atoi(pf) & 7) : 0;
   return hipSuccess;
 }
 
@@ -3733,8 +3984,11 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   // after k_htab's kind switch
-  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
+  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl,
+                                                             a.geom.prefine)));
   TIMED(tm, kKProg, s, (k_pscan<<<a.geom.grid_ps, kPScanThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
+  if (a.geom.prefine)
+    TIMED(tm, kKProg, s, (k_prefine<<<(3 * B + 63) / 64, 64, kPrefineLds, s>>>(a.desc, a.ws, a.pctl, B)));
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));

@@ -63,6 +63,7 @@ struct LaunchGeom {
   int32_t grid1;     // persistent k_huff1 grid (occupancy x CUs)
   int32_t grid3;     // persistent k_huff3 grid
   int32_t grid_ps;   // persistent k_pscan grid (waves)
+  int32_t prefine;   // components whose AC refinement scans k_prefine decodes in lane mode (bit c; 0: none)
 };
 
 // Coefficient-buffer images of a batch (k_plan zeroes, k_pwalk registers, k_pscan

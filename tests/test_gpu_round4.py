@@ -196,3 +196,50 @@ def test_kept_slice_of_an_output_is_not_refilled(gpu_device):
     for (a, b), (sa, sb) in zip(kept, snaps):
         assert torch.equal(a, sa) and torch.equal(b, sb)
     assert len(set(ptrs)) < nb  # the batches nobody kept were refilled in place
+
+
+@pytest.mark.parametrize("comps", [7, 6])
+def test_lane_mode_refinement_bit_exact(gpu_device, monkeypatch, comps):
+    """k_prefine (DINO_PREFINE_COMPS: AC refinement scans decoded one lane per image and
+    component, measured and off by default): the progressive zoo, the damaged streams and
+    the test writer's progressions decode bit-exact with Pillow with every component (7) or
+    the chroma components (6) in lane mode."""
+    from tests import jpeg_writer as jw
+    from tests.test_emu_cpu import _damaged_streams
+    from tests.test_gpu_parity import _to_dev
+    from tests.test_gpu_round2 import _prog_zoo
+    from tests.test_multiscan_cpu import multiscan_cases
+    from dataloader_amd.engine import IngestEngine
+    from oracle import cpu_ref
+    monkeypatch.setenv("DINO_PREFINE_COMPS", str(comps))
+    rng = np.random.default_rng(74)
+    cases = [("zoo", j) for j in _prog_zoo(rng)] + list(_damaged_streams(rng)) + \
+        multiscan_cases(rng, sizes=((83, 61), (130, 97)))
+    img = textured_rgb(48, 40, rng)
+    for k, (w, h) in enumerate(((48, 40), (333, 250))):  # two refinements of luma, chroma refined in between
+        img = textured_rgb(w, h, rng)
+        cases.append((f"refine_chain_{k}", jw.encode(img, [jw.scan((0, 1, 2), 0, 0, 0, 0), jw.scan((0,), 1, 63, 0, 2),
+                                                         jw.scan((1,), 1, 63, 0, 1), jw.scan((2,), 1, 63, 0, 1),
+                                                         jw.scan((0,), 1, 63, 2, 1), jw.scan((1,), 1, 63, 1, 0),
+                                                         jw.scan((0,), 1, 63, 1, 0), jw.scan((2,), 1, 63, 1, 0)],
+                                                     progressive=True)))
+    jpegs = [j for _, j in cases]
+    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
+    d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    bad = []
+    for i, (name, j) in enumerate(cases):
+        ref = cpu_ref.decode_rgb(j)
+        if ref is None:
+            if info[i, 0] >= 0:
+                bad.append((name, "status", int(info[i, 0])))
+            continue
+        ref = np.asarray(ref)
+        if info[i, 0] != 0:
+            bad.append((name, "status", int(info[i, 0])))
+            continue
+        got = eng.copy_rgb(i, ref.shape[1], ref.shape[0]).cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad.append((name, int((got != ref).sum())))
+    eng.close()
+    assert not bad, bad
