@@ -53,6 +53,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "images/sec decode+10-crop, device-resident (JPEG bytes in HBM), 1/2/4/8 GPU"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 VFINAL_MAX_S = 128  # kernels.hip kVFinalMaxS: views up to this size run k_vfinal (vertical pass + epilogue fused)
+FUSE_MAX_W = 2304  # kernels.hip kFuseMaxW: 4:2:0 images up to this width run k_ycolor (luma IDCT + colour fused)
 
 
 # ----------------------------------------------------------------------------- synthetic data
@@ -147,6 +148,12 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     s_unfused = float(np.mean([len(j) if not f else 0 for j, f in zip(jpegs, fz)]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
     per_blk = entry_bytes_per_block + 8.0       # sparse entries + the 8-byte block record
+    fu = [w <= FUSE_MAX_W for w, _ in dims]      # (synthetic encodes are all 4:2:0)
+    chroma_fused = float(np.mean([b / 3 if f else 0 for b, f in zip(nblk, fu)]))
+    luma_fused = 2 * chroma_fused
+    blocks_unfused = blocks - 3 * chroma_fused
+    blocks_idct = blocks - luma_fused
+    px_fused = float(np.mean([w * h if f else 0 for (w, h), f in zip(dims, fu)]))
     ab = {
         "path": s_jpeg + out,                       # S_jpeg + 1 044 480 B (bf16)
         "k_destuff": s_jpeg,                         # per launch: count pass reads, write pass reads + writes
@@ -155,8 +162,12 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
         "k_huff1": s_jpeg + blk_fused * per_blk,
         # re-decode of the other images: entropy bytes in, sparse entries + records out
         "k_huff3": s_unfused + (blocks - blk_fused) * per_blk,
-        "k_idct": blocks * per_blk + blocks * 64,
-        "k_color": blocks * 64 + px * 3,
+        # 4:2:0 images at most FUSE_MAX_W wide: k_idct transforms their chroma planes only and
+        # k_ycolor their luma blocks (entries in) + the chroma planes in + RGB out (no luma plane);
+        # k_color converts the other images from their planes
+        "k_idct": blocks_idct * (per_blk + 64),
+        "k_ycolor": luma_fused * per_blk + chroma_fused * 64 + px_fused * 3,
+        "k_color": blocks_unfused * 64 + (px - px_fused) * 3,
         "k_final_global": (3 + out_bytes * 3) * n_g * g * g,
         "k_final_local": (3 + out_bytes * 3) * n_l * l * l,
         "s_jpeg": s_jpeg,

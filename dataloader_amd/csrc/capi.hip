@@ -203,7 +203,7 @@ int dino_augment(dino_ctx* c, const dino_aug_config* cfg, const dino_view_params
     return fail(DINO_EINVAL, "dino_augment: dino_set_norm covers %s%lld images, fewer than the batch", "", c->norm_n);
   hipStream_t s = (hipStream_t)stream;
   AugmentArgs a{c->d_desc, c->last_batch, d_params, c->d_plan, c->d_ws, c->d_aws, c->aws_size, c->d_gcrop, {}, *cfg,
-                c->d_norm};
+                c->d_norm, c->geom.grid_hr};
   for (int v = 0; v < nv; ++v) {
     if (!d_views[v]) return fail(DINO_EINVAL, "dino_augment: null output pointer for view %s%lld", "", v);
     a.views.p[v] = d_views[v];

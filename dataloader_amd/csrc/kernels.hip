@@ -614,18 +614,33 @@ constexpr uint32_t kBinfoAbsDc = 1u << 15;
 // one 8-byte record per block carries the DC too (a difference until k_dcscan sums
 // it in place; absolute with restart intervals).  k_idct scatters the entries into
 // its LDS block.
+#ifndef DINO_SINK_CHUNKS
+#define DINO_SINK_CHUNKS 2
+#endif
+#ifndef DINO_SINK_PAIRS
+#define DINO_SINK_PAIRS 0
+#endif
+constexpr int kSinkChunks = DINO_SINK_CHUNKS;  // 16-byte entry chunks a lane stores together (1, 2, 4)
+constexpr bool kSinkPairs = DINO_SINK_PAIRS;   // block records stored as aligned 16-byte pairs
 struct SparseSink {
   uint32_t* ent;   // image entry area
   uint2* binfo;    // image block info
-  uint32_t n;      // halfwords stored (relative to the image entry area), multiple of 8
+  uint32_t n;      // halfwords in whole chunks (relative to the image entry area), multiple of 8
   uint32_t k;      // halfwords buffered in w0..w3
   uint32_t w0, w1, w2, w3;
+  uint4 pend[kSinkChunks > 1 ? kSinkChunks - 1 : 1];  // whole chunks not stored yet (kc of them)
+  uint32_t kc;
+  uint2 prec;      // record of the even block pb of an open pair (kSinkPairs)
+  int32_t pb;
+  bool hrec;
   uint32_t bstart, dcw, n16, n32;
   bool wide;       // the open block has switched to u32 entries
   int32_t b;
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
+    kc = 0;
+    hrec = false;
   }
   __device__ void begin(int32_t blk) {
     b = blk;
@@ -642,10 +657,30 @@ struct SparseSink {
     w2 = __builtin_amdgcn_alignbyte(w3, w2, 2);
     w3 = __builtin_amdgcn_alignbyte(h, w3, 2);
   }
+  // a lane's region starts 256-byte aligned, so a group of kSinkChunks chunks is aligned too
+  __device__ void chunk_done() {
+    const uint4 w = make_uint4(w0, w1, w2, w3);
+    if (kSinkChunks == 1) {
+#ifndef DINO_DIAG_NOENT  // traffic diagnosis builds only: entries not stored (output invalid)
+      *(uint4*)(ent + (n >> 1)) = w;
+#endif
+    } else if (kc == kSinkChunks - 1) {
+      uint4* dst = (uint4*)(ent + ((n - 8 * kc) >> 1));
+#pragma unroll
+      for (int j = 0; j < kSinkChunks - 1; ++j) dst[j] = pend[j];
+      dst[kSinkChunks - 1] = w;
+      kc = 0;
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSinkChunks - 1; ++j)
+        if (j == (int)kc) pend[j] = w;
+      ++kc;
+    }
+  }
   __device__ void put(uint32_t h) {
     shift_in(h);
     if (++k == 8) {
-      *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
+      chunk_done();
       n += 8;
       k = 0;
     }
@@ -666,14 +701,35 @@ struct SparseSink {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void end() { binfo[b] = make_uint2(bstart, n16 | (n32 << 7) | dcw); }
+  __device__ void record(int32_t blk, uint2 r) {
+    if (!kSinkPairs) {
+      binfo[blk] = r;
+    } else if (blk & 1) {  // odd block: completes the pair opened by blk - 1 (if this lane opened it)
+      if (hrec) *(uint4*)(binfo + blk - 1) = make_uint4(prec.x, prec.y, r.x, r.y);
+      else binfo[blk] = r;
+      hrec = false;
+    } else {
+      prec = r;
+      pb = blk;
+      hrec = true;
+    }
+  }
+  __device__ void end() { record(b, make_uint2(bstart, n16 | (n32 << 7) | dcw)); }
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
-  __device__ void zero(int32_t blk) { binfo[blk] = make_uint2(n + k, kBinfoAbsDc); }
+  __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
   __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
-    if (k) {
+    if (k)
       for (uint32_t j = k; j < 8; ++j) shift_in(0u);
+    if (kSinkChunks > 1) {
+      uint4* dst = (uint4*)(ent + ((n - 8 * kc) >> 1));
+#pragma unroll
+      for (int j = 0; j < kSinkChunks - 1; ++j)
+        if (j < (int)kc) dst[j] = pend[j];
+      if (k) dst[kc] = make_uint4(w0, w1, w2, w3);
+    } else if (k) {
       *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
     }
+    if (kSinkPairs && hrec) binfo[pb] = prec;  // a lone even block (the lane's last record)
   }
 };
 
@@ -2067,6 +2123,91 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define DINO_IDCT_WGS 32
 #endif
 constexpr int kIdctWgs = DINO_IDCT_WGS;  // workgroups per image (grid-stride over its blocks)
+
+// The steps of one 8-lane group's block (k_idct, k_ycolor).  sb: the group's LDS block,
+// rows of 9 words, all zero on entry.
+// Dense coefficients (kind 1): lane l loads row l of the block (8 int16 = one 16-byte load).
+__device__ __forceinline__ void idct_group_dense(int32_t* sb, int l, const uint8_t* blk) {
+  const uint4 q = *(const uint4*)(blk + l * 16);
+  const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sb[l * 9 + j] = (int32_t)(int16_t)(w4[j >> 1] >> (16 * (j & 1)));
+}
+// Sparse entries (kind 0): the block record bi and the block's halfword entries
+// l, l + 8, .. (kIdctPre of them) already loaded into pre[]; halfword entries
+// (zigzag | int10 value << 6), then u32 entries from the next even halfword (see
+// SparseSink); the DC is int16 (absolute after k_dcscan).
+#ifndef DINO_IDCT_PRE
+#define DINO_IDCT_PRE 2
+#endif
+constexpr int kIdctPre = DINO_IDCT_PRE;  // halfword entries per lane loaded a block ahead (8 lanes: 8 kIdctPre)
+__device__ __forceinline__ void idct_load_pre(uint32_t* pre, int l, uint2 bi, const uint16_t* ent16) {
+  const uint32_t c = bi.y & 0x7Fu;
+#pragma unroll
+  for (int m = 0; m < kIdctPre; ++m) pre[m] = l + 8 * m < (int)c ? ent16[bi.x + l + 8 * m] : 0u;
+}
+__device__ __forceinline__ void idct_group_sparse(int32_t* sb, int l, const uint8_t* s_nat, uint2 bi, const uint32_t* pre,
+                                                  const uint16_t* ent16, const uint32_t* ent) {
+  if (l == 0) sb[0] = (int32_t)bi.y >> 16;
+  const uint32_t c16 = bi.y & 0x7Fu, c32 = (bi.y >> 7) & 0x7Fu;
+#pragma unroll
+  for (int m = 0; m < kIdctPre; ++m)
+    if (l + 8 * m < (int)c16) sb[s_nat[pre[m] & 63u]] = (int32_t)(int16_t)pre[m] >> 6;
+  for (uint32_t j = l + 8 * kIdctPre; j < c16; j += 8) {
+    const uint32_t h = ent16[bi.x + j];
+    sb[s_nat[h & 63u]] = (int32_t)(int16_t)h >> 6;
+  }
+  const uint32_t* e32 = ent + ((bi.x + c16 + 1) >> 1);
+  for (uint32_t j = l; j < c32; j += 8) {
+    const uint32_t e = e32[j];
+    sb[s_nat[e & 63u]] = (int32_t)(int16_t)(e >> 16);
+  }
+}
+// Dequantize + pass 1 on column l (reads and writes only this lane's column).
+__device__ __forceinline__ void idct_group_pass1(int32_t* sb, int l, const uint16_t* q) {
+  int32_t raw[8], qq[8], wcol[8];
+  bool acz = true;  // rows 1..7 of this column are zero
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    raw[r] = sb[r * 9 + l];
+    qq[r] = (int32_t)(int16_t)q[r * 8 + l];
+    if (r) acz = acz && raw[r] == 0;
+  }
+  // libjpeg-turbo's SIMD pass 1 decides its DC-only shortcut for the whole block
+  const int gsh = threadIdx.x & 56;  // this group's first lane within the wave
+  idct_pass1(raw, qq, ((__ballot(acz) >> gsh) & 0xFFu) == 0xFFu, wcol);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) sb[r * 9 + l] = wcol[r];
+}
+// Pass 2 on row l: returns output row l (8 samples); the row is cleared for the next block.
+__device__ __forceinline__ uint64_t idct_group_pass2(int32_t* sb, int l) {
+  int32_t row[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) row[j] = sb[l * 9 + j];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
+  union {
+    uint8_t b[8];
+    uint64_t u;
+  } o;
+  idct_pass2(row, o.b);
+  return o.u;
+}
+
+// Images whose luma IDCT and colour conversion run fused in k_ycolor: YCbCr 4:2:0 with
+// fancy h2v2 chroma (k_color's fast420 case), at most kFuseMaxW pixels wide (the band's
+// luma rows live in LDS).  k_idct transforms only their chroma planes; k_color skips them.
+#ifndef DINO_FUSE_MAX_W
+#define DINO_FUSE_MAX_W 2304
+#endif
+constexpr int kFuseMaxW = DINO_FUSE_MAX_W;  // 0: no image is fused (A/B)
+__device__ __forceinline__ bool fused_420(const ImgDesc& d) {
+  if (kFuseMaxW == 0 || d.status != DINO_IMG_OK || d.kind == 2 || d.ncomp != 3 || d.color != kYCbCr) return false;
+  const CompDesc &c0 = d.comp[0], &c1 = d.comp[1], &c2 = d.comp[2];
+  return d.width <= kFuseMaxW && d.max_h == 2 && d.max_v == 2 && c0.h == 2 && c0.v == 2 && c1.h == 1 && c1.v == 1 &&
+         c2.h == 1 && c2.v == 1 && c1.dw > 2 && c1.dw == c2.dw && c1.dh == c2.dh;
+}
+
 __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const BlkIdx bk = xcd_blk();
   // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
@@ -2119,26 +2260,25 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     return r;
   };
   const int T = (int)tot, step = gridDim.x * kIdctBlocksPerWg;
+  // the luma plane of a k_ycolor image is transformed there, band by band
+  const int G0 = fused_420(d) ? (int)nb0 : 0;
   // The next block's record is loaded one iteration ahead, and its first 16 entries
   // at the end of the current iteration (once the record has arrived), so the
   // scatter at the top of an iteration normally waits on nothing.
-  int gn = bk.x * kIdctBlocksPerWg + grp;
-  Blk nx = locate(gn < T ? gn : 0);
+  int gn = G0 + bk.x * kIdctBlocksPerWg + grp;
+  Blk nx = locate(gn < T ? gn : G0);
   uint2 bin = make_uint2(0u, 0u);
   if (!dense && gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
   const uint16_t* ent16 = (const uint16_t*)ent;
-  uint32_t ea = 0, eb = 0;  // halfword entries l and l + 8 of the next block
+  uint32_t pre[kIdctPre] = {};  // the next block's first halfword entries (l, l + 8, ..)
   auto first_entries = [&]() {
-    if (dense) return;
-    const uint32_t c = bin.y & 0x7Fu;
-    ea = l < c ? ent16[bin.x + l] : 0u;
-    eb = l + 8 < c ? ent16[bin.x + l + 8] : 0u;
+    if (!dense) idct_load_pre(pre, l, bin, ent16);
   };
   if (gn < T) first_entries();
 #pragma unroll
   for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
   __syncthreads();
-  for (int g0 = bk.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
+  for (int g0 = G0 + bk.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
     const bool valid = gn < T;
     const Blk cur = nx;
     const uint2 bi = bin;
@@ -2148,61 +2288,19 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
       bin = make_uint2(0u, 0u);
       if (!dense && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
     }
-    if (valid && dense) {  // lane l: row l of the block (8 int16 = one 16-byte load)
+    if (valid && dense) {
       const CompDesc& cc = d.comp[cur.c];
-      const uint4 q = *(const uint4*)(ws + d.coef_off + cc.coef_off + ((int64_t)cur.by * cc.bw + cur.bx) * 128 + l * 16);
-      const uint32_t w4[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sb[l * 9 + j] = (int32_t)(int16_t)(w4[j >> 1] >> (16 * (j & 1)));
+      idct_group_dense(sb, l, ws + d.coef_off + cc.coef_off + ((int64_t)cur.by * cc.bw + cur.bx) * 128);
     } else if (valid) {
-      if (l == 0) sb[0] = (int32_t)bi.y >> 16;  // DC (int16, absolute after k_dcscan)
-      // halfword entries (zigzag | int10 value << 6), then u32 entries from the next
-      // even halfword (see SparseSink)
-      const uint32_t c16 = bi.y & 0x7Fu, c32 = (bi.y >> 7) & 0x7Fu;
-      if (l < c16) sb[s_nat[ea & 63u]] = (int32_t)(int16_t)ea >> 6;
-      if (l + 8 < c16) sb[s_nat[eb & 63u]] = (int32_t)(int16_t)eb >> 6;
-      for (uint32_t j = l + 16; j < c16; j += 8) {
-        const uint32_t h = ent16[bi.x + j];
-        sb[s_nat[h & 63u]] = (int32_t)(int16_t)h >> 6;
-      }
-      const uint32_t* e32 = ent + ((bi.x + c16 + 1) >> 1);
-      for (uint32_t j = l; j < c32; j += 8) {
-        const uint32_t e = e32[j];
-        sb[s_nat[e & 63u]] = (int32_t)(int16_t)(e >> 16);
-      }
+      idct_group_sparse(sb, l, s_nat, bi, pre, ent16, ent);
     }
     wave_lds_sync();
     const CompDesc& cd = d.comp[cur.c];
-    if (valid) {  // dequantize + pass 1 on column l (reads and writes only this lane's column)
-      const uint16_t* q = d.qt[cd.tq];
-      int32_t raw[8], qq[8], wcol[8];
-      bool acz = true;  // rows 1..7 of this column are zero
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        raw[r] = sb[r * 9 + l];
-        qq[r] = (int32_t)(int16_t)q[r * 8 + l];
-        if (r) acz = acz && raw[r] == 0;
-      }
-      // libjpeg-turbo's SIMD pass 1 decides its DC-only shortcut for the whole block
-      const int gsh = threadIdx.x & 56;  // this group's first lane within the wave
-      idct_pass1(raw, qq, ((__ballot(acz) >> gsh) & 0xFFu) == 0xFFu, wcol);
-#pragma unroll
-      for (int r = 0; r < 8; ++r) sb[r * 9 + l] = wcol[r];
-    }
+    if (valid) idct_group_pass1(sb, l, d.qt[cd.tq]);
     wave_lds_sync();
-    if (valid) {  // pass 2 on row l, then the row is cleared for the next block
-      int32_t row[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) row[j] = sb[l * 9 + j];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
-      union {
-        uint8_t b[8];
-        uint64_t u;
-      } o;
-      idct_pass2(row, o.b);
+    if (valid) {
       const int pitch = cd.bw * 8;
-      *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = o.u;
+      *(uint64_t*)(planes + cd.plane_off + ((int64_t)cur.by * 8 + l) * pitch + cur.bx * 8) = idct_group_pass2(sb, l);
     }
     if (gn < T) first_entries();
     wave_lds_sync();
@@ -2271,7 +2369,7 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
                                                const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const BlkIdx bk = xcd_blk();
   const ImgDesc& d = desc[bk.y];
-  if (d.status != DINO_IMG_OK) return;
+  if (d.status != DINO_IMG_OK || fused_420(d)) return;
   if (d.kind == 2) {  // pre-decoded RGB container: copy the pixels into the workspace
     const uint8_t* src = bytes + offsets[bk.y] + d.scan_off;
     uint32_t* dst = (uint32_t*)(ws + d.rgb_off);
@@ -2417,6 +2515,159 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
 }
 
 // ---------------------------------------------------------------------------
+// k_ycolor: grid (gx, B); one band (one luma block row = 8 pixel rows, full width)
+// per workgroup turn, for the fused_420 images
+// ---------------------------------------------------------------------------
+// The band's luma blocks are transformed by 8-lane groups as in k_idct (the next
+// block's record loaded one block ahead, its first entries at the end of the current
+// one), but their rows go to LDS instead of the luma plane; then k_color's 4:2:0 quad
+// conversion runs with Y from LDS and Cb / Cr from the planes k_idct wrote.  The luma
+// plane never reaches HBM (k_idct writes it and k_color reads it back for every other
+// image).  A band's output is the contiguous RGB range of its 8 rows, whose length 24 W
+// is a multiple of 12: quads never straddle two bands.
+constexpr int kFuseYPitch = kFuseMaxW + 32;  // 8 words mod 64 banks: a wave's row stores hit 64 banks
+#ifndef DINO_YCOLOR_WGS
+#define DINO_YCOLOR_WGS 32
+#endif
+constexpr int kYcolorWgs = DINO_YCOLOR_WGS;  // workgroups per image (grid-stride over its bands)
+
+__global__ void __launch_bounds__(256) k_ycolor(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+  const BlkIdx bk = xcd_blk();
+  __shared__ int32_t s_blk[kIdctBlocksPerWg][72];
+  __shared__ uint8_t s_nat[80];
+  __shared__ __attribute__((aligned(16))) uint8_t s_y[8 * (kFuseMaxW ? kFuseYPitch : 8)];
+  const ImgDesc& d = desc[bk.y];
+  if (!fused_420(d)) return;
+  const int W = d.width, H = d.height;
+  const int nband = (H + 7) >> 3;
+  if (bk.x >= nband) return;
+  const int t = threadIdx.x;
+  if (t < 80) s_nat[t] = (uint8_t)((kNaturalOrder[t] >> 3) * 9 + (kNaturalOrder[t] & 7));
+  const int grp = t >> 3, l = t & 7;
+  int32_t* sb = s_blk[grp];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
+  const bool dense = d.kind == 1;
+  const CompDesc& cy = d.comp[0];
+  const uint16_t* qt = d.qt[cy.tq];
+  int moff0 = 0;  // first luma position inside the MCU
+  for (int i = d.blocks_per_mcu - 1; i >= 0; --i)
+    if (d.mcu_comp[i] == 0) moff0 = i;
+  const uint32_t* ent = (const uint32_t*)(ws + d.coef_off);
+  const uint16_t* ent16 = (const uint16_t*)ent;
+  const uint2* binfo = (const uint2*)(ws + d.binfo_off);
+  const int nbx = (W + 7) >> 3;
+  const PlaneView p1 = make_plane_view(d, ws, 1), p2 = make_plane_view(d, ws, 2);
+  uint32_t* rgb = (uint32_t*)(ws + d.rgb_off);
+  const int64_t npx = (int64_t)W * H;
+  // quad walk of a band: thread t starts at pixel 4t, then advances 1024 pixels per turn
+  const int dy = 1024 / W, dx = 1024 - dy * W;
+  const int y0 = (4 * t) / W, x0 = 4 * t - y0 * W;
+  // sparse record of luma block (j, k) (decode order: MCU (j/2, k/2), position moff0 + 2 (k&1) + (j&1))
+  auto record = [&](int j, int k) {
+    const int b = ((k >> 1) * d.mcus_x + (j >> 1)) * d.blocks_per_mcu + moff0 + (k & 1) * 2 + (j & 1);
+    return b < d.total_blocks ? binfo[b] : make_uint2(0u, 0u);
+  };
+  __syncthreads();
+  for (int k = bk.x; k < nband; k += gridDim.x) {
+    // the band's luma blocks (block row k): group grp takes blocks grp, grp + 32, ...
+    int jn = grp;
+    uint2 bin = make_uint2(0u, 0u);
+    uint32_t pre[kIdctPre] = {};  // the next block's first halfword entries (l, l + 8, ..)
+    auto first_entries = [&]() { idct_load_pre(pre, l, bin, ent16); };
+    if (!dense && jn < nbx) {
+      bin = record(jn, k);
+      first_entries();
+    }
+    for (int j0 = 0; j0 < nbx; j0 += kIdctBlocksPerWg) {
+      const int j = jn;
+      const bool valid = j < nbx;
+      const uint2 bi = bin;
+      jn += kIdctBlocksPerWg;
+      if (!dense && jn < nbx) bin = record(jn, k);
+      if (valid && dense) idct_group_dense(sb, l, ws + d.coef_off + cy.coef_off + ((int64_t)k * cy.bw + j) * 128);
+      else if (valid) idct_group_sparse(sb, l, s_nat, bi, pre, ent16, ent);
+      wave_lds_sync();
+      if (valid) idct_group_pass1(sb, l, qt);
+      wave_lds_sync();
+      if (valid) *(uint64_t*)(s_y + l * kFuseYPitch + j * 8) = idct_group_pass2(sb, l);
+      if (!dense && jn < nbx) first_entries();
+      wave_lds_sync();
+    }
+    __syncthreads();
+    // colour: the band's quads (pixel 8kW + 4q, output words 3 (2kW + q) ..)
+    const int rows = min(8, H - 8 * k);
+    const int nq = (rows * W + 3) >> 2;
+    const int64_t qb = (int64_t)2 * k * W, pb = (int64_t)8 * k * W;
+    int y = y0, x = x0;
+    for (int q = t; q < nq; q += 256) {
+      union {
+        uint8_t b[12];
+        uint32_t w[3];
+      } o;
+      const int gy = 8 * k + y;
+      if (x + 3 < W) {  // Y from LDS; Cb / Cr words at column x/2 - 1 of the nearer and the farther row
+        const uint32_t* yp = (const uint32_t*)(s_y + y * kFuseYPitch + (x & ~3));
+        const uint32_t yw = __builtin_amdgcn_alignbyte(yp[1], yp[0], (uint32_t)(x & 3));
+        const int r = gy >> 1;
+        const int rf = (gy & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
+        const int c0 = x >> 1, cc = c0 - 1;
+        const uint32_t csh = (uint32_t)(cc & 3);
+        const uint32_t edge = (c0 == 0 ? 1u : 0u) | (c0 + 1 >= p1.dw ? 2u : 0u) | (c0 + 2 >= p1.dw ? 4u : 0u);
+        const uint32_t* cp[4] = {(const uint32_t*)(p1.p + (int64_t)r * p1.pitch + (cc & ~3)),
+                                 (const uint32_t*)(p1.p + (int64_t)rf * p1.pitch + (cc & ~3)),
+                                 (const uint32_t*)(p2.p + (int64_t)r * p2.pitch + (cc & ~3)),
+                                 (const uint32_t*)(p2.p + (int64_t)rf * p2.pitch + (cc & ~3))};
+        uint32_t cw[8];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          cw[2 * m] = cp[m][0];
+          cw[2 * m + 1] = cp[m][1];
+        }
+        int cb[4], cr[4];
+        h2v2_quad(__builtin_amdgcn_alignbyte(cw[1], cw[0], csh), __builtin_amdgcn_alignbyte(cw[3], cw[2], csh), x, edge,
+                  cb);
+        h2v2_quad(__builtin_amdgcn_alignbyte(cw[5], cw[4], csh), __builtin_amdgcn_alignbyte(cw[7], cw[6], csh), x, edge,
+                  cr);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) ycc_to_rgb((int)((yw >> (8 * m)) & 255u), cb[m], cr[m], o.b + 3 * m);
+      } else {  // a quad that wraps a row: per pixel, same arithmetic
+        int py = y, px = x;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          if (pb + 4 * q + m < npx) {
+            const int g = 8 * k + py;
+            const int r = g >> 1, c = px >> 1;
+            const int rn = (g & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
+            const int cn = (px & 1) ? min(c + 1, p1.dw - 1) : max(c - 1, 0);
+            const int bias = (px & 1) ? 7 : 8;
+            const int tb = pv_at(p1, c, r) * 3 + pv_at(p1, c, rn), nb = pv_at(p1, cn, r) * 3 + pv_at(p1, cn, rn);
+            const int tr = pv_at(p2, c, r) * 3 + pv_at(p2, c, rn), nr = pv_at(p2, cn, r) * 3 + pv_at(p2, cn, rn);
+            ycc_to_rgb(s_y[py * kFuseYPitch + px], (tb * 3 + nb + bias) >> 4, (tr * 3 + nr + bias) >> 4, o.b + 3 * m);
+          } else {
+            o.b[3 * m] = o.b[3 * m + 1] = o.b[3 * m + 2] = 0;
+          }
+          if (++px == W) {
+            px = 0;
+            ++py;
+          }
+        }
+      }
+      rgb[3 * (qb + q)] = o.w[0];
+      rgb[3 * (qb + q) + 1] = o.w[1];
+      rgb[3 * (qb + q) + 2] = o.w[2];
+      x += dx;
+      y += dy;
+      if (x >= W) {
+        x -= W;
+        ++y;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Augment half
 // ---------------------------------------------------------------------------
 __global__ void k_params(const ImgDesc* __restrict__ desc, int B, dino_aug_config cfg, uint64_t seed,
@@ -2465,6 +2716,8 @@ __device__ bool params_valid(const dino_view_params& p, const ImgDesc& d, int S)
   return true;
 }
 
+__device__ int hr_view_chunks(int S, int cw, int ch, int kh);
+
 // k_vsizes: one lane per view: validity and scratch bytes into plan[i] (htmp_off holds
 // the size and rcoef_off the offset of the coefficient tables inside it until k_vplan
 // places the view), so that the single-workgroup scan only reads packed records.
@@ -2486,6 +2739,8 @@ __global__ void __launch_bounds__(256) k_vsizes(const ImgDesc* __restrict__ desc
   vp.kv = kv;
   vp.htmp_off = a;
   vp.rcoef_off = kh ? align16((int64_t)prm[i].crop_h * S * 3) : 0;
+  vp.hr_chunks = ok && kh ? hr_view_chunks(S, prm[i].crop_w, prm[i].crop_h, kh) : 0;
+  vp.hr_base = 0;
   plan[i] = vp;
 }
 
@@ -2498,24 +2753,35 @@ __global__ void __launch_bounds__(1024) k_vplan(ImgDesc* __restrict__ desc, cons
                                                 int B, int nv, int n_global, int gsize, int lsize, int64_t aws_size,
                                                 ViewPlan* __restrict__ plan) {
   __shared__ int64_t part[1024];
+  __shared__ int2 hpart[1024];
   const int t = threadIdx.x, N = B * nv;
   for (int b = t; b < B; b += 1024) desc[b].aug_status = 0;
   const int per = (N + 1023) / 1024;
   int64_t local = 0;
+  int2 hl = make_int2(0, 0);  // k_hresize work items of this thread's global / local views
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
-    if (i < N) local += plan[i].htmp_off;  // k_vsizes: the view's scratch bytes
+    if (i < N) {
+      local += plan[i].htmp_off;  // k_vsizes: the view's scratch bytes
+      if ((i % nv) < n_global) hl.x += plan[i].hr_chunks;
+      else hl.y += plan[i].hr_chunks;
+    }
   }
   part[t] = local;
+  hpart[t] = hl;
   __syncthreads();
   for (int s = 1; s < 1024; s <<= 1) {
     int64_t v = t >= s ? part[t - s] : 0;
+    int2 hv = t >= s ? hpart[t - s] : make_int2(0, 0);
     __syncthreads();
     part[t] += v;
+    hpart[t].x += hv.x;
+    hpart[t].y += hv.y;
     __syncthreads();
   }
   const bool fits = part[1023] <= aws_size;
   int64_t base = part[t] - local;
+  int2 hb = make_int2(hpart[t].x - hl.x, hpart[t].y - hl.y);
   for (int k = 0; k < per; ++k) {
     int i = t * per + k;
     if (i >= N) continue;
@@ -2524,6 +2790,13 @@ __global__ void __launch_bounds__(1024) k_vplan(ImgDesc* __restrict__ desc, cons
     vp.ok = vp.ok && fits;
     vp.htmp_off = base;
     vp.rcoef_off += base;
+    if ((i % nv) < n_global) {
+      vp.hr_base = hb.x;
+      hb.x += vp.hr_chunks;
+    } else {
+      vp.hr_base = hb.y;
+      hb.y += vp.hr_chunks;
+    }
     plan[i] = vp;
     base += a;
   }
@@ -2636,14 +2909,14 @@ __host__ __device__ __forceinline__ bool hresize_mfma_ok(int S, int cw, int kh) 
 #define DINO_HRESIZE_MIN_ROWS 8
 #endif
 constexpr int kHresizeMinRows = DINO_HRESIZE_MIN_ROWS;  // rows per band the slice width is chosen for
-#ifndef DINO_HRESIZE_WGS
-#define DINO_HRESIZE_WGS 4
+#ifndef DINO_HRESIZE_BANDS
+#define DINO_HRESIZE_BANDS 8
 #endif
-constexpr int kHresizeWgs = DINO_HRESIZE_WGS;  // workgroups per view (each loops over the view's tiles)
-#ifndef DINO_HRESIZE_PREFETCH
-#define DINO_HRESIZE_PREFETCH 0
+constexpr int kHrBandsPerItem = DINO_HRESIZE_BANDS;  // row bands of one slice per work item
+constexpr int kHrDirectItems = 4;                    // work items of a direct-path view
+#ifndef DINO_HRESIZE_OCC
+#define DINO_HRESIZE_OCC 1  // launch-bounds occupancy hint (A/B: 6 caps the VGPRs at 80, with a small spill)
 #endif
-constexpr int kHrPre = DINO_HRESIZE_PREFETCH;  // staging items per thread loaded one tile ahead (0: none)
 
 // Tile shape of a view's horizontal pass: the widest slice of outputs (all of S,
 // else a multiple of 8) whose taps (16 bytes per output + 16 per output and group
@@ -2678,6 +2951,39 @@ __device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
   t.R = R;
   t.R3p = 3 * R + 2;
   return t;
+}
+
+// Work items of a view's horizontal pass (k_vsizes): kHrBandsPerItem row bands of one
+// slice each, so that a batch of mixed crop sizes spreads over the persistent grid in
+// pieces of similar size (a large crop's view is many items, a small one's few).
+__device__ int hr_view_chunks(int S, int cw, int ch, int kh) {
+  if (hresize_mfma_ok(S, cw, kh)) return 0;  // k_hresize_mfma's view
+  const HrTile t = hresize_tile(S, cw, kh);
+  if (t.R < 1) return kHrDirectItems;
+  const int nsl = (S + t.sw - 1) / t.sw, nbands = (ch + t.R - 1) / t.R;
+  return nsl * ((nbands + kHrBandsPerItem - 1) / kHrBandsPerItem);
+}
+
+// The view of work item c among the nc class views (b, v0 + j), j = view index mod nvc:
+// the last view whose first item is <= c (views without items share their successor's
+// first item).  64-ary search by each wave: two rounds of loads for 4096 views.
+__device__ __forceinline__ int hr_find_view(const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int nc, int c) {
+  int lo = 0, len = nc;
+  const int lane = threadIdx.x & 63;
+  while (len > 1) {
+    const int step = (len + 63) >> 6;
+    const int cand = lo + lane * step;
+    bool le = false;
+    if (cand < lo + len) {
+      const int b = cand / nvc;
+      le = plan[b * nv + v0 + (cand - b * nvc)].hr_base <= c;
+    }
+    const uint64_t m = __ballot(le);  // bit 0 set: plan[lo].hr_base <= c holds throughout
+    const int last = 63 - __builtin_clzll(m);
+    lo += last * step;
+    len = min(step, len - last * step);
+  }
+  return lo;
 }
 
 // One tile: nr staged rows x the outputs [x0, x0 + sw) of a slice.  Lane (row pair, x)
@@ -2751,152 +3057,111 @@ __device__ __forceinline__ void hresize_tile_dot(const uint32_t* __restrict__ ro
 // Horizontal pass in tiles of (slice of outputs) x (band of rows), shaped by
 // hresize_tile: the slice's taps always come from LDS, and the band stages only the
 // source columns the slice reads [xmin(x0), xmin(x1-1) + xcnt(x1-1)), so wide crops
-// take narrower slices to keep >= kHresizeMinRows rows per band.
-__global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
-                                                 const ViewPlan* __restrict__ plan, int nv, int v0,
+// take narrower slices to keep >= kHresizeMinRows rows per band.  A persistent grid
+// takes the class's work items (kHrBandsPerItem bands of one slice, hr_view_chunks) in
+// turn: with mixed crop sizes (C3) a fixed number of workgroups per view left the
+// largest views' workgroups running alone at the end of the launch.
+__global__ void __launch_bounds__(256, DINO_HRESIZE_OCC) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                                 const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int B,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
-  const BlkIdx bk = xcd_blk();
+  main_prio();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int b = bk.z;
-  const int i = b * nv + v0 + bk.y;
-  const ViewPlan vp = plan[i];
-  if (!vp.ok || !vp.kh) return;
-  const dino_view_params p = prm[i];
-  const ImgDesc& d = desc[b];
-  const int S = p.out_size, W = d.width, cw = p.crop_w, kh = vp.kh;
-  if (hresize_mfma_ok(S, cw, kh)) return;  // k_hresize_mfma's view
-  const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);
-  const int32_t* gt = gb + 4 * S;
-  const int4* ghx = (const int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
-  const uint4* ghg = (const uint4*)(ghx + S);
-  const uint8_t* rgb = ws + d.rgb_off;
-  uint8_t* tmp = aws + vp.htmp_off;
-  const int64_t cpl = (int64_t)p.crop_h * S;
-  const int ng_max = (kh + 3) / 4;
-  const int ngp = ng_max | 1;  // tap groups per output in LDS: odd, so 16 lanes' b128 reads hit distinct banks
-  const HrTile tl = hresize_tile(S, cw, kh);
-  const int sw = tl.sw, pitch = tl.pitch, R = tl.R, R3p = tl.R3p;
-  const int nsl = sw > 0 ? (S + sw - 1) / sw : 0;
-  if (R < 1) {  // direct path: taps and pixels from global memory (crops too wide for LDS)
-    const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
-    const CoefView cv{gb, gt, kh};
-    for (int64_t e = (int64_t)bk.x * blockDim.x + threadIdx.x; e < cpl; e += (int64_t)gridDim.x * blockDim.x) {
-      const int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
-      for (int c = 0; c < 3; ++c) tmp[c * cpl + e] = hresize_at(src, cv, r, x, c);
+  const int nc = B * nvc;
+  // persistent grid over the class's work items (k_vplan's per-class prefix)
+  const ViewPlan vl = plan[(B - 1) * nv + v0 + nvc - 1];
+  const int nitems_all = vl.hr_base + vl.hr_chunks;
+  for (int c = blockIdx.x; c < nitems_all; c += gridDim.x) {
+    const int j = hr_find_view(plan, nv, v0, nvc, nc, c);
+    const int b = j / nvc;
+    const int i = b * nv + v0 + (j - b * nvc);
+    const ViewPlan vp = plan[i];
+    if (!vp.ok || !vp.kh) continue;  // (no items: not reached)
+    const int item = c - vp.hr_base;
+    const dino_view_params p = prm[i];
+    const ImgDesc& d = desc[b];
+    const int S = p.out_size, W = d.width, cw = p.crop_w, kh = vp.kh;
+    const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);
+    const int32_t* gt = gb + 4 * S;
+    const int4* ghx = (const int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
+    const uint4* ghg = (const uint4*)(ghx + S);
+    const uint8_t* rgb = ws + d.rgb_off;
+    uint8_t* tmp = aws + vp.htmp_off;
+    const int64_t cpl = (int64_t)p.crop_h * S;
+    const int ng_max = (kh + 3) / 4;
+    const int ngp = ng_max | 1;  // tap groups per output in LDS: odd, so 16 lanes' b128 reads hit distinct banks
+    const HrTile tl = hresize_tile(S, cw, kh);
+    const int sw = tl.sw, pitch = tl.pitch, R = tl.R, R3p = tl.R3p;
+    if (R < 1) {  // direct path: taps and pixels from global memory (crops too wide for LDS)
+      const SrcView src{rgb + ((int64_t)p.crop_top * W + p.crop_left) * 3, (int64_t)W * 3, 3, 1};
+      const CoefView cv{gb, gt, kh};
+      for (int64_t e = (int64_t)item * blockDim.x + threadIdx.x; e < cpl; e += (int64_t)kHrDirectItems * blockDim.x) {
+        const int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
+        for (int ch = 0; ch < 3; ++ch) tmp[ch * cpl + e] = hresize_at(src, cv, r, x, ch);
+      }
+      continue;
     }
-    return;
-  }
-  // LDS: the staged rows first (an edge output's zero-tap over-read stays inside the rows'
-  // pad), then the slice's taps
-  uint32_t* rows = (uint32_t*)smem;
-  int4* lx = (int4*)(smem + ((hresize_rows_bytes(pitch, R, ng_max) + 15) & ~15));
-  uint4* lg = (uint4*)(lx + sw);
-  const int nbands = (p.crop_h + R - 1) / R;
-  const int ntiles = nsl * nbands;
-  // Tile u: slice sl (outputs [x0, x0 + swn)), band of rows [r0, r0 + nr), source columns
-  // staged from c0 in ngroups groups of 4 pixels.
-  struct Tile {
-    int sl, x0, swn, r0, nr, c0, ngroups;
-  };
-  auto tile_of = [&](int u) {
-    Tile T;
-    T.sl = u / nbands;
-    const int band = u - T.sl * nbands;
-    T.x0 = T.sl * sw;
-    T.swn = min(sw, S - T.x0);
-    T.r0 = band * R;
-    T.nr = min(R, p.crop_h - T.r0);
-    T.c0 = ghx[T.x0].x & ~3;  // first source column staged (4-aligned within the crop)
-    const int c1 = min(cw, ghx[T.x0 + T.swn - 1].x + gb[2 * (T.x0 + T.swn - 1) + 1]);
-    T.ngroups = (c1 - T.c0 + 3) >> 2;
-    return T;
-  };
-  // staging item e of tile T: row e / ngroups, group e % ngroups (12 source bytes = 4 pixels)
-  auto item_src = [&](const Tile& T, int e, int* r, int* g) {
-    *r = e / T.ngroups;
-    *g = e - *r * T.ngroups;
-    return rgb + ((int64_t)(p.crop_top + T.r0 + *r) * W + p.crop_left + T.c0) * 3 + 12 * *g;
-  };
-  auto stage_put = [&](int r, int g, const uint8_t* src, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-    const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
-    const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);  // R0 G0 B0 R1
-    const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);  // G1 B1 R2 G2
-    const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);  // B2 R3 G3 B3
-    // de-interleave 4 pixels into one word per channel (v_perm byte selects), sign bit flipped
-    const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
-    const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
-    const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
-    uint32_t* dst = rows + g * R3p + 3 * r;
-    dst[0] = cr ^ 0x80808080u;
-    dst[1] = cg ^ 0x80808080u;
-    dst[2] = cb ^ 0x80808080u;
-  };
-  // The first kHrPre staging items of each thread are loaded one tile ahead (during the
-  // previous tile's dot products), the rest when the tile starts.
-  uint32_t pf[kHrPre > 0 ? kHrPre : 1][4];
-  auto prefetch = [&](const Tile& T) {
-#pragma unroll
-    for (int j = 0; j < kHrPre; ++j) {
-      const int e = (int)threadIdx.x + j * (int)blockDim.x;
-      if (e < T.nr * T.ngroups) {
-        int r, g;
-        const uint8_t* src = item_src(T, e, &r, &g);
+    // LDS: the staged rows first (an edge output's zero-tap over-read stays inside the rows'
+    // pad), then the slice's taps
+    uint32_t* rows = (uint32_t*)smem;
+    int4* lx = (int4*)(smem + ((hresize_rows_bytes(pitch, R, ng_max) + 15) & ~15));
+    uint4* lg = (uint4*)(lx + sw);
+    const int nbands = (p.crop_h + R - 1) / R;
+    const int nbg = (nbands + kHrBandsPerItem - 1) / kHrBandsPerItem;
+    // the item: slice sl (outputs [x0, x0 + swn)), bands [band0, band1)
+    const int sl = item / nbg;
+    const int band0 = (item - sl * nbg) * kHrBandsPerItem, band1 = min(nbands, band0 + kHrBandsPerItem);
+    const int x0 = sl * sw, swn = min(sw, S - x0);
+    const int c0 = ghx[x0].x & ~3;  // first source column staged (4-aligned within the crop)
+    const int c1 = min(cw, ghx[x0 + swn - 1].x + gb[2 * (x0 + swn - 1) + 1]);
+    const int ngroups = (c1 - c0 + 3) >> 2;  // staged groups of 4 pixels per row
+    // taps of the slice -> LDS (the previous item ended with a barrier)
+    for (int k = threadIdx.x; k < swn; k += blockDim.x) lx[k] = ghx[x0 + k];
+    for (int k = threadIdx.x; k < swn * ng_max; k += blockDim.x) {
+      const int g = k / swn, xl = k - g * swn;
+      lg[xl * ngp + g] = ghg[(int64_t)g * S + x0 + xl];
+    }
+    for (int band = band0; band < band1; ++band) {
+      const int r0 = band * R, nr = min(R, p.crop_h - r0);
+      // staging item e: row e / ngroups, group e % ngroups (12 source bytes = 4 pixels ->
+      // one word per channel, de-interleaved by v_perm byte selects, sign bit flipped)
+      const int nst = nr * ngroups;
+      for (int e = (int)threadIdx.x; e < nst; e += blockDim.x) {
+        const int r = e / ngroups, g = e - r * ngroups;
+        const uint8_t* src = rgb + ((int64_t)(p.crop_top + r0 + r) * W + p.crop_left + c0) * 3 + 12 * g;
         const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
-        pf[j][0] = a0[0];
-        pf[j][1] = a0[1];
-        pf[j][2] = a0[2];
-        pf[j][3] = a0[3];
+        const uint32_t w0 = a0[0], w1 = a0[1], w2 = a0[2], w3 = a0[3];
+        const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
+        const uint32_t q0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);  // R0 G0 B0 R1
+        const uint32_t q1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);  // G1 B1 R2 G2
+        const uint32_t q2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);  // B2 R3 G3 B3
+        const uint32_t cr = __builtin_amdgcn_perm(q2, __builtin_amdgcn_perm(q1, q0, 0x0C060300u), 0x05020100u);
+        const uint32_t cg = __builtin_amdgcn_perm(q2, __builtin_amdgcn_perm(q1, q0, 0x0C070401u), 0x06020100u);
+        const uint32_t cb = __builtin_amdgcn_perm(q2, __builtin_amdgcn_perm(q1, q0, 0x0C0C0502u), 0x07040100u);
+        uint32_t* dst = rows + g * R3p + 3 * r;
+        dst[0] = cr ^ 0x80808080u;
+        dst[1] = cg ^ 0x80808080u;
+        dst[2] = cb ^ 0x80808080u;
       }
-    }
-  };
-  int cur = -1;
-  if (kHrPre && (int)bk.x < ntiles) prefetch(tile_of(bk.x));
-  for (int u = bk.x; u < ntiles; u += gridDim.x) {
-    const Tile T = tile_of(u);
-    if (T.sl != cur) {  // taps of the slice -> LDS (the previous tile ended with a barrier)
-      for (int k = threadIdx.x; k < T.swn; k += blockDim.x) lx[k] = ghx[T.x0 + k];
-      for (int k = threadIdx.x; k < T.swn * ng_max; k += blockDim.x) {
-        const int g = k / T.swn, xl = k - g * T.swn;
-        lg[xl * ngp + g] = ghg[(int64_t)g * S + T.x0 + xl];
-      }
-      cur = T.sl;
-    }
-    const int nitems = T.nr * T.ngroups;
-#pragma unroll
-    for (int j = 0; j < kHrPre; ++j) {
-      const int e = (int)threadIdx.x + j * (int)blockDim.x;
-      if (e < nitems) {
-        int r, g;
-        const uint8_t* src = item_src(T, e, &r, &g);
-        stage_put(r, g, src, pf[j][0], pf[j][1], pf[j][2], pf[j][3]);
-      }
-    }
-    for (int e = (int)threadIdx.x + kHrPre * (int)blockDim.x; e < nitems; e += blockDim.x) {
-      int r, g;
-      const uint8_t* src = item_src(T, e, &r, &g);
-      const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
-      stage_put(r, g, src, a0[0], a0[1], a0[2], a0[3]);
-    }
-    __syncthreads();
-    if (kHrPre && u + (int)gridDim.x < ntiles) prefetch(tile_of(u + gridDim.x));
-    switch (ng_max) {
+      __syncthreads();
+      switch (ng_max) {
 #define DINO_HR_CASE(N) \
   case N: \
-    hresize_tile_dot<N>(rows, R3p, T.nr, T.r0, T.x0, T.swn, T.c0, S, ng_max, ngp, lx, lg, tmp, cpl); \
+    hresize_tile_dot<N>(rows, R3p, nr, r0, x0, swn, c0, S, ng_max, ngp, lx, lg, tmp, cpl); \
     break;
-      DINO_HR_CASE(1)
-      DINO_HR_CASE(2)
-      DINO_HR_CASE(3)
-      DINO_HR_CASE(4)
-      DINO_HR_CASE(5)
-      DINO_HR_CASE(6)
-      DINO_HR_CASE(7)
-      DINO_HR_CASE(8)
+        DINO_HR_CASE(1)
+        DINO_HR_CASE(2)
+        DINO_HR_CASE(3)
+        DINO_HR_CASE(4)
+        DINO_HR_CASE(5)
+        DINO_HR_CASE(6)
+        DINO_HR_CASE(7)
+        DINO_HR_CASE(8)
 #undef DINO_HR_CASE
-      default:
-        hresize_tile_dot<0>(rows, R3p, T.nr, T.r0, T.x0, T.swn, T.c0, S, ng_max, ngp, lx, lg, tmp, cpl);
+        default:
+          hresize_tile_dot<0>(rows, R3p, nr, r0, x0, swn, c0, S, ng_max, ngp, lx, lg, tmp, cpl);
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -3916,7 +4181,7 @@ static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_d
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
                                                        "k_vert_local", "k_dcscan", "k_htab", "k_hseg", "k_huff2",
-                                                       "k_huff3", "k_prog", "k_pwalk"};
+                                                       "k_huff3", "k_prog", "k_pwalk", "k_ycolor"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -3963,6 +4228,10 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
                                kPrefineLds)) != hipSuccess)
     return e;
   g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hresize), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kHresizeLds)) != hipSuccess)
+    return e;
+  g->grid_hr = persistent_grid(reinterpret_cast<const void*>(&k_hresize), kHresizeLds, cus);
   // scan waves: one per CU by default.  A scan's serial decode runs on the CU's one scalar
   // unit, which the CU's waves share: two scan waves on a CU each run at about half speed
   // (DINO_PSCAN_PER_CU: waves per CU, measured in profiles/r03_prog_*).
@@ -3996,6 +4265,7 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKIdct, s, (k_idct<<<dim3(kIdctWgs, B), 256, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
+  if (kFuseMaxW) TIMED(tm, kKYcolor, s, (k_ycolor<<<dim3(kYcolorWgs, B), 256, 0, s>>>(a.desc, a.ws)));
   return hipGetLastError();
 }
 
@@ -4020,7 +4290,7 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
           (k_hresize_mfma<<<dim3((S + 63) / 64, nvc, B), 256, kHrMfmaLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
                                                                                  a.aws)));
   TIMED(tm, kKHresize, s,
-        (k_hresize<<<dim3(kHresizeWgs, nvc, B), 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws, a.aws)));
+        (k_hresize<<<a.grid_hr, 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, nvc, B, a.ws, a.aws)));
   if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS
     const int lds = (int)sizeof(FinalLds) + vfinal_tile_bytes(S) + 3 * 256 * (int)sizeof(OutT);
     TIMED(tm, kfin, s,

@@ -30,6 +30,8 @@ struct ViewPlan {
   int32_t kh, kv;     // taps per output of the horizontal / vertical pass (0 = pass skipped)
   int32_t ok;         // image decoded and scratch available
   uint32_t lsum;      // sum of L over the crop before the contrast op (k_vert atomics)
+  int32_t hr_chunks;  // k_hresize work items of the view (k_vsizes)
+  int32_t hr_base;    // its first work item among its class's views (global / local, k_vplan)
 };
 
 
@@ -38,7 +40,7 @@ struct ViewPlan {
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuff1, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
   kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKProg,
-  kKPwalk, kKNumKernels
+  kKPwalk, kKYcolor, kKNumKernels
 };
 
 struct KernelTimer {
@@ -64,6 +66,7 @@ struct LaunchGeom {
   int32_t grid3;     // persistent k_huff3 grid
   int32_t grid_ps;   // persistent k_pscan grid (waves)
   int32_t prefine;   // components whose AC refinement scans k_prefine decodes in lane mode (bit c; 0: none)
+  int32_t grid_hr;   // persistent k_hresize grid (occupancy x CUs)
 };
 
 // Coefficient-buffer images of a batch (k_plan zeroes, k_pwalk registers, k_pscan
@@ -109,6 +112,7 @@ struct AugmentArgs {
   ViewPtrs views;          // n_views output pointers (device memory)
   dino_aug_config cfg;
   const float* norm;       // per-image {mean[3], std[3]} ([0, 1] scale), nullable -> cfg.mean / cfg.std
+  int32_t grid_hr;         // LaunchGeom::grid_hr
 };
 
 // Decode-only recipe (dino_resize_batch).

@@ -39,9 +39,19 @@ constexpr int kEntHalfwordsPerBlock = 128;
 // (uint2 per block), component planes, RGB, speculative checkpoints, Huffman
 // tables, lane records, destuff part counts.
 struct ChunkSizes {
-  int64_t ent, rst, coef, binfo, plane, rgb, cps, htab, hlane, dspart;
-  DHD int64_t total() const { return ent + rst + coef + binfo + plane + rgb + cps + htab + hlane + dspart; }
+  int64_t ent, rst, coef, binfo, plane, rgb, cps, htab, hlane, dspart, tail;
+  DHD int64_t sum() const { return ent + rst + coef + binfo + plane + rgb + cps + htab + hlane + dspart; }
+  DHD int64_t total() const { return sum() + tail; }
 };
+
+// Image areas start 256-byte aligned (tail pads each image), and so does the sparse entry
+// area (rst pads ent + rst): a lane's entry region starts at a multiple of 256 bytes in
+// memory too (SparseSink stores groups of up to 64 bytes aligned to their size).
+DHD int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+DHD ChunkSizes chunk_finish(ChunkSizes z) {
+  z.tail = align256(z.sum()) - z.sum();
+  return z;
+}
 
 // Destuff work items of an image: 32 KiB parts of its scan (>= 1, so that the
 // descriptor is always completed by k_destuff_write); none for kinds 1 and 2.
@@ -56,7 +66,7 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   ChunkSizes z{};
   if (d.status != DINO_IMG_OK) return z;
   z.rgb = align16((int64_t)d.width * d.height * 3 + 16);
-  if (d.kind == 2) return z;
+  if (d.kind == 2) return chunk_finish(z);
   int64_t p = 0;
   for (int c = 0; c < d.ncomp; ++c) p += (int64_t)d.comp[c].bw * d.comp[c].bh * 64;
   z.plane = align16(p);
@@ -64,10 +74,10 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
     z.ent = align16((int64_t)d.scan_len + 64);  // each scan's destuffed bytes (k_pscan)
     z.coef = align16(d.coef_bytes);
     z.htab = kPRegionBytes;  // scan list + decoder tables (k_pwalk -> k_pscan)
-    return z;
+    return chunk_finish(z);
   }
   z.ent = align16((int64_t)d.scan_len + 64);
-  z.rst = align16(4 * ((int64_t)d.n_rst_max + 1));
+  z.rst = align256(z.ent + 4 * ((int64_t)d.n_rst_max + 1)) - z.ent;
   z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;
   z.binfo = align16((int64_t)d.total_blocks * 8);
   const int64_t lanes = huff_lanes_cap(d);
@@ -75,7 +85,7 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   z.htab = align16((int64_t)sizeof(HuffTables));
   z.hlane = align16(lanes * (int64_t)sizeof(LaneRec));
   z.dspart = 16 * (int64_t)ds_parts(d);
-  return z;
+  return chunk_finish(z);
 }
 
 // A restart image that k_htab moves to the coefficient-buffer path keeps its baseline

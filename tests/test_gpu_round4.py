@@ -243,3 +243,40 @@ def test_lane_mode_refinement_bit_exact(gpu_device, monkeypatch, comps):
             bad.append((name, int((got != ref).sum())))
     eng.close()
     assert not bad, bad
+
+
+def test_fused_luma_colour_bands_bit_exact(gpu_device):
+    """k_ycolor (luma IDCT + 4:2:0 colour conversion per 8-row band, the luma plane kept in
+    LDS): widths on both sides of its 2304-pixel limit and of every residue
+    mod 4 (quads that wrap a row), heights that end inside a band, the smallest fancy-upsampled
+    chroma (3 samples wide) next to box-upsampled 2-sample chroma, baseline, restart-interval
+    and progressive files, and the unfused samplings in the same batch: bit-exact with Pillow."""
+    from tests.test_gpu_parity import _to_dev
+    from dataloader_amd.engine import IngestEngine
+    from oracle import cpu_ref
+    rng = np.random.default_rng(404)
+    cases = []
+    for w, h in ((2304, 17), (2305, 9), (2303, 23), (2302, 8), (2301, 31), (5, 5), (4, 4), (6, 3), (13, 11),
+                 (641, 479), (96, 1), (1, 40)):
+        cases.append((f"base_{w}x{h}", encode_jpeg(textured_rgb(w, h, rng), quality=90, subsampling=2)))
+    cases.append(("prog_1000x9", encode_jpeg(textured_rgb(1000, 9, rng), subsampling=2, progressive=True)))
+    cases.append(("prog_333x250", encode_jpeg(textured_rgb(333, 250, rng), subsampling=2, progressive=True)))
+    cases.append(("rst_777x333", encode_jpeg(textured_rgb(777, 333, rng), subsampling=2, restart_mcus=5)))
+    cases.append(("s422_300x200", encode_jpeg(textured_rgb(300, 200, rng), subsampling=1)))
+    cases.append(("s444_301x201", encode_jpeg(textured_rgb(301, 201, rng), subsampling=0)))
+    cases.append(("gray_250x90", encode_jpeg(textured_rgb(250, 90, rng), gray=True)))
+    jpegs = [j for _, j in cases]
+    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
+    d_bytes, d_off = _to_dev(jpegs, gpu_device)
+    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
+    bad = []
+    for i, (name, j) in enumerate(cases):
+        ref = np.asarray(cpu_ref.decode_rgb(j))
+        if info[i, 0] != 0:
+            bad.append((name, "status", int(info[i, 0])))
+            continue
+        got = eng.copy_rgb(i, ref.shape[1], ref.shape[0]).cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad.append((name, int((got != ref).sum())))
+    eng.close()
+    assert not bad, bad
