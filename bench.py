@@ -53,7 +53,7 @@ sys.path.insert(0, str(ROOT))
 METRIC = "images/sec decode+10-crop, device-resident (JPEG bytes in HBM), 1/2/4/8 GPU"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 VFINAL_MAX_S = 128  # kernels.hip kVFinalMaxS: views up to this size run k_vfinal (vertical pass + epilogue fused)
-FUSE_MAX_W = 2304  # kernels.hip kFuseMaxW: 4:2:0 images up to this width run k_ycolor (luma IDCT + colour fused)
+FUSE_MAX_W = 2304  # kernels.hip kFuseMaxW: with DINO_FUSE=1, 4:2:0 images up to this width run k_ycolor
 
 
 # ----------------------------------------------------------------------------- synthetic data
@@ -148,7 +148,8 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     s_unfused = float(np.mean([len(j) if not f else 0 for j, f in zip(jpegs, fz)]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
     per_blk = entry_bytes_per_block + 8.0       # sparse entries + the 8-byte block record
-    fu = [w <= FUSE_MAX_W for w, _ in dims]      # (synthetic encodes are all 4:2:0)
+    fuse_on = os.environ.get("DINO_FUSE") == "1"  # the library's opt-in (LaunchGeom::fuse)
+    fu = [fuse_on and w <= FUSE_MAX_W for w, _ in dims]  # (synthetic encodes are all 4:2:0)
     chroma_fused = float(np.mean([b / 3 if f else 0 for b, f in zip(nblk, fu)]))
     luma_fused = 2 * chroma_fused
     blocks_unfused = blocks - 3 * chroma_fused

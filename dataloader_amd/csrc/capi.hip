@@ -103,7 +103,7 @@ int dino_ctx_create(int device, const dino_limits* limits, dino_ctx** out) {
       (e = hipMallocAsync((void**)&c->d_ws, c->ws_size, nullptr)) != hipSuccess ||
       (e = hipMallocAsync((void**)&c->d_aws, c->aws_size, nullptr)) != hipSuccess ||
       (e = hipStreamSynchronize(nullptr)) != hipSuccess ||
-      (e = hipMalloc(&c->d_plan, sizeof(ViewPlan) * nrec)) != hipSuccess ||
+      (e = hipMalloc(&c->d_plan, sizeof(ViewPlan) * (nrec + 1))) != hipSuccess ||  // + k_hresize's item counters
       (e = hipMalloc(&c->d_params, sizeof(dino_view_params) * nrec)) != hipSuccess ||
       (e = hipMalloc((void**)&c->d_pctl, pctl_bytes(L.max_batch))) != hipSuccess) {
     dino_ctx_destroy(c);

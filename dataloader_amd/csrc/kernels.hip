@@ -2138,7 +2138,7 @@ __device__ __forceinline__ void idct_group_dense(int32_t* sb, int l, const uint8
 // (zigzag | int10 value << 6), then u32 entries from the next even halfword (see
 // SparseSink); the DC is int16 (absolute after k_dcscan).
 #ifndef DINO_IDCT_PRE
-#define DINO_IDCT_PRE 2
+#define DINO_IDCT_PRE 4
 #endif
 constexpr int kIdctPre = DINO_IDCT_PRE;  // halfword entries per lane loaded a block ahead (8 lanes: 8 kIdctPre)
 __device__ __forceinline__ void idct_load_pre(uint32_t* pre, int l, uint2 bi, const uint16_t* ent16) {
@@ -2194,21 +2194,23 @@ __device__ __forceinline__ uint64_t idct_group_pass2(int32_t* sb, int l) {
   return o.u;
 }
 
-// Images whose luma IDCT and colour conversion run fused in k_ycolor: YCbCr 4:2:0 with
-// fancy h2v2 chroma (k_color's fast420 case), at most kFuseMaxW pixels wide (the band's
-// luma rows live in LDS).  k_idct transforms only their chroma planes; k_color skips them.
+// Images whose luma IDCT and colour conversion run fused in k_ycolor when the ctx fuses
+// (LaunchGeom::fuse, env DINO_FUSE=1; measured and off by default): YCbCr
+// 4:2:0 with fancy h2v2 chroma (k_color's fast420 case), at most kFuseMaxW pixels wide
+// (the band's luma rows live in LDS).  k_idct transforms only their chroma planes; k_color
+// skips them.
 #ifndef DINO_FUSE_MAX_W
 #define DINO_FUSE_MAX_W 2304
 #endif
-constexpr int kFuseMaxW = DINO_FUSE_MAX_W;  // 0: no image is fused (A/B)
-__device__ __forceinline__ bool fused_420(const ImgDesc& d) {
-  if (kFuseMaxW == 0 || d.status != DINO_IMG_OK || d.kind == 2 || d.ncomp != 3 || d.color != kYCbCr) return false;
+constexpr int kFuseMaxW = DINO_FUSE_MAX_W;
+__device__ __forceinline__ bool fused_420(const ImgDesc& d, int fuse) {
+  if (!fuse || d.status != DINO_IMG_OK || d.kind == 2 || d.ncomp != 3 || d.color != kYCbCr) return false;
   const CompDesc &c0 = d.comp[0], &c1 = d.comp[1], &c2 = d.comp[2];
   return d.width <= kFuseMaxW && d.max_h == 2 && d.max_v == 2 && c0.h == 2 && c0.v == 2 && c1.h == 1 && c1.v == 1 &&
          c2.h == 1 && c2.v == 1 && c1.dw > 2 && c1.dw == c2.dw && c1.dh == c2.dh;
 }
 
-__global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+__global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws, int fuse) {
   const BlkIdx bk = xcd_blk();
   // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
   // (pass 2) accesses of a wave's 8 groups x 8 lanes hit 64 distinct banks
@@ -2261,7 +2263,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
   };
   const int T = (int)tot, step = gridDim.x * kIdctBlocksPerWg;
   // the luma plane of a k_ycolor image is transformed there, band by band
-  const int G0 = fused_420(d) ? (int)nb0 : 0;
+  const int G0 = fused_420(d, fuse) ? (int)nb0 : 0;
   // The next block's record is loaded one iteration ahead, and its first 16 entries
   // at the end of the current iteration (once the record has arrived), so the
   // scatter at the top of an iteration normally waits on nothing.
@@ -2366,10 +2368,10 @@ constexpr int kColorBatch = DINO_COLOR_BATCH;  // quads whose loads a lane issue
 // two words per chroma row instead of per-pixel byte loads; edges, quads that wrap
 // a row and other samplings use the per-pixel path (same arithmetic).
 __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
-                                               const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
+                                               const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws, int fuse) {
   const BlkIdx bk = xcd_blk();
   const ImgDesc& d = desc[bk.y];
-  if (d.status != DINO_IMG_OK || fused_420(d)) return;
+  if (d.status != DINO_IMG_OK || fused_420(d, fuse)) return;
   if (d.kind == 2) {  // pre-decoded RGB container: copy the pixels into the workspace
     const uint8_t* src = bytes + offsets[bk.y] + d.scan_off;
     uint32_t* dst = (uint32_t*)(ws + d.rgb_off);
@@ -2535,9 +2537,9 @@ __global__ void __launch_bounds__(256) k_ycolor(const ImgDesc* __restrict__ desc
   const BlkIdx bk = xcd_blk();
   __shared__ int32_t s_blk[kIdctBlocksPerWg][72];
   __shared__ uint8_t s_nat[80];
-  __shared__ __attribute__((aligned(16))) uint8_t s_y[8 * (kFuseMaxW ? kFuseYPitch : 8)];
+  __shared__ __attribute__((aligned(16))) uint8_t s_y[8 * kFuseYPitch];
   const ImgDesc& d = desc[bk.y];
-  if (!fused_420(d)) return;
+  if (!fused_420(d, 1)) return;
   const int W = d.width, H = d.height;
   const int nband = (H + 7) >> 3;
   if (bk.x >= nband) return;
@@ -2756,6 +2758,7 @@ __global__ void __launch_bounds__(1024) k_vplan(ImgDesc* __restrict__ desc, cons
   __shared__ int2 hpart[1024];
   const int t = threadIdx.x, N = B * nv;
   for (int b = t; b < B; b += 1024) desc[b].aug_status = 0;
+  if (t == 0) plan[N] = ViewPlan{};  // k_hresize's work-item counters (global, local views): hr_chunks, hr_base
   const int per = (N + 1023) / 1024;
   int64_t local = 0;
   int2 hl = make_int2(0, 0);  // k_hresize work items of this thread's global / local views
@@ -2914,6 +2917,10 @@ constexpr int kHresizeMinRows = DINO_HRESIZE_MIN_ROWS;  // rows per band the sli
 #endif
 constexpr int kHrBandsPerItem = DINO_HRESIZE_BANDS;  // row bands of one slice per work item
 constexpr int kHrDirectItems = 4;                    // work items of a direct-path view
+#ifndef DINO_HRESIZE_DYNAMIC
+#define DINO_HRESIZE_DYNAMIC 1
+#endif
+constexpr bool kHrDynamic = DINO_HRESIZE_DYNAMIC;  // work items from a counter (else blockIdx + k gridDim)
 #ifndef DINO_HRESIZE_OCC
 #define DINO_HRESIZE_OCC 1  // launch-bounds occupancy hint (A/B: 6 caps the VGPRs at 80, with a small spill)
 #endif
@@ -3061,21 +3068,41 @@ __device__ __forceinline__ void hresize_tile_dot(const uint32_t* __restrict__ ro
 // takes the class's work items (kHrBandsPerItem bands of one slice, hr_view_chunks) in
 // turn: with mixed crop sizes (C3) a fixed number of workgroups per view left the
 // largest views' workgroups running alone at the end of the launch.
+__device__ __forceinline__ void hresize_item(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                             const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int nc, int c,
+                                             const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws, uint8_t* smem);
+
 __global__ void __launch_bounds__(256, DINO_HRESIZE_OCC) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
-                                                 const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int B,
+                                                 ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int B,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
   main_prio();
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ int s_item[2];
   const int nc = B * nvc;
-  // persistent grid over the class's work items (k_vplan's per-class prefix)
+  // persistent grid over the class's work items (k_vplan's per-class prefix), taken in turn
+  // from the class's counter (zeroed by k_vplan), the next one fetched while this one runs
   const ViewPlan vl = plan[(B - 1) * nv + v0 + nvc - 1];
   const int nitems_all = vl.hr_base + vl.hr_chunks;
-  for (int c = blockIdx.x; c < nitems_all; c += gridDim.x) {
+  int* ctr = v0 == 0 ? &plan[B * nv].hr_chunks : &plan[B * nv].hr_base;
+  if (threadIdx.x == 0) s_item[0] = kHrDynamic ? atomicAdd(ctr, 1) : (int)blockIdx.x;
+  __syncthreads();
+  for (int it = 0, c = s_item[0]; c < nitems_all; ++it) {
+    if (threadIdx.x == 0) s_item[(it + 1) & 1] = kHrDynamic ? atomicAdd(ctr, 1) : c + (int)gridDim.x;
+    hresize_item(desc, prm, plan, nv, v0, nvc, nc, c, ws, aws, smem);
+    __syncthreads();
+    c = s_item[(it + 1) & 1];
+  }
+}
+
+__device__ __forceinline__ void hresize_item(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+                                             const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int nc, int c,
+                                             const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws, uint8_t* smem) {
+  {
     const int j = hr_find_view(plan, nv, v0, nvc, nc, c);
     const int b = j / nvc;
     const int i = b * nv + v0 + (j - b * nvc);
     const ViewPlan vp = plan[i];
-    if (!vp.ok || !vp.kh) continue;  // (no items: not reached)
+    if (!vp.ok || !vp.kh) return;  // (no items: not reached)
     const int item = c - vp.hr_base;
     const dino_view_params p = prm[i];
     const ImgDesc& d = desc[b];
@@ -3098,7 +3125,7 @@ __global__ void __launch_bounds__(256, DINO_HRESIZE_OCC) k_hresize(const ImgDesc
         const int r = (int)(e / S), x = (int)(e - (int64_t)r * S);
         for (int ch = 0; ch < 3; ++ch) tmp[ch * cpl + e] = hresize_at(src, cv, r, x, ch);
       }
-      continue;
+      return;
     }
     // LDS: the staged rows first (an edge output's zero-tap over-read stays inside the rows'
     // pad), then the slice's taps
@@ -4240,6 +4267,8 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
   g->grid_ps = per_cu * cus;
   const char* pf = getenv("DINO_PREFINE_COMPS");
   g->prefine = pf ? (atoi(pf) & 7) : 0;
+  const char* fu = getenv("DINO_FUSE");
+  g->fuse = fu && fu[0] == '1';
   return hipSuccess;
 }
 
@@ -4263,9 +4292,10 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKHuff3, s, (k_huff3<<<grid3, kHuffThreads, kHuff3LdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
-  TIMED(tm, kKIdct, s, (k_idct<<<dim3(kIdctWgs, B), 256, 0, s>>>(a.desc, a.ws)));
-  TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
-  if (kFuseMaxW) TIMED(tm, kKYcolor, s, (k_ycolor<<<dim3(kYcolorWgs, B), 256, 0, s>>>(a.desc, a.ws)));
+  const int fuse = a.geom.fuse;
+  TIMED(tm, kKIdct, s, (k_idct<<<dim3(kIdctWgs, B), 256, 0, s>>>(a.desc, a.ws, fuse)));
+  TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws, fuse)));
+  if (fuse) TIMED(tm, kKYcolor, s, (k_ycolor<<<dim3(kYcolorWgs, B), 256, 0, s>>>(a.desc, a.ws)));
   return hipGetLastError();
 }
 

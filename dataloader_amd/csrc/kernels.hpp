@@ -67,6 +67,7 @@ struct LaunchGeom {
   int32_t grid_ps;   // persistent k_pscan grid (waves)
   int32_t prefine;   // components whose AC refinement scans k_prefine decodes in lane mode (bit c; 0: none)
   int32_t grid_hr;   // persistent k_hresize grid (occupancy x CUs)
+  int32_t fuse;      // 4:2:0 luma IDCT + colour fused in k_ycolor (env DINO_FUSE=1; off by default)
 };
 
 // Coefficient-buffer images of a batch (k_plan zeroes, k_pwalk registers, k_pscan

@@ -245,15 +245,17 @@ def test_lane_mode_refinement_bit_exact(gpu_device, monkeypatch, comps):
     assert not bad, bad
 
 
-def test_fused_luma_colour_bands_bit_exact(gpu_device):
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_fused_luma_colour_bands_bit_exact(gpu_device, monkeypatch, fuse):
     """k_ycolor (luma IDCT + 4:2:0 colour conversion per 8-row band, the luma plane kept in
-    LDS): widths on both sides of its 2304-pixel limit and of every residue
+    LDS; opt-in, DINO_FUSE=1): widths on both sides of its 2304-pixel limit and of every residue
     mod 4 (quads that wrap a row), heights that end inside a band, the smallest fancy-upsampled
     chroma (3 samples wide) next to box-upsampled 2-sample chroma, baseline, restart-interval
     and progressive files, and the unfused samplings in the same batch: bit-exact with Pillow."""
     from tests.test_gpu_parity import _to_dev
     from dataloader_amd.engine import IngestEngine
     from oracle import cpu_ref
+    monkeypatch.setenv("DINO_FUSE", fuse)  # read by dino_ctx_create (measured and off by default)
     rng = np.random.default_rng(404)
     cases = []
     for w, h in ((2304, 17), (2305, 9), (2303, 23), (2302, 8), (2301, 31), (5, 5), (4, 4), (6, 3), (13, 11),
