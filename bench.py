@@ -797,6 +797,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--e2e-in-flight", type=int, default=3, help="MI355XBackend(max_in_flight) of the e2e leg")
     ap.add_argument("--e2e-feed", default="native", choices=["native", "python"],
                     help="e2e host half: the native shard feed (C++ threads) or the Python prefetch thread")
+    ap.add_argument("--legs", default="fp8,c3,c2_dri,c2_prog,e2e",
+                    help="extra legs to run (comma list; the default line runs all)")
     ap.add_argument("--prog-mix", type=float, default=1.0 / 16,
                     help="c2_prog leg: share of progressive images per batch (0: skip the leg)")
     return ap
@@ -875,17 +877,19 @@ def dry_run(args, rank: int, world: int, local_rank: int) -> int:
 
 def run_rank(args, rank: int, world: int, local_rank: int) -> int:
     extras = world == 1 and not args.no_extras
+    legs_on = set(args.legs.split(","))
     procs = _procs(args, world)
     # synthetic data first, before anything initialises the GPU in this process
     uniq = make_unique(args.unique, args.width, args.height, 1 + rank, args.mixed, procs, args.progressive_frac,
                        args.restart_mcus)
     if extras:
         print(f"bench: rank {rank}: synthesising the c3 / c2_dri sets", file=sys.stderr, flush=True)
-        uniq_c3 = make_unique(args.extra_unique, 0, 0, 11 + rank, True, procs) if not args.mixed else None
+        uniq_c3 = make_unique(args.extra_unique, 0, 0, 11 + rank, True, procs) \
+            if not args.mixed and "c3" in legs_on else None
         uniq_dri = make_unique(args.extra_unique, args.width, args.height, 21 + rank, False, procs, 0.0, 4) \
-            if not args.restart_mcus else None
+            if not args.restart_mcus and "c2_dri" in legs_on else None
         uniq_prog = make_unique(64, args.width, args.height, 31 + rank, False, procs, 1.0) \
-            if args.prog_mix > 0 and not args.mixed else None
+            if args.prog_mix > 0 and not args.mixed and "c2_prog" in legs_on else None
 
     import torch
     devices = visible_devices()
@@ -970,7 +974,7 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
     legs = {}
     if extras:
         n_extra = max(args.batch * (args.steps + args.warmup), 8 * B)
-        if args.dtype == "bf16" and not args.mixed and not args.restart_mcus:
+        if args.dtype == "bf16" and not args.mixed and not args.restart_mcus and "fp8" in legs_on:
             print("bench: fp8 leg", file=sys.stderr, flush=True)
             _, s_fp8, (p, _, _) = leg(uniq, args.images, False, "fp8", False, "fp8", args.steps, args.warmup)
             p.close()
@@ -996,7 +1000,7 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
             legs["c2_prog"] = run_prog_leg(args, uniq, uniq_prog, rank, world, cfg, B, dist)
             legs["c2_prog"]["vs_c2"] = round(legs["c2_prog"]["value"] / (world * args.steps * B / dt), 4)
     e2e = None
-    if args.e2e or extras:
+    if args.e2e or (extras and "e2e" in legs_on):
         print("bench: e2e leg", file=sys.stderr, flush=True)
         e2e = run_e2e(args, uniq, rank, world, cfg, B, dist)
 

@@ -579,6 +579,14 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
   return nbits <= kHuffSegBits ? 1 : (int)((nbits + kHuffSegBits - 1) / kHuffSegBits);
 }
 
+#ifndef DINO_SINK_LDS
+#define DINO_SINK_LDS 8
+#endif
+// Entry words a lane buffers in LDS before it stores them as one aligned group (0: SparseSink's
+// register shift register; 8 / 16: 32 / 64-byte groups, no VGPRs for the buffer).
+// Word w of lane t sits at [w][t], so the lanes' halfword writes never share a bank.
+constexpr int kSinkLds = DINO_SINK_LDS;
+
 struct HuffLds {     // k_huff1
   ImgDesc sd;
   HuffTables tab;
@@ -586,6 +594,9 @@ struct HuffLds {     // k_huff1
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
+// k_huff1's write pass (single-segment images) decodes values, not skips: the SparseSink
+// buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
+static_assert(sizeof(HuffSkip) >= (size_t)kSinkLds * 4 * kHuffThreads, "sink buffers fit the skip tables");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
@@ -593,6 +604,7 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
   ImgDesc sd;
   alignas(16) uint8_t tab[kHuffTabBytesNoSkip];  // a HuffTables without its skip member
   int32_t img, item;
+  uint32_t sink[(kSinkLds ? kSinkLds : 1) * kHuffThreads];  // SparseSink buffers (kSinkLds)
 };
 
 static_assert(sizeof(ImgDesc) % 16 == 8 || sizeof(ImgDesc) % 16 == 0, "ImgDesc layout");
@@ -636,6 +648,15 @@ struct SparseSink {
   uint32_t bstart, dcw, n16, n32;
   bool wide;       // the open block has switched to u32 entries
   int32_t b;
+  uint32_t* lb;    // kSinkLds: this lane's buffer column in LDS (word w at lb[w * kHuffThreads])
+  __device__ void lds_flush(uint32_t words) {  // the buffer's first `words` words -> entries at n
+    uint4* dst = (uint4*)(ent + (n >> 1));
+#pragma unroll
+    for (int q = 0; q < (kSinkLds ? kSinkLds : 4) / 4; ++q)
+      if ((uint32_t)(4 * q) < words)
+        dst[q] = make_uint4(lb[(4 * q) * kHuffThreads], lb[(4 * q + 1) * kHuffThreads], lb[(4 * q + 2) * kHuffThreads],
+                            lb[(4 * q + 3) * kHuffThreads]);
+  }
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
@@ -678,6 +699,15 @@ struct SparseSink {
     }
   }
   __device__ void put(uint32_t h) {
+    if (kSinkLds) {
+      ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[k & 1] = (uint16_t)h;
+      if (++k == 2 * kSinkLds) {
+        lds_flush(kSinkLds);
+        n += 2 * kSinkLds;
+        k = 0;
+      }
+      return;
+    }
     shift_in(h);
     if (++k == 8) {
       chunk_done();
@@ -718,6 +748,16 @@ struct SparseSink {
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
   __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
+    if (kSinkLds) {
+      if (k) {
+        if (k & 1) ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[1] = 0;
+        const uint32_t used = (k + 1) >> 1, words = (used + 3) & ~3u;
+        for (uint32_t w = used; w < words; ++w) lb[w * kHuffThreads] = 0u;
+        lds_flush(words);
+      }
+      if (kSinkPairs && hrec) binfo[pb] = prec;
+      return;
+    }
     if (k)
       for (uint32_t j = k; j < 8; ++j) shift_in(0u);
     if (kSinkChunks > 1) {
@@ -972,6 +1012,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
         SparseSink sink;
         sink.ent = (uint32_t*)(ws + sd.coef_off);
         sink.binfo = (uint2*)(ws + sd.binfo_off);
+        sink.lb = reinterpret_cast<uint32_t*>(&L.tab.skip) + t;
         sink.open((int32_t)blk0);
         decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
                                  nbits, sink);
@@ -1068,6 +1109,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
     SparseSink sink;
     sink.ent = (uint32_t*)(ws + sd.coef_off);
     sink.binfo = (uint2*)(ws + sd.binfo_off);
+    sink.lb = L.sink + t;
     const int i = (item - sd.h_item_base) * kHuffThreads + t;
     if (sd.restart_interval > 0) {
       // restart intervals are independent: one lane per interval, absolute DC

@@ -1,14 +1,17 @@
 #!/bin/bash
 # A/B: the C2 and C3 bench lines (no CPU baseline, no extra legs) for every build/lib_<name>.so given,
 # on one box; optionally the GPU tests first (TESTS=1, on the in-tree library).
-# usage: [TESTS=1] scripts/gpu_ab_c23.sh TAG name1 name2 ...
+# usage: [TESTS=1 [TESTLIB=name]] scripts/gpu_ab_c23.sh TAG name1 name2 ...
 set -o pipefail
 TAG=$1; shift
 cd "${GRAFT_REPO_ROOT:-/root/repo}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 if [ "${TESTS:-0}" = 1 ]; then
+  # TESTLIB=name: the tests run on build/lib_<name>.so instead of the in-tree library
+  if [ -n "${TESTLIB:-}" ]; then export DINO_INGEST_LIB=build/lib_${TESTLIB}.so; fi
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
     > gpurun_out/${TAG}_gputests.log 2>&1 || { tail -30 gpurun_out/${TAG}_gputests.log; exit 1; }
   tail -2 gpurun_out/${TAG}_gputests.log
+  unset DINO_INGEST_LIB
 fi
 for n in "$@"; do
   DINO_INGEST_LIB=build/lib_$n.so timeout -k 10 300 python bench.py --steps 40 --warmup 5 --no-cpu-baseline --no-extras \

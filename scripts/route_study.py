@@ -27,6 +27,7 @@ def main() -> None:
     ap.add_argument("--routes", default="device,auto,host,side")
     ap.add_argument("--side-ahead", type=int, default=24)
     ap.add_argument("--warm", type=int, default=3, help="batches before the timed region")
+    ap.add_argument("--repeat", type=int, default=1, help="runs of each (k, route) in this process")
     args = ap.parse_args()
     B = args.batch
     base = make_unique(B, 640, 480, 1, False, 8)
@@ -40,7 +41,7 @@ def main() -> None:
             for t in range(k):
                 j[(t * B) // max(k, 1) + b % max(1, B // max(k, 1))] = prog[(b * k + t) % len(prog)]
             batches.append(j)
-        for route in args.routes.split(","):
+        for route in [r for r in args.routes.split(",") for _ in range(args.repeat)]:
             if k == 0 and route not in ("auto", "side"):
                 continue
             src = iter(batches)
