@@ -179,6 +179,31 @@ _END = object()
 # not hold pinned tensors while the interpreter finalises them
 _LIVE: "weakref.WeakSet[MI355XAugPipeline]" = weakref.WeakSet()
 
+# One torch stream per (device, role, index) for the life of the process: every pipeline
+# reuses the streams of the first one.  HIP multiplexes streams onto a few hardware queues
+# (GPU_MAX_HW_QUEUES, 4 by default) in creation order, so fresh streams for each pipeline
+# land on other queues than the first pipeline's did, and a second side-route pipeline in
+# a process ran at 68-70k img/s against 101k for the first (profiles/r04_side_repeat_*).
+# The first request on a device takes the usual roles' streams in one fixed order (the
+# order a feed-driven side-route pipeline asks for them), so the mapping does not depend
+# on which kind of pipeline a process builds first.
+_ROLE_STREAMS: dict = {}
+_ROLE_LOCK = threading.Lock()
+_ROLE_ORDER = (("copy", 0), ("slot", 0), ("slot", 1), ("slot", 2), ("side_copy", 0), ("side_copy", 1))
+
+
+def role_stream(device, role: str, k: int = 0) -> torch.cuda.Stream:
+    dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    with _ROLE_LOCK:
+        if not any(key[0] == idx for key in _ROLE_STREAMS):
+            for r, j in _ROLE_ORDER:
+                _ROLE_STREAMS[(idx, r, j)] = torch.cuda.Stream(device=idx)
+        st = _ROLE_STREAMS.get((idx, role, k))
+        if st is None:
+            st = _ROLE_STREAMS[(idx, role, k)] = torch.cuda.Stream(device=idx)
+        return st
+
 
 @atexit.register
 def _close_live() -> None:
@@ -318,7 +343,7 @@ class MI355XAugPipeline:
         # H2D copies of the native feed's batches, off the slots' streams (DINO_COPY_STREAM=0: on them)
         self._copy_stream = None
         if (self._feed and depth > 1 and os.environ.get("DINO_COPY_STREAM", "1") != "0") or self._side_ahead:
-            self._copy_stream = torch.cuda.Stream(device=device)
+            self._copy_stream = role_stream(device, "copy")
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
@@ -327,7 +352,7 @@ class MI355XAugPipeline:
             if k == 0 and engine is not None:
                 eng = engine
             else:
-                stream = torch.cuda.Stream(device=device) if self.depth > 1 else None
+                stream = role_stream(device, "slot", k) if self.depth > 1 else None
                 eng = IngestEngine(device, max_batch=self._batch_size, max_views=aug_cfg.n_views,
                                    max_crop_size=max_crop, max_image_dim=max_image_dim,
                                    workspace_bytes=workspace_bytes, stream=stream)

@@ -98,12 +98,13 @@ class _SideEngine:
     Consecutive launches of a context are ordered by the dedicated stream itself."""
 
     def __init__(self, device: torch.device, max_images: int, max_image_dim: int, cu_count: int = 0,
-                 dedicated: bool = True):
+                 dedicated: bool = True, index: int = 0):
+        from .pipeline import role_stream
         self.raw = _create_stream(device.index or 0, int(cu_count)) if dedicated else None
-        self.stream = self.raw if dedicated else torch.cuda.Stream(device=device)
+        self.stream = self.raw if dedicated else role_stream(device, "side", index)
         self.eng = IngestEngine(device, max_batch=max_images, max_views=1, max_crop_size=8,
                                 max_image_dim=max_image_dim, workspace_bytes=64 << 20, stream=self.stream)
-        self.copy = torch.cuda.Stream(device=device)  # this context's torch stream (allocations, copies)
+        self.copy = role_stream(device, "side_copy", index)  # this context's torch stream (allocations, copies)
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
         self.keep = None                             # host / device inputs of the mini-batch in flight
 
@@ -173,7 +174,8 @@ class DeviceSideDecoder:
             if e.idle():
                 return e
         if len(self._engines) < self.cap:
-            e = _SideEngine(self.device, self.max_images, self.max_image_dim, self.cu_count, self.dedicated)
+            e = _SideEngine(self.device, self.max_images, self.max_image_dim, self.cu_count, self.dedicated,
+                            index=len(self._engines))
             self._engines.append(e)
             return e
         e = self._engines[self._rr % len(self._engines)]

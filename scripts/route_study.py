@@ -28,6 +28,8 @@ def main() -> None:
     ap.add_argument("--side-ahead", type=int, default=24)
     ap.add_argument("--warm", type=int, default=3, help="batches before the timed region")
     ap.add_argument("--repeat", type=int, default=1, help="runs of each (k, route) in this process")
+    ap.add_argument("--backend", action="store_true",
+                    help="build through MI355XBackend.build_pipeline + build_pipeline_iterator (as bench's c2_prog)")
     args = ap.parse_args()
     B = args.batch
     base = make_unique(B, 640, 480, 1, False, 8)
@@ -45,9 +47,23 @@ def main() -> None:
             if k == 0 and route not in ("auto", "side"):
                 continue
             src = iter(batches)
-            pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=1, depth=3, multiscan_route=route,
-                                     side_ahead=args.side_ahead)
-            it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
+            if args.backend:
+                from dataloader_amd.backend import MI355XBackend
+                from dataloader_amd.config import DinoV2AugSpec, PipelineConfig
+
+                class _Src:
+                    _batch_size, _resolution_src = B, None
+
+                    def __call__(self):
+                        return next(src)
+                spec = DinoV2AugSpec(aug_cfg=cfg)
+                be = MI355XBackend(multiscan_route=route)
+                pipe = be.build_pipeline(_Src(), spec, PipelineConfig(device_id=0, seed=1, gpu_queue=6), None)
+                it = be.build_pipeline_iterator(pipe, spec, spec.output_map, B)
+            else:
+                pipe = MI355XAugPipeline(lambda: next(src), cfg, B, seed=1, depth=3, multiscan_route=route,
+                                         side_ahead=args.side_ahead)
+                it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
             n = 0
             t0 = None
             for i, _ in enumerate(it):

@@ -144,7 +144,7 @@ def test_side_route_reads_page_locked_spans_batches(gpu_device, tmp_path):
 def test_side_pipeline_close_destroys_streams_and_reopens(gpu_device):
     """a side pipeline is created, run and closed, three times in one process;
     every close destroys its dedicated streams (no stream is left alive for the process),
-    and every run gives the same views."""
+    every run gives the same views, and every pipeline launches on the same slot streams."""
     from dataloader_amd import progside
     from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
     rng = np.random.default_rng(72)
@@ -154,9 +154,13 @@ def test_side_pipeline_close_destroys_streams_and_reopens(gpu_device):
     names = [f"view_{i}" for i in range(cfg.n_views)]
     base = progside.live_streams()
     runs = []
+    slot_streams = []
     for _ in range(3):
         pipe = MI355XAugPipeline(_ListSource(batches), cfg, B, seed=13, depth=2, multiscan_route="side",
                                  host_workers=2, side_ahead=2)
+        # every pipeline reuses the process's role streams (pipeline.role_stream): the same
+        # hardware-queue mapping as the first pipeline's
+        slot_streams.append([sl.engine.stream.cuda_stream for sl in pipe._slots])
         outs = _collect(MI355XPipelineIterator(pipe, names, B))
         assert pipe.flush_stats()["side_decoded"] == 3 * nb
         assert progside.live_streams() > base
@@ -169,6 +173,7 @@ def test_side_pipeline_close_destroys_streams_and_reopens(gpu_device):
         for a, b in zip(runs[0], outs):
             for name in a:
                 assert torch.equal(a[name], b[name]), name
+    assert slot_streams[0] == slot_streams[1] == slot_streams[2]
 
 
 def test_kept_slice_of_an_output_is_not_refilled(gpu_device):
