@@ -799,6 +799,8 @@ def build_parser() -> argparse.ArgumentParser:
                     help="e2e host half: the native shard feed (C++ threads) or the Python prefetch thread")
     ap.add_argument("--legs", default="fp8,c3,c2_dri,c2_prog,e2e",
                     help="extra legs to run (comma list; the default line runs all)")
+    ap.add_argument("--only-leg", default="", choices=["", "c2_prog"],
+                    help="internal: run this leg alone and print its JSON (the c2_prog leg runs in a child process)")
     ap.add_argument("--prog-mix", type=float, default=1.0 / 16,
                     help="c2_prog leg: share of progressive images per batch (0: skip the leg)")
     return ap
@@ -828,7 +830,41 @@ def main(argv: list[str] | None = None) -> int:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dry_run:
         return dry_run(args, rank, world, local_rank)
+    if args.only_leg == "c2_prog":
+        return run_prog_leg_only(args)
     return run_rank(args, rank, world, local_rank)
+
+
+def run_prog_leg_only(args) -> int:
+    """The c2_prog leg in a process of its own (what a training job has: one pipeline per
+    process).  Run after the other legs in their process it measured 57-70k img/s against
+    95-110k in a fresh one (hardware-queue state left by earlier pipelines)."""
+    procs = _procs(args, 1)
+    uniq = make_unique(args.unique, args.width, args.height, 1, False, procs, 0.0, 0)
+    uniq_prog = make_unique(64, args.width, args.height, 31, False, procs, 1.0)
+    import torch
+    torch.cuda.set_device(0)
+    from dataloader_amd.config import DINOAugConfig
+    res = run_prog_leg(args, uniq, uniq_prog, 0, 1, DINOAugConfig(), args.batch, None)
+    print(json.dumps(res), flush=True)
+    return 0
+
+
+def run_prog_leg_child(args) -> dict:
+    """Start ``bench.py --only-leg c2_prog`` as a child process (same data seeds and sizes)
+    and return its leg record."""
+    import subprocess
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--only-leg", "c2_prog", "--steps", str(args.steps),
+           "--warmup", str(args.warmup), "--batch", str(args.batch), "--unique", str(args.unique),
+           "--procs", str(args.procs), "--width", str(args.width), "--height", str(args.height),
+           "--prog-mix", str(args.prog_mix), "--gpu-queue", str(args.gpu_queue)]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
+    if out.returncode != 0:
+        raise RuntimeError(f"c2_prog child failed ({out.returncode}): {out.stderr[-2000:]}")
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    res["process"] = "child (a fresh process, as a training job's loader)"
+    return res
 
 
 def _init_group(world: int):
@@ -888,8 +924,8 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
             if not args.mixed and "c3" in legs_on else None
         uniq_dri = make_unique(args.extra_unique, args.width, args.height, 21 + rank, False, procs, 0.0, 4) \
             if not args.restart_mcus and "c2_dri" in legs_on else None
-        uniq_prog = make_unique(64, args.width, args.height, 31 + rank, False, procs, 1.0) \
-            if args.prog_mix > 0 and not args.mixed and "c2_prog" in legs_on else None
+        # (the c2_prog leg synthesises its own sets in its child process)
+        prog_on = args.prog_mix > 0 and not args.mixed and "c2_prog" in legs_on
 
     import torch
     devices = visible_devices()
@@ -994,10 +1030,10 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
             p.close()
             legs["c2_dri"] = dict(s_dri, workload=f"C2 with restart markers every 4 MCUs (DRI), "
                                                   f"{args.extra_unique} distinct encodes, {args.dtype} out")
-        if uniq_prog is not None:
+        if prog_on:
             print("bench: c2_prog leg", file=sys.stderr, flush=True)
             torch.cuda.empty_cache()
-            legs["c2_prog"] = run_prog_leg(args, uniq, uniq_prog, rank, world, cfg, B, dist)
+            legs["c2_prog"] = run_prog_leg_child(args)
             legs["c2_prog"]["vs_c2"] = round(legs["c2_prog"]["value"] / (world * args.steps * B / dt), 4)
     e2e = None
     if args.e2e or (extras and "e2e" in legs_on):

@@ -431,6 +431,20 @@ DHD void state_step(BitCursor& cur, const BitReader& br, const HuffImage& im, in
     huff_step<kWin>(cur, br, im, blk, z);
 }
 
+// A guessed start state for the range starting at bit `to`: decode state-only from an
+// earlier bit `from` (block-in-MCU 0, zigzag 0 guessed there) up to the first step
+// boundary >= to.  By then the decode has usually fallen into the true codeword and
+// MCU-phase sequence (the sync distance), so the range's first decode starts from the
+// true state more often and the sync rounds redo fewer ranges.
+template <int kWin>
+DHD HState decode_lookback(const BitReader& br, const HuffImage& im, uint32_t from, uint32_t to) {
+  BitCursor cur;
+  bc_init<kWin>(cur, br, from);
+  int32_t blk = 0, z = 0;
+  while (cur.pos < to) state_step<kWin>(cur, br, im, blk, z);
+  return HState{cur.pos, blk, z};
+}
+
 // What a lane learns by decoding the steps that start in [st.pos, end).
 struct RangeOut {
   HState end;      // state at the first step boundary >= end

@@ -951,6 +951,11 @@ __device__ uint64_t g_huff_phase[kPhaseItems][5];
   } while (0)
 #endif
 
+#ifndef DINO_HUFF_LOOKBACK
+#define DINO_HUFF_LOOKBACK 0
+#endif
+constexpr int kHuffLookback = DINO_HUFF_LOOKBACK;  // bits a lane decodes before its range to guess its start state
+
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
   main_prio();
@@ -979,6 +984,10 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     HState myS{(uint32_t)i * (uint32_t)sd.h_sub, 0, 0};  // this lane's start state and first-decode
     RangeOut myR1{};                                      // result stay in registers; only R is shared
     HUFF_PHASE(0, wall_clock64());
+    if (kHuffLookback > 0 && active && i > 0) {  // guess the start state from kHuffLookback bits earlier
+      const uint32_t to = myS.pos, from = to > (uint32_t)kHuffLookback ? to - (uint32_t)kHuffLookback : 0u;
+      myS = decode_lookback<kHuffSrc>(br, im, from, to);
+    }
     if (active) {
       myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
       L.R[t] = myR1;
