@@ -952,7 +952,7 @@ __device__ uint64_t g_huff_phase[kPhaseItems][5];
 #endif
 
 #ifndef DINO_HUFF_LOOKBACK
-#define DINO_HUFF_LOOKBACK 0
+#define DINO_HUFF_LOOKBACK 2048
 #endif
 constexpr int kHuffLookback = DINO_HUFF_LOOKBACK;  // bits a lane decodes before its range to guess its start state
 
