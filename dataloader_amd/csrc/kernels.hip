@@ -586,6 +586,14 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 // register shift register; 8 / 16: 32 / 64-byte groups, no VGPRs for the buffer).
 // Word w of lane t sits at [w][t], so the lanes' halfword writes never share a bank.
 constexpr int kSinkLds = DINO_SINK_LDS;
+#ifndef DINO_SINK_RECS
+#define DINO_SINK_RECS 0
+#endif
+// Block records a lane buffers in LDS (after its entry words) and stores as one aligned
+// 8 x kSinkRecs-byte group when the group is complete (0: each record stored alone).
+constexpr int kSinkRecs = DINO_SINK_RECS;
+static_assert(kSinkRecs == 0 || (kSinkLds > 0 && (kSinkRecs == 2 || kSinkRecs == 4)), "record groups");
+constexpr int kSinkWords = kSinkLds + 2 * kSinkRecs;  // LDS words per lane
 
 struct HuffLds {     // k_huff1
   ImgDesc sd;
@@ -596,7 +604,7 @@ struct HuffLds {     // k_huff1
 };
 // k_huff1's write pass (single-segment images) decodes values, not skips: the SparseSink
 // buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
-static_assert(sizeof(HuffSkip) >= (size_t)kSinkLds * 4 * kHuffThreads, "sink buffers fit the skip tables");
+static_assert(sizeof(HuffSkip) >= (size_t)kSinkWords * 4 * kHuffThreads, "sink buffers fit the skip tables");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
@@ -604,7 +612,7 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
   ImgDesc sd;
   alignas(16) uint8_t tab[kHuffTabBytesNoSkip];  // a HuffTables without its skip member
   int32_t img, item;
-  uint32_t sink[(kSinkLds ? kSinkLds : 1) * kHuffThreads];  // SparseSink buffers (kSinkLds)
+  uint32_t sink[(kSinkWords ? kSinkWords : 1) * kHuffThreads];  // SparseSink buffers (kSinkLds, kSinkRecs)
 };
 
 static_assert(sizeof(ImgDesc) % 16 == 8 || sizeof(ImgDesc) % 16 == 0, "ImgDesc layout");
@@ -649,6 +657,23 @@ struct SparseSink {
   bool wide;       // the open block has switched to u32 entries
   int32_t b;
   uint32_t* lb;    // kSinkLds: this lane's buffer column in LDS (word w at lb[w * kHuffThreads])
+  uint32_t rmask;  // kSinkRecs: buffered records of blocks rbase + j (bit j)
+  int32_t rbase;
+  __device__ void rec_flush() {
+    if (!rmask) return;
+    uint32_t* rw = lb + kSinkLds * kHuffThreads;
+    if (rmask == (1u << kSinkRecs) - 1) {
+      uint4* dst = (uint4*)(binfo + rbase);
+#pragma unroll
+      for (int q = 0; q < (kSinkRecs ? kSinkRecs : 2) / 2; ++q)
+        dst[q] = make_uint4(rw[(4 * q) * kHuffThreads], rw[(4 * q + 1) * kHuffThreads], rw[(4 * q + 2) * kHuffThreads],
+                            rw[(4 * q + 3) * kHuffThreads]);
+    } else {
+      for (int j = 0; j < kSinkRecs; ++j)
+        if ((rmask >> j) & 1u) binfo[rbase + j] = make_uint2(rw[(2 * j) * kHuffThreads], rw[(2 * j + 1) * kHuffThreads]);
+    }
+    rmask = 0;
+  }
   __device__ void lds_flush(uint32_t words) {  // the buffer's first `words` words -> entries at n
     uint4* dst = (uint4*)(ent + (n >> 1));
 #pragma unroll
@@ -662,6 +687,7 @@ struct SparseSink {
     k = 0;
     kc = 0;
     hrec = false;
+    rmask = 0;
   }
   __device__ void begin(int32_t blk) {
     b = blk;
@@ -732,6 +758,18 @@ struct SparseSink {
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
   __device__ void record(int32_t blk, uint2 r) {
+    if (kSinkRecs) {
+      const int32_t g = blk & ~(kSinkRecs - 1);
+      if (rmask && g != rbase) rec_flush();
+      rbase = g;
+      const int j = blk - g;
+      uint32_t* rw = lb + kSinkLds * kHuffThreads;
+      rw[(2 * j) * kHuffThreads] = r.x;
+      rw[(2 * j + 1) * kHuffThreads] = r.y;
+      rmask |= 1u << j;
+      if (rmask == (1u << kSinkRecs) - 1) rec_flush();
+      return;
+    }
     if (!kSinkPairs) {
       binfo[blk] = r;
     } else if (blk & 1) {  // odd block: completes the pair opened by blk - 1 (if this lane opened it)
@@ -756,6 +794,7 @@ struct SparseSink {
         lds_flush(words);
       }
       if (kSinkPairs && hrec) binfo[pb] = prec;
+      if (kSinkRecs) rec_flush();
       return;
     }
     if (k)
