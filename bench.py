@@ -799,8 +799,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="e2e host half: the native shard feed (C++ threads) or the Python prefetch thread")
     ap.add_argument("--legs", default="fp8,c3,c2_dri,c2_prog,e2e",
                     help="extra legs to run (comma list; the default line runs all)")
-    ap.add_argument("--only-leg", default="", choices=["", "c2_prog"],
-                    help="internal: run this leg alone and print its JSON (the c2_prog leg runs in a child process)")
+    ap.add_argument("--only-leg", default="", choices=["", "c2_prog", "e2e"],
+                    help="internal: run this leg alone and print its JSON (the c2_prog and, at N = 1, e2e "
+                         "legs run in child processes)")
     ap.add_argument("--prog-mix", type=float, default=1.0 / 16,
                     help="c2_prog leg: share of progressive images per batch (0: skip the leg)")
     return ap
@@ -830,38 +831,48 @@ def main(argv: list[str] | None = None) -> int:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dry_run:
         return dry_run(args, rank, world, local_rank)
-    if args.only_leg == "c2_prog":
-        return run_prog_leg_only(args)
+    if args.only_leg:
+        return run_leg_only(args)
     return run_rank(args, rank, world, local_rank)
 
 
-def run_prog_leg_only(args) -> int:
-    """The c2_prog leg in a process of its own (what a training job has: one pipeline per
-    process).  Run after the other legs in their process it measured 57-70k img/s against
-    95-110k in a fresh one (hardware-queue state left by earlier pipelines)."""
+def run_leg_only(args) -> int:
+    """One host-fed leg in a process of its own (what a training job has: one loader
+    pipeline per process).  After the other legs in their process the c2_prog leg measured
+    57-70k img/s against 95-110k in a fresh one, and the e2e leg 95-127k against 135-142k
+    (state left by earlier pipelines)."""
     procs = _procs(args, 1)
-    uniq = make_unique(args.unique, args.width, args.height, 1, False, procs, 0.0, 0)
-    uniq_prog = make_unique(64, args.width, args.height, 31, False, procs, 1.0)
+    uniq = make_unique(args.unique, args.width, args.height, 1, args.mixed, procs, args.progressive_frac,
+                       args.restart_mcus)
+    uniq_prog = make_unique(64, args.width, args.height, 31, False, procs, 1.0) if args.only_leg == "c2_prog" else None
     import torch
     torch.cuda.set_device(0)
     from dataloader_amd.config import DINOAugConfig
-    res = run_prog_leg(args, uniq, uniq_prog, 0, 1, DINOAugConfig(), args.batch, None)
+    if args.only_leg == "c2_prog":
+        res = run_prog_leg(args, uniq, uniq_prog, 0, 1, DINOAugConfig(), args.batch, None)
+    else:
+        res = run_e2e(args, uniq, 0, 1, DINOAugConfig(), args.batch, None)
     print(json.dumps(res), flush=True)
     return 0
 
 
-def run_prog_leg_child(args) -> dict:
-    """Start ``bench.py --only-leg c2_prog`` as a child process (same data seeds and sizes)
+def run_leg_child(args, leg: str) -> dict:
+    """Start ``bench.py --only-leg <leg>`` as a child process (same data seeds and sizes)
     and return its leg record."""
     import subprocess
-    cmd = [sys.executable, str(Path(__file__).resolve()), "--only-leg", "c2_prog", "--steps", str(args.steps),
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--only-leg", leg, "--steps", str(args.steps),
            "--warmup", str(args.warmup), "--batch", str(args.batch), "--unique", str(args.unique),
            "--procs", str(args.procs), "--width", str(args.width), "--height", str(args.height),
-           "--prog-mix", str(args.prog_mix), "--gpu-queue", str(args.gpu_queue)]
+           "--prog-mix", str(args.prog_mix), "--gpu-queue", str(args.gpu_queue),
+           "--progressive-frac", str(args.progressive_frac), "--restart-mcus", str(args.restart_mcus),
+           "--shard-size", str(args.shard_size), "--gather-threads", str(args.gather_threads),
+           "--e2e-in-flight", str(args.e2e_in_flight), "--e2e-feed", args.e2e_feed]
+    if args.mixed:
+        cmd.append("--mixed")
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     if out.returncode != 0:
-        raise RuntimeError(f"c2_prog child failed ({out.returncode}): {out.stderr[-2000:]}")
+        raise RuntimeError(f"{leg} child failed ({out.returncode}): {out.stderr[-2000:]}")
     res = json.loads(out.stdout.strip().splitlines()[-1])
     res["process"] = "child (a fresh process, as a training job's loader)"
     return res
@@ -1033,12 +1044,13 @@ def run_rank(args, rank: int, world: int, local_rank: int) -> int:
         if prog_on:
             print("bench: c2_prog leg", file=sys.stderr, flush=True)
             torch.cuda.empty_cache()
-            legs["c2_prog"] = run_prog_leg_child(args)
+            legs["c2_prog"] = run_leg_child(args, "c2_prog")
             legs["c2_prog"]["vs_c2"] = round(legs["c2_prog"]["value"] / (world * args.steps * B / dt), 4)
     e2e = None
     if args.e2e or (extras and "e2e" in legs_on):
         print("bench: e2e leg", file=sys.stderr, flush=True)
-        e2e = run_e2e(args, uniq, rank, world, cfg, B, dist)
+        # N = 1: in a child process, as c2_prog (N > 1: in the ranks, for their barriers)
+        e2e = run_leg_child(args, "e2e") if world == 1 else run_e2e(args, uniq, rank, world, cfg, B, dist)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
