@@ -86,3 +86,41 @@ def test_rank_count_must_match_gpus_flag():
     r = _run(["--gpus", "3", "--dry-run"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0",
                                              "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29999"})
     assert r.returncode != 0 and "--gpus 3" in r.stderr
+
+
+@pytest.mark.parametrize("leg", ["c2_prog", "e2e"])
+def test_host_fed_legs_run_in_a_child_process(monkeypatch, leg):
+    """The c2_prog and (N = 1) e2e legs run as ``bench.py --only-leg <leg>`` children with
+    the parent's data sizes and seeds (one loader pipeline per process, as in training;
+    DESIGN.md §5), without the parent's rank environment; a failing child fails the leg."""
+    args = bench.build_parser().parse_args(["--steps", "7", "--warmup", "2", "--batch", "64", "--unique", "32",
+                                            "--mixed", "--gather-threads", "3"])
+    seen = {}
+
+    class _Done:
+        returncode = 0
+        stdout = json.dumps({"value": 1.0}) + "\n"
+        stderr = ""
+
+    def fake_run(cmd, **kw):
+        seen["cmd"], seen["env"] = cmd, kw.get("env", {})
+        return _Done()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setenv("RANK", "0")
+    res = bench.run_leg_child(args, leg)
+    cmd = seen["cmd"]
+    assert cmd[1].endswith("bench.py") and cmd[cmd.index("--only-leg") + 1] == leg
+    for flag, val in (("--steps", "7"), ("--warmup", "2"), ("--batch", "64"), ("--unique", "32"),
+                      ("--gather-threads", "3")):
+        assert cmd[cmd.index(flag) + 1] == val
+    assert "--mixed" in cmd and "RANK" not in seen["env"]
+    assert res["value"] == 1.0 and res["process"].startswith("child")
+
+    class _Fail(_Done):
+        returncode = 3
+        stderr = "boom"
+
+    monkeypatch.setattr(subprocess, "run", lambda cmd, **kw: _Fail())
+    with pytest.raises(RuntimeError, match="boom"):
+        bench.run_leg_child(args, leg)
