@@ -594,6 +594,12 @@ constexpr int kSinkLds = DINO_SINK_LDS;
 constexpr int kSinkRecs = DINO_SINK_RECS;
 static_assert(kSinkRecs == 0 || (kSinkLds > 0 && (kSinkRecs == 2 || kSinkRecs == 4)), "record groups");
 constexpr int kSinkWords = kSinkLds + 2 * kSinkRecs;  // LDS words per lane
+#ifndef DINO_SINK_LDS3
+#define DINO_SINK_LDS3 16
+#endif
+// k_huff3's entry buffer (its own LDS, not k_huff1's borrowed skip tables)
+constexpr int kSinkLds3 = DINO_SINK_LDS3;
+constexpr int kSinkWords3 = kSinkLds3 + 2 * kSinkRecs;
 
 struct HuffLds {     // k_huff1
   ImgDesc sd;
@@ -612,7 +618,7 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
   ImgDesc sd;
   alignas(16) uint8_t tab[kHuffTabBytesNoSkip];  // a HuffTables without its skip member
   int32_t img, item;
-  uint32_t sink[(kSinkWords ? kSinkWords : 1) * kHuffThreads];  // SparseSink buffers (kSinkLds, kSinkRecs)
+  uint32_t sink[(kSinkWords3 ? kSinkWords3 : 1) * kHuffThreads];  // SparseSink buffers (kSinkLds3, kSinkRecs)
 };
 
 static_assert(sizeof(ImgDesc) % 16 == 8 || sizeof(ImgDesc) % 16 == 0, "ImgDesc layout");
@@ -642,7 +648,8 @@ constexpr uint32_t kBinfoAbsDc = 1u << 15;
 #endif
 constexpr int kSinkChunks = DINO_SINK_CHUNKS;  // 16-byte entry chunks a lane stores together (1, 2, 4)
 constexpr bool kSinkPairs = DINO_SINK_PAIRS;   // block records stored as aligned 16-byte pairs
-struct SparseSink {
+template <int W>  // entry words buffered per lane in LDS (W: k_huff1, W3: k_huff3)
+struct SparseSinkT {
   uint32_t* ent;   // image entry area
   uint2* binfo;    // image block info
   uint32_t n;      // halfwords in whole chunks (relative to the image entry area), multiple of 8
@@ -656,12 +663,12 @@ struct SparseSink {
   uint32_t bstart, dcw, n16, n32;
   bool wide;       // the open block has switched to u32 entries
   int32_t b;
-  uint32_t* lb;    // kSinkLds: this lane's buffer column in LDS (word w at lb[w * kHuffThreads])
+  uint32_t* lb;    // W: this lane's buffer column in LDS (word w at lb[w * kHuffThreads])
   uint32_t rmask;  // kSinkRecs: buffered records of blocks rbase + j (bit j)
   int32_t rbase;
   __device__ void rec_flush() {
     if (!rmask) return;
-    uint32_t* rw = lb + kSinkLds * kHuffThreads;
+    uint32_t* rw = lb + W * kHuffThreads;
     if (rmask == (1u << kSinkRecs) - 1) {
       uint4* dst = (uint4*)(binfo + rbase);
 #pragma unroll
@@ -677,7 +684,7 @@ struct SparseSink {
   __device__ void lds_flush(uint32_t words) {  // the buffer's first `words` words -> entries at n
     uint4* dst = (uint4*)(ent + (n >> 1));
 #pragma unroll
-    for (int q = 0; q < (kSinkLds ? kSinkLds : 4) / 4; ++q)
+    for (int q = 0; q < (W ? W : 4) / 4; ++q)
       if ((uint32_t)(4 * q) < words)
         dst[q] = make_uint4(lb[(4 * q) * kHuffThreads], lb[(4 * q + 1) * kHuffThreads], lb[(4 * q + 2) * kHuffThreads],
                             lb[(4 * q + 3) * kHuffThreads]);
@@ -725,11 +732,11 @@ struct SparseSink {
     }
   }
   __device__ void put(uint32_t h) {
-    if (kSinkLds) {
+    if (W) {
       ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[k & 1] = (uint16_t)h;
-      if (++k == 2 * kSinkLds) {
-        lds_flush(kSinkLds);
-        n += 2 * kSinkLds;
+      if (++k == 2 * W) {
+        lds_flush(W);
+        n += 2 * W;
         k = 0;
       }
       return;
@@ -763,7 +770,7 @@ struct SparseSink {
       if (rmask && g != rbase) rec_flush();
       rbase = g;
       const int j = blk - g;
-      uint32_t* rw = lb + kSinkLds * kHuffThreads;
+      uint32_t* rw = lb + W * kHuffThreads;
       rw[(2 * j) * kHuffThreads] = r.x;
       rw[(2 * j + 1) * kHuffThreads] = r.y;
       rmask |= 1u << j;
@@ -786,7 +793,7 @@ struct SparseSink {
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
   __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
-    if (kSinkLds) {
+    if (W) {
       if (k) {
         if (k & 1) ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[1] = 0;
         const uint32_t used = (k + 1) >> 1, words = (used + 3) & ~3u;
@@ -811,6 +818,7 @@ struct SparseSink {
     if (kSinkPairs && hrec) binfo[pb] = prec;  // a lone even block (the lane's last record)
   }
 };
+using SparseSink = SparseSinkT<kSinkLds>;
 
 // Lane geometry of a non-restart image: range [i*sub, end) of every active lane.
 __device__ __forceinline__ uint32_t lane_range_end(const ImgDesc& d, int i, uint32_t nbits) {
@@ -1154,7 +1162,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
     HuffImage im;
     hi_init(im, reinterpret_cast<const HuffTables*>(L.tab), sd.mcu_comp, sd.blocks_per_mcu);
     const uint32_t* words = (const uint32_t*)(ws + sd.ent_off);
-    SparseSink sink;
+    SparseSinkT<kSinkLds3> sink;
     sink.ent = (uint32_t*)(ws + sd.coef_off);
     sink.binfo = (uint2*)(ws + sd.binfo_off);
     sink.lb = L.sink + t;
