@@ -610,7 +610,10 @@ struct HuffLds {     // k_huff1
 };
 // k_huff1's write pass (single-segment images) decodes values, not skips: the SparseSink
 // buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
-static_assert(sizeof(HuffSkip) >= (size_t)kSinkWords * 4 * kHuffThreads, "sink buffers fit the skip tables");
+// (and the range results R, which follow the tables and are read before the write pass)
+static_assert(offsetof(HuffLds, R) == offsetof(HuffLds, tab) + sizeof(HuffTables), "R follows the tables");
+static_assert(sizeof(HuffSkip) + sizeof(RangeOut) * kHuffThreads >= (size_t)kSinkWords * 4 * kHuffThreads,
+              "sink buffers fit the skip tables and R");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
