@@ -53,7 +53,6 @@ sys.path.insert(0, str(ROOT))
 METRIC = "images/sec decode+10-crop, device-resident (JPEG bytes in HBM), 1/2/4/8 GPU"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 VFINAL_MAX_S = 128  # kernels.hip kVFinalMaxS: views up to this size run k_vfinal (vertical pass + epilogue fused)
-FUSE_MAX_W = 2304  # kernels.hip kFuseMaxW: with DINO_FUSE=1, 4:2:0 images up to this width run k_ycolor
 
 
 # ----------------------------------------------------------------------------- synthetic data
@@ -148,13 +147,6 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     s_unfused = float(np.mean([len(j) if not f else 0 for j, f in zip(jpegs, fz)]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
     per_blk = entry_bytes_per_block + 8.0       # sparse entries + the 8-byte block record
-    fuse_on = os.environ.get("DINO_FUSE") == "1"  # the library's opt-in (LaunchGeom::fuse)
-    fu = [fuse_on and w <= FUSE_MAX_W for w, _ in dims]  # (synthetic encodes are all 4:2:0)
-    chroma_fused = float(np.mean([b / 3 if f else 0 for b, f in zip(nblk, fu)]))
-    luma_fused = 2 * chroma_fused
-    blocks_unfused = blocks - 3 * chroma_fused
-    blocks_idct = blocks - luma_fused
-    px_fused = float(np.mean([w * h if f else 0 for (w, h), f in zip(dims, fu)]))
     ab = {
         "path": s_jpeg + out,                       # S_jpeg + 1 044 480 B (bf16)
         "k_destuff": s_jpeg,                         # per launch: count pass reads, write pass reads + writes
@@ -163,12 +155,9 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
         "k_huff1": s_jpeg + blk_fused * per_blk,
         # re-decode of the other images: entropy bytes in, sparse entries + records out
         "k_huff3": s_unfused + (blocks - blk_fused) * per_blk,
-        # 4:2:0 images at most FUSE_MAX_W wide: k_idct transforms their chroma planes only and
-        # k_ycolor their luma blocks (entries in) + the chroma planes in + RGB out (no luma plane);
-        # k_color converts the other images from their planes
-        "k_idct": blocks_idct * (per_blk + 64),
-        "k_ycolor": luma_fused * per_blk + chroma_fused * 64 + px_fused * 3,
-        "k_color": blocks_unfused * 64 + (px - px_fused) * 3,
+        # entries + records in, planes out; planes in, RGB out
+        "k_idct": blocks * (per_blk + 64),
+        "k_color": blocks * 64 + px * 3,
         "k_final_global": (3 + out_bytes * 3) * n_g * g * g,
         "k_final_local": (3 + out_bytes * 3) * n_l * l * l,
         "s_jpeg": s_jpeg,
@@ -613,30 +602,41 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
                           dali_fp8_output=args.dtype == "fp8")
     backend = MI355XBackend(max_in_flight=args.e2e_in_flight)
     depth = backend.queue_depth(pcfg, B)
-    n = (args.warmup + args.steps + depth + 4) * B
-    jpegs = [uniq[i % len(uniq)] for i in range(n)]
-    shards = make_shards(jpegs, args.shard_size)
+    # steady state: a timed window of e2e_steps batches after e2e_warmup, over a
+    # set of at least 4 x the side look-ahead (the look-ahead then never spans the set)
+    steps, warm = args.e2e_steps, max(args.warmup, args.e2e_warmup)
+    look = backend.side_look_ahead(pcfg, None, depth)
+    n_batches = max(warm + steps + depth + 8, 4 * look)
+    n = n_batches * B
+    # distinct shard files (Stage 1's output); their contents repeat a few tars of the distinct
+    # encodes so that the bench holds only those in memory
+    per = args.shard_size
+    n_shards = -(-n // per)
+    blobs = [make_shards([uniq[(k * 7919 + i) % len(uniq)] for i in range(per)], per)[0]
+             for k in range(min(n_shards, 8))]
     cache = ShmShardCache(job_id=f"dino_bench_{os.getpid()}", base_dir="/dev/shm", max_gb=64.0)
     try:
-        paths = [f"/synthetic/rank{rank}/shard-{k:05d}.tar" for k in range(len(shards))]
-        for p, t in zip(paths, shards):
-            cache.put(p, t)  # Stage 1 (filesystem -> /dev/shm) is outside the timed region
-        del shards
+        paths = [f"/synthetic/rank{rank}/shard-{k:05d}.tar" for k in range(n_shards)]
+        for k, p in enumerate(paths):
+            cache.put(p, blobs[k % len(blobs)])  # Stage 1 (filesystem -> /dev/shm) is outside the timed region
+        del blobs
         if args.e2e_feed == "native":
-            feeder = NativeShardFeed(cache, paths, B, nthreads=args.gather_threads, slots=depth + 3)
+            # seeded per-epoch shard order + in-shard sample order (hpc_source.py:263, 461-467)
+            feeder = NativeShardFeed(cache, paths, B, nthreads=args.gather_threads, slots=depth + 3,
+                                     shuffle=True, seed=1234 + rank, rank=0, world=1)  # per-rank path set
         else:
             feeder = ShardBatchFeeder(cache, paths, B, nthreads=args.gather_threads)
         spec = DinoV2AugSpec(aug_cfg=cfg)
         pipe = backend.build_pipeline(feeder, spec, pcfg, None)
         it = backend.build_pipeline_iterator(pipe, spec, spec.output_map, B)
-        for _ in range(args.warmup):
+        for _ in range(warm):
             out = next(it)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         sampler = _GilSampler() if os.environ.get("DINO_GIL_SAMPLER") else None
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             out = next(it)
         torch.cuda.synchronize()
         if world > 1:
@@ -649,13 +649,15 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
         bad = {k: v for k, v in st["status"].items() if k != 0}
         if bad:
             raise RuntimeError(f"e2e decode failures: {bad}")
-        res = {"e2e_images_per_s": round(world * args.steps * B / dt, 1),
+        res = {"e2e_images_per_s": round(world * steps * B / dt, 1),
                "statuses_checked": int(st["images"]), "batches_accounted": int(st["batches"]),
-               "e2e_ms_per_step": round(dt / args.steps * 1e3, 3),
+               "e2e_ms_per_step": round(dt / steps * 1e3, 3),
+               "e2e_steps": steps, "e2e_warmup": warm, "e2e_set_batches": n_batches, "e2e_shards": n_shards,
+               "e2e_shuffle": args.e2e_feed == "native", "e2e_side_look_ahead": look,
                "e2e_shard_prepare_ms_total": round(getattr(feeder, "index_seconds", 0.0) * 1e3, 3),
                "e2e_shard_wait_ms_total": round(getattr(feeder, "wait_seconds", 0.0) * 1e3, 3),
                "e2e_gather_threads": args.gather_threads, "e2e_batches_in_flight": pipe.depth,
-               "e2e_host_ms_per_batch": {k: round(v * 1e3 / max(1, args.warmup + args.steps), 3)
+               "e2e_host_ms_per_batch": {k: round(v * 1e3 / max(1, warm + steps), 3)
                                          for k, v in pipe.host_seconds.items()},
                "e2e_prefetch_ahead": pipe.prefetch_ahead,
                "e2e_feed": args.e2e_feed,
@@ -793,6 +795,8 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--e2e", action="store_true", help="C5 end-to-end leg even with --no-extras or N > 1")
     ap.add_argument("--gpu-queue", type=int, default=6, help="PipelineConfig.gpu_queue of the e2e leg")
     ap.add_argument("--shard-size", type=int, default=1000, help="samples per synthetic tar shard (e2e)")
+    ap.add_argument("--e2e-steps", type=int, default=200, help="timed batches of the e2e leg (steady state)")
+    ap.add_argument("--e2e-warmup", type=int, default=16, help="untimed batches of the e2e leg (at least --warmup)")
     ap.add_argument("--gather-threads", type=int, default=8, help="copier threads of the e2e feed")
     ap.add_argument("--e2e-in-flight", type=int, default=3, help="MI355XBackend(max_in_flight) of the e2e leg")
     ap.add_argument("--e2e-feed", default="native", choices=["native", "python"],
@@ -866,6 +870,7 @@ def run_leg_child(args, leg: str) -> dict:
            "--prog-mix", str(args.prog_mix), "--gpu-queue", str(args.gpu_queue),
            "--progressive-frac", str(args.progressive_frac), "--restart-mcus", str(args.restart_mcus),
            "--shard-size", str(args.shard_size), "--gather-threads", str(args.gather_threads),
+           "--e2e-steps", str(args.e2e_steps), "--e2e-warmup", str(args.e2e_warmup),
            "--e2e-in-flight", str(args.e2e_in_flight), "--e2e-feed", args.e2e_feed]
     if args.mixed:
         cmd.append("--mixed")

@@ -68,6 +68,7 @@ def load() -> ctypes.CDLL:
         "dino_feed_set_cfg": (i32, [vp, ctypes.POINTER(DinoAugConfig)]),
         "dino_feed_set_shard_wait": (i32, [vp, i32]),
         "dino_feed_set_shuffle": (i32, [vp, i32, ctypes.c_uint64]),
+        "dino_feed_set_epoch": (i32, [vp, ctypes.c_uint64]),
         "dino_feed_next": (i32, [vp, i32, ctypes.POINTER(DinoFeedBatch)]),
         "dino_feed_copy": (i32, [vp, i32, vp, vp, vp]),
         "dino_feed_release": (i32, [vp, i32]),
@@ -125,6 +126,6 @@ def exported_symbols() -> list[str]:
             "dino_augment_need", "dino_decode_spans", "dino_run_batch_spans", "dino_probe_spans",
             "dino_host_register", "dino_host_unregister", "dino_copy_h2d", "dino_gather_probe",
             "dino_feed_create", "dino_feed_destroy", "dino_feed_push", "dino_feed_end_epoch", "dino_feed_set_cfg",
-            "dino_feed_set_shard_wait", "dino_feed_set_shuffle",
+            "dino_feed_set_shard_wait", "dino_feed_set_shuffle", "dino_feed_set_epoch",
             "dino_feed_next", "dino_feed_copy", "dino_feed_release", "dino_feed_reset", "dino_feed_stats",
             "dino_feed_last_error", "dino_stream_create", "dino_stream_destroy"]

@@ -6,7 +6,9 @@ Satisfies the structural ``BackendProtocol`` of reference
 runs Stage 3 on the GPU.  Method-by-method:
 
 * ``name`` / ``supports_fp8`` / ``supports_gpu``     protocol.py:22-29
-* ``build_shard_cache``   -> in-process LRU (Stage 1 stays host-side; cpu.py:86-145)
+* ``build_shard_cache``   -> :class:`tario.ShmShardCache`, the node-shared /dev/shm cache
+  the GPU peer builds (dali_backend.py:85-105 -> NodeSharedShardCache): the node master
+  loads shards, the other ranks wait for its writes; the native feed reads its files
 * ``build_pipeline``      -> :class:`MI355XAugPipeline` (dispatch as cpu.py:649-709):
   DinoV2 multi-crop, LeJEPA and Eval view recipes on the same kernels; UserAugSpec ->
   :class:`MI355XUserAugPipeline` (decode-only recipe, ``dino_resize_batch``, then aug_fn);
@@ -21,55 +23,16 @@ runs Stage 3 on the GPU.  Method-by-method:
 from __future__ import annotations
 
 import contextlib
-import threading
-from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Any
+from typing import TYPE_CHECKING, Any
 
 import torch
 
 from . import _lib
 from .pipeline import MI355XAugPipeline, MI355XPipelineIterator
 
-
-class InProcessShardCache:
-    """LRU of whole shard files in process memory (same contract as cpu.py:86-145)."""
-
-    def __init__(self, job_id: str = "mi355x", node_master: bool = True, max_gb: float = 1.0,
-                 prefetch_window: int = 4, timeout_s: float = 30.0, warn_threshold: float = 0.85) -> None:
-        self._max_bytes = int(max_gb * (1 << 30))
-        self._lru: OrderedDict[str, bytes] = OrderedDict()
-        self._total = 0
-        self._lock = threading.Lock()
-
-    def prefetch(self, shard_path: str) -> None:
-        """No-op (no async prefetch in-process)."""
-
-    def get(self, shard_path: str) -> bytes:
-        with self._lock:
-            if shard_path in self._lru:
-                self._lru.move_to_end(shard_path)
-                return self._lru[shard_path]
-        with open(shard_path, "rb") as f:
-            data = f.read()
-        with self._lock:
-            while self._lru and self._total + len(data) > self._max_bytes:
-                _, old = self._lru.popitem(last=False)
-                self._total -= len(old)
-            self._lru[shard_path] = data
-            self._total += len(data)
-        return data
-
-    @contextlib.contextmanager
-    def get_view(self, shard_path: str):
-        yield memoryview(self.get(shard_path))
-
-    @property
-    def utilisation(self) -> float:
-        if self._max_bytes == 0:
-            return 0.0
-        with self._lock:
-            return self._total / self._max_bytes
+if TYPE_CHECKING:
+    from .tario import ShmShardCache
 
 
 class DeviceH2DStream:
@@ -172,6 +135,7 @@ class MI355XBackend:
     # 16 -> 84.8k img/s, 48 -> 92.2-94.9k; profiles/r04_side_ahead.jsonl): a side decode pool
     # takes ~45 ms, about 13 batch launches, so the look-ahead must cover several of them
     SIDE_AHEAD = 48
+    PREFETCH = 1  # host-half batches prepared ahead by the pipeline's prefetch thread
 
     def side_look_ahead(self, pipeline_cfg: Any, source: Any, depth: int) -> int:
         """Batches the side route pulls ahead of their launch (DALI's CPU prefetch queue plays
@@ -186,7 +150,10 @@ class MI355XBackend:
         mq = getattr(source, "_meta_queue", None)
         cap = getattr(mq, "maxsize", 0) or 0
         if cap > 0:
-            want = min(want, cap - depth - 6)  # 4 in the prefetch queue, 1 being prepared, 1 spare
+            # the largest look-ahead whose worst case (MI355XAugPipeline.pulled_bound) leaves one
+            # FIFO entry spare
+            while want > 1 and MI355XAugPipeline.pulled_bound(depth, self.PREFETCH, want) + 1 > cap:
+                want -= 1
         return max(1, int(want))
 
     def queue_depth(self, pipeline_cfg: Any, batch_size: int, n_views: int = 10, max_crop: int = 224) -> int:
@@ -217,8 +184,17 @@ class MI355XBackend:
 
     def build_shard_cache(self, job_id: str = "mi355x", node_master: bool = True, max_gb: float = 1.0,
                           prefetch_window: int = 4, timeout_s: float = 30.0, warn_threshold: float = 0.85,
-                          **kwargs: Any) -> InProcessShardCache:
-        return InProcessShardCache(job_id, node_master, max_gb, prefetch_window, timeout_s, warn_threshold)
+                          **kwargs: Any) -> "ShmShardCache":
+        """The node-local /dev/shm shard cache (reference DALIBackend.build_shard_cache,
+        dali_backend.py:85-105): ``/dev/shm/<job_id>/<sha1(path)[:16]>`` files in the reference's
+        format, written by the node master (``node_master``: local rank 0, loader.py:467) and
+        waited for by the other ranks for up to ``timeout_s`` seconds; ``max_gb`` budget with LRU
+        eviction; ``prefetch_window`` concurrent background loads; a warning past
+        ``warn_threshold`` of the budget.  ``base_dir`` (keyword, default /dev/shm) relocates it."""
+        from .tario import ShmShardCache
+        return ShmShardCache(job_id=job_id, node_master=node_master, max_gb=max_gb,
+                             base_dir=kwargs.get("base_dir", "/dev/shm"), shard_timeout_s=timeout_s,
+                             prefetch_window=prefetch_window, warn_threshold=warn_threshold)
 
     def build_pipeline(self, source: Any, aug_spec: Any, pipeline_cfg: Any, specs: Any = None) -> MI355XAugPipeline:
         """Dispatch as CPUBackend.build_pipeline (cpu.py:649-709): DinoV2 multi-crop, LeJEPA
@@ -273,7 +249,7 @@ class MI355XBackend:
             norm=norm,
             view_names=names,
             depth=depth,
-            prefetch=1,
+            prefetch=self.PREFETCH,
             host_workers=self._host_workers,
             start_host_pool=True,
             multiscan_route=self._multiscan_route,

@@ -6,9 +6,13 @@
 // _ReaderAdapter.__call__ (shard_reader.py:346-376) hand Stage 3 a Python list of JPEG
 // arrays per batch; here a batch never becomes Python objects:
 //
-//   opener thread   mmap a shard-cache file ([data_len:u64][magic:u64] + tar, reference
+//   opener threads  mmap a shard-cache file ([data_len:u64][magic:u64] + tar, reference
 //                   shard_cache.py:83-85, 584-609), fault its pages in, index the tar
-//                   (dino_tar_index), up to `lookahead` shards ahead of the packer;
+//                   (dino_tar_index), up to `lookahead` shards ahead of the packer; one
+//                   thread per shard of the look-ahead (at most kMaxOpeners), so that two
+//                   shards' page population overlaps (measured at 8 ranks per node: the
+//                   single opener held a feed to 0.82-0.9x the device rate);
+//                   the shards reach the packer in push order whatever order they finish in;
 //   packer thread   takes the next B samples (a batch may straddle shards; the last partial
 //                   batch of an epoch is dropped, dali_backend.py:187), packs them into a
 //                   pinned slot with `nthreads` copier threads and probes each image right
@@ -37,6 +41,7 @@
 #include <condition_variable>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -59,6 +64,7 @@ int feed_fail(int code, const std::string& msg) {
 }
 
 constexpr uint64_t kShardMagic = 0xDEADBEEFCAFEF00Dull;
+constexpr int kMaxOpeners = 4;
 #ifndef MADV_POPULATE_READ
 #define MADV_POPULATE_READ 22
 #endif
@@ -315,14 +321,17 @@ struct dino_feed {
   int32_t wait_ms = 0;                 // > 0: wait that long for a shard the node master has not written yet
   bool shuffle = false;                // seeded in-shard sample order
   uint64_t shuffle_seed = 0;
-  uint64_t epoch = 0;                  // epochs since create (the shuffle key)
+  uint64_t epoch = 0;                  // the shuffle key: epochs since create, or dino_feed_set_epoch's
   std::unique_ptr<CopyPool> pool;
   std::vector<Slot> slots;
   std::mutex m;
   std::condition_variable cv;          // any state change
   std::deque<std::string> pending;     // paths pushed, not yet opened
   std::deque<std::shared_ptr<Shard>> opened;  // opened shards, in order (front: being consumed)
-  int opening = 0;                     // shards the opener is working on
+  int opening = 0;                     // shards the openers are working on
+  int64_t open_next = 0;               // push-order ticket of the next shard an opener takes
+  int64_t open_done = 0;               // ticket of the next shard to append to `opened`
+  std::map<int64_t, std::shared_ptr<Shard>> parked;  // finished out of order (null: failed)
   bool epoch_end = false;              // no more pushes this epoch
   bool epoch_done = false;             // the packer found fewer than B samples left after epoch_end
   bool stop = false;
@@ -331,7 +340,8 @@ struct dino_feed {
   std::string error;                   // first shard error of the epoch (reported once by next)
   int64_t shards_failed = 0, shards_done = 0, batches = 0;
   double t_open = 0, t_pack = 0, t_slot_wait = 0, t_sample_wait = 0;
-  std::thread opener, packer;
+  std::vector<std::thread> openers;
+  std::thread packer;
 
   void opener_loop();
   void packer_loop();
@@ -341,12 +351,15 @@ struct dino_feed {
 void dino_feed::opener_loop() {
   std::unique_lock<std::mutex> lk(m);
   for (;;) {
-    cv.wait(lk, [&] { return stop || (!pending.empty() && (int)opened.size() + opening < lookahead + 1); });
+    cv.wait(lk, [&] {
+      return stop || (!pending.empty() && (int)(opened.size() + parked.size()) + opening < lookahead + 1);
+    });
     if (stop) return;
     auto sh = std::make_shared<Shard>();
     sh->path = pending.front();
     pending.pop_front();
     ++opening;
+    const int64_t ticket = open_next++;
     const int64_t gen = generation;
     const int32_t wait = wait_ms;
     const bool shuf = shuffle;
@@ -369,8 +382,14 @@ void dino_feed::opener_loop() {
       if (!err.empty()) {  // reference hpc_source.py:358-366: a shard I/O error is logged and skipped
         ++shards_failed;
         if (error.empty()) error = err;
-      } else {
-        opened.push_back(std::move(sh));
+        sh.reset();
+      }
+      parked.emplace(ticket, std::move(sh));
+      // hand the shards on in push order
+      for (auto it = parked.find(open_done); it != parked.end(); it = parked.find(open_done)) {
+        if (it->second) opened.push_back(std::move(it->second));
+        parked.erase(it);
+        ++open_done;
       }
     }
     cv.notify_all();
@@ -527,7 +546,7 @@ int dino_feed_create(int32_t batch, int32_t nthreads, int32_t nslots, int32_t lo
     }
   }
   dino_feed* p = f.release();
-  p->opener = std::thread([p] { p->opener_loop(); });
+  for (int k = 0; k < std::min(p->lookahead, kMaxOpeners); ++k) p->openers.emplace_back([p] { p->opener_loop(); });
   p->packer = std::thread([p] { p->packer_loop(); });
   *out = p;
   return DINO_OK;
@@ -540,7 +559,8 @@ int dino_feed_destroy(dino_feed* f) {
     f->stop = true;
   }
   f->cv.notify_all();
-  if (f->opener.joinable()) f->opener.join();
+  for (auto& t : f->openers)
+    if (t.joinable()) t.join();
   if (f->packer.joinable()) f->packer.join();
   for (auto& s : f->slots) {  // copies still reading a slot finish first
     if (s.state == kCopying) (void)hipEventSynchronize(s.ev);
@@ -593,6 +613,13 @@ int dino_feed_set_shuffle(dino_feed* f, int32_t enable, uint64_t seed) {
   std::lock_guard<std::mutex> g(f->m);
   f->shuffle = enable != 0;
   f->shuffle_seed = seed;
+  return DINO_OK;
+}
+
+int dino_feed_set_epoch(dino_feed* f, uint64_t epoch) {
+  if (!f) return feed_fail(DINO_EINVAL, "dino_feed_set_epoch: null feed");
+  std::lock_guard<std::mutex> g(f->m);
+  f->epoch = epoch;
   return DINO_OK;
 }
 
@@ -679,6 +706,8 @@ int dino_feed_reset(dino_feed* f) {
     ++f->epoch;
     f->pending.clear();
     f->opened.clear();
+    f->parked.clear();
+    f->open_done = f->open_next;  // shards still being opened belong to the old generation
     f->epoch_end = f->epoch_done = false;
     f->error.clear();
     for (auto& s : f->slots)

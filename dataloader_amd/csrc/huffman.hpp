@@ -150,10 +150,7 @@ DHD uint32_t br_peek32(const BitReader& br, uint32_t pos) {
 // kPrefetchWords refills (~32 bits each) after it is issued: the speculative decode
 // kernels keep one stream line per lane live, ~L2-sized in all, so a refill often comes
 // from the Infinity Cache or HBM rather than L2.
-#ifndef DINO_HUFF_PREFETCH
-#define DINO_HUFF_PREFETCH 1
-#endif
-constexpr int kPrefetchWords = DINO_HUFF_PREFETCH;
+constexpr int kPrefetchWords = 1;
 struct BitCursor {
   uint64_t buf;        // next bits, MSB first
   int32_t nbits;       // valid bits in buf
@@ -419,16 +416,10 @@ DHD void skip_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int
 // Lane-level routines of the self-synchronising parallel decode (k_huffman).
 // ---------------------------------------------------------------------------
 
-#ifndef DINO_HUFF_SKIP
-#define DINO_HUFF_SKIP 1
-#endif
-// The step of the state-only decodes (skip_step; huff_step in A/B builds).
+// The step of the state-only decodes (skip_step; huff_step there measured slower).
 template <int kWin>
 DHD void state_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
-  if (DINO_HUFF_SKIP)
-    skip_step<kWin>(cur, br, im, blk, z);
-  else
-    huff_step<kWin>(cur, br, im, blk, z);
+  skip_step<kWin>(cur, br, im, blk, z);
 }
 
 // A guessed start state for the range starting at bit `to`: decode state-only from an
@@ -451,18 +442,9 @@ struct RangeOut {
   int32_t nblk;    // blocks whose DC step starts in the range
 };
 
-#ifndef DINO_HUFF_CHECKPOINTS
-#define DINO_HUFF_CHECKPOINTS 16
-#endif
-constexpr int kHuffCheckpoints = DINO_HUFF_CHECKPOINTS;  // block boundaries recorded per lane by the first decode
-#ifndef DINO_HUFF_CP_DENSE
-#define DINO_HUFF_CP_DENSE 4
-#endif
-#ifndef DINO_HUFF_CP_STRIDE
-#define DINO_HUFF_CP_STRIDE 8
-#endif
-constexpr int kHuffCpDense = DINO_HUFF_CP_DENSE;    // leading blocks that all get a checkpoint
-constexpr int kHuffCpStride = DINO_HUFF_CP_STRIDE;  // then every kHuffCpStride-th block (power of 2)
+constexpr int kHuffCheckpoints = 16;  // block boundaries recorded per lane by the first decode
+constexpr int kHuffCpDense = 4;    // leading blocks that all get a checkpoint
+constexpr int kHuffCpStride = 8;  // then every kHuffCpStride-th block (power of 2)
 
 // A block boundary (state before a DC step) seen by a lane's first decode:
 // bit position, block-in-MCU index c and the blocks started before it.

@@ -33,38 +33,21 @@
 
 namespace dino {
 
-// XCD-aware workgroup coordinates.  The dispatcher deals a launch's workgroups round-robin
-// over the 8 XCDs (ids equal mod 8 share an XCD and its 4 MiB L2); renumbered, each XCD owns
-// a contiguous range of the grid in (z, y, x) order, i.e. whole images, so the workgroups
-// that read one image's planes / RGB / crop rows share one L2 (cdna guide §5.5 T1, the
-// bijective form for grids not divisible by 8).  Speed only: no result depends on placement.
-#ifndef DINO_XCD_REMAP
-#define DINO_XCD_REMAP 0
-#endif
-constexpr uint32_t kXcds = 8;
+// Workgroup coordinates of a (x, y = image, z) grid.  (An XCD-aware renumbering, each XCD
+// owning whole images so that one image's workgroups share one L2, was measured and dropped:
+// the per-image kernels' working sets are small against the 4 MiB L2s.)
 struct BlkIdx {
   int x, y, z;
 };
 // Issue priority of the batch kernels' waves (s_setprio): above the progressive side
 // decode's scan waves (k_pscan keeps the default 0), so that a SIMD running both issues the
-// batch's instruction first when both are ready (A/B: DINO_MAIN_PRIO).
-#ifndef DINO_MAIN_PRIO
-#define DINO_MAIN_PRIO 3
-#endif
-__device__ __forceinline__ void main_prio() {
-  if (DINO_MAIN_PRIO > 0) __builtin_amdgcn_s_setprio(DINO_MAIN_PRIO);
-}
+// batch's instruction first when both are ready (measured: side route 95.6k -> 97.3k img/s).
+__device__ __forceinline__ void main_prio() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ BlkIdx xcd_blk() {
   main_prio();
   const uint32_t X = gridDim.x, Y = gridDim.y, Z = gridDim.z;
   uint32_t L = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
-  if (DINO_XCD_REMAP) {
-    const uint32_t n = X * Y * Z;
-    if (n > kXcds) {
-      const uint32_t q = n / kXcds, r = n % kXcds, xcd = L % kXcds;
-      L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + L / kXcds;
-    }
-  }
+  (void)Z;
   BlkIdx b;
   b.x = (int)(L % X);
   L /= X;
@@ -579,27 +562,13 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
   return nbits <= kHuffSegBits ? 1 : (int)((nbits + kHuffSegBits - 1) / kHuffSegBits);
 }
 
-#ifndef DINO_SINK_LDS
-#define DINO_SINK_LDS 8
-#endif
-// Entry words a lane buffers in LDS before it stores them as one aligned group (0: SparseSink's
-// register shift register; 8 / 16: 32 / 64-byte groups, no VGPRs for the buffer).
+// Entry words a lane buffers in LDS before it stores them as one aligned group: 32-byte
+// groups in k_huff1 (its buffers borrow the skip tables' LDS), 64-byte groups in k_huff3.
 // Word w of lane t sits at [w][t], so the lanes' halfword writes never share a bank.
-constexpr int kSinkLds = DINO_SINK_LDS;
-#ifndef DINO_SINK_RECS
-#define DINO_SINK_RECS 0
-#endif
-// Block records a lane buffers in LDS (after its entry words) and stores as one aligned
-// 8 x kSinkRecs-byte group when the group is complete (0: each record stored alone).
-constexpr int kSinkRecs = DINO_SINK_RECS;
-static_assert(kSinkRecs == 0 || (kSinkLds > 0 && (kSinkRecs == 2 || kSinkRecs == 4)), "record groups");
-constexpr int kSinkWords = kSinkLds + 2 * kSinkRecs;  // LDS words per lane
-#ifndef DINO_SINK_LDS3
-#define DINO_SINK_LDS3 16
-#endif
-// k_huff3's entry buffer (its own LDS, not k_huff1's borrowed skip tables)
-constexpr int kSinkLds3 = DINO_SINK_LDS3;
-constexpr int kSinkWords3 = kSinkLds3 + 2 * kSinkRecs;
+// (Measured and dropped, DESIGN.md §5: a register shift register instead of LDS, block
+// records buffered and stored in pairs or groups, 64-byte groups in k_huff1.)
+constexpr int kSinkLds = 8;
+constexpr int kSinkLds3 = 16;
 
 struct HuffLds {     // k_huff1
   ImgDesc sd;
@@ -612,7 +581,7 @@ struct HuffLds {     // k_huff1
 // buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
 // (and the range results R, which follow the tables and are read before the write pass)
 static_assert(offsetof(HuffLds, R) == offsetof(HuffLds, tab) + sizeof(HuffTables), "R follows the tables");
-static_assert(sizeof(HuffSkip) + sizeof(RangeOut) * kHuffThreads >= (size_t)kSinkWords * 4 * kHuffThreads,
+static_assert(sizeof(HuffSkip) + sizeof(RangeOut) * kHuffThreads >= (size_t)kSinkLds * 4 * kHuffThreads,
               "sink buffers fit the skip tables and R");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
@@ -621,7 +590,7 @@ struct HuffLds3 {    // k_huff3 (no lane exchange)
   ImgDesc sd;
   alignas(16) uint8_t tab[kHuffTabBytesNoSkip];  // a HuffTables without its skip member
   int32_t img, item;
-  uint32_t sink[(kSinkWords3 ? kSinkWords3 : 1) * kHuffThreads];  // SparseSink buffers (kSinkLds3, kSinkRecs)
+  uint32_t sink[kSinkLds3 * kHuffThreads];  // SparseSink buffers
 };
 
 static_assert(sizeof(ImgDesc) % 16 == 8 || sizeof(ImgDesc) % 16 == 0, "ImgDesc layout");
@@ -634,60 +603,30 @@ constexpr uint32_t kBinfoAbsDc = 1u << 15;
 // Sparse coefficient output.  A lane appends its blocks' non-zero AC coefficients
 // to a private region of the image's entry area that starts at 128 halfwords per
 // block before its first block (a block needs at most 127, so regions never
-// overlap), buffered eight halfwords at a time into 16-byte stores so that each lane
-// writes whole contiguous lines instead of scattered 2-byte coefficients into a
-// dense block.  A coefficient takes one halfword, zigzag index | (int10 value << 6),
+// overlap), buffered in LDS (W words per lane) and stored as aligned W-word groups, so
+// that each lane writes whole contiguous lines instead of scattered 2-byte coefficients
+// into a dense block.  A coefficient takes one halfword, zigzag index | (int10 value << 6),
 // while its value fits 10 bits; from the block's first coefficient that does not,
 // the rest of the block is written as u32 entries (zigzag | int16 value << 16) at the
 // next even halfword.  binfo[b] = {first halfword, n16 | n32 << 7 | (int16 DC << 16)}:
 // one 8-byte record per block carries the DC too (a difference until k_dcscan sums
 // it in place; absolute with restart intervals).  k_idct scatters the entries into
 // its LDS block.
-#ifndef DINO_SINK_CHUNKS
-#define DINO_SINK_CHUNKS 2
-#endif
-#ifndef DINO_SINK_PAIRS
-#define DINO_SINK_PAIRS 0
-#endif
-constexpr int kSinkChunks = DINO_SINK_CHUNKS;  // 16-byte entry chunks a lane stores together (1, 2, 4)
-constexpr bool kSinkPairs = DINO_SINK_PAIRS;   // block records stored as aligned 16-byte pairs
-template <int W>  // entry words buffered per lane in LDS (W: k_huff1, W3: k_huff3)
+template <int W>  // entry words buffered per lane in LDS
 struct SparseSinkT {
+  static_assert(W % 4 == 0 && W > 0, "whole 16-byte chunks");
   uint32_t* ent;   // image entry area
   uint2* binfo;    // image block info
-  uint32_t n;      // halfwords in whole chunks (relative to the image entry area), multiple of 8
-  uint32_t k;      // halfwords buffered in w0..w3
-  uint32_t w0, w1, w2, w3;
-  uint4 pend[kSinkChunks > 1 ? kSinkChunks - 1 : 1];  // whole chunks not stored yet (kc of them)
-  uint32_t kc;
-  uint2 prec;      // record of the even block pb of an open pair (kSinkPairs)
-  int32_t pb;
-  bool hrec;
+  uint32_t n;      // halfwords in stored groups (relative to the image entry area), multiple of 2 W
+  uint32_t k;      // halfwords buffered in LDS
   uint32_t bstart, dcw, n16, n32;
   bool wide;       // the open block has switched to u32 entries
   int32_t b;
-  uint32_t* lb;    // W: this lane's buffer column in LDS (word w at lb[w * kHuffThreads])
-  uint32_t rmask;  // kSinkRecs: buffered records of blocks rbase + j (bit j)
-  int32_t rbase;
-  __device__ void rec_flush() {
-    if (!rmask) return;
-    uint32_t* rw = lb + W * kHuffThreads;
-    if (rmask == (1u << kSinkRecs) - 1) {
-      uint4* dst = (uint4*)(binfo + rbase);
-#pragma unroll
-      for (int q = 0; q < (kSinkRecs ? kSinkRecs : 2) / 2; ++q)
-        dst[q] = make_uint4(rw[(4 * q) * kHuffThreads], rw[(4 * q + 1) * kHuffThreads], rw[(4 * q + 2) * kHuffThreads],
-                            rw[(4 * q + 3) * kHuffThreads]);
-    } else {
-      for (int j = 0; j < kSinkRecs; ++j)
-        if ((rmask >> j) & 1u) binfo[rbase + j] = make_uint2(rw[(2 * j) * kHuffThreads], rw[(2 * j + 1) * kHuffThreads]);
-    }
-    rmask = 0;
-  }
+  uint32_t* lb;    // this lane's buffer column in LDS (word w at lb[w * kHuffThreads])
   __device__ void lds_flush(uint32_t words) {  // the buffer's first `words` words -> entries at n
     uint4* dst = (uint4*)(ent + (n >> 1));
 #pragma unroll
-    for (int q = 0; q < (W ? W : 4) / 4; ++q)
+    for (int q = 0; q < W / 4; ++q)
       if ((uint32_t)(4 * q) < words)
         dst[q] = make_uint4(lb[(4 * q) * kHuffThreads], lb[(4 * q + 1) * kHuffThreads], lb[(4 * q + 2) * kHuffThreads],
                             lb[(4 * q + 3) * kHuffThreads]);
@@ -695,9 +634,6 @@ struct SparseSinkT {
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
-    kc = 0;
-    hrec = false;
-    rmask = 0;
   }
   __device__ void begin(int32_t blk) {
     b = blk;
@@ -706,48 +642,12 @@ struct SparseSinkT {
     n16 = n32 = 0;
     wide = false;
   }
-  // w0..w3 are a shift register of halfwords: a new one enters at the top and the
-  // eighth push has moved the first to the bottom (four v_alignbyte per push)
-  __device__ void shift_in(uint32_t h) {
-    w0 = __builtin_amdgcn_alignbyte(w1, w0, 2);
-    w1 = __builtin_amdgcn_alignbyte(w2, w1, 2);
-    w2 = __builtin_amdgcn_alignbyte(w3, w2, 2);
-    w3 = __builtin_amdgcn_alignbyte(h, w3, 2);
-  }
-  // a lane's region starts 256-byte aligned, so a group of kSinkChunks chunks is aligned too
-  __device__ void chunk_done() {
-    const uint4 w = make_uint4(w0, w1, w2, w3);
-    if (kSinkChunks == 1) {
-#ifndef DINO_DIAG_NOENT  // traffic diagnosis builds only: entries not stored (output invalid)
-      *(uint4*)(ent + (n >> 1)) = w;
-#endif
-    } else if (kc == kSinkChunks - 1) {
-      uint4* dst = (uint4*)(ent + ((n - 8 * kc) >> 1));
-#pragma unroll
-      for (int j = 0; j < kSinkChunks - 1; ++j) dst[j] = pend[j];
-      dst[kSinkChunks - 1] = w;
-      kc = 0;
-    } else {
-#pragma unroll
-      for (int j = 0; j < kSinkChunks - 1; ++j)
-        if (j == (int)kc) pend[j] = w;
-      ++kc;
-    }
-  }
+  // a lane's region starts 256-byte aligned, so a group of W words is aligned too
   __device__ void put(uint32_t h) {
-    if (W) {
-      ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[k & 1] = (uint16_t)h;
-      if (++k == 2 * W) {
-        lds_flush(W);
-        n += 2 * W;
-        k = 0;
-      }
-      return;
-    }
-    shift_in(h);
-    if (++k == 8) {
-      chunk_done();
-      n += 8;
+    ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[k & 1] = (uint16_t)h;
+    if (++k == 2 * W) {
+      lds_flush(W);
+      n += 2 * W;
       k = 0;
     }
   }
@@ -767,58 +667,17 @@ struct SparseSinkT {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void record(int32_t blk, uint2 r) {
-    if (kSinkRecs) {
-      const int32_t g = blk & ~(kSinkRecs - 1);
-      if (rmask && g != rbase) rec_flush();
-      rbase = g;
-      const int j = blk - g;
-      uint32_t* rw = lb + W * kHuffThreads;
-      rw[(2 * j) * kHuffThreads] = r.x;
-      rw[(2 * j + 1) * kHuffThreads] = r.y;
-      rmask |= 1u << j;
-      if (rmask == (1u << kSinkRecs) - 1) rec_flush();
-      return;
-    }
-    if (!kSinkPairs) {
-      binfo[blk] = r;
-    } else if (blk & 1) {  // odd block: completes the pair opened by blk - 1 (if this lane opened it)
-      if (hrec) *(uint4*)(binfo + blk - 1) = make_uint4(prec.x, prec.y, r.x, r.y);
-      else binfo[blk] = r;
-      hrec = false;
-    } else {
-      prec = r;
-      pb = blk;
-      hrec = true;
-    }
-  }
+  __device__ void record(int32_t blk, uint2 r) { binfo[blk] = r; }
   __device__ void end() { record(b, make_uint2(bstart, n16 | (n32 << 7) | dcw)); }
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
-  __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-word tail store stays inside it
-    if (W) {
-      if (k) {
-        if (k & 1) ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[1] = 0;
-        const uint32_t used = (k + 1) >> 1, words = (used + 3) & ~3u;
-        for (uint32_t w = used; w < words; ++w) lb[w * kHuffThreads] = 0u;
-        lds_flush(words);
-      }
-      if (kSinkPairs && hrec) binfo[pb] = prec;
-      if (kSinkRecs) rec_flush();
-      return;
+  __device__ void close() {  // the region is a multiple of 8 halfwords: a whole-chunk tail store stays inside it
+    if (k) {
+      if (k & 1) ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[1] = 0;
+      const uint32_t used = (k + 1) >> 1, words = (used + 3) & ~3u;
+      for (uint32_t w = used; w < words; ++w) lb[w * kHuffThreads] = 0u;
+      lds_flush(words);
     }
-    if (k)
-      for (uint32_t j = k; j < 8; ++j) shift_in(0u);
-    if (kSinkChunks > 1) {
-      uint4* dst = (uint4*)(ent + ((n - 8 * kc) >> 1));
-#pragma unroll
-      for (int j = 0; j < kSinkChunks - 1; ++j)
-        if (j < (int)kc) dst[j] = pend[j];
-      if (k) dst[kc] = make_uint4(w0, w1, w2, w3);
-    } else if (k) {
-      *(uint4*)(ent + (n >> 1)) = make_uint4(w0, w1, w2, w3);
-    }
-    if (kSinkPairs && hrec) binfo[pb] = prec;  // a lone even block (the lane's last record)
   }
 };
 using SparseSink = SparseSinkT<kSinkLds>;
@@ -957,11 +816,8 @@ __device__ int huff_item_image(const ImgDesc* desc, int B, int item) {
 // decoded completely by k_huff1 (its lanes' start states are final after the
 // in-segment rounds).  Long ranges stay with k_huff3: in k_huff1 their second
 // decode would double the longest serial chain of the launch.
-#ifndef DINO_HUFF_FUSE_SUB_BITS
-#define DINO_HUFF_FUSE_SUB_BITS 3072
-#endif
 __device__ __forceinline__ bool huff_single_segment(const ImgDesc& d) {
-  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= DINO_HUFF_FUSE_SUB_BITS;
+  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= 3072;
 }
 
 // Loads work item `item`'s image descriptor and tables into LDS; false past the end.
@@ -1001,10 +857,7 @@ __device__ uint64_t g_huff_phase[kPhaseItems][5];
   } while (0)
 #endif
 
-#ifndef DINO_HUFF_LOOKBACK
-#define DINO_HUFF_LOOKBACK 2048
-#endif
-constexpr int kHuffLookback = DINO_HUFF_LOOKBACK;  // bits a lane decodes before its range to guess its start state
+constexpr int kHuffLookback = 2048;  // bits a lane decodes before its range to guess its start state
 
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
@@ -1248,36 +1101,6 @@ struct WaveMarkerFinder {
   }
 };
 
-// Lane-mode AC refinement (k_prefine): the AC refinement scans of a component leave k_pscan
-// (which only destuffs them) for k_prefine, one lane per (image, component), when every
-// refinement scan of the component is a single-component scan without restart intervals
-// and no scan other than a refinement follows one it overlaps (nothing k_pscan decodes
-// reads their coefficients).  The components that may go to lane mode (bit c) come from the
-// environment (DINO_PREFINE_COMPS, read per ctx; default 0: none).  Measured and not the
-// default (profiles/r04_prefine_*): a lane decodes a scan ~3.5x slower than a scan wave
-// (its serial chain is a divergent VALU chain with LDS lookups, ~2 900 cycles per symbol
-// against ~840), so lane mode cuts the side decode's issue slots to ~1/64 of a wave per scan
-// but a 64-image pool takes 225 ms (all components) or 43 ms (chroma only) instead of 31 ms,
-// and the side route measured 36k / 96k img/s against 101k in wave mode.
-__device__ __forceinline__ bool scan_is_ac_refine(const ScanRec& a, bool prog) { return prog && a.ss > 0 && a.ah > 0; }
-__device__ int prog_lane_refine(const ScanRec* scans, int n, bool prog) {
-  if (!prog) return 0;
-  int mask = 0, bad = 0;
-  for (int i = 0; i < n; ++i) {
-    if (!scan_is_ac_refine(scans[i], prog)) continue;
-    const int c = scans[i].comp[0] & 3;
-    mask |= 1 << c;
-    if (scans[i].ns != 1 || scans[i].restart_interval != 0) bad |= 1 << c;
-    for (int j = i + 1; j < n; ++j)
-      if (!scan_is_ac_refine(scans[j], prog) && scans_overlap(scans[i], scans[j])) bad |= 1 << c;
-  }
-  return mask & ~bad;
-}
-// The scan goes to k_prefine (the component bit of PHdr::pad[0]).
-__device__ __forceinline__ bool scan_lane_refine(int lanemask, const ScanRec& a, bool prog) {
-  return scan_is_ac_refine(a, prog) && ((lanemask >> (a.comp[0] & 3)) & 1);
-}
-
 constexpr int kPWalkThreads = 256;
 struct PWalkLds {
   ImgDesc d;
@@ -1293,7 +1116,7 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
                                                          const int64_t* __restrict__ offsets,
                                                          const int64_t* __restrict__ lengths,
                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
-                                                         PCtl* __restrict__ pctl, int prefine) {
+                                                         PCtl* __restrict__ pctl) {
   __shared__ PWalkLds L;
   const int img = blockIdx.x, t = threadIdx.x;
   if (desc[img].status != DINO_IMG_OK || desc[img].kind != 1) return;
@@ -1352,7 +1175,7 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
   if (t == 0) {
     hd->n_scans = n;
     hd->n_levels = nlev;
-    hd->pad[0] = prog_lane_refine(L.scans, n, dl.progressive != 0) & prefine;
+    hd->pad[0] = 0;
   }
   // libjpeg's zeroed coefficient arrays
   {
@@ -1838,17 +1661,14 @@ __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, con
 }
 
 // Scan waves per workgroup: each wave takes its own tickets; the waves of one workgroup
-// sit on different SIMDs of the CU (DINO_PSCAN_WAVES, measured in profiles/r03_prog_*).
-#ifndef DINO_PSCAN_WAVES
-#define DINO_PSCAN_WAVES 4
-#endif
-constexpr int kPScanThreads = 64 * DINO_PSCAN_WAVES;
+// sit on different SIMDs of the CU (4, measured in profiles/r03_prog_*).
+constexpr int kPScanThreads = 64 * 4;
 __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restrict__ bytes,
                                                          const int64_t* __restrict__ offsets,
                                                          const int64_t* __restrict__ lengths,
                                                          const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
                                                          PCtl* __restrict__ pctl) {
-  __shared__ int16_t s_stage[DINO_PSCAN_WAVES][16 * 64];
+  __shared__ int16_t s_stage[4][16 * 64];
   const int lane = threadIdx.x & 63;
   const DINO_CONST PCtl* cc = (const DINO_CONST PCtl*)pctl;
   const uint32_t nprog = cc->nprog;
@@ -1876,17 +1696,6 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
     tb.load((const PTab*)(region + kPTabOff), ps->tslots, lane);
     uint32_t* clean = (uint32_t*)(ws + d->ent_off + ((sr.data_off - d->scan_off + 3) & ~3));
     const uint32_t dlen = sr.restart_interval == 0 ? wave_destuff(p, len, sr.data_off, (uint8_t*)clean, lane) : 0u;
-    if (scan_lane_refine(hd->pad[0], sr, d->progressive != 0)) {
-      // decoded by k_prefine (lane mode): its destuffed length for the lane's reader, and its
-      // completion for the level count (no scan k_pscan decodes depends on it)
-      if (lane == 0) ((PScan*)(region + kPScanOff) + j)->pad = (int32_t)dlen;
-      __threadfence();
-      if (lane == 0) {
-        __hip_atomic_store(&((PHdr*)region)->prog[j], 0x7FFFFFFF, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(&((PHdr*)region)->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      continue;
-    }
     const bool pipe = ps->pipe != 0;
     if (sr.level > 0 && !pipe) {  // the previous level's scans of this image (earlier tickets, running or done)
       int32_t* dn = &((PHdr*)region)->done[sr.level - 1];
@@ -1938,210 +1747,6 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
 #endif
     __threadfence();  // this scan's coefficient stores before its completion count
     if (lane == 0) __hip_atomic_fetch_add(&((PHdr*)region)->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_prefine: the AC refinement scans of the images k_pwalk marked (prog_lane_refine), one
-// lane per (image, component): the lane decodes the component's refinement scans in scan
-// order over the component's blocks (decode_mcu_AC_refine, r_refine_block), its own stream
-// and its own table, with no other lane of the wave involved.  A wave thus advances 64
-// scans per instruction instead of one (k_pscan runs one scan per wave, its serial chain on
-// the scalar unit): a refinement scan costs ~1/64 of a wave's issue slots, so the side
-// decode leaves the batch kernels their issue slots, at the price of a longer latency per
-// scan (the side look-ahead covers it).
-//   per lane: the scan's 9-bit lookahead (1 KiB) and the block being refined (128 B) in
-//   LDS; the block's coefficients loaded one block ahead (8 x 16 B), its zigzag non-zero
-//   mask from those registers; changed coefficients stored one by one.
-// ---------------------------------------------------------------------------
-constexpr int kPrefineLds = 64 * (1024 + 64 + 256) + 64 * 128 + 80;
-
-// Per-lane bit reader over a destuffed scan (4-byte aligned, zero padded to a dword; bits
-// past the data read as zeros, libjpeg's fill): a 64-bit window kept >= 33 bits full from a
-// staged 16-byte chunk, the next chunk's load in flight a whole chunk ahead (on gfx9 a load's
-// wait also waits for every store issued before it: the refinement stores blocks, so a
-// refill loaded just before its use would wait for those stores).
-struct LaneClean {
-  const uint32_t* src;
-  uint32_t nw, nbits, pos, next;  // nw: dwords holding data; next: index of the chunk in flight
-  uint64_t buf;
-  int32_t nb, cw;                  // valid window bits; words of `cur` not yet consumed
-  uint4 cur, fly;
-  __device__ __forceinline__ uint4 ldq(uint32_t q) const {  // chunk q: 4 dword loads, clamped
-    const uint32_t w = 4u * q;
-    return make_uint4(src[w < nw ? w : 0u], src[w + 1 < nw ? w + 1 : 0u], src[w + 2 < nw ? w + 2 : 0u],
-                      src[w + 3 < nw ? w + 3 : 0u]);
-  }
-  __device__ __forceinline__ uint32_t take() {  // the next big-endian word of the stream (0 past the data)
-    if (cw == 0) {
-      cur = fly;
-      ++next;
-      fly = ldq(next);
-      cw = 4;
-    }
-    const uint32_t x = cw == 4 ? cur.x : (cw == 3 ? cur.y : (cw == 2 ? cur.z : cur.w));
-    const uint32_t wi = 4u * (next - 1u) + (uint32_t)(4 - cw);
-    --cw;
-    return wi < nw ? __builtin_bswap32(x) : 0u;
-  }
-  __device__ __forceinline__ void fill() {
-    while (nb <= 32) {
-      buf |= (uint64_t)take() << (32 - nb);
-      nb += 32;
-    }
-  }
-  __device__ __forceinline__ void init(const uint32_t* s, uint32_t nbytes) {
-    src = s;
-    nw = (nbytes + 3) >> 2;
-    nbits = nbytes * 8u;
-    pos = 0;
-    next = 0;
-    fly = ldq(0);
-    cw = 0;
-    buf = 0;
-    nb = 0;
-    fill();
-  }
-  __device__ __forceinline__ uint32_t peek() const { return (uint32_t)(buf >> 32); }
-  __device__ __forceinline__ void skip(int n) {
-    buf <<= n;
-    nb -= n;
-    pos += (uint32_t)n;
-    fill();
-  }
-  __device__ __forceinline__ bool insuff() const { return pos > nbits; }
-};
-
-// A lane's decoder table in LDS: the 9-bit lookahead and the long-code search data (a
-// lane reading the PTab in global memory for a long code would stall its whole wave).
-constexpr int kLaneTabBytes = 1024 + 64 + 256;
-struct LaneTab {
-  const DINO_LDS uint16_t* look;
-  const DINO_LDS int32_t* mv;    // maxcode[10..16], valoffset[10..16] (16 words)
-  const DINO_LDS uint8_t* hv;    // huffval[256]
-  __device__ __forceinline__ void lookup(int, uint32_t p, int* sym, int* len) const {
-    const uint32_t e = look[p >> (32 - kPLookBits)];
-    if (e) {
-      *sym = (int)(e >> 4);
-      *len = (int)(e & 15u);
-      return;
-    }
-    const uint32_t p17 = p >> 15;
-    int l = 17, off = 0;
-    for (int q = 16 - kPLookBits - 1; q >= 0; --q) {  // the shortest matching length wins
-      if ((int32_t)(p17 >> (17 - (kPLookBits + 1 + q))) <= mv[q]) {
-        l = kPLookBits + 1 + q;
-        off = mv[8 + q];
-      }
-    }
-    *len = l;
-    *sym = l > 16 ? 0 : (int)hv[((int)(p17 >> (17 - (l > 16 ? 16 : l))) + off) & 255];  // (l 17: JWRN_HUFF_BAD_CODE)
-  }
-};
-
-__global__ void __launch_bounds__(64) k_prefine(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
-                                                const PCtl* __restrict__ pctl, int maxb) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int lane = threadIdx.x;
-  DINO_LDS uint8_t* nat = (DINO_LDS uint8_t*)(smem + 64 * kLaneTabBytes + 64 * 128);
-  for (int q = lane; q < 80; q += 64) nat[q] = kNaturalOrder[q];
-  __syncthreads();
-  const int g = blockIdx.x * 64 + lane;
-  const int c = g / maxb, k = g - c * maxb;
-  if (c >= 3 || k >= (int)pctl->nprog) return;
-  const int img = pctl->pimg[k];
-  const ImgDesc& d = desc[img];
-  if (d.status != DINO_IMG_OK || d.kind != 1 || c >= d.ncomp) return;
-  uint8_t* region = ws + d.htab_off;
-  const PHdr* hd = (const PHdr*)region;
-  if (!((hd->pad[0] >> c) & 1)) return;
-  DINO_LDS uint8_t* ltab = (DINO_LDS uint8_t*)smem + lane * kLaneTabBytes;
-  DINO_LDS int16_t* blk = (DINO_LDS int16_t*)(smem + 64 * kLaneTabBytes) + lane * 64;
-  int16_t* coef = (int16_t*)(ws + d.coef_off);
-  const CompDesc& cd = d.comp[c];
-  const int64_t plane = cd.coef_off / 2;
-  const int32_t bw = cd.bw, mcx = ceil_div(cd.dw, 8), mcy = ceil_div(cd.dh, 8);
-  const int64_t nmcu = (int64_t)mcx * mcy;
-  const int n = hd->n_scans;
-  for (int j = 0; j < n; ++j) {
-    const PScan ps = ((const PScan*)(region + kPScanOff))[j];
-    const ScanRec& sr = ps.sr;
-    if (!(sr.ss > 0 && sr.ah > 0 && sr.comp[0] == c)) continue;
-    const PTab* tab = (const PTab*)(region + kPTabOff) + pbyte64(ps.tslots, 4);
-    {  // lookahead, maxcode / valoffset of lengths 10..16, huffval -> the lane's LDS table
-      const uint4* src = (const uint4*)tab->look;
-      DINO_LDS uint4* dst = (DINO_LDS uint4*)ltab;
-#pragma unroll 4
-      for (int q = 0; q < (1 << kPLookBits) * 2 / 16; ++q) dst[q] = src[q];
-      DINO_LDS int32_t* mv = (DINO_LDS int32_t*)(ltab + 1024);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        mv[q] = q < 7 ? tab->maxcode[kPLookBits + 1 + q] : 0;
-        mv[8 + q] = q < 7 ? tab->valoffset[kPLookBits + 1 + q] : 0;
-      }
-      const uint4* hs = (const uint4*)tab->huffval;
-      DINO_LDS uint4* hd4 = (DINO_LDS uint4*)(ltab + 1024 + 64);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) hd4[q] = hs[q];
-    }
-    LaneTab lt{(const DINO_LDS uint16_t*)ltab, (const DINO_LDS int32_t*)(ltab + 1024),
-               (const DINO_LDS uint8_t*)(ltab + 1024 + 64)};
-    LaneClean r;
-    r.init((const uint32_t*)(ws + d.ent_off + ((sr.data_off - d.scan_off + 3) & ~3)), (uint32_t)ps.pad);
-    const int ss = sr.ss, se = sr.se, al = sr.al;
-    int32_t eobrun = 0;
-    uint4 nxt[8];
-    {
-      const uint4* b4 = (const uint4*)(coef + plane);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
-    }
-    int32_t bx = 0, by = 0;
-    for (int64_t m = 0; m < nmcu; ++m) {
-      const int64_t e0 = plane + ((int64_t)by * bw + bx) * 64;
-      uint64_t nzz = 0;
-      {
-        uint32_t w[32];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          ((DINO_LDS uint4*)blk)[q] = nxt[q];
-          w[4 * q] = nxt[q].x;
-          w[4 * q + 1] = nxt[q].y;
-          w[4 * q + 2] = nxt[q].z;
-          w[4 * q + 3] = nxt[q].w;
-        }
-#pragma unroll
-        for (int kk = 1; kk < 64; ++kk) {  // constant indices: registers only
-          const int pos = kNaturalOrder[kk];
-          nzz |= (uint64_t)(((w[pos >> 1] >> (16 * (pos & 1))) & 0xFFFFu) != 0) << kk;
-        }
-      }
-      if (++bx == mcx) {
-        bx = 0;
-        ++by;
-      }
-      if (m + 1 < nmcu) {  // the next block's coefficients load while this one decodes
-        const uint4* b4 = (const uint4*)(coef + plane + ((int64_t)by * bw + bx) * 64);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) nxt[q] = b4[q];
-      }
-      if (r.insuff()) continue;
-      uint64_t corr, nzn, neg;
-      r_refine_block(r, lt, ss, se, nzz, &eobrun, &corr, &nzn, &neg);
-      bool changed = false;
-      for (uint64_t mm = corr | nzn; mm; mm &= mm - 1) {
-        const int kk = __builtin_ctzll(mm);
-        const int pos = nat[kk];
-        const int16_t v = ac_refine_value(blk[pos], (corr >> kk) & 1u, (nzn >> kk) & 1u, (neg >> kk) & 1u, al);
-        changed |= v != blk[pos];
-        blk[pos] = v;
-      }
-      if (changed) {  // the refined block back as eight 16-byte stores
-        uint4* b4 = (uint4*)(coef + e0);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) b4[q] = ((const DINO_LDS uint4*)blk)[q];
-      }
-    }
   }
 }
 
@@ -2220,12 +1825,9 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#ifndef DINO_IDCT_WGS
-#define DINO_IDCT_WGS 32
-#endif
-constexpr int kIdctWgs = DINO_IDCT_WGS;  // workgroups per image (grid-stride over its blocks)
+constexpr int kIdctWgs = 32;  // workgroups per image (grid-stride over its blocks)
 
-// The steps of one 8-lane group's block (k_idct, k_ycolor).  sb: the group's LDS block,
+// The steps of one 8-lane group's block (k_idct).  sb: the group's LDS block,
 // rows of 9 words, all zero on entry.
 // Dense coefficients (kind 1): lane l loads row l of the block (8 int16 = one 16-byte load).
 __device__ __forceinline__ void idct_group_dense(int32_t* sb, int l, const uint8_t* blk) {
@@ -2238,10 +1840,7 @@ __device__ __forceinline__ void idct_group_dense(int32_t* sb, int l, const uint8
 // l, l + 8, .. (kIdctPre of them) already loaded into pre[]; halfword entries
 // (zigzag | int10 value << 6), then u32 entries from the next even halfword (see
 // SparseSink); the DC is int16 (absolute after k_dcscan).
-#ifndef DINO_IDCT_PRE
-#define DINO_IDCT_PRE 4
-#endif
-constexpr int kIdctPre = DINO_IDCT_PRE;  // halfword entries per lane loaded a block ahead (8 lanes: 8 kIdctPre)
+constexpr int kIdctPre = 4;  // halfword entries per lane loaded a block ahead (8 lanes: 8 kIdctPre)
 __device__ __forceinline__ void idct_load_pre(uint32_t* pre, int l, uint2 bi, const uint16_t* ent16) {
   const uint32_t c = bi.y & 0x7Fu;
 #pragma unroll
@@ -2295,23 +1894,7 @@ __device__ __forceinline__ uint64_t idct_group_pass2(int32_t* sb, int l) {
   return o.u;
 }
 
-// Images whose luma IDCT and colour conversion run fused in k_ycolor when the ctx fuses
-// (LaunchGeom::fuse, env DINO_FUSE=1; measured and off by default): YCbCr
-// 4:2:0 with fancy h2v2 chroma (k_color's fast420 case), at most kFuseMaxW pixels wide
-// (the band's luma rows live in LDS).  k_idct transforms only their chroma planes; k_color
-// skips them.
-#ifndef DINO_FUSE_MAX_W
-#define DINO_FUSE_MAX_W 2304
-#endif
-constexpr int kFuseMaxW = DINO_FUSE_MAX_W;
-__device__ __forceinline__ bool fused_420(const ImgDesc& d, int fuse) {
-  if (!fuse || d.status != DINO_IMG_OK || d.kind == 2 || d.ncomp != 3 || d.color != kYCbCr) return false;
-  const CompDesc &c0 = d.comp[0], &c1 = d.comp[1], &c2 = d.comp[2];
-  return d.width <= kFuseMaxW && d.max_h == 2 && d.max_v == 2 && c0.h == 2 && c0.v == 2 && c1.h == 1 && c1.v == 1 &&
-         c2.h == 1 && c2.v == 1 && c1.dw > 2 && c1.dw == c2.dw && c1.dh == c2.dh;
-}
-
-__global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws, int fuse) {
+__global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const BlkIdx bk = xcd_blk();
   // rows of 9 words, blocks 72 words apart: both the column (pass 1) and the row
   // (pass 2) accesses of a wave's 8 groups x 8 lanes hit 64 distinct banks
@@ -2363,13 +1946,11 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
     return r;
   };
   const int T = (int)tot, step = gridDim.x * kIdctBlocksPerWg;
-  // the luma plane of a k_ycolor image is transformed there, band by band
-  const int G0 = fused_420(d, fuse) ? (int)nb0 : 0;
   // The next block's record is loaded one iteration ahead, and its first 16 entries
   // at the end of the current iteration (once the record has arrived), so the
   // scatter at the top of an iteration normally waits on nothing.
-  int gn = G0 + bk.x * kIdctBlocksPerWg + grp;
-  Blk nx = locate(gn < T ? gn : G0);
+  int gn = bk.x * kIdctBlocksPerWg + grp;
+  Blk nx = locate(gn < T ? gn : 0);
   uint2 bin = make_uint2(0u, 0u);
   if (!dense && gn < T && nx.b >= 0 && nx.b < d.total_blocks) bin = binfo[nx.b];
   const uint16_t* ent16 = (const uint16_t*)ent;
@@ -2381,7 +1962,7 @@ __global__ void __launch_bounds__(256) k_idct(const ImgDesc* __restrict__ desc, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
   __syncthreads();
-  for (int g0 = G0 + bk.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
+  for (int g0 = bk.x * kIdctBlocksPerWg; g0 < T; g0 += step) {
     const bool valid = gn < T;
     const Blk cur = nx;
     const uint2 bi = bin;
@@ -2454,14 +2035,8 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, uint32
   out[3] = odd ? o3 : e3;
 }
 
-#ifndef DINO_COLOR_WGS
-#define DINO_COLOR_WGS 16
-#endif
-constexpr int kColorWgs = DINO_COLOR_WGS;  // workgroups per image
-#ifndef DINO_COLOR_BATCH
-#define DINO_COLOR_BATCH 1
-#endif
-constexpr int kColorBatch = DINO_COLOR_BATCH;  // quads whose loads a lane issues together (A/B: 4 and 8 slower)
+constexpr int kColorWgs = 16;  // workgroups per image
+constexpr int kColorBatch = 1;  // quads whose loads a lane issues together (measured: 4 and 8 slower)
 
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
 // the RGB area is padded by 16 bytes, so the last partial quad may store whole words).
@@ -2469,10 +2044,10 @@ constexpr int kColorBatch = DINO_COLOR_BATCH;  // quads whose loads a lane issue
 // two words per chroma row instead of per-pixel byte loads; edges, quads that wrap
 // a row and other samplings use the per-pixel path (same arithmetic).
 __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes, const int64_t* __restrict__ offsets,
-                                               const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws, int fuse) {
+                                               const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
   const BlkIdx bk = xcd_blk();
   const ImgDesc& d = desc[bk.y];
-  if (d.status != DINO_IMG_OK || fused_420(d, fuse)) return;
+  if (d.status != DINO_IMG_OK) return;
   if (d.kind == 2) {  // pre-decoded RGB container: copy the pixels into the workspace
     const uint8_t* src = bytes + offsets[bk.y] + d.scan_off;
     uint32_t* dst = (uint32_t*)(ws + d.rgb_off);
@@ -2614,159 +2189,6 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
       rgb[3 * q + 1] = o.w[1];
       rgb[3 * q + 2] = o.w[2];
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_ycolor: grid (gx, B); one band (one luma block row = 8 pixel rows, full width)
-// per workgroup turn, for the fused_420 images
-// ---------------------------------------------------------------------------
-// The band's luma blocks are transformed by 8-lane groups as in k_idct (the next
-// block's record loaded one block ahead, its first entries at the end of the current
-// one), but their rows go to LDS instead of the luma plane; then k_color's 4:2:0 quad
-// conversion runs with Y from LDS and Cb / Cr from the planes k_idct wrote.  The luma
-// plane never reaches HBM (k_idct writes it and k_color reads it back for every other
-// image).  A band's output is the contiguous RGB range of its 8 rows, whose length 24 W
-// is a multiple of 12: quads never straddle two bands.
-constexpr int kFuseYPitch = kFuseMaxW + 32;  // 8 words mod 64 banks: a wave's row stores hit 64 banks
-#ifndef DINO_YCOLOR_WGS
-#define DINO_YCOLOR_WGS 32
-#endif
-constexpr int kYcolorWgs = DINO_YCOLOR_WGS;  // workgroups per image (grid-stride over its bands)
-
-__global__ void __launch_bounds__(256) k_ycolor(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws) {
-  const BlkIdx bk = xcd_blk();
-  __shared__ int32_t s_blk[kIdctBlocksPerWg][72];
-  __shared__ uint8_t s_nat[80];
-  __shared__ __attribute__((aligned(16))) uint8_t s_y[8 * kFuseYPitch];
-  const ImgDesc& d = desc[bk.y];
-  if (!fused_420(d, 1)) return;
-  const int W = d.width, H = d.height;
-  const int nband = (H + 7) >> 3;
-  if (bk.x >= nband) return;
-  const int t = threadIdx.x;
-  if (t < 80) s_nat[t] = (uint8_t)((kNaturalOrder[t] >> 3) * 9 + (kNaturalOrder[t] & 7));
-  const int grp = t >> 3, l = t & 7;
-  int32_t* sb = s_blk[grp];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) sb[l * 9 + j] = 0;
-  const bool dense = d.kind == 1;
-  const CompDesc& cy = d.comp[0];
-  const uint16_t* qt = d.qt[cy.tq];
-  int moff0 = 0;  // first luma position inside the MCU
-  for (int i = d.blocks_per_mcu - 1; i >= 0; --i)
-    if (d.mcu_comp[i] == 0) moff0 = i;
-  const uint32_t* ent = (const uint32_t*)(ws + d.coef_off);
-  const uint16_t* ent16 = (const uint16_t*)ent;
-  const uint2* binfo = (const uint2*)(ws + d.binfo_off);
-  const int nbx = (W + 7) >> 3;
-  const PlaneView p1 = make_plane_view(d, ws, 1), p2 = make_plane_view(d, ws, 2);
-  uint32_t* rgb = (uint32_t*)(ws + d.rgb_off);
-  const int64_t npx = (int64_t)W * H;
-  // quad walk of a band: thread t starts at pixel 4t, then advances 1024 pixels per turn
-  const int dy = 1024 / W, dx = 1024 - dy * W;
-  const int y0 = (4 * t) / W, x0 = 4 * t - y0 * W;
-  // sparse record of luma block (j, k) (decode order: MCU (j/2, k/2), position moff0 + 2 (k&1) + (j&1))
-  auto record = [&](int j, int k) {
-    const int b = ((k >> 1) * d.mcus_x + (j >> 1)) * d.blocks_per_mcu + moff0 + (k & 1) * 2 + (j & 1);
-    return b < d.total_blocks ? binfo[b] : make_uint2(0u, 0u);
-  };
-  __syncthreads();
-  for (int k = bk.x; k < nband; k += gridDim.x) {
-    // the band's luma blocks (block row k): group grp takes blocks grp, grp + 32, ...
-    int jn = grp;
-    uint2 bin = make_uint2(0u, 0u);
-    uint32_t pre[kIdctPre] = {};  // the next block's first halfword entries (l, l + 8, ..)
-    auto first_entries = [&]() { idct_load_pre(pre, l, bin, ent16); };
-    if (!dense && jn < nbx) {
-      bin = record(jn, k);
-      first_entries();
-    }
-    for (int j0 = 0; j0 < nbx; j0 += kIdctBlocksPerWg) {
-      const int j = jn;
-      const bool valid = j < nbx;
-      const uint2 bi = bin;
-      jn += kIdctBlocksPerWg;
-      if (!dense && jn < nbx) bin = record(jn, k);
-      if (valid && dense) idct_group_dense(sb, l, ws + d.coef_off + cy.coef_off + ((int64_t)k * cy.bw + j) * 128);
-      else if (valid) idct_group_sparse(sb, l, s_nat, bi, pre, ent16, ent);
-      wave_lds_sync();
-      if (valid) idct_group_pass1(sb, l, qt);
-      wave_lds_sync();
-      if (valid) *(uint64_t*)(s_y + l * kFuseYPitch + j * 8) = idct_group_pass2(sb, l);
-      if (!dense && jn < nbx) first_entries();
-      wave_lds_sync();
-    }
-    __syncthreads();
-    // colour: the band's quads (pixel 8kW + 4q, output words 3 (2kW + q) ..)
-    const int rows = min(8, H - 8 * k);
-    const int nq = (rows * W + 3) >> 2;
-    const int64_t qb = (int64_t)2 * k * W, pb = (int64_t)8 * k * W;
-    int y = y0, x = x0;
-    for (int q = t; q < nq; q += 256) {
-      union {
-        uint8_t b[12];
-        uint32_t w[3];
-      } o;
-      const int gy = 8 * k + y;
-      if (x + 3 < W) {  // Y from LDS; Cb / Cr words at column x/2 - 1 of the nearer and the farther row
-        const uint32_t* yp = (const uint32_t*)(s_y + y * kFuseYPitch + (x & ~3));
-        const uint32_t yw = __builtin_amdgcn_alignbyte(yp[1], yp[0], (uint32_t)(x & 3));
-        const int r = gy >> 1;
-        const int rf = (gy & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
-        const int c0 = x >> 1, cc = c0 - 1;
-        const uint32_t csh = (uint32_t)(cc & 3);
-        const uint32_t edge = (c0 == 0 ? 1u : 0u) | (c0 + 1 >= p1.dw ? 2u : 0u) | (c0 + 2 >= p1.dw ? 4u : 0u);
-        const uint32_t* cp[4] = {(const uint32_t*)(p1.p + (int64_t)r * p1.pitch + (cc & ~3)),
-                                 (const uint32_t*)(p1.p + (int64_t)rf * p1.pitch + (cc & ~3)),
-                                 (const uint32_t*)(p2.p + (int64_t)r * p2.pitch + (cc & ~3)),
-                                 (const uint32_t*)(p2.p + (int64_t)rf * p2.pitch + (cc & ~3))};
-        uint32_t cw[8];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          cw[2 * m] = cp[m][0];
-          cw[2 * m + 1] = cp[m][1];
-        }
-        int cb[4], cr[4];
-        h2v2_quad(__builtin_amdgcn_alignbyte(cw[1], cw[0], csh), __builtin_amdgcn_alignbyte(cw[3], cw[2], csh), x, edge,
-                  cb);
-        h2v2_quad(__builtin_amdgcn_alignbyte(cw[5], cw[4], csh), __builtin_amdgcn_alignbyte(cw[7], cw[6], csh), x, edge,
-                  cr);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) ycc_to_rgb((int)((yw >> (8 * m)) & 255u), cb[m], cr[m], o.b + 3 * m);
-      } else {  // a quad that wraps a row: per pixel, same arithmetic
-        int py = y, px = x;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          if (pb + 4 * q + m < npx) {
-            const int g = 8 * k + py;
-            const int r = g >> 1, c = px >> 1;
-            const int rn = (g & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
-            const int cn = (px & 1) ? min(c + 1, p1.dw - 1) : max(c - 1, 0);
-            const int bias = (px & 1) ? 7 : 8;
-            const int tb = pv_at(p1, c, r) * 3 + pv_at(p1, c, rn), nb = pv_at(p1, cn, r) * 3 + pv_at(p1, cn, rn);
-            const int tr = pv_at(p2, c, r) * 3 + pv_at(p2, c, rn), nr = pv_at(p2, cn, r) * 3 + pv_at(p2, cn, rn);
-            ycc_to_rgb(s_y[py * kFuseYPitch + px], (tb * 3 + nb + bias) >> 4, (tr * 3 + nr + bias) >> 4, o.b + 3 * m);
-          } else {
-            o.b[3 * m] = o.b[3 * m + 1] = o.b[3 * m + 2] = 0;
-          }
-          if (++px == W) {
-            px = 0;
-            ++py;
-          }
-        }
-      }
-      rgb[3 * (qb + q)] = o.w[0];
-      rgb[3 * (qb + q) + 1] = o.w[1];
-      rgb[3 * (qb + q) + 2] = o.w[2];
-      x += dx;
-      y += dy;
-      if (x >= W) {
-        x -= W;
-        ++y;
-      }
-    }
-    __syncthreads();
   }
 }
 
@@ -2977,54 +2399,15 @@ __global__ void __launch_bounds__(256) k_rcoeffs(const dino_view_params* __restr
   }
 }
 
-#ifndef DINO_HRESIZE_MFMA
-#define DINO_HRESIZE_MFMA 0
-#endif
-#ifndef DINO_HRESIZE_MFMA_STEPS
-#define DINO_HRESIZE_MFMA_STEPS 2
-#endif
-#ifndef DINO_HRESIZE_MFMA_PITCH
-#define DINO_HRESIZE_MFMA_PITCH 320
-#endif
-constexpr int kHrMfmaMaxSteps = DINO_HRESIZE_MFMA_STEPS;  // 64-column K steps per 16-column block
-constexpr int kHrMfmaMaxK = 64 * kHrMfmaMaxSteps;
-constexpr int kHrMfmaMaxPitch = DINO_HRESIZE_MFMA_PITCH;  // bytes per staged row (views needing more: v_dot4 kernel)
-constexpr int kHrMfmaLds = 2 * 3 * 16 * kHrMfmaMaxPitch;  // 2 band buffers x 3 planes x 16 rows
-constexpr int kHrMfmaPre = 4;                        // staging items per thread loaded a band ahead
-typedef int32_t hr_v4i __attribute__((ext_vector_type(4)));
-
-// Conservative per-view test from the view geometry alone (both kernels evaluate it):
-// a 16-column block spans <= 15 cw / S + 1 + kh source columns, + 15 for its 16-byte
-// aligned start; a 64-column group <= 63 cw / S + 1 + kh, + 15 + 64 of read slack.
-__host__ __device__ __forceinline__ bool hresize_mfma_ok(int S, int cw, int kh) {
-  if (!DINO_HRESIZE_MFMA || kh <= 0) return false;
-  const int64_t blk = (15ll * cw + S - 1) / S + 1 + kh + 15;
-  const int64_t grp = (63ll * cw + S - 1) / S + 1 + kh + 15 + 64;
-  return blk <= kHrMfmaMaxK && ((grp + 15) & ~15ll) <= kHrMfmaMaxPitch;
-}
-
 // Horizontal pass.  A workgroup owns bands of R source rows of one view.  The
 // crop's pixels for those rows are staged in LDS as RGBX words (each lane turns
 // 12 source bytes = 4 pixels into one 16-byte LDS store); the view's taps are
 // staged in LDS too when they fit.  Each lane then resamples one (row, x) with
 // one LDS word per tap and writes the three channels to planar temp rows
 // [3][crop_h][S].  Crops too wide for LDS take a direct (global) path.
-#ifndef DINO_HRESIZE_MIN_ROWS
-#define DINO_HRESIZE_MIN_ROWS 8
-#endif
-constexpr int kHresizeMinRows = DINO_HRESIZE_MIN_ROWS;  // rows per band the slice width is chosen for
-#ifndef DINO_HRESIZE_BANDS
-#define DINO_HRESIZE_BANDS 8
-#endif
-constexpr int kHrBandsPerItem = DINO_HRESIZE_BANDS;  // row bands of one slice per work item
-constexpr int kHrDirectItems = 4;                    // work items of a direct-path view
-#ifndef DINO_HRESIZE_DYNAMIC
-#define DINO_HRESIZE_DYNAMIC 1
-#endif
-constexpr bool kHrDynamic = DINO_HRESIZE_DYNAMIC;  // work items from a counter (else blockIdx + k gridDim)
-#ifndef DINO_HRESIZE_OCC
-#define DINO_HRESIZE_OCC 1  // launch-bounds occupancy hint (A/B: 6 caps the VGPRs at 80, with a small spill)
-#endif
+constexpr int kHresizeMinRows = 8;  // rows per band the slice width is chosen for
+constexpr int kHrBandsPerItem = 8;  // row bands of one slice per work item
+constexpr int kHrDirectItems = 4;  // work items of a direct-path view
 
 // Tile shape of a view's horizontal pass: the widest slice of outputs (all of S,
 // else a multiple of 8) whose taps (16 bytes per output + 16 per output and group
@@ -3065,7 +2448,6 @@ __device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
 // slice each, so that a batch of mixed crop sizes spreads over the persistent grid in
 // pieces of similar size (a large crop's view is many items, a small one's few).
 __device__ int hr_view_chunks(int S, int cw, int ch, int kh) {
-  if (hresize_mfma_ok(S, cw, kh)) return 0;  // k_hresize_mfma's view
   const HrTile t = hresize_tile(S, cw, kh);
   if (t.R < 1) return kHrDirectItems;
   const int nsl = (S + t.sw - 1) / t.sw, nbands = (ch + t.R - 1) / t.R;
@@ -3173,7 +2555,7 @@ __device__ __forceinline__ void hresize_item(const ImgDesc* __restrict__ desc, c
                                              const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int nc, int c,
                                              const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws, uint8_t* smem);
 
-__global__ void __launch_bounds__(256, DINO_HRESIZE_OCC) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+__global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int B,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
   main_prio();
@@ -3185,10 +2567,10 @@ __global__ void __launch_bounds__(256, DINO_HRESIZE_OCC) k_hresize(const ImgDesc
   const ViewPlan vl = plan[(B - 1) * nv + v0 + nvc - 1];
   const int nitems_all = vl.hr_base + vl.hr_chunks;
   int* ctr = v0 == 0 ? &plan[B * nv].hr_chunks : &plan[B * nv].hr_base;
-  if (threadIdx.x == 0) s_item[0] = kHrDynamic ? atomicAdd(ctr, 1) : (int)blockIdx.x;
+  if (threadIdx.x == 0) s_item[0] = atomicAdd(ctr, 1);
   __syncthreads();
   for (int it = 0, c = s_item[0]; c < nitems_all; ++it) {
-    if (threadIdx.x == 0) s_item[(it + 1) & 1] = kHrDynamic ? atomicAdd(ctr, 1) : c + (int)gridDim.x;
+    if (threadIdx.x == 0) s_item[(it + 1) & 1] = atomicAdd(ctr, 1);
     hresize_item(desc, prm, plan, nv, v0, nvc, nc, c, ws, aws, smem);
     __syncthreads();
     c = s_item[(it + 1) & 1];
@@ -3293,186 +2675,6 @@ __device__ __forceinline__ void hresize_item(const ImgDesc* __restrict__ desc, c
   }
 }
 
-// Horizontal pass on the matrix cores (round 3).  The horizontal resample of a band of
-// 16 crop rows to 16 output columns is a product of the rows' pixels (16 x K source
-// columns) with a banded weight matrix (K x 16: column x holds its taps at source columns
-// [xmin(x), xmin(x) + cnt(x)), zero elsewhere).  Same exact integer sums as the v_dot4
-// path: pixels sign-flipped to int8 (p - 128), taps as three signed base-256 digit
-// planes, one v_mfma_i32_16x16x64_i8 per channel, digit and 64-column step; the digit
-// sums recombine to Pillow's int32 sum (+ the 128 x sum-of-taps correction).
-// A workgroup owns 64 output columns of one view (4 waves x 16 columns); each wave
-// builds its weight fragments once (global taps -> registers) and sweeps the crop's
-// rows in bands of 16 that the workgroup stages in LDS as planar sign-flipped rows
-// (16-byte aligned, so each A fragment is one ds_read_b128).  Views whose 16-column
-// blocks need more than kHrMfmaMaxK source columns, or whose 64-column span does not fit
-// the staging budget, keep the v_dot4 kernel (hresize_mfma_ok decides for both).
-__global__ void __launch_bounds__(256) k_hresize_mfma(const ImgDesc* __restrict__ desc,
-                                                      const dino_view_params* __restrict__ prm,
-                                                      const ViewPlan* __restrict__ plan, int nv, int v0,
-                                                      const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int b = blockIdx.z;
-  const int i = b * nv + v0 + blockIdx.y;
-  const ViewPlan vp = plan[i];
-  if (!vp.ok || !vp.kh) return;
-  const dino_view_params p = prm[i];
-  const int S = p.out_size, cw = p.crop_w, kh = vp.kh;
-  if (!hresize_mfma_ok(S, cw, kh)) return;
-  const int xg0 = 64 * (int)blockIdx.x;
-  if (xg0 >= S) return;
-  const ImgDesc& d = desc[b];
-  const int W = d.width;
-  const int32_t* gb = (const int32_t*)(aws + vp.rcoef_off);  // [S][2]: xmin, cnt
-  const int32_t* gt = gb + 4 * S;                            // [S][kh] taps
-  const int4* ghx = (const int4*)(aws + vp.rcoef_off + align16((int64_t)S * (4 + vp.kh + vp.kv) * 4));
-  const uint8_t* rgb = ws + d.rgb_off;
-  uint8_t* tmp = aws + vp.htmp_off;
-  const int64_t cpl = (int64_t)p.crop_h * S;
-  const int ncols = min(64, S - xg0);
-  const int c0 = gb[2 * xg0] & ~15;  // staged source columns [c0, c1), 16-aligned start
-  const int c1 = min(cw, gb[2 * (xg0 + ncols - 1)] + gb[2 * (xg0 + ncols - 1) + 1]);
-  const int pitch = ((c1 - c0 + 15) & ~15) + 64;  // + the read slack of the last K step
-  const int plane = 16 * pitch;
-  const int ngroups = (c1 - c0 + 3) >> 2;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int xb = xg0 + 16 * w;  // this wave's 16 output columns
-  const bool wact = xb < xg0 + ncols;
-  const int ncw = wact ? min(16, S - xb) : 0;
-  const int kb = wact ? (gb[2 * xb] & ~15) : c0;
-  const int nk = wact ? (gb[2 * (xb + ncw - 1)] + gb[2 * (xb + ncw - 1) + 1] - kb + 63) >> 6 : 0;
-  // weight fragments: lane (column xb + (lane & 15), k quarter lane >> 4) holds, per K step
-  // s and digit, the 16 digits of source columns kb + 64 s + 16 (lane >> 4) + j
-  hr_v4i bw[kHrMfmaMaxSteps][3];
-  const int xo = xb + (lane & 15);
-  const bool cval = wact && (lane & 15) < ncw;
-  const int xm = cval ? gb[2 * xo] : 0, cnt = cval ? gb[2 * xo + 1] : 0;
-  const int32_t corr = cval ? ghx[xo].z : 0;
-#pragma unroll
-  for (int s = 0; s < kHrMfmaMaxSteps; ++s) {
-    uint32_t dg[3][4] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-    if (s < nk) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        const int t = kb + 64 * s + 16 * (lane >> 4) + j - xm;
-        const int32_t kt = t >= 0 && t < cnt ? gt[(int64_t)xo * kh + t] : 0;
-        const int32_t d0 = (int32_t)(int8_t)(uint8_t)(kt & 0xFF);
-        const int32_t r1 = (kt - d0) >> 8;
-        const int32_t d1 = (int32_t)(int8_t)(uint8_t)(r1 & 0xFF);
-        const int32_t d2 = (r1 - d1) >> 8;
-        dg[0][j >> 2] |= (uint32_t)(uint8_t)d0 << (8 * (j & 3));
-        dg[1][j >> 2] |= (uint32_t)(uint8_t)d1 << (8 * (j & 3));
-        dg[2][j >> 2] |= (uint32_t)(uint8_t)d2 << (8 * (j & 3));
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      bw[s][q][0] = (int32_t)dg[q][0];
-      bw[s][q][1] = (int32_t)dg[q][1];
-      bw[s][q][2] = (int32_t)dg[q][2];
-      bw[s][q][3] = (int32_t)dg[q][3];
-    }
-  }
-  const int arow = lane & 15, acol = kb - c0 + 16 * (lane >> 4);
-  const int nbands = (p.crop_h + 15) >> 4;
-  // staging item e of band r0: row e / ngroups, group e % ngroups (12 source bytes = 4 pixels)
-  auto src_of = [&](int r0, int e, int* r, int* g) {
-    *r = e / ngroups;
-    *g = e - *r * ngroups;
-    return rgb + ((int64_t)(p.crop_top + r0 + *r) * W + p.crop_left + c0) * 3 + 12 * *g;
-  };
-  auto put = [&](uint8_t* buf, int r, int g, const uint8_t* src, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-    const uint32_t sh = 8u * (uint32_t)((uintptr_t)src & 3);
-    const uint32_t b0 = (uint32_t)((((uint64_t)w1 << 32) | w0) >> sh);
-    const uint32_t b1 = (uint32_t)((((uint64_t)w2 << 32) | w1) >> sh);
-    const uint32_t b2 = (uint32_t)((((uint64_t)w3 << 32) | w2) >> sh);
-    const uint32_t cr = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C060300u), 0x05020100u);
-    const uint32_t cg = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C070401u), 0x06020100u);
-    const uint32_t cb = __builtin_amdgcn_perm(b2, __builtin_amdgcn_perm(b1, b0, 0x0C0C0502u), 0x07040100u);
-    uint8_t* dst = buf + r * pitch + 4 * g;
-    *(uint32_t*)dst = cr ^ 0x80808080u;
-    *(uint32_t*)(dst + plane) = cg ^ 0x80808080u;
-    *(uint32_t*)(dst + 2 * plane) = cb ^ 0x80808080u;
-  };
-  // band k is staged in buffer k & 1: the first kHrMfmaPre items of each thread are loaded
-  // while the previous band's MFMAs run, the rest when the band is stored
-  uint32_t pf[kHrMfmaPre][4];
-  auto prefetch = [&](int r0) {
-    const int n = min(16, p.crop_h - r0) * ngroups;
-#pragma unroll
-    for (int j = 0; j < kHrMfmaPre; ++j) {
-      const int e = (int)threadIdx.x + j * (int)blockDim.x;
-      if (e < n) {
-        int r, g;
-        const uint32_t* a0 = (const uint32_t*)((uintptr_t)src_of(r0, e, &r, &g) & ~(uintptr_t)3);
-        pf[j][0] = a0[0];
-        pf[j][1] = a0[1];
-        pf[j][2] = a0[2];
-        pf[j][3] = a0[3];
-      }
-    }
-  };
-  auto store = [&](int r0, uint8_t* buf) {
-    const int n = min(16, p.crop_h - r0) * ngroups;
-#pragma unroll
-    for (int j = 0; j < kHrMfmaPre; ++j) {
-      const int e = (int)threadIdx.x + j * (int)blockDim.x;
-      if (e < n) {
-        int r, g;
-        const uint8_t* src = src_of(r0, e, &r, &g);
-        put(buf, r, g, src, pf[j][0], pf[j][1], pf[j][2], pf[j][3]);
-      }
-    }
-    for (int e = (int)threadIdx.x + kHrMfmaPre * (int)blockDim.x; e < n; e += blockDim.x) {
-      int r, g;
-      const uint8_t* src = src_of(r0, e, &r, &g);
-      const uint32_t* a0 = (const uint32_t*)((uintptr_t)src & ~(uintptr_t)3);
-      put(buf, r, g, src, a0[0], a0[1], a0[2], a0[3]);
-    }
-  };
-  prefetch(0);
-  store(0, smem);
-  __syncthreads();
-  for (int k = 0; k < nbands; ++k) {
-    const int r0 = 16 * k, nr = min(16, p.crop_h - r0);
-    uint8_t* cur = smem + (k & 1) * 3 * plane;
-    if (k + 1 < nbands) prefetch(r0 + 16);  // lands during this band's MFMAs
-    if (wact) {
-      hr_v4i acc[3][3];
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) acc[c][q] = hr_v4i{0, 0, 0, 0};
-      const uint8_t* rowp = cur + (arow < nr ? arow : nr - 1) * pitch + acol;  // (rows >= nr: not stored)
-#pragma unroll
-      for (int s = 0; s < kHrMfmaMaxSteps; ++s) {
-        if (s < nk) {
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            const hr_v4i a = *(const hr_v4i*)(rowp + c * plane + 64 * s);
-#pragma unroll
-            for (int q = 0; q < 3; ++q) acc[c][q] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, bw[s][q], acc[c][q], 0, 0, 0);
-          }
-        }
-      }
-      if (cval) {
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int r = r0 + 4 * (lane >> 4) + kk;  // C/D: column lane & 15, row 4 (lane >> 4) + kk
-          if (r >= r0 + nr) break;
-          const int64_t o = (int64_t)r * S + xo;
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            tmp[c * cpl + o] = clip8_acc((int32_t)((uint32_t)acc[c][0][kk] + ((uint32_t)acc[c][1][kk] << 8) +
-                                                   ((uint32_t)acc[c][2][kk] << 16) + (uint32_t)corr));
-        }
-      }
-    }
-    // band k + 1 into the other buffer (band k - 1's readers passed the last barrier)
-    if (k + 1 < nbands) store(r0 + 16, smem + ((k + 1) & 1) * 3 * plane);
-    __syncthreads();
-  }
-}
-
 // Per-view slot of the u8 crop planes [3][S][S] (global views first, then local views).
 __device__ __forceinline__ int64_t crop_slot(const dino_aug_config& cfg, int B, int b, int v) {
   const int64_t g3 = 3ll * cfg.global_size * cfg.global_size, l3 = 3ll * cfg.local_size * cfg.local_size;
@@ -3494,10 +2696,7 @@ struct FastDiv {
 // band of vert_rows(S) output rows; adds the band's L sum to the view's counter.
 // Fast path (planar temp rows, S % 4 == 0): a lane produces 4 adjacent pixels
 // from one 4-byte load per channel and tap and stores one word per plane.
-#ifndef DINO_VERT_ROWS
-#define DINO_VERT_ROWS 8
-#endif
-constexpr int kVertRows = DINO_VERT_ROWS;
+constexpr int kVertRows = 8;
 // rows per workgroup: 16 for the small (local) views, whose 8-row bands are short
 __host__ __device__ __forceinline__ int vert_rows(int S) { return S > 128 ? kVertRows : 2 * kVertRows; }
 
@@ -3697,10 +2896,7 @@ __host__ __device__ __forceinline__ int final_tile_bytes(int S) {
   return 3 * (final_rows(S) + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad);
 }
 
-#ifndef DINO_BLUR_REG_KS
-#define DINO_BLUR_REG_KS 7
-#endif
-constexpr int kBlurRegKs = DINO_BLUR_REG_KS;  // blur kernels up to this size keep their weights in registers
+constexpr int kBlurRegKs = 7;  // blur kernels up to this size keep their weights in registers
 template <int KS, typename OutT>
 __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, int tp, int64_t tplane, int nr, int y0,
                                               int S, int ks_rt, const float* __restrict__ k2, bool solarize,
@@ -3898,14 +3094,8 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
 __host__ __device__ __forceinline__ int vfinal_tile_bytes(int S) {
   return 3 * (S + 2 * kMaxBlurPad) * final_tile_pitch(S, kMaxBlurPad) + 16;
 }
-#ifndef DINO_VFINAL_MAX_S
-#define DINO_VFINAL_MAX_S 128
-#endif
-constexpr int kVFinalMaxS = DINO_VFINAL_MAX_S;  // views up to this size take the fused kernel
-#ifndef DINO_VFINAL_THREADS
-#define DINO_VFINAL_THREADS 512
-#endif
-constexpr int kVFinalThreads = DINO_VFINAL_THREADS;  // 8 waves per view: the vertical pass is load-latency bound
+constexpr int kVFinalMaxS = 128;  // views up to this size take the fused kernel
+constexpr int kVFinalThreads = 512;  // 8 waves per view: the vertical pass is load-latency bound
 
 template <typename OutT>
 __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
@@ -4309,7 +3499,7 @@ static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_d
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
                                                        "k_vert_local", "k_dcscan", "k_htab", "k_hseg", "k_huff2",
-                                                       "k_huff3", "k_prog", "k_pwalk", "k_ycolor"};
+                                                       "k_huff3", "k_prog", "k_pwalk"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -4349,12 +3539,6 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
     return e;
   g->grid_ds = 4 * cus;
   g->grid3 = persistent_grid(reinterpret_cast<const void*>(&k_huff3), kHuff3LdsBytes, cus);
-  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hresize_mfma), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               kHrMfmaLds)) != hipSuccess)
-    return e;
-  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_prefine), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               kPrefineLds)) != hipSuccess)
-    return e;
   g->grid1 = persistent_grid(reinterpret_cast<const void*>(&k_huff1), kHuffLdsBytes, cus);
   if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_hresize), hipFuncAttributeMaxDynamicSharedMemorySize,
                                kHresizeLds)) != hipSuccess)
@@ -4366,10 +3550,6 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
   const char* pc = getenv("DINO_PSCAN_PER_CU");
   const int per_cu = pc && atoi(pc) > 0 ? atoi(pc) : 1;
   g->grid_ps = per_cu * cus;
-  const char* pf = getenv("DINO_PREFINE_COMPS");
-  g->prefine = pf ? (atoi(pf) & 7) : 0;
-  const char* fu = getenv("DINO_FUSE");
-  g->fuse = fu && fu[0] == '1';
   return hipSuccess;
 }
 
@@ -4383,20 +3563,15 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   // after k_htab's kind switch
-  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl,
-                                                             a.geom.prefine)));
+  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
   TIMED(tm, kKProg, s, (k_pscan<<<a.geom.grid_ps, kPScanThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
-  if (a.geom.prefine)
-    TIMED(tm, kKProg, s, (k_prefine<<<(3 * B + 63) / 64, 64, kPrefineLds, s>>>(a.desc, a.ws, a.pctl, B)));
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));
   TIMED(tm, kKHuff3, s, (k_huff3<<<grid3, kHuffThreads, kHuff3LdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKDcscan, s, (k_dcscan<<<B, kDcScanThreads, 0, s>>>(a.desc, a.ws)));
-  const int fuse = a.geom.fuse;
-  TIMED(tm, kKIdct, s, (k_idct<<<dim3(kIdctWgs, B), 256, 0, s>>>(a.desc, a.ws, fuse)));
-  TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws, fuse)));
-  if (fuse) TIMED(tm, kKYcolor, s, (k_ycolor<<<dim3(kYcolorWgs, B), 256, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKIdct, s, (k_idct<<<dim3(kIdctWgs, B), 256, 0, s>>>(a.desc, a.ws)));
+  TIMED(tm, kKColor, s, (k_color<<<dim3(kColorWgs, B), 256, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   return hipGetLastError();
 }
 
@@ -4416,10 +3591,6 @@ static hipError_t launch_augment_class(const AugmentArgs& a, int v0, int nvc, in
   const int kvert = v0 == 0 ? kKVertGlobal : kKVertLocal;
   const int rc_threads = S < 256 ? (S + 63) / 64 * 64 : 256;  // one lane per output column
   TIMED(tm, kKRcoeffs, s, (k_rcoeffs<<<dim3(nvc, B), rc_threads, 0, s>>>(a.params, a.plan, nv, v0, a.aws)));
-  if (DINO_HRESIZE_MFMA)
-    TIMED(tm, kKHresize, s,
-          (k_hresize_mfma<<<dim3((S + 63) / 64, nvc, B), 256, kHrMfmaLds, s>>>(a.desc, a.params, a.plan, nv, v0, a.ws,
-                                                                                 a.aws)));
   TIMED(tm, kKHresize, s,
         (k_hresize<<<a.grid_hr, 256, kHresizeLds, s>>>(a.desc, a.params, a.plan, nv, v0, nvc, B, a.ws, a.aws)));
   if (S <= kVFinalMaxS) {  // small views: vertical pass and epilogue fused, the view stays in LDS

@@ -7,22 +7,13 @@ namespace dino {
 
 // Per-(image, view) scratch placement, written by k_vplan.
 // Lanes of k_huffman (one workgroup per image).
-#ifndef DINO_HUFF_THREADS
-#define DINO_HUFF_THREADS 256
-#endif
-constexpr int kHuffThreads = DINO_HUFF_THREADS;
+constexpr int kHuffThreads = 256;
 // Bits of entropy-coded stream per Huffman work item (kHuffThreads lanes); an image
 // larger than this is decoded by several workgroups (k_huff1 / k_huff3).
-#ifndef DINO_HUFF_SEG_KBITS
-#define DINO_HUFF_SEG_KBITS 2048
-#endif
-constexpr int64_t kHuffSegBits = (int64_t)DINO_HUFF_SEG_KBITS * 1024;
+constexpr int64_t kHuffSegBits = (int64_t)2048 * 1024;
 
 // LDS of k_hresize: taps (when they fit in kHresizeTapLds) + planar rows of one band.
-#ifndef DINO_HRESIZE_LDS_KB
-#define DINO_HRESIZE_LDS_KB 26
-#endif
-constexpr int kHresizeLds = DINO_HRESIZE_LDS_KB * 1024;
+constexpr int kHresizeLds = 26 * 1024;
 
 struct ViewPlan {
   int64_t htmp_off;   // horizontal-pass rows (crop_h x S x 3 u8) in the augment workspace
@@ -40,7 +31,7 @@ struct ViewPlan {
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuff1, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
   kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKProg,
-  kKPwalk, kKYcolor, kKNumKernels
+  kKPwalk, kKNumKernels
 };
 
 struct KernelTimer {
@@ -65,9 +56,7 @@ struct LaunchGeom {
   int32_t grid1;     // persistent k_huff1 grid (occupancy x CUs)
   int32_t grid3;     // persistent k_huff3 grid
   int32_t grid_ps;   // persistent k_pscan grid (waves)
-  int32_t prefine;   // components whose AC refinement scans k_prefine decodes in lane mode (bit c; 0: none)
   int32_t grid_hr;   // persistent k_hresize grid (occupancy x CUs)
-  int32_t fuse;      // 4:2:0 luma IDCT + colour fused in k_ycolor (env DINO_FUSE=1; off by default)
 };
 
 // Coefficient-buffer images of a batch (k_plan zeroes, k_pwalk registers, k_pscan

@@ -55,17 +55,42 @@ def _out_code(out_dtype) -> int:
     return _DTYPES.get(out_dtype, OUT_BF16)
 
 
-def _unshared(t: torch.Tensor) -> bool:
-    """Nothing outside the pipeline holds ``t`` or its memory: the tensor object is referenced
-    only by the slot's view cache list, its outputs dict and the caller's loop variable (plus
-    the call's argument, this parameter and getrefcount's own), and its storage only by ``t``
-    (a view, slice or chunk the caller kept shares the storage and raises its use count)."""
-    if sys.getrefcount(t) > 6:
+def _refcounts(views) -> list[int]:
+    """``sys.getrefcount`` of each tensor of ``views``, every one taken through this same
+    code path (the loop variable and getrefcount's argument included), so that the counts
+    compare with ``_REFS_PIPELINE_ONLY``, measured through it at import: how many references
+    an interpreter version adds on this path is then never assumed (CPython 3.11
+    moved a call's argument reference into the callee's frame)."""
+    out = []
+    for t in views:
+        out.append(sys.getrefcount(t))
+    return out
+
+
+def _calibrate_refs() -> int:
+    """The count ``_refcounts`` reports for a tensor that only a slot holds: its view-cache
+    list and its outputs dict (the probe holds one more reference, its local ``t``)."""
+    t = torch.empty(0)
+    cache, outputs = [t], {"view_0": t}
+    n = _refcounts(cache)[0] - 1
+    del outputs
+    return n
+
+
+_REFS_PIPELINE_ONLY = _calibrate_refs()
+
+
+def _all_unshared(views) -> bool:
+    """Nothing outside the pipeline holds any tensor of ``views`` or its memory: each tensor
+    object is referenced only by the slot's view cache list and outputs dict, and its storage
+    only by the tensor (a view, slice or chunk the caller kept shares the storage and raises
+    its use count)."""
+    if any(n > _REFS_PIPELINE_ONLY for n in _refcounts(views)):
         return False
     use_count = getattr(torch._C, "_storage_Use_Count", None)
     if use_count is None:  # no way to see views: never reuse
         return False
-    return use_count(t.untyped_storage()._cdata) <= 2  # t + the temporary storage object
+    return all(use_count(t.untyped_storage()._cdata) <= 2 for t in views)  # t + the temporary storage object
 
 
 class _Slot:
@@ -187,21 +212,47 @@ _LIVE: "weakref.WeakSet[MI355XAugPipeline]" = weakref.WeakSet()
 # The first request on a device takes the usual roles' streams in one fixed order (the
 # order a feed-driven side-route pipeline asks for them), so the mapping does not depend
 # on which kind of pipeline a process builds first.
+#
+# A set of role streams belongs to one live pipeline at a time: pipelines alive
+# together (train + val loaders) take different sets, so one's kernels never queue behind the
+# other's on a shared stream; a set is handed to the next pipeline once its owner closes.
 _ROLE_STREAMS: dict = {}
 _ROLE_LOCK = threading.Lock()
 _ROLE_ORDER = (("copy", 0), ("slot", 0), ("slot", 1), ("slot", 2), ("side_copy", 0), ("side_copy", 1))
+_SETS_BUSY: dict = {}   # device index -> stream-set ids held by live pipelines
 
 
-def role_stream(device, role: str, k: int = 0) -> torch.cuda.Stream:
+def _dev_index(device) -> int:
     dev = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
-    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    return dev.index if dev.index is not None else torch.cuda.current_device()
+
+
+def acquire_stream_set(device) -> int:
+    """The lowest stream-set id no live pipeline on ``device`` holds (released by ``close``)."""
+    idx = _dev_index(device)
     with _ROLE_LOCK:
-        if not any(key[0] == idx for key in _ROLE_STREAMS):
+        busy = _SETS_BUSY.setdefault(idx, set())
+        s = 0
+        while s in busy:
+            s += 1
+        busy.add(s)
+        return s
+
+
+def release_stream_set(device, s: int) -> None:
+    with _ROLE_LOCK:
+        _SETS_BUSY.get(_dev_index(device), set()).discard(s)
+
+
+def role_stream(device, role: str, k: int = 0, stream_set: int = 0) -> torch.cuda.Stream:
+    idx = _dev_index(device)
+    with _ROLE_LOCK:
+        if not any(key[:2] == (idx, stream_set) for key in _ROLE_STREAMS):
             for r, j in _ROLE_ORDER:
-                _ROLE_STREAMS[(idx, r, j)] = torch.cuda.Stream(device=idx)
-        st = _ROLE_STREAMS.get((idx, role, k))
+                _ROLE_STREAMS[(idx, stream_set, r, j)] = torch.cuda.Stream(device=idx)
+        st = _ROLE_STREAMS.get((idx, stream_set, role, k))
         if st is None:
-            st = _ROLE_STREAMS[(idx, role, k)] = torch.cuda.Stream(device=idx)
+            st = _ROLE_STREAMS[(idx, stream_set, role, k)] = torch.cuda.Stream(device=idx)
         return st
 
 
@@ -310,6 +361,7 @@ class MI355XAugPipeline:
         self._route = "device" if multiscan_route == "side" else multiscan_route  # what route_mask sees
         self._side = None
         self._ahead: deque = deque()   # prepared batches waiting for launch (side path)
+        self._side_hot = 0             # batches the look-ahead stays engaged for (see _pull_side)
         self._source_end = False
         workers = int(host_workers) if host_workers else min(8, os.cpu_count() or 1)
         self._host = fallback.HostDecoder(workers)
@@ -342,8 +394,10 @@ class MI355XAugPipeline:
         self._held: deque = deque()   # the feed's next batch, prepared one ahead (Pillow hand-overs start early)
         # H2D copies of the native feed's batches, off the slots' streams (DINO_COPY_STREAM=0: on them)
         self._copy_stream = None
+        self._device_arg = device
+        self._stream_set = acquire_stream_set(device)
         if (self._feed and depth > 1 and os.environ.get("DINO_COPY_STREAM", "1") != "0") or self._side_ahead:
-            self._copy_stream = role_stream(device, "copy")
+            self._copy_stream = role_stream(device, "copy", 0, self._stream_set)
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
@@ -352,7 +406,7 @@ class MI355XAugPipeline:
             if k == 0 and engine is not None:
                 eng = engine
             else:
-                stream = role_stream(device, "slot", k) if self.depth > 1 else None
+                stream = role_stream(device, "slot", k, self._stream_set) if self.depth > 1 else None
                 eng = IngestEngine(device, max_batch=self._batch_size, max_views=aug_cfg.n_views,
                                    max_crop_size=max_crop, max_image_dim=max_image_dim,
                                    workspace_bytes=workspace_bytes, stream=stream)
@@ -365,6 +419,20 @@ class MI355XAugPipeline:
             sizes = self._sizes()
             self._feed_sizes = sizes
             self._source.configure(max_image_dim=self._max_image_dim, cfg=self._cfg(*sizes))
+
+    @staticmethod
+    def side_queue(prefetch_ahead: int, side_ahead: int) -> int:
+        """The prefetch thread's queue length on the side route (see ``_pull_one``)."""
+        return prefetch_ahead + min(side_ahead, 4)
+
+    @staticmethod
+    def pulled_bound(depth: int, prefetch_ahead: int, side_ahead: int) -> int:
+        """Most batches pulled from the source and not yet handed over, on the side route: the
+        look-ahead, the prefetch queue, one being prepared on the prefetch thread and the
+        batches in flight.  A source whose metadata FIFO pairs each pulled batch with its
+        hand-over (reference _ReaderAdapter._meta_queue, shard_reader.py:98, 357-375) must
+        hold this many."""
+        return side_ahead + MI355XAugPipeline.side_queue(prefetch_ahead, side_ahead) + 1 + depth
 
     @property
     def engine(self) -> IngestEngine:
@@ -466,7 +534,7 @@ class MI355XAugPipeline:
         allocator's record_stream rule, applied at reuse)."""
         key = (batch, cfg.n_global, cfg.n_local, cfg.global_size, cfg.local_size, cfg.out_dtype)
         vc = sl.view_cache
-        if vc is not None and vc[0] == key and all(_unshared(t) for t in vc[1]):
+        if vc is not None and vc[0] == key and _all_unshared(vc[1]):
             if sl.consumer is not None and sl.engine.stream is not None:
                 ev = torch.cuda.Event()
                 ev.record(sl.consumer)
@@ -595,7 +663,7 @@ class MI355XAugPipeline:
             # launch: a queue longer than prefetch_ahead lets the look-ahead grow by up to 4
             # batches per launch (a queue of 1 would keep it where it starts) without pulling
             # many more batches from the source than the look-ahead holds
-            self._prefetcher = _Prefetcher(self, self.prefetch_ahead + min(self._side_ahead, 4))
+            self._prefetcher = _Prefetcher(self, self.side_queue(self.prefetch_ahead, self._side_ahead))
         return self._prefetcher.get(block)
 
     def _side_submit(self, pb: _Prepared) -> None:
@@ -611,7 +679,8 @@ class MI355XAugPipeline:
         if not len(idx):
             return
         if self._side is None:
-            self._side = progside.DeviceSideDecoder(self.device, max_image_dim=self._max_image_dim)
+            self._side = progside.DeviceSideDecoder(self.device, max_image_dim=self._max_image_dim,
+                                                    stream_set=self._stream_set)
         if pb.jpegs is not None:
             imgs = {int(i): pb.jpegs[i] for i in idx}
         elif pb.feed is not None:
@@ -676,10 +745,18 @@ class MI355XAugPipeline:
 
     def _pull_side(self) -> _Prepared:
         """The side path's look-ahead: keep up to side_ahead prepared batches, each with its
-        side decode started as it arrives; hand out the oldest."""
+        side decode started as it arrives; hand out the oldest.
+
+        The look-ahead is engaged only while coefficient-buffer images are about: a batch
+        with one (re)arms it for the next ``side_ahead`` batches pulled.  Disengaged, the
+        pipeline pulls one batch at a time and launches it from its own host buffer (feed
+        slot / pinned staging) as the plain route does, so a stream of baseline JPEGs pays
+        neither the HBM staging copy nor the look-ahead's extra buffers (with
+        the look-ahead always on the e2e rate fell from 145.6k to 125.6k img/s)."""
         t0 = time.perf_counter()
         try:
-            while not self._source_end and len(self._ahead) < self._side_ahead:
+            while not self._source_end and (not self._ahead or
+                                            (self._side_hot > 0 and len(self._ahead) < self._side_ahead)):
                 try:
                     pb = self._pull_one(block=not self._ahead)
                 except StopIteration:
@@ -688,7 +765,15 @@ class MI355XAugPipeline:
                 if pb is None:
                     break
                 self._side_submit(pb)
-                self._stage_on_device(pb)
+                if pb.side is not None:
+                    if self._side_hot == 0:  # engaging: the batches already ahead free their host buffers too
+                        for q in self._ahead:
+                            self._stage_on_device(q)
+                    self._side_hot = self._side_ahead
+                elif self._side_hot > 0:
+                    self._side_hot -= 1
+                if self._side_hot > 0:
+                    self._stage_on_device(pb)
                 self._ahead.append(pb)
             if not self._ahead:
                 raise StopIteration
@@ -1017,6 +1102,7 @@ class MI355XAugPipeline:
                     self._side.close()
                 for sl in self._slots:
                     sl.engine.close()
+                release_stream_set(self._device_arg, self._stream_set)
 
     def __del__(self):
         try:

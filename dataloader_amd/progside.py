@@ -98,13 +98,13 @@ class _SideEngine:
     Consecutive launches of a context are ordered by the dedicated stream itself."""
 
     def __init__(self, device: torch.device, max_images: int, max_image_dim: int, cu_count: int = 0,
-                 dedicated: bool = True, index: int = 0):
+                 dedicated: bool = True, index: int = 0, stream_set: int = 0):
         from .pipeline import role_stream
         self.raw = _create_stream(device.index or 0, int(cu_count)) if dedicated else None
-        self.stream = self.raw if dedicated else role_stream(device, "side", index)
+        self.stream = self.raw if dedicated else role_stream(device, "side", index, stream_set)
         self.eng = IngestEngine(device, max_batch=max_images, max_views=1, max_crop_size=8,
                                 max_image_dim=max_image_dim, workspace_bytes=64 << 20, stream=self.stream)
-        self.copy = role_stream(device, "side_copy", index)  # this context's torch stream (allocations, copies)
+        self.copy = role_stream(device, "side_copy", index, stream_set)  # this context's torch stream (allocations, copies)
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
         self.keep = None                             # host / device inputs of the mini-batch in flight
 
@@ -129,7 +129,7 @@ class DeviceSideDecoder:
     every context still has a mini-batch in flight (backpressure)."""
 
     def __init__(self, device: torch.device, max_images: int = 512, min_images: int | None = None,
-                 engines: int | None = None, max_image_dim: int = 0):
+                 engines: int | None = None, max_image_dim: int = 0, stream_set: int = 0):
         import os
         # measured (scripts/route_study.py, 16 progressive per 256-image batch, dedicated queues,
         # look-ahead 64, profiles/r03_side_pools.jsonl): pools of 16 images on 2 contexts 11.2k img/s,
@@ -148,6 +148,7 @@ class DeviceSideDecoder:
         self.min_images = max(1, min(int(min_images), self.max_images))
         self.cap = max(1, int(engines))
         self.max_image_dim = int(max_image_dim)
+        self.stream_set = int(stream_set)  # the owning pipeline's role streams (pipeline.acquire_stream_set)
         self._engines: list[_SideEngine] = []
         self._rr = 0
         self._pool: list = []   # (job, batch index, JPEG bytes)
@@ -175,7 +176,7 @@ class DeviceSideDecoder:
                 return e
         if len(self._engines) < self.cap:
             e = _SideEngine(self.device, self.max_images, self.max_image_dim, self.cu_count, self.dedicated,
-                            index=len(self._engines))
+                            index=len(self._engines), stream_set=self.stream_set)
             self._engines.append(e)
             return e
         e = self._engines[self._rr % len(self._engines)]

@@ -7,8 +7,10 @@ This is the feed of the Stage-3 device path:
   ``/dev/shm/<job_id>/<sha1(path)[:16]>`` laid out as ``[data_len:u64][magic:u64]``
   + tar bytes, magic ``0xDEADBEEFCAFEF00D`` written last (``:83-85, :689-703``),
   mmapped zero-copy (``get_view``, ``:584-609``).  The node master loads missing
-  shards synchronously and evicts LRU files over budget; the asyncio prefetch,
-  inotify waits and heartbeat of the reference are control plane (out of scope).
+  shards (``prefetch``: in the background, at most ``prefetch_window`` at once) and
+  evicts LRU files over budget; the other ranks wait for its writes (inotify,
+  ``:373-449``).  The heartbeat, orphan purge and signal handlers of the reference
+  are control plane (out of scope).
 * :func:`index_tar` — ``dino_tar_index`` (C++, ``csrc/tario.cpp``) over a mapped
   shard: WebDataset samples (key, .jpg range, .json range) without Python
   per-member work.
@@ -305,9 +307,11 @@ class ShmShardCache:
     :func:`index_tar` and :class:`ShardBatchFeeder` consume) and ``close``.
     """
 
+    WARN_INTERVAL_S = 60.0  # reference _SHM_WARN_INTERVAL
+
     def __init__(self, job_id: str = "dino", node_master: bool = True, max_gb: float = 128.0,
                  base_dir: str | os.PathLike = "/dev/shm", max_mapped: int = 256,
-                 shard_timeout_s: float = 300.0) -> None:
+                 shard_timeout_s: float = 300.0, prefetch_window: int = 4, warn_threshold: float = 0.85) -> None:
         self._base = Path(base_dir) / job_id
         self._base.mkdir(parents=True, exist_ok=True)
         self._node_master = node_master
@@ -318,6 +322,13 @@ class ShmShardCache:
         self._lock = threading.Lock()
         self._maps: OrderedDict[str, _Mapped] = OrderedDict()
         self._max_mapped = max_mapped
+        # the node master's background loads (reference prefetch: at most prefetch_window
+        # concurrent filesystem -> /dev/shm copies, shard_cache.py:548-559, 633)
+        self._window = max(1, int(prefetch_window))
+        self._pool = None
+        self._in_flight: dict = {}
+        self._warn_threshold = float(warn_threshold)
+        self._last_warn = 0.0
 
     @property
     def base(self) -> Path:
@@ -344,14 +355,27 @@ class ShmShardCache:
         if not self._node_master:
             wait_ready(shm, self.shard_timeout_s)
             return shm
+        with self._lock:
+            fut = self._in_flight.get(shard_path)
+        if fut is not None:  # a background load of this shard: wait for it (reference get_view, :588-595)
+            fut.result()
+            return shm
+        self._load(shard_path)
+        return shm
+
+    def _load(self, shard_path: str) -> None:
+        """Filesystem -> /dev/shm (node master; reference _load_one, shard_cache.py:624-688)."""
         with open(shard_path, "rb") as f:
             data = f.read()
         self.put(shard_path, data)
-        return shm
 
     def put(self, shard_path: str, data) -> Path:
-        """Write shard bytes into the cache (node master), evicting LRU shards over budget."""
+        """Write shard bytes into the cache (node master), evicting LRU shards over budget.  A
+        shard larger than the whole budget raises at once (reference [FIX-EVICT-EARLY], :648-655)."""
         n = len(data) if not isinstance(data, np.ndarray) else data.nbytes
+        if n > self._max_bytes:
+            raise RuntimeError(f"ShmShardCache: shard {shard_path!r} ({n >> 20} MB) exceeds the entire shm budget "
+                               f"({self._max_bytes >> 30} GB). Increase node_shm_gb.")
         shm = self._path(shard_path)
         with self._lock:
             while self._lru and self._total + n > self._max_bytes:
@@ -362,7 +386,22 @@ class ShmShardCache:
         with self._lock:
             self._lru[shard_path] = n
             self._total += n
+        self._check_utilisation()
         return shm
+
+    def _check_utilisation(self) -> None:
+        """Warn (at most once a minute) when the cache is over ``warn_threshold`` of its budget
+        (reference _update_utilisation_metric, shard_cache.py:738-753)."""
+        import time
+        import warnings
+        util = self.utilisation
+        now = time.monotonic()
+        if util >= self._warn_threshold and now - self._last_warn >= self.WARN_INTERVAL_S:
+            self._last_warn = now
+            warnings.warn(f"/dev/shm utilisation is {util * 100:.1f}% (threshold {self._warn_threshold * 100:.0f}%). "
+                          "Increase node_shm_gb or reduce shard_prefetch_window. Budget: "
+                          f"{self._max_bytes / (1 << 30):.1f} GB, used: {self._total / (1 << 30):.1f} GB.",
+                          RuntimeWarning, stacklevel=3)
 
     def _drop(self, shard_path: str) -> None:
         m = self._maps.get(shard_path)
@@ -372,8 +411,25 @@ class ShmShardCache:
             self._path(shard_path).unlink()
 
     def prefetch(self, shard_path: str) -> None:
-        if self._node_master:
-            self._ensure(shard_path)
+        """Schedule a shard for background loading (node master only; reference :548-559): at
+        most ``prefetch_window`` loads run at once, a shard already cached or loading is skipped."""
+        if not self._node_master:
+            return
+        if is_ready(self._path(shard_path)):
+            return
+        with self._lock:
+            if shard_path in self._in_flight:
+                return
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._pool = ThreadPoolExecutor(max_workers=self._window, thread_name_prefix="shard-io")
+            fut = self._pool.submit(self._load, shard_path)
+            self._in_flight[shard_path] = fut
+
+        def _done(_f, p=shard_path):
+            with self._lock:
+                self._in_flight.pop(p, None)
+        fut.add_done_callback(_done)
 
     def _acquire(self, shard_path: str) -> _Mapped:
         shm = self._ensure(shard_path)
@@ -423,6 +479,9 @@ class ShmShardCache:
             return self._total / self._max_bytes
 
     def close(self, remove: bool = False) -> None:
+        pool, self._pool = self._pool, None
+        if pool is not None:
+            pool.shutdown(wait=True, cancel_futures=True)
         with self._lock:
             for m in self._maps.values():
                 m.close()
@@ -748,6 +807,9 @@ class NativeShardFeed:
                             "dino_feed_set_shard_wait")
             self._check(lib.dino_feed_set_shuffle(self._feed, int(self._shuffle), self._seed & (2**64 - 1)),
                         "dino_feed_set_shuffle")
+        # the in-shard order is keyed by this epoch, as the shard order is (a resumed
+        # reset(epoch=k) on a fresh feed keyed the samples by the number of resets instead)
+        self._check(lib.dino_feed_set_epoch(self._feed, int(self.epoch) & (2**64 - 1)), "dino_feed_set_epoch")
         for p in self.epoch_order():
             shm = self._cache._ensure(p) if self._cache.node_master else self._cache.path_of(p)
             self._check(lib.dino_feed_push(self._feed, str(shm).encode()), "dino_feed_push")

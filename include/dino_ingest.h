@@ -388,6 +388,10 @@ int dino_feed_set_shard_wait(dino_feed* feed, int32_t timeout_ms);
 /* enable != 0: each shard's samples are taken in a seeded random order keyed by (seed, epoch,
  * shard path) (the extraction step's shuffle buffer, hpc_source.py:461-467). */
 int dino_feed_set_shuffle(dino_feed* feed, int32_t enable, uint64_t seed);
+/* The epoch that keys the shuffle of the shards opened from now on (default: epochs since create,
+ * i.e. dino_feed_reset calls), so that a job resumed at epoch k gets epoch k's sample order
+ * (reference ShardIterator.reset_epoch, hpc_source.py:242-273). */
+int dino_feed_set_epoch(dino_feed* feed, uint64_t epoch);
 /* Next packed batch in order (blocks up to timeout_ms; < 0: forever). */
 int dino_feed_next(dino_feed* feed, int32_t timeout_ms, dino_feed_batch* out);
 /* H2D copies of a handed-out slot (bytes, offsets) on `stream`; the slot is reused after they retire. */

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Round-4 closing GPU session: parity tests + smoke, the driver's default bench line, depth-1
-# rocprofv3 kernel summaries (C2, C3) and the FETCH / WRITE PMC passes (C2, C3).
-# usage: scripts/gpu_r4_final.sh TAG [tests|bench|prof|pmc|all]
+# GPU session: parity tests + smoke, the driver's default bench line, depth-1 rocprofv3
+# kernel summaries (C2, C3) and the FETCH / WRITE PMC passes (C2, C3).
+# usage: scripts/gpu_session.sh TAG [tests|bench|prof|pmc|all]  (comma list)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${1:-r4z}
+TAG=${1:-r5}
 WHAT=${2:-all}
 has() { [ "$WHAT" = all ] || [[ ",$WHAT," == *",$1,"* ]]; }
 if has tests; then

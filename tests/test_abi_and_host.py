@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import ctypes
 import re
+import struct
 from pathlib import Path
 
 import numpy as np
@@ -91,18 +92,36 @@ def test_backend_protocol_surface():
 
 
 def test_shard_cache_lru(tmp_path):
+    """build_shard_cache gives the node-shared /dev/shm cache (reference dali_backend.py:85-105):
+    reference file format, LRU eviction over the budget, background prefetch, a shard larger
+    than the whole budget raises ([FIX-EVICT-EARLY])."""
+    from dataloader_amd import tario
     from dataloader_amd.backend import MI355XBackend
-    cache = MI355XBackend().build_shard_cache(max_gb=100 / (1 << 30))
+    cache = MI355XBackend().build_shard_cache(job_id="lru", node_master=True, max_gb=100 / (1 << 30),
+                                              prefetch_window=2, timeout_s=5.0, warn_threshold=0.5,
+                                              base_dir=tmp_path / "shm")
+    assert isinstance(cache, tario.ShmShardCache) and cache.node_master and cache.shard_timeout_s == 5.0
     paths = []
     for i in range(3):
         p = tmp_path / f"s{i}.tar"
         p.write_bytes(bytes([i]) * 40)
         paths.append(str(p))
-    for p in paths:
-        assert len(cache.get(p)) == 40
+    with pytest.warns(RuntimeWarning, match="utilisation"):
+        for p in paths:
+            assert cache.get(p) == bytes([paths.index(p)]) * 40
     assert cache.utilisation <= 1.0
+    assert not tario.is_ready(cache.path_of(paths[0])) and tario.is_ready(cache.path_of(paths[2]))  # evicted
     with cache.get_view(paths[-1]) as mv:
         assert bytes(mv[:1]) == b"\x02"
+    raw = cache.path_of(paths[2]).read_bytes()
+    assert struct.unpack("QQ", raw[:16]) == (40, tario.READY_MAGIC) and raw[16:] == b"\x02" * 40
+    cache.prefetch(paths[0])                               # background load, then a blocking get
+    assert cache.get(paths[0]) == b"\x00" * 40
+    big = tmp_path / "big.tar"
+    big.write_bytes(b"x" * 200)
+    with pytest.raises(RuntimeError, match="exceeds the entire shm budget"):
+        cache.get(str(big))
+    cache.close(remove=True)
 
 
 def test_masking_generator_validation_matches_reference():
@@ -182,10 +201,22 @@ def test_backend_side_look_ahead_fits_the_metadata_fifo():
         def __init__(self, n):
             self._meta_queue = queue.Queue(maxsize=n)
 
+    from dataloader_amd.pipeline import MI355XAugPipeline
+
     be = MI355XBackend()
+    # worst case pulled and not handed over: look-ahead + prefetch queue (1 + min(ahead, 4)) +
+    # 1 being prepared + the batches in flight; one FIFO entry stays spare
+    assert MI355XAugPipeline.pulled_bound(3, 1, 48) == 48 + 5 + 1 + 3
     assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 48
     assert be.side_look_ahead(PipelineConfig(), object(), 3) == 48
-    assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 6
-    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), Src(64), 3) == 64 - 3 - 6
+    assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 7
+    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), Src(64), 3) == 64 - 3 - 7
     assert be.side_look_ahead(PipelineConfig(cpu_queue=60), object(), 3) == 60
     assert MI355XBackend(side_ahead=8).side_look_ahead(PipelineConfig(), Src(64), 3) == 8
+    assert MI355XBackend(side_ahead=80).side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7
+    for cap in (12, 20, 64):
+        for depth in (1, 3, 6):
+            for cq in (1, 16, 60, 200):
+                a = be.side_look_ahead(PipelineConfig(cpu_queue=cq), Src(cap), depth)
+                if a > 1:
+                    assert MI355XAugPipeline.pulled_bound(depth, be.PREFETCH, a) + 1 <= cap, (cap, depth, cq)

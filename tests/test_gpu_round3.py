@@ -24,7 +24,6 @@ from dataloader_amd.config import DINOAugConfig, DinoV2AugSpec, PipelineConfig
 from dataloader_amd.engine import IngestEngine, pack_jpegs
 from dataloader_amd.synthetic import encode_jpeg, textured_rgb
 from oracle import cpu_ref
-from tests.helpers import record_to_params
 
 pytestmark = pytest.mark.gpu
 
@@ -125,16 +124,15 @@ def test_prefetch_thread_epochs_and_reset(gpu_device):
     pipe.close()
 
 
-def _check_pipeline_views(pipe, jpegs, out, nv, tol=0.05):
+def _check_pipeline_views(pipe, jpegs, out, nv):
+    """The views of the pipeline's last batch against the oracle: bit-exact except blur, which
+    may differ by one uint8 level on <= 0.5 % of a view's values."""
+    from tests.test_gpu_parity import _check_views
     recs = pipe.last_params()
-    for b, jpg in enumerate(jpegs):
-        img = cpu_ref.decode_rgb(jpg)
-        for v in range(nv):
-            p = record_to_params(recs[b * nv + v])
-            ref = cpu_ref.augment_one(jpg, p, decoded=img, out_dtype=torch.float32)
-            got = out[f"view_{v}"][b].float().cpu()
-            err = (ref - got).abs()
-            assert err.max().item() <= tol, (b, v, err.max().item())
+    views = [out[f"view_{v}"] for v in range(nv)]
+    dt = views[0].dtype
+    cfg = pipe._aug_cfg
+    _check_views(jpegs, views, recs, nv, dt, cfg.mean, cfg.std)
 
 
 def test_wide_and_tall_jpegs_on_device_and_over_a_limit(gpu_device):

@@ -10,7 +10,8 @@ lifetime, and output-buffer reuse under caller-held views.
 * closing a side pipeline destroys its dedicated streams, and a new one works in the same
   process (the segfault at close, gpurun_out/ss2.err);
 * a caller that keeps only a slice of an output keeps its data (reuse was decided
-  on the tensor object's refcount, blind to views).
+  on the tensor object's refcount, blind to views);
+* the colour conversion's quad and band edge cases.
 """
 
 from __future__ import annotations
@@ -203,64 +204,15 @@ def test_kept_slice_of_an_output_is_not_refilled(gpu_device):
     assert len(set(ptrs)) < nb  # the batches nobody kept were refilled in place
 
 
-@pytest.mark.parametrize("comps", [7, 6])
-def test_lane_mode_refinement_bit_exact(gpu_device, monkeypatch, comps):
-    """k_prefine (DINO_PREFINE_COMPS: AC refinement scans decoded one lane per image and
-    component, measured and off by default): the progressive zoo, the damaged streams and
-    the test writer's progressions decode bit-exact with Pillow with every component (7) or
-    the chroma components (6) in lane mode."""
-    from tests import jpeg_writer as jw
-    from tests.test_emu_cpu import _damaged_streams
-    from tests.test_gpu_parity import _to_dev
-    from tests.test_gpu_round2 import _prog_zoo
-    from tests.test_multiscan_cpu import multiscan_cases
-    from dataloader_amd.engine import IngestEngine
-    from oracle import cpu_ref
-    monkeypatch.setenv("DINO_PREFINE_COMPS", str(comps))
-    rng = np.random.default_rng(74)
-    cases = [("zoo", j) for j in _prog_zoo(rng)] + list(_damaged_streams(rng)) + \
-        multiscan_cases(rng, sizes=((83, 61), (130, 97)))
-    img = textured_rgb(48, 40, rng)
-    for k, (w, h) in enumerate(((48, 40), (333, 250))):  # two refinements of luma, chroma refined in between
-        img = textured_rgb(w, h, rng)
-        cases.append((f"refine_chain_{k}", jw.encode(img, [jw.scan((0, 1, 2), 0, 0, 0, 0), jw.scan((0,), 1, 63, 0, 2),
-                                                         jw.scan((1,), 1, 63, 0, 1), jw.scan((2,), 1, 63, 0, 1),
-                                                         jw.scan((0,), 1, 63, 2, 1), jw.scan((1,), 1, 63, 1, 0),
-                                                         jw.scan((0,), 1, 63, 1, 0), jw.scan((2,), 1, 63, 1, 0)],
-                                                     progressive=True)))
-    jpegs = [j for _, j in cases]
-    eng = IngestEngine(gpu_device, max_batch=len(jpegs), max_views=10, max_crop_size=224)
-    d_bytes, d_off = _to_dev(jpegs, gpu_device)
-    info = eng.decode(d_bytes, d_off, len(jpegs)).cpu().numpy()
-    bad = []
-    for i, (name, j) in enumerate(cases):
-        ref = cpu_ref.decode_rgb(j)
-        if ref is None:
-            if info[i, 0] >= 0:
-                bad.append((name, "status", int(info[i, 0])))
-            continue
-        ref = np.asarray(ref)
-        if info[i, 0] != 0:
-            bad.append((name, "status", int(info[i, 0])))
-            continue
-        got = eng.copy_rgb(i, ref.shape[1], ref.shape[0]).cpu().numpy()
-        if not np.array_equal(got, ref):
-            bad.append((name, int((got != ref).sum())))
-    eng.close()
-    assert not bad, bad
-
-
-@pytest.mark.parametrize("fuse", ["1", "0"])
-def test_fused_luma_colour_bands_bit_exact(gpu_device, monkeypatch, fuse):
-    """k_ycolor (luma IDCT + 4:2:0 colour conversion per 8-row band, the luma plane kept in
-    LDS; opt-in, DINO_FUSE=1): widths on both sides of its 2304-pixel limit and of every residue
-    mod 4 (quads that wrap a row), heights that end inside a band, the smallest fancy-upsampled
-    chroma (3 samples wide) next to box-upsampled 2-sample chroma, baseline, restart-interval
-    and progressive files, and the unfused samplings in the same batch: bit-exact with Pillow."""
+def test_colour_quads_and_band_edges_bit_exact(gpu_device):
+    """k_idct + k_color over widths of every residue mod 4 (4:2:0 quads that wrap a row), heights
+    that end inside an 8-row band, the smallest fancy-upsampled chroma (3 samples wide) next to
+    box-upsampled 2-sample chroma, baseline, restart-interval and progressive files, and other
+    samplings in the same batch: bit-exact with Pillow (the round-4 fused k_ycolor was measured
+    slower and removed; these are its edge cases on the kernels that remain)."""
     from tests.test_gpu_parity import _to_dev
     from dataloader_amd.engine import IngestEngine
     from oracle import cpu_ref
-    monkeypatch.setenv("DINO_FUSE", fuse)  # read by dino_ctx_create (measured and off by default)
     rng = np.random.default_rng(404)
     cases = []
     for w, h in ((2304, 17), (2305, 9), (2303, 23), (2302, 8), (2301, 31), (5, 5), (4, 4), (6, 3), (13, 11),

@@ -156,7 +156,9 @@ def test_shm_cache_format_and_views(tmp_path):
     tar = make_shard(5, seed=4)
     src = tmp_path / "shard-000.tar"
     src.write_bytes(tar)
-    cache.prefetch(str(src))                                   # node master loads it
+    cache.prefetch(str(src))                                   # node master loads it (in the background)
+    cache.prefetch(str(src))                                   # loading already: not scheduled twice
+    assert cache.get(str(src)) == tar                          # waits for the background load
     shm = tmp_path / "job" / hashlib.sha1(str(src).encode()).hexdigest()[:16]
     raw = shm.read_bytes()
     assert struct.unpack_from("QQ", raw) == (len(tar), 0xDEADBEEFCAFEF00D) and raw[16:] == tar
@@ -344,11 +346,17 @@ def test_native_feed_batches_epochs_and_errors(tmp_path, nthreads):
     cache.close(remove=True)
 
 
-def _feed_reader(base, job, paths, rank, world, timeout_s, q):
+def _feed_reader(base, job, paths, rank, world, timeout_s, q, via_backend=False):
     """A non-master rank (spawned process): drive NativeShardFeed over the node cache while the
-    master is still writing it; report the bytes of every batch."""
+    master is still writing it; report the bytes of every batch.  ``via_backend``: the cache comes
+    from the drop-in factory, MI355XBackend.build_shard_cache (reference dali_backend.py:85-105)."""
     from dataloader_amd import tario as t
-    cache = t.ShmShardCache(job_id=job, base_dir=base, node_master=False, shard_timeout_s=timeout_s)
+    if via_backend:
+        from dataloader_amd.backend import MI355XBackend
+        cache = MI355XBackend().build_shard_cache(job_id=job, node_master=False, max_gb=1.0, prefetch_window=4,
+                                                  timeout_s=timeout_s, warn_threshold=0.85, base_dir=base)
+    else:
+        cache = t.ShmShardCache(job_id=job, base_dir=base, node_master=False, shard_timeout_s=timeout_s)
     feed = t.NativeShardFeed(cache, paths, 4, rank=rank, world=world, nthreads=2, slots=3)
     out = []
     try:
@@ -441,6 +449,56 @@ def test_non_master_ranks_wait_for_the_node_master(tmp_path):
     master.close(remove=True)
 
 
+def test_backend_shard_cache_master_and_readers(tmp_path):
+    """the drop-in factory gives the node-shared cache.  One master (this process,
+    ``build_shard_cache(node_master=True)``) loads the shards from the filesystem in the
+    background (``prefetch``); two non-master processes (``node_master=False``) drive the native
+    feed over it while it is being written; each gets every batch bit-identical to a pre-written
+    cache."""
+    import multiprocessing as mp
+
+    from dataloader_amd.backend import MI355XBackend
+    shards = [make_shard(n, seed=90 + k) for k, n in enumerate([9, 6, 8, 7, 5])]
+    src_dir = tmp_path / "lustre"
+    src_dir.mkdir()
+    paths = []
+    for k, t in enumerate(shards):
+        p = src_dir / f"shard-{k:03d}.tar"
+        p.write_bytes(t)
+        paths.append(str(p))
+    expect = {r: _expected_batches(tmp_path, shards, paths, r, 2) for r in range(2)}
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_feed_reader, args=(tmp_path, "nodejob", paths, r, 2, 60.0, q, True))
+             for r in range(2)]
+    for pr in procs:
+        pr.start()
+    master = None
+    try:
+        import time
+        time.sleep(1.0)                                  # readers up and waiting before the master exists
+        master = MI355XBackend().build_shard_cache(job_id="nodejob", node_master=True, max_gb=1.0,
+                                                   prefetch_window=2, timeout_s=60.0, warn_threshold=0.85,
+                                                   base_dir=tmp_path)
+        for p in paths:
+            master.prefetch(p)
+        got = {}
+        for _ in procs:
+            r, batches, errs = q.get(timeout=120)
+            got[r] = (batches, errs)
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+    for r in range(2):
+        batches, errs = got[r]
+        assert errs == [] and batches == expect[r] and len(batches) > 0, r
+    for p, t in zip(paths, shards):                      # the master's own view of its cache
+        assert master.get(p) == t
+    master.close(remove=True)
+
+
 def test_native_feed_shuffle_orders(tmp_path):
     """shuffle=True: the reference's per-epoch shard order (numpy default_rng(seed + rank +
     epoch * 997).shuffle, hpc_source.py:263, 488-500) and a seeded in-shard order; the same
@@ -477,6 +535,13 @@ def test_native_feed_shuffle_orders(tmp_path):
     assert e0 != plain                                   # samples shuffled inside each shard
     first = {img for _, img, _ in oracle_samples(shards[paths.index(order[0])])}
     assert set(e0[:8]) == first                          # ... but shard by shard
-    for f in (f1, f2):
+    # resume: a fresh feed reset to epoch 2 gives the epoch-2 order of a feed that ran
+    # epochs 0 and 1, shard order and in-shard order alike
+    f1.reset()
+    e2 = epoch_imgs(f1)
+    f3 = tario.NativeShardFeed(cache, paths, 4, nthreads=2, shuffle=True, seed=5)
+    f3.reset(epoch=2)
+    assert f3.epoch_order() == f1.epoch_order() and epoch_imgs(f3) == e2 != e1
+    for f in (f1, f2, f3):
         f.close()
     cache.close(remove=True)
