@@ -495,15 +495,23 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 // reaches a block boundary the first decode also passed through (same bit
 // position, same block-in-MCU index), everything after it is what the first
 // decode already found: its end state and remaining block count are reused.
+// `match` (optional): the matched checkpoint's position and first-decode block index
+// ({0xFFFFFFFF, -1}: none; the re-decode ran to the range end).
+struct SyncMatch {
+  uint32_t pos;
+  int32_t m0;
+};
 template <int kWin>
 DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
-                               const Checkpoint* cps, int cstride, int ncp, RangeOut first) {
+                               const Checkpoint* cps, int cstride, int ncp, RangeOut first,
+                               SyncMatch* match = nullptr) {
   st = sanitize(st, im.blocks_per_mcu);
   int32_t nblk = 0;
   int j = 0;
   BitCursor cur;
   bc_init<kWin>(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;
+  if (match) *match = SyncMatch{0xFFFFFFFFu, -1};
   // the next checkpoint at or after the position, kept in registers: memory is only
   // read when the decode passes one (every kHuffCpStride blocks), not at every block
   Checkpoint cp = ncp > 0 ? cps[0] : Checkpoint{0xFFFFFFFFu, 0u};
@@ -513,6 +521,7 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
       if (cp.pos == cur.pos && (int32_t)(cp.cn & 15u) == blk) {
         RangeOut r = first;
         r.nblk = nblk + first.nblk - (int32_t)(cp.cn >> 4);
+        if (match) *match = SyncMatch{cp.pos, (int32_t)(cp.cn >> 4)};
         return r;
       }
       nblk++;
@@ -587,6 +596,129 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
     }
   }
   return cur.pos;
+}
+
+// The first (speculative) decode of a range that also emits the range's blocks: one pass
+// that is decode_range (end state at the first step boundary >= rend, blocks whose DC
+// step starts before rend, checkpoints) and, if `st` turns out to be the true state,
+// decode_write (the blocks opened before wend, values included) at once, so that a lane
+// whose guessed start state the sync rounds confirm never decodes its range again.
+// Blocks go to the sink under local indices 0, 1, .. (their absolute index is only known
+// after the block scan), as long as sink.room(j) holds (kEmitOverflow past that: the lane
+// is then rewritten from its true state).  The insufficient-data rule of decode_write stops
+// the emission with kEmitInsufficient (every later block of the image is zero).  Once
+// the emission has stopped, the decode goes on state-only up to rend.
+constexpr int32_t kEmitOverflow = 1, kEmitInsufficient = 2;
+struct EmitOut {
+  RangeOut r;       // as decode_range's
+  int32_t nemit;    // blocks emitted (local indices [0, nemit))
+  int32_t flags;    // kEmitOverflow | kEmitInsufficient
+};
+template <int kWin, typename Sink>
+DHD EmitOut decode_emit(const BitReader& br, const HuffImage& im, HState st, uint32_t rend, uint32_t wend,
+                        uint32_t avail, Checkpoint* cps, int cstride, int kmax, int32_t* ncp, Sink& sink) {
+  st = sanitize(st, im.blocks_per_mcu);
+  EmitOut o;
+  o.nemit = 0;
+  o.flags = 0;
+  int32_t nblk = 0;
+  int n = 0;
+  bool ended = false;
+  HState endS{0u, 0, 0};
+  BitCursor cur;
+  bc_init<kWin>(cur, br, st.pos);
+  int32_t blk = st.c, z = st.z;
+  // the previous lane's block: state only (decode_write skips it, decode_range passes it)
+  while (z != 0) {
+    if (!ended && cur.pos >= rend) {
+      endS = HState{cur.pos, blk, z};
+      ended = true;
+    }
+    state_step<kWin>(cur, br, im, blk, z);
+  }
+  bool emitting = cur.pos < wend;
+  bool open = false;
+  // one step per iteration (blocks opened and closed inside the loop, as decode_write)
+  for (;;) {
+    if (z == 0) {  // a block boundary
+      if (!ended && cur.pos >= rend) {
+        endS = HState{cur.pos, blk, z};
+        ended = true;
+      }
+      if (!ended) {
+        if (n < kmax && (nblk < kHuffCpDense || (nblk & (kHuffCpStride - 1)) == 0))
+          cps[(n++) * cstride] = Checkpoint{cur.pos, ((uint32_t)nblk << 4) | (uint32_t)blk};
+        nblk++;
+      }
+      if (emitting && !open) {
+        if (blk == 0 && cur.pos > avail) {  // insufficient_data before this MCU: the rest stays zero
+          o.flags |= kEmitInsufficient;
+          emitting = false;
+        } else if (!sink.room(o.nemit)) {
+          o.flags |= kEmitOverflow;
+          emitting = false;
+        } else {
+          sink.begin(o.nemit);
+          open = true;
+        }
+      }
+      if (!emitting && ended) break;
+    }
+    if (open) {
+      const StepOut so = huff_step<kWin>(cur, br, im, blk, z);
+      if (so.kind == 0) sink.dc((int16_t)so.value);
+      else if (so.kind == 1) sink.ac(so.zz, (int16_t)so.value);
+      if (so.block_done) {
+        sink.end();
+        ++o.nemit;
+        open = false;
+        if (cur.pos >= wend) emitting = false;
+      }
+    } else {
+      state_step<kWin>(cur, br, im, blk, z);
+    }
+    if (!ended && cur.pos >= rend && z != 0) {  // the first step boundary >= rend, inside a block
+      endS = HState{cur.pos, blk, z};
+      ended = true;
+    }
+    if (!emitting && !open && ended) break;
+  }
+  o.r.end = endS;
+  o.r.nblk = nblk;
+  *ncp = n;
+  return o;
+}
+
+// decode_write's emission from a true state `st` up to the block boundary at bit position
+// `stop` (exclusive: the block starting there is not emitted), for the prefix of a lane
+// whose first decode joins the true decode at a checkpoint at `stop`.  Returns the blocks
+// emitted (absolute indices first_block, ..).
+template <int kWin, typename Sink>
+DHD int32_t decode_write_prefix(const BitReader& br, const HuffImage& im, HState st, uint32_t stop, int32_t first_block,
+                                int32_t total_blocks, Sink& sink) {
+  st = sanitize(st, im.blocks_per_mcu);
+  BitCursor cur;
+  bc_init<kWin>(cur, br, st.pos);
+  int32_t blk = st.c, z = st.z;
+  while (z != 0) huff_step<kWin>(cur, br, im, blk, z);  // the previous lane's block
+  int32_t b = first_block;
+  bool open = false;
+  while (b < total_blocks) {
+    if (!open) {
+      if (cur.pos >= stop) break;
+      sink.begin(b);
+      open = true;
+    }
+    const StepOut so = huff_step<kWin>(cur, br, im, blk, z);
+    if (so.kind == 0) sink.dc((int16_t)so.value);
+    else if (so.kind == 1) sink.ac(so.zz, (int16_t)so.value);
+    if (so.block_done) {
+      sink.end();
+      ++b;
+      open = false;
+    }
+  }
+  return b - first_block;
 }
 
 // Element offset (int16 units) of absolute block b inside the image's coefficient area.

@@ -126,6 +126,7 @@ __device__ void plan_place(ImgDesc& d, const ChunkSizes& z, int64_t base, int64_
   d.ent_off = base;
   d.rst_off = d.ent_off + z.ent;
   d.coef_off = d.rst_off + z.rst;
+  d.emit_off = d.coef_off + (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;  // (emit_reserved images)
   d.binfo_off = d.coef_off + z.coef;
   d.plane_off = d.binfo_off + z.binfo;
   d.rgb_off = d.plane_off + z.plane;
@@ -563,7 +564,7 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 }
 
 // Entry words a lane buffers in LDS before it stores them as one aligned group: 32-byte
-// groups in k_huff1 (its buffers borrow the skip tables' LDS), 64-byte groups in k_huff3.
+// groups in k_huff1, 64-byte groups in k_huff3.
 // Word w of lane t sits at [w][t], so the lanes' halfword writes never share a bank.
 // (Measured and dropped, DESIGN.md §5: a register shift register instead of LDS, block
 // records buffered and stored in pairs or groups, 64-byte groups in k_huff1.)
@@ -576,13 +577,10 @@ struct HuffLds {     // k_huff1
   RangeOut R[kHuffThreads];
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
+  // SparseSink buffers of the emitting first decode and of the prefix / rewrite writes
+  // (their own LDS: other waves of the item still run state-only decodes on the skip tables)
+  uint32_t sink[kSinkLds * kHuffThreads];
 };
-// k_huff1's write pass (single-segment images) decodes values, not skips: the SparseSink
-// buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
-// (and the range results R, which follow the tables and are read before the write pass)
-static_assert(offsetof(HuffLds, R) == offsetof(HuffLds, tab) + sizeof(HuffTables), "R follows the tables");
-static_assert(sizeof(HuffSkip) + sizeof(RangeOut) * kHuffThreads >= (size_t)kSinkLds * 4 * kHuffThreads,
-              "sink buffers fit the skip tables and R");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
@@ -616,7 +614,9 @@ template <int W>  // entry words buffered per lane in LDS
 struct SparseSinkT {
   static_assert(W % 4 == 0 && W > 0, "whole 16-byte chunks");
   uint32_t* ent;   // image entry area
-  uint2* binfo;    // image block info
+  uint2* binfo;    // image block info (emission: the lane's top record, records grow down)
+  int32_t rdir;    // record b at binfo[rdir * b]: 1, or -1 in an emission region
+  uint32_t rlim;   // emission: room(j) holds while entries + a whole block stay below record j
   uint32_t n;      // halfwords in stored groups (relative to the image entry area), multiple of 2 W
   uint32_t k;      // halfwords buffered in LDS
   uint32_t bstart, dcw, n16, n32;
@@ -634,7 +634,19 @@ struct SparseSinkT {
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
+    rdir = 1;
   }
+  // An emission region [base, base + cap) halfwords (decode_emit): entries from its bottom,
+  // record j at halfwords base + cap - 4 (j + 1).
+  __device__ void open_emit(uint32_t base, uint32_t cap) {
+    n = base;
+    k = 0;
+    binfo = (uint2*)(ent + ((base + cap) >> 1)) - 1;
+    rdir = -1;
+    rlim = base + cap - 4 - (kEntHalfwordsPerBlock + 2 * W);
+  }
+  // block j fits: its entries (<= 128 halfwords + the group padding) end below its record
+  __device__ bool room(int32_t j) const { return n + k + 4u * (uint32_t)j <= rlim; }
   __device__ void begin(int32_t blk) {
     b = blk;
     bstart = n + k;
@@ -667,7 +679,7 @@ struct SparseSinkT {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void record(int32_t blk, uint2 r) { binfo[blk] = r; }
+  __device__ void record(int32_t blk, uint2 r) { binfo[rdir * blk] = r; }
   __device__ void end() { record(b, make_uint2(bstart, n16 | (n32 << 7) | dcw)); }
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
@@ -817,7 +829,7 @@ __device__ int huff_item_image(const ImgDesc* desc, int B, int item) {
 // in-segment rounds).  Long ranges stay with k_huff3: in k_huff1 their second
 // decode would double the longest serial chain of the launch.
 __device__ __forceinline__ bool huff_single_segment(const ImgDesc& d) {
-  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= 3072;
+  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= kHuffFuseSubBits && emit_reserved(d);
 }
 
 // Loads work item `item`'s image descriptor and tables into LDS; false past the end.
@@ -843,22 +855,55 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
 }
 
 #ifdef DINO_HUFF_PHASES
-// Phase timestamps of k_huff1 work items (instrumented builds only, scripts/huff_phases.py):
-// [item][0..4] = start, after the first decode, after the sync rounds, end; [item][4] = rounds.
+// Phase data of k_huff1 work items (instrumented builds only, scripts/huff_phases.py):
+// [item][0] start, [1] the last lane's end of its look-back, [2] after the first decode,
+// [3] after the sync rounds, [4] end (wall_clock64); [5] rounds | single-segment << 32;
+// [6] lanes re-decoded, [7] their summed bits up to the matched checkpoint, [8] the
+// largest such prefix, [9] re-decoded lanes that matched no checkpoint, [10] lanes whose
+// emission region filled, [11] lanes of single-segment items written again whole.
 constexpr int kPhaseItems = 8192;
-__device__ uint64_t g_huff_phase[kPhaseItems][5];
+constexpr int kPhaseSlots = 12;
+__device__ uint64_t g_huff_phase[kPhaseItems][kPhaseSlots];
 #define HUFF_PHASE(k, v)                                              \
   do {                                                               \
     if (threadIdx.x == 0 && item < kPhaseItems) g_huff_phase[item][k] = (v); \
+  } while (0)
+#define HUFF_PHASE_ADD(k, v)                                                         \
+  do {                                                                              \
+    if (item < kPhaseItems) atomicAdd((unsigned long long*)&g_huff_phase[item][k], (unsigned long long)(v)); \
+  } while (0)
+#define HUFF_PHASE_MAX(k, v)                                                         \
+  do {                                                                              \
+    if (item < kPhaseItems) atomicMax((unsigned long long*)&g_huff_phase[item][k], (unsigned long long)(v)); \
   } while (0)
 #else
 #define HUFF_PHASE(k, v) \
   do {                   \
   } while (0)
+#define HUFF_PHASE_ADD(k, v) \
+  do {                       \
+  } while (0)
+#define HUFF_PHASE_MAX(k, v) \
+  do {                       \
+  } while (0)
 #endif
 
 constexpr int kHuffLookback = 2048;  // bits a lane decodes before its range to guess its start state
 
+// k_huff1 per work item: every lane guesses its start state from kHuffLookback bits before
+// its range (decode_lookback), decodes its range from the guess (the first decode), then
+// sync rounds inside the item re-decode the ranges whose start state changed, stopping at
+// the first checkpoint the first decode also passed.  Items of a multi-segment or a long-
+// range image leave their lane records to k_huff2 / k_huff3.  A single-segment image
+// (huff_single_segment) is finished here: its first decode emits every lane's blocks into
+// the lane's emission region (decode_emit), and after the rounds and the block scan
+//   * a lane whose guess the rounds confirmed copies its block records into place (its
+//     entries stay where they were emitted);
+//   * a lane re-decoded from its true state that joined its first decode at a checkpoint
+//     writes the blocks up to that checkpoint (decode_write_prefix, into its blk0 region of
+//     the entry area) and copies the records of its first decode from there on;
+//   * any other lane (no checkpoint matched, emission region full) writes its range again
+//     from its true state (decode_write), as every lane did before round 5.
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
   main_prio();
@@ -878,6 +923,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
     const int i = (item - sd.h_item_base) * kHuffThreads + t;  // lane index within the image
     const bool active = i < sd.h_lanes;
+    const bool single = huff_single_segment(sd);
     const uint32_t rend = lane_range_end(sd, i, nbits);
     LaneRec* lr = (LaneRec*)(ws + sd.hlane_off);
     // checkpoint k of lane i at [k][lane]: a wave's lanes write neighbouring words
@@ -891,12 +937,32 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       const uint32_t to = myS.pos, from = to > (uint32_t)kHuffLookback ? to - (uint32_t)kHuffLookback : 0u;
       myS = decode_lookback<kHuffSrc>(br, im, from, to);
     }
+    HUFF_PHASE_MAX(1, wall_clock64());
+    const HState guess = myS;
+    SyncMatch match{0xFFFFFFFFu, -1};
+    SparseSink sink;
+    sink.ent = (uint32_t*)(ws + sd.coef_off);
+    sink.lb = L.sink + t;
+    int32_t nemit = 0, eflags = 0;
     if (active) {
-      myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
+      if (single) {  // the first decode emits the lane's blocks into its emission region
+        const uint32_t cap = (uint32_t)emit_lane_cap(sd.h_sub);
+        const uint32_t ebase = (uint32_t)((sd.emit_off - sd.coef_off) >> 1) + (uint32_t)i * cap;
+        sink.open_emit(ebase, cap + (i == sd.h_lanes - 1 ? (uint32_t)kEmitLastExtra : 0u));
+        const EmitOut e = decode_emit<kHuffSrc>(br, im, myS, rend, lane_write_end(sd, i), nbits, cps, cstride,
+                                                kHuffCheckpoints, &ncp, sink);
+        sink.close();
+        myR1 = e.r;
+        nemit = e.nemit;
+        eflags = e.flags;
+      } else {
+        myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
+      }
       L.R[t] = myR1;
     }
+    const uint2* erec = sink.binfo;  // single: the lane's record 0 (record j at erec[-j])
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
-    HUFF_PHASE(1, wall_clock64());
+    HUFF_PHASE(2, wall_clock64());
     int round = 0;
     for (; round < kHuffThreads + 1; ++round) {
       HState want;
@@ -908,27 +974,51 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       __syncthreads();
       if (redo) {
         myS = want;
-        L.R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1);
+        L.R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1, &match);
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
     const RangeOut res = L.R[t];
-    HUFF_PHASE(2, wall_clock64());
-    HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
-    if (huff_single_segment(sd)) {
-      // the whole image is this segment: its start states are final, so the blocks
-      // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
+    HUFF_PHASE(3, wall_clock64());
+    HUFF_PHASE(5, (uint64_t)round | ((uint64_t)(single ? 1 : 0) << 32));
+    const bool confirmed = hstate_eq(guess, myS);
+#ifdef DINO_HUFF_PHASES
+    if (active && !confirmed) {
+      HUFF_PHASE_ADD(6, 1);
+      if (match.m0 >= 0) {
+        HUFF_PHASE_ADD(7, match.pos - myS.pos);
+        HUFF_PHASE_MAX(8, match.pos - myS.pos);
+      } else {
+        HUFF_PHASE_ADD(9, 1);
+      }
+    }
+    if (active && single && (eflags & kEmitOverflow)) HUFF_PHASE_ADD(10, 1);
+#endif
+    if (single) {
+      // the whole image is this segment: its start states are final (k_huff2 and k_huff3 skip it)
       uint32_t tot;
       const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)res.nblk : 0u, L.wave, &tot);
       if (active) {
-        SparseSink sink;
-        sink.ent = (uint32_t*)(ws + sd.coef_off);
-        sink.binfo = (uint2*)(ws + sd.binfo_off);
-        sink.lb = reinterpret_cast<uint32_t*>(&L.tab.skip) + t;
+        uint2* binfo = (uint2*)(ws + sd.binfo_off);
+        const int32_t total = sd.total_blocks;
+        sink.binfo = binfo;
         sink.open((int32_t)blk0);
-        decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
-                                 nbits, sink);
-        sink.close();
+        if (!(eflags & kEmitOverflow) && (confirmed || match.m0 >= 0)) {
+          int32_t b = (int32_t)blk0, j = 0;
+          if (!confirmed) {  // the true blocks up to the checkpoint where the first decode joined
+            b += decode_write_prefix<kHuffSrc>(br, im, myS, match.pos, (int32_t)blk0, total, sink);
+            sink.close();
+            j = match.m0;
+          }
+          for (; j < nemit && b < total; ++j, ++b) binfo[b] = erec[-j];
+          if (eflags & kEmitInsufficient)  // the rest of the image is zero blocks (decode_write's rule)
+            for (; b < total; ++b) binfo[b] = make_uint2(0u, kBinfoAbsDc);
+        } else {
+          HUFF_PHASE_ADD(11, 1);
+          decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, total, (int32_t*)nullptr, nbits,
+                                 sink);
+          sink.close();
+        }
       }
     } else if (active) {
       LaneRec& o = lr[i];
@@ -938,7 +1028,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       o.ncp = ncp;
     }
     __syncthreads();
-    HUFF_PHASE(3, wall_clock64());
+    HUFF_PHASE(4, wall_clock64());
   }
 }
 
@@ -3658,7 +3748,10 @@ hipError_t copy_huff_phases(uint64_t* host, int64_t n_items) {
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return e;
   const int64_t n = n_items < kPhaseItems ? n_items : kPhaseItems;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_huff_phase), sizeof(uint64_t) * 5 * n);
+  e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_huff_phase), sizeof(uint64_t) * kPhaseSlots * n);
+  if (e != hipSuccess) return e;
+  static uint64_t zeros[kPhaseItems][kPhaseSlots];  // the counters start from zero for the next launches
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_huff_phase), zeros, sizeof(zeros));
 }
 #endif
 

@@ -22,6 +22,11 @@ struct LaneRec {
 };
 static_assert(sizeof(LaneRec) == 68, "LaneRec layout");
 
+// Image areas start 256-byte aligned (tail pads each image), and so does the sparse entry
+// area (rst pads ent + rst): a lane's entry region starts at a multiple of 256 bytes in
+// memory too (SparseSink stores groups of up to 64 bytes aligned to their size).
+DHD int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+
 // Lanes reserved for the speculative Huffman decode (restart images decode per interval).
 DHD int32_t huff_lanes_cap(const ImgDesc& d) {
   if (d.restart_interval > 0 || d.kind != 0) return 0;
@@ -32,6 +37,28 @@ DHD int32_t huff_lanes_cap(const ImgDesc& d) {
 
 // Sparse entry capacity per block (see SparseSink): 63 u32 entries + 1 alignment halfword.
 constexpr int kEntHalfwordsPerBlock = 128;
+
+// k_huff1's emission area.  An image whose entropy stream is one work item with lane
+// ranges of at most kHuffFuseSubBits bits is finished by k_huff1, whose first decode emits
+// each lane's blocks into a region of its own (decode_emit): lane i's region is
+// [i cap, (i + 1) cap) halfwords of the area, cap = emit_lane_cap(h_sub) (a range of s bits
+// emits at most s + 128 halfwords of entries, see SparseSink), the last lane's region is
+// kEmitLastExtra halfwords longer (the MCU it may decode past the data).  The lane's block
+// records grow down from the top of its region.  Reserved from the raw scan length, so the
+// plan (and the host probe) and k_huff1 agree on which images have it.
+constexpr int kHuffFuseSubBits = 3072;
+constexpr int64_t kEmitMaxBits = (int64_t)kHuffThreads * kHuffFuseSubBits;
+constexpr int32_t kEmitLastExtra = 2048;
+DHD bool emit_reserved(const ImgDesc& d) {
+  return d.kind == 0 && d.restart_interval == 0 && ((int64_t)d.scan_len + 64) * 8 <= kEmitMaxBits;
+}
+DHD int32_t emit_lane_cap(int32_t sub) { return (sub + 256 + 127) & ~127; }
+// h_lanes x cap <= (bits + sub) + 383 h_lanes halfwords (h_lanes <= kHuffThreads, sub <= kHuffFuseSubBits)
+DHD int64_t emit_area_bytes(const ImgDesc& d) {
+  if (!emit_reserved(d)) return 0;
+  const int64_t bits = ((int64_t)d.scan_len + 64) * 8;
+  return align256(2 * (bits + kHuffFuseSubBits + 383 * (int64_t)kHuffThreads + kEmitLastExtra));
+}
 
 // Byte sizes of an image's workspace regions, in chunk order: destuffed entropy
 // bytes, restart offsets, coefficients (baseline: sparse entries, 128 halfwords of
@@ -44,10 +71,6 @@ struct ChunkSizes {
   DHD int64_t total() const { return sum() + tail; }
 };
 
-// Image areas start 256-byte aligned (tail pads each image), and so does the sparse entry
-// area (rst pads ent + rst): a lane's entry region starts at a multiple of 256 bytes in
-// memory too (SparseSink stores groups of up to 64 bytes aligned to their size).
-DHD int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 DHD ChunkSizes chunk_finish(ChunkSizes z) {
   z.tail = align256(z.sum()) - z.sum();
   return z;
@@ -78,7 +101,7 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   }
   z.ent = align16((int64_t)d.scan_len + 64);
   z.rst = align256(z.ent + 4 * ((int64_t)d.n_rst_max + 1)) - z.ent;
-  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;
+  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2 + emit_area_bytes(d);
   z.binfo = align16((int64_t)d.total_blocks * 8);
   const int64_t lanes = huff_lanes_cap(d);
   z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);
