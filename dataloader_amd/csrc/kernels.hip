@@ -890,13 +890,51 @@ __device__ uint64_t g_huff_phase[kPhaseItems][kPhaseSlots];
 
 constexpr int kHuffLookback = 2048;  // bits a lane decodes before its range to guess its start state
 
+// Lane i's emission region (halfwords from the image's entry area; see emit_area_bytes).
+__device__ __forceinline__ void emit_region(const ImgDesc& d, int i, uint32_t* base, uint32_t* cap) {
+  const uint32_t c = (uint32_t)emit_lane_cap(d.h_sub);
+  *base = (uint32_t)((d.emit_off - d.coef_off) >> 1) + (uint32_t)i * c;
+  *cap = c + (i == d.h_lanes - 1 ? (uint32_t)kEmitLastExtra : 0u);
+}
+
+// A lane's blocks in place once its true start state S and first block blk0 are known: the
+// records of its emitting first decode copied (all of them if the guess was confirmed; from
+// the matched checkpoint on, after a prefix written from S, if it was re-decoded), or its
+// range written again from S (no checkpoint matched, emission region full).
+template <typename Sink>
+__device__ void lane_finish(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint8_t* __restrict__ ws, int i,
+                            HState S, bool redone, SyncMatch M, int32_t nemit, int32_t eflags, int32_t blk0,
+                            uint32_t nbits, Sink& sink) {
+  uint2* binfo = (uint2*)(ws + d.binfo_off);
+  const int32_t total = d.total_blocks;
+  sink.binfo = binfo;
+  sink.open(blk0);
+  if (!(eflags & kEmitOverflow) && (!redone || M.m0 >= 0)) {
+    int32_t b = blk0, j = 0;
+    if (redone) {  // the true blocks up to the checkpoint where the first decode joined
+      b += decode_write_prefix<kHuffSrc>(br, im, S, M.pos, blk0, total, sink);
+      sink.close();
+      j = M.m0;
+    }
+    uint32_t ebase, ecap;
+    emit_region(d, i, &ebase, &ecap);
+    const uint2* erec = (const uint2*)((const uint32_t*)(ws + d.coef_off) + ((ebase + ecap) >> 1)) - 1;
+    for (; j < nemit && b < total; ++j, ++b) binfo[b] = erec[-j];
+    if (eflags & kEmitInsufficient)  // the rest of the image is zero blocks (decode_write's rule)
+      for (; b < total; ++b) binfo[b] = make_uint2(0u, kBinfoAbsDc);
+  } else {
+    decode_write<kHuffSrc>(br, im, S, lane_write_end(d, i), blk0, total, (int32_t*)nullptr, nbits, sink);
+    sink.close();
+  }
+}
+
 // k_huff1 per work item: every lane guesses its start state from kHuffLookback bits before
-// its range (decode_lookback), decodes its range from the guess (the first decode), then
-// sync rounds inside the item re-decode the ranges whose start state changed, stopping at
-// the first checkpoint the first decode also passed.  Items of a multi-segment or a long-
-// range image leave their lane records to k_huff2 / k_huff3.  A single-segment image
-// (huff_single_segment) is finished here: its first decode emits every lane's blocks into
-// the lane's emission region (decode_emit), and after the rounds and the block scan
+// its range (decode_lookback), decodes its range from the guess (the first decode, which
+// emits the lane's blocks into its emission region: decode_emit), then sync rounds inside
+// the item re-decode the ranges whose start state changed, stopping at the first checkpoint
+// the first decode also passed.  Items of a multi-segment or a long-range image leave their
+// lane records to k_huff2 / k_huff3.  A single-segment image (huff_single_segment) is
+// finished here: after the rounds and the block scan, lane_finish places each lane's blocks:
 //   * a lane whose guess the rounds confirmed copies its block records into place (its
 //     entries stay where they were emitted);
 //   * a lane re-decoded from its true state that joined its first decode at a checkpoint
@@ -944,23 +982,18 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     sink.ent = (uint32_t*)(ws + sd.coef_off);
     sink.lb = L.sink + t;
     int32_t nemit = 0, eflags = 0;
-    if (active) {
-      if (single) {  // the first decode emits the lane's blocks into its emission region
-        const uint32_t cap = (uint32_t)emit_lane_cap(sd.h_sub);
-        const uint32_t ebase = (uint32_t)((sd.emit_off - sd.coef_off) >> 1) + (uint32_t)i * cap;
-        sink.open_emit(ebase, cap + (i == sd.h_lanes - 1 ? (uint32_t)kEmitLastExtra : 0u));
-        const EmitOut e = decode_emit<kHuffSrc>(br, im, myS, rend, lane_write_end(sd, i), nbits, cps, cstride,
-                                                kHuffCheckpoints, &ncp, sink);
-        sink.close();
-        myR1 = e.r;
-        nemit = e.nemit;
-        eflags = e.flags;
-      } else {
-        myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
-      }
+    if (active) {  // the first decode emits the lane's blocks into its emission region
+      uint32_t ebase, ecap;
+      emit_region(sd, i, &ebase, &ecap);
+      sink.open_emit(ebase, ecap);
+      const EmitOut e = decode_emit<kHuffSrc>(br, im, myS, rend, lane_write_end(sd, i), nbits, cps, cstride,
+                                              kHuffCheckpoints, &ncp, sink);
+      sink.close();
+      myR1 = e.r;
+      nemit = e.nemit;
+      eflags = e.flags;
       L.R[t] = myR1;
     }
-    const uint2* erec = sink.binfo;  // single: the lane's record 0 (record j at erec[-j])
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
     HUFF_PHASE(2, wall_clock64());
     int round = 0;
@@ -992,40 +1025,24 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
         HUFF_PHASE_ADD(9, 1);
       }
     }
-    if (active && single && (eflags & kEmitOverflow)) HUFF_PHASE_ADD(10, 1);
+    if (active && (eflags & kEmitOverflow)) HUFF_PHASE_ADD(10, 1);
+    if (active && single && ((eflags & kEmitOverflow) || (!confirmed && match.m0 < 0))) HUFF_PHASE_ADD(11, 1);
 #endif
     if (single) {
       // the whole image is this segment: its start states are final (k_huff2 and k_huff3 skip it)
       uint32_t tot;
       const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)res.nblk : 0u, L.wave, &tot);
-      if (active) {
-        uint2* binfo = (uint2*)(ws + sd.binfo_off);
-        const int32_t total = sd.total_blocks;
-        sink.binfo = binfo;
-        sink.open((int32_t)blk0);
-        if (!(eflags & kEmitOverflow) && (confirmed || match.m0 >= 0)) {
-          int32_t b = (int32_t)blk0, j = 0;
-          if (!confirmed) {  // the true blocks up to the checkpoint where the first decode joined
-            b += decode_write_prefix<kHuffSrc>(br, im, myS, match.pos, (int32_t)blk0, total, sink);
-            sink.close();
-            j = match.m0;
-          }
-          for (; j < nemit && b < total; ++j, ++b) binfo[b] = erec[-j];
-          if (eflags & kEmitInsufficient)  // the rest of the image is zero blocks (decode_write's rule)
-            for (; b < total; ++b) binfo[b] = make_uint2(0u, kBinfoAbsDc);
-        } else {
-          HUFF_PHASE_ADD(11, 1);
-          decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, total, (int32_t*)nullptr, nbits,
-                                 sink);
-          sink.close();
-        }
-      }
+      if (active)
+        lane_finish(br, im, sd, ws, i, myS, !confirmed, match, nemit, eflags, (int32_t)blk0, nbits, sink);
     } else if (active) {
       LaneRec& o = lr[i];
       o.S = myS;
       o.R = res;
       o.R1 = myR1;
       o.ncp = ncp;
+      o.flags = (confirmed ? 0 : kLaneRedone) | (eflags << 1);
+      o.nemit = nemit;
+      o.M = match;
     }
     __syncthreads();
     HUFF_PHASE(4, wall_clock64());
@@ -1072,8 +1089,11 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
         if (lr[i].pad) {
           const HState want = lr[i].W;
           lr[i].S = want;
+          lr[i].flags |= kLaneRedone;
+          SyncMatch m;
           lr[i].R = decode_range_sync<kHuffSrc>(br, im, want, lane_range_end(d, i, nbits),
-                                             cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1);
+                                             cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1, &m);
+          lr[i].M = m;
         }
       }
       __syncthreads();
@@ -1129,13 +1149,11 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
           sink.close();
         }
       }
-    } else if (i < sd.h_lanes) {
+    } else if (i < sd.h_lanes) {  // the lane's emitted blocks in place (k_huff1's lane_finish)
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
-      sink.open(r.blk0);
-      decode_write<kHuffSrc>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr,
-                               br.nbytes * 8u, sink);
-      sink.close();
+      lane_finish(br, im, sd, ws, i, r.S, (r.flags & kLaneRedone) != 0, r.M, r.nemit, r.flags >> 1, r.blk0,
+                  br.nbytes * 8u, sink);
     }
     __syncthreads();
   }

@@ -19,8 +19,12 @@ struct LaneRec {
   int32_t blk0;   // first block the lane emits (k_huff2 scan)
   HState W;       // k_huff2 scratch: wanted start state
   int32_t pad;
+  int32_t flags;  // kLaneRedone | the first decode's EmitOut::flags << 1
+  int32_t nemit;  // blocks the first decode emitted
+  SyncMatch M;    // the last re-decode's matched checkpoint
 };
-static_assert(sizeof(LaneRec) == 68, "LaneRec layout");
+static_assert(sizeof(LaneRec) == 84, "LaneRec layout");
+constexpr int32_t kLaneRedone = 1;
 
 // Image areas start 256-byte aligned (tail pads each image), and so does the sparse entry
 // area (rst pads ent + rst): a lane's entry region starts at a multiple of 256 bytes in
@@ -38,26 +42,23 @@ DHD int32_t huff_lanes_cap(const ImgDesc& d) {
 // Sparse entry capacity per block (see SparseSink): 63 u32 entries + 1 alignment halfword.
 constexpr int kEntHalfwordsPerBlock = 128;
 
-// k_huff1's emission area.  An image whose entropy stream is one work item with lane
-// ranges of at most kHuffFuseSubBits bits is finished by k_huff1, whose first decode emits
-// each lane's blocks into a region of its own (decode_emit): lane i's region is
-// [i cap, (i + 1) cap) halfwords of the area, cap = emit_lane_cap(h_sub) (a range of s bits
-// emits at most s + 128 halfwords of entries, see SparseSink), the last lane's region is
-// kEmitLastExtra halfwords longer (the MCU it may decode past the data).  The lane's block
-// records grow down from the top of its region.  Reserved from the raw scan length, so the
-// plan (and the host probe) and k_huff1 agree on which images have it.
-constexpr int kHuffFuseSubBits = 3072;
-constexpr int64_t kEmitMaxBits = (int64_t)kHuffThreads * kHuffFuseSubBits;
+// The emission area of the speculative decode (images without restart intervals).  k_huff1's
+// first decode emits each lane's blocks into a region of its own (decode_emit): lane i's
+// region is [i cap, (i + 1) cap) halfwords of the area, cap = emit_lane_cap(h_sub) (half a
+// halfword per bit of range + 256: a q85 photo's entries and records take ~0.15 halfwords per
+// bit; a lane that fills its region is written again from its true state), the last lane's
+// region is kEmitLastExtra halfwords longer (the MCU it may decode past the data).  The lane's
+// block records grow down from the top of its region.
+constexpr int kHuffFuseSubBits = 3072;  // single-segment images with ranges up to this are finished by k_huff1
 constexpr int32_t kEmitLastExtra = 2048;
-DHD bool emit_reserved(const ImgDesc& d) {
-  return d.kind == 0 && d.restart_interval == 0 && ((int64_t)d.scan_len + 64) * 8 <= kEmitMaxBits;
-}
-DHD int32_t emit_lane_cap(int32_t sub) { return (sub + 256 + 127) & ~127; }
-// h_lanes x cap <= (bits + sub) + 383 h_lanes halfwords (h_lanes <= kHuffThreads, sub <= kHuffFuseSubBits)
+DHD bool emit_reserved(const ImgDesc& d) { return d.kind == 0 && d.restart_interval == 0; }
+DHD int32_t emit_lane_cap(int32_t sub) { return ((sub >> 1) + 256 + 127) & ~127; }
+// h_lanes x cap <= (nbits + sub) / 2 + 383 h_lanes halfwords; sub <= kHuffSegBits / kHuffThreads + 32
 DHD int64_t emit_area_bytes(const ImgDesc& d) {
   if (!emit_reserved(d)) return 0;
   const int64_t bits = ((int64_t)d.scan_len + 64) * 8;
-  return align256(2 * (bits + kHuffFuseSubBits + 383 * (int64_t)kHuffThreads + kEmitLastExtra));
+  const int64_t sub = kHuffSegBits / kHuffThreads + 32;
+  return align256(2 * ((bits + sub) / 2 + 1 + 383 * (int64_t)huff_lanes_cap(d) + kEmitLastExtra));
 }
 
 // Byte sizes of an image's workspace regions, in chunk order: destuffed entropy

@@ -94,11 +94,18 @@ class IngestEngine:
         _lib.check(self.lib.dino_copy_h2d(ctypes.c_void_p(d_dst.data_ptr() + dst_off), ctypes.c_void_p(host_addr),
                                           int(nbytes), s), "dino_copy_h2d")
 
+    def _to_current(self) -> None:
+        """Order torch's current stream after this engine's launches, so that a tensor the
+        engine just filled on its own stream can be used (``.cpu()``, ops) on the current one."""
+        if self.stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
     def copy_rgb(self, index: int, width: int, height: int) -> torch.Tensor:
         with self.on_stream():
             out = torch.zeros(height, width, 3, dtype=torch.uint8, device=self.device)
         _lib.check(self.lib.dino_copy_rgb(self._ctx, index, _ptr(out), self._s()),
                    "dino_copy_rgb")
+        self._to_current()
         return out
 
     def debug_region(self, index: int, region: int, nbytes: int) -> torch.Tensor:
@@ -106,6 +113,7 @@ class IngestEngine:
             out = torch.zeros(nbytes, dtype=torch.uint8, device=self.device)
         _lib.check(self.lib.dino_debug_region(self._ctx, index, region, _ptr(out), nbytes,
                                               self._s()), "dino_debug_region")
+        self._to_current()
         return out
 
     KERNEL_NAMES = ["k_parse", "k_plan", "k_destuff", "k_huff1", "k_idct", "k_color", "k_params", "k_vplan",
