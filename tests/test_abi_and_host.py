@@ -220,3 +220,48 @@ def test_backend_side_look_ahead_fits_the_metadata_fifo():
                 a = be.side_look_ahead(PipelineConfig(cpu_queue=cq), Src(cap), depth)
                 if a > 1:
                     assert MI355XAugPipeline.pulled_bound(depth, be.PREFETCH, a) + 1 <= cap, (cap, depth, cq)
+
+
+def test_side_look_ahead_engages_only_with_coefficient_buffer_images():
+    """on the side route the look-ahead (up to side_ahead batches pulled ahead and
+    staged in HBM) is engaged only while progressive images are about: a stream of baseline
+    batches is pulled one at a time and never staged; a batch with a progressive image arms it
+    for side_ahead batches (the batches already ahead are staged too); then it disengages."""
+    from collections import deque
+
+    from dataloader_amd.pipeline import MI355XAugPipeline
+
+    class PB:
+        def __init__(self, k, prog):
+            self.k, self.prog, self.side, self.staged = k, prog, None, False
+
+    prog_at = {5, 6}
+    src = iter(range(40))
+    p = MI355XAugPipeline.__new__(MI355XAugPipeline)
+    p._side_ahead, p._side_hot, p._ahead, p._source_end = 4, 0, deque(), False
+    p._side = None
+    p.host_seconds = {"wait": 0.0}
+    p.stats = {}
+    pulled = []
+
+    def pull_one(block):
+        k = next(src)
+        pulled.append(k)
+        return PB(k, k in prog_at)
+
+    def side_submit(pb):
+        pb.side = object() if pb.prog else None
+
+    def stage(pb):
+        pb.staged = True
+
+    p._pull_one, p._side_submit, p._stage_on_device = pull_one, side_submit, stage
+    out = [p._pull_side() for _ in range(16)]
+    assert [pb.k for pb in out] == list(range(16))           # order kept
+    staged = {pb.k for pb in out if pb.staged}
+    # cold: one at a time (batches 0-4 pulled only as they are handed out, never staged); batch 5
+    # arms the look-ahead; it stays engaged for side_ahead batches after the last progressive one
+    assert not staged & {0, 1, 2, 3, 4}
+    assert {5, 6, 7, 8, 9} <= staged and max(staged) <= 6 + 4
+    assert not staged & set(range(11, 16))
+    assert pulled[:6] == [0, 1, 2, 3, 4, 5]
