@@ -890,39 +890,50 @@ __device__ uint64_t g_huff_phase[kPhaseItems][kPhaseSlots];
 
 constexpr int kHuffLookback = 2048;  // bits a lane decodes before its range to guess its start state
 
-// Lane i's emission region (halfwords from the image's entry area; see emit_area_bytes).
-__device__ __forceinline__ void emit_region(const ImgDesc& d, int i, uint32_t* base, uint32_t* cap) {
+// Lane i's emission region in area `a` (0: first decode, 1: re-decodes; halfwords from the
+// image's entry area; see emit_area_bytes).
+__device__ __forceinline__ void emit_region(const ImgDesc& d, int i, int a, uint32_t* base, uint32_t* cap) {
   const uint32_t c = (uint32_t)emit_lane_cap(d.h_sub);
-  *base = (uint32_t)((d.emit_off - d.coef_off) >> 1) + (uint32_t)i * c;
+  *base = (uint32_t)((d.emit_off - d.coef_off + a * emit_area_bytes(d)) >> 1) + (uint32_t)i * c;
   *cap = c + (i == d.h_lanes - 1 ? (uint32_t)kEmitLastExtra : 0u);
 }
+// The records of lane i's region in area a: record j at the returned pointer [-j].
+__device__ __forceinline__ const uint2* emit_records(const ImgDesc& d, const uint8_t* ws, int i, int a) {
+  uint32_t base, cap;
+  emit_region(d, i, a, &base, &cap);
+  return (const uint2*)((const uint32_t*)(ws + d.coef_off) + ((base + cap) >> 1)) - 1;
+}
 
-// A lane's blocks in place once its true start state S and first block blk0 are known: the
-// records of its emitting first decode copied (all of them if the guess was confirmed; from
-// the matched checkpoint on, after a prefix written from S, if it was re-decoded), or its
-// range written again from S (no checkpoint matched, emission region full).
+// A lane's blocks in place once its true start state S and first block blk0 are known, from
+// what its decodes emitted: a confirmed guess: the first decode's records; a re-decode that
+// joined the first decode at a checkpoint: the re-decode's records (the blocks before the
+// checkpoint), then the first decode's from there on; a re-decode that joined nothing: its
+// own records.  Only the 8-byte records move (the entries stay where they were emitted).  A
+// lane whose emission is incomplete (region full) writes its range again from S.
 template <typename Sink>
 __device__ void lane_finish(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint8_t* __restrict__ ws, int i,
-                            HState S, bool redone, SyncMatch M, int32_t nemit, int32_t eflags, int32_t blk0,
-                            uint32_t nbits, Sink& sink) {
+                            HState S, bool redone, SyncMatch M, int32_t nemit1, int32_t eflags1, int32_t nemit2,
+                            int32_t eflags2, int32_t blk0, uint32_t nbits, Sink& sink) {
   uint2* binfo = (uint2*)(ws + d.binfo_off);
   const int32_t total = d.total_blocks;
-  sink.binfo = binfo;
-  sink.open(blk0);
-  if (!(eflags & kEmitOverflow) && (!redone || M.m0 >= 0)) {
-    int32_t b = blk0, j = 0;
-    if (redone) {  // the true blocks up to the checkpoint where the first decode joined
-      b += decode_write_prefix<kHuffSrc>(br, im, S, M.pos, blk0, total, sink);
-      sink.close();
-      j = M.m0;
+  const bool matched = redone && M.m0 >= 0;
+  const bool ok = !redone ? !(eflags1 & kEmitOverflow)
+                          : (matched ? !(eflags1 & kEmitOverflow) && eflags2 == 0 : !(eflags2 & kEmitOverflow));
+  if (ok) {
+    int32_t b = blk0;
+    if (redone) {
+      const uint2* r2 = emit_records(d, ws, i, 1);
+      for (int32_t j = 0; j < nemit2 && b < total; ++j, ++b) binfo[b] = r2[-j];
     }
-    uint32_t ebase, ecap;
-    emit_region(d, i, &ebase, &ecap);
-    const uint2* erec = (const uint2*)((const uint32_t*)(ws + d.coef_off) + ((ebase + ecap) >> 1)) - 1;
-    for (; j < nemit && b < total; ++j, ++b) binfo[b] = erec[-j];
-    if (eflags & kEmitInsufficient)  // the rest of the image is zero blocks (decode_write's rule)
+    if (!redone || matched) {
+      const uint2* r1 = emit_records(d, ws, i, 0);
+      for (int32_t j = matched ? M.m0 : 0; j < nemit1 && b < total; ++j, ++b) binfo[b] = r1[-j];
+    }
+    if ((redone && !matched ? eflags2 : eflags1) & kEmitInsufficient)  // the rest: zero blocks (decode_write)
       for (; b < total; ++b) binfo[b] = make_uint2(0u, kBinfoAbsDc);
   } else {
+    sink.binfo = binfo;
+    sink.open(blk0);
     decode_write<kHuffSrc>(br, im, S, lane_write_end(d, i), blk0, total, (int32_t*)nullptr, nbits, sink);
     sink.close();
   }
@@ -981,10 +992,11 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     SparseSink sink;
     sink.ent = (uint32_t*)(ws + sd.coef_off);
     sink.lb = L.sink + t;
-    int32_t nemit = 0, eflags = 0;
+    int32_t nemit = 0, eflags = 0, nemit2 = 0, eflags2 = 0;
+    uint32_t ebase, ecap, ebase2, ecap2;
+    emit_region(sd, i, 0, &ebase, &ecap);
+    emit_region(sd, i, 1, &ebase2, &ecap2);
     if (active) {  // the first decode emits the lane's blocks into its emission region
-      uint32_t ebase, ecap;
-      emit_region(sd, i, &ebase, &ecap);
       sink.open_emit(ebase, ecap);
       const EmitOut e = decode_emit<kHuffSrc>(br, im, myS, rend, lane_write_end(sd, i), nbits, cps, cstride,
                                               kHuffCheckpoints, &ncp, sink);
@@ -1005,9 +1017,15 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
         redo = !hstate_eq(want, myS);
       }
       __syncthreads();
-      if (redo) {
+      if (redo) {  // from the corrected state, emitting into the lane's re-decode region
         myS = want;
-        L.R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1, &match);
+        sink.open_emit(ebase2, ecap2);
+        const EmitOut e = decode_sync_emit<kHuffSrc>(br, im, want, rend, lane_write_end(sd, i), nbits, cps, cstride, ncp,
+                                                     myR1, &match, sink);
+        sink.close();
+        nemit2 = e.nemit;
+        eflags2 = e.flags;
+        L.R[t] = e.r;
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
@@ -1026,22 +1044,24 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       }
     }
     if (active && (eflags & kEmitOverflow)) HUFF_PHASE_ADD(10, 1);
-    if (active && single && ((eflags & kEmitOverflow) || (!confirmed && match.m0 < 0))) HUFF_PHASE_ADD(11, 1);
+    if (active && single && (((eflags | eflags2) & kEmitOverflow))) HUFF_PHASE_ADD(11, 1);
 #endif
     if (single) {
       // the whole image is this segment: its start states are final (k_huff2 and k_huff3 skip it)
       uint32_t tot;
       const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)res.nblk : 0u, L.wave, &tot);
       if (active)
-        lane_finish(br, im, sd, ws, i, myS, !confirmed, match, nemit, eflags, (int32_t)blk0, nbits, sink);
+        lane_finish(br, im, sd, ws, i, myS, !confirmed, match, nemit, eflags, nemit2, eflags2, (int32_t)blk0, nbits,
+                    sink);
     } else if (active) {
       LaneRec& o = lr[i];
       o.S = myS;
       o.R = res;
       o.R1 = myR1;
       o.ncp = ncp;
-      o.flags = (confirmed ? 0 : kLaneRedone) | (eflags << 1);
+      o.flags = (confirmed ? 0 : kLaneRedone) | (eflags << 1) | (eflags2 << 3);
       o.nemit = nemit;
+      o.nemit2 = nemit2;
       o.M = match;
     }
     __syncthreads();
@@ -1058,6 +1078,7 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
   main_prio();
   __shared__ HuffTables s_tab;
   __shared__ uint32_t s_wave[kHuff2Threads / 64];
+  __shared__ uint32_t s_sink[kSinkLds * kHuff2Threads];
   const ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
   if (d.status != DINO_IMG_OK || d.kind != 0 || d.restart_interval > 0 || huff_single_segment(d)) return;
@@ -1075,6 +1096,9 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
     const BitReader br{(const uint32_t*)(ws + d.ent_off), (uint32_t)d.ent_len};
     const uint32_t nbits = (uint32_t)d.ent_len * 8u;
     const Checkpoint* cps = (const Checkpoint*)(ws + d.cps_off);
+    SparseSink sink;
+    sink.ent = (uint32_t*)(ws + d.coef_off);
+    sink.lb = s_sink + t;
     for (int round = 0; round <= n; ++round) {
       int any = 0;
       for (int i = 1 + t; i < n; i += kHuff2Threads) {
@@ -1089,11 +1113,17 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
         if (lr[i].pad) {
           const HState want = lr[i].W;
           lr[i].S = want;
-          lr[i].flags |= kLaneRedone;
           SyncMatch m;
-          lr[i].R = decode_range_sync<kHuffSrc>(br, im, want, lane_range_end(d, i, nbits),
-                                             cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1, &m);
+          uint32_t eb, ec;
+          emit_region(d, i, 1, &eb, &ec);
+          sink.open_emit(eb, ec);
+          const EmitOut e = decode_sync_emit<kHuffSrc>(br, im, want, lane_range_end(d, i, nbits), lane_write_end(d, i),
+                                                       nbits, cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1, &m, sink);
+          sink.close();
+          lr[i].R = e.r;
           lr[i].M = m;
+          lr[i].nemit2 = e.nemit;
+          lr[i].flags = (lr[i].flags & 7) | kLaneRedone | (e.flags << 3);
         }
       }
       __syncthreads();
@@ -1152,8 +1182,8 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
     } else if (i < sd.h_lanes) {  // the lane's emitted blocks in place (k_huff1's lane_finish)
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
-      lane_finish(br, im, sd, ws, i, r.S, (r.flags & kLaneRedone) != 0, r.M, r.nemit, r.flags >> 1, r.blk0,
-                  br.nbytes * 8u, sink);
+      lane_finish(br, im, sd, ws, i, r.S, (r.flags & kLaneRedone) != 0, r.M, r.nemit, (r.flags >> 1) & 3, r.nemit2,
+                  (r.flags >> 3) & 3, r.blk0, br.nbytes * 8u, sink);
     }
     __syncthreads();
   }

@@ -204,9 +204,11 @@ struct BlockListSink {
 };
 
 // k_huff1 on a single-segment image: look-back guess, emitting first decode, sync rounds
-// (matched checkpoints kept), block scan, then per lane: its emission as it is (guess
-// confirmed), a prefix write up to the matched checkpoint + the emission from there, or a
-// rewrite from the true state (no match, record overflow).  stats: {rounds, lanes
+// whose re-decodes emit too (matched checkpoints kept), block scan, then per lane the
+// records placed (kernels.hip lane_finish): the first decode's blocks (guess confirmed), the
+// re-decode's blocks up to the checkpoint where it joined the first decode + the first
+// decode's from there, or the re-decode's blocks alone (no checkpoint joined); a lane whose
+// emission is incomplete is rewritten from its true state.  stats: {rounds, lanes
 // re-decoded, lanes, lanes rewritten whole}.
 template <int kWin>
 inline void model_huffman_emit(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
@@ -218,12 +220,13 @@ inline void model_huffman_emit(const BitReader& br, const HuffImage& im, const I
   n = std::max(1, std::min(n, (int)((nbits + sub - 1) / sub)));
   std::vector<HState> S(n), G(n);
   std::vector<RangeOut> R(n), R1(n);
-  std::vector<EmitOut> E(n);
+  std::vector<EmitOut> E(n), E2(n);
   std::vector<SyncMatch> M(n, SyncMatch{0xFFFFFFFFu, -1});
   std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
   std::vector<int32_t> ncp(n);
-  std::vector<BlockListSink> emit(n);
+  std::vector<BlockListSink> emit(n), emit2(n);
   for (auto& e : emit) e.max_rec = max_rec;
+  for (auto& e : emit2) e.max_rec = max_rec;
   auto rend = [&](int i) -> uint32_t { return i == n - 1 ? nbits : (uint32_t)(i + 1) * sub; };
   auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
   for (int i = 0; i < n; ++i) {
@@ -246,7 +249,10 @@ inline void model_huffman_emit(const BitReader& br, const HuffImage& im, const I
     for (int i = 1; i < n; ++i) {
       if (!redo[i]) continue;
       S[i] = want[i];
-      R[i] = decode_range_sync<kWin>(br, im, S[i], rend(i), &cps[(size_t)i * kHuffCheckpoints], 1, ncp[i], R1[i], &M[i]);
+      emit2[i].blocks.clear();
+      E2[i] = decode_sync_emit<kWin>(br, im, S[i], rend(i), wend(i), nbits, &cps[(size_t)i * kHuffCheckpoints], 1,
+                                     ncp[i], R1[i], &M[i], emit2[i]);
+      R[i] = E2[i].r;
       any = true;
     }
     ++rounds;
@@ -255,20 +261,21 @@ inline void model_huffman_emit(const BitReader& br, const HuffImage& im, const I
   int32_t blk0 = 0;
   sink.dcd = dcd;
   for (int i = 0; i < n; ++i) {
-    const bool confirmed = hstate_eq(S[i], G[i]);
-    redone += !confirmed;
-    const bool ok = !(E[i].flags & kEmitOverflow) && (confirmed || M[i].m0 >= 0);
+    const bool re = !hstate_eq(S[i], G[i]);
+    redone += re;
+    const bool matched = re && M[i].m0 >= 0;
+    const int32_t f1 = E[i].flags, f2 = re ? E2[i].flags : 0;
+    const bool ok = !re ? !(f1 & kEmitOverflow) : (matched ? !(f1 & kEmitOverflow) && f2 == 0 : !(f2 & kEmitOverflow));
     if (!ok) {  // rewrite from the true state
       ++whole;
       decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, nbits, sink);
     } else {
-      int32_t b = blk0, j0 = 0;
-      if (!confirmed) {  // the true blocks up to the checkpoint where the first decode joined
-        b += decode_write_prefix<kWin>(br, im, S[i], M[i].pos, blk0, total_blocks, sink);
-        j0 = M[i].m0;
-      }
-      for (int32_t j = j0; j < E[i].nemit && b < total_blocks; ++j, ++b) emit[i].replay(j, b, sink);
-      if (E[i].flags & kEmitInsufficient)
+      int32_t b = blk0;
+      if (re)
+        for (int32_t j = 0; j < E2[i].nemit && b < total_blocks; ++j, ++b) emit2[i].replay(j, b, sink);
+      if (!re || matched)
+        for (int32_t j = matched ? M[i].m0 : 0; j < E[i].nemit && b < total_blocks; ++j, ++b) emit[i].replay(j, b, sink);
+      if ((re && !matched ? f2 : f1) & kEmitInsufficient)
         for (; b < total_blocks; ++b) sink.zero(b);
     }
     blk0 += R[i].nblk;
