@@ -132,7 +132,7 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
     blocks = float(np.mean(nblk))
 
     # images k_huff1 finishes itself (one 2 Mbit segment, lane ranges <= 3072 bits,
-    # kernels.hip huff_single_segment); the others are placed by k_huff3
+    # kernels.hip huff_single_segment); the others are written by k_huff3
     def fused(j):
         if b"\xff\xdd" in j[:2048]:  # restart intervals: k_huff3 decodes one interval per lane
             return False
@@ -144,20 +144,17 @@ def algorithmic_bytes(jpegs, g: int, l: int, n_g: int, n_l: int, out_bytes: int,
         return sub <= 3072
     fz = [fused(j) for j in jpegs]
     blk_fused = float(np.mean([b if f else 0 for b, f in zip(nblk, fz)]))
-    dri = [b"\xff\xdd" in j[:2048] for j in jpegs]
-    blk_dri = float(np.mean([b if r else 0 for b, r in zip(nblk, dri)]))
-    s_dri = float(np.mean([len(j) if r else 0 for j, r in zip(jpegs, dri)]))
+    s_unfused = float(np.mean([len(j) if not f else 0 for j, f in zip(jpegs, fz)]))
     out = out_bytes * 3 * (n_g * g * g + n_l * l * l)
     per_blk = entry_bytes_per_block + 8.0       # sparse entries + the 8-byte block record
     ab = {
         "path": s_jpeg + out,                       # S_jpeg + 1 044 480 B (bf16)
         "k_destuff": s_jpeg,                         # per launch: count pass reads, write pass reads + writes
-        # the emitting first decode (round 5): the entropy stream in, every block's sparse
-        # entries + record out (DRI images: k_huff3 decodes them); the images it finishes
-        # itself also have their records copied into place (8 B read + 8 B written per block)
-        "k_huff1": (s_jpeg - s_dri) + (blocks - blk_dri) * per_blk + blk_fused * 16,
-        # places the other images' emitted blocks (records copied), decodes the DRI images
-        "k_huff3": (blocks - blk_fused - blk_dri) * 16 + s_dri + blk_dri * per_blk,
+        # first (speculative) decode reads the entropy stream; for the images it finishes
+        # itself it also writes their sparse coefficient entries + block records (measured)
+        "k_huff1": s_jpeg + blk_fused * per_blk,
+        # re-decode of the other images: entropy bytes in, sparse entries + records out
+        "k_huff3": s_unfused + (blocks - blk_fused) * per_blk,
         # entries + records in, planes out; planes in, RGB out
         "k_idct": blocks * (per_blk + 64),
         "k_color": blocks * 64 + px * 3,

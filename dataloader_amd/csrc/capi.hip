@@ -165,6 +165,12 @@ int dino_copy_rgb(dino_ctx* c, int32_t index, uint8_t* d_rgb, void* stream) {
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_copy_rgb");
 }
 
+int dino_pixel_ops_all(int32_t op, int32_t param, uint8_t* d_out, void* stream) {
+  if (!d_out || op < 0 || op > 2) return fail(DINO_EINVAL, "dino_pixel_ops_all: bad args%s%lld");
+  hipError_t e = launch_pixel_ops(op, param & 255, d_out, (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_pixel_ops_all");
+}
+
 static int check_cfg(const dino_ctx* c, const dino_aug_config* cfg) {
   if (!cfg) return fail(DINO_EINVAL, "null dino_aug_config%s%lld");
   const int nv = cfg->n_global + cfg->n_local;

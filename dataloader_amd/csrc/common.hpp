@@ -53,7 +53,7 @@ struct ImgDesc {
   int64_t ent_off, rst_off, plane_off, rgb_off;
   int64_t coef_off;        // sparse AC entries (u32, 64 per block of capacity; k_huffman SparseSink)
   int64_t cps_off;         // k_huffman checkpoints (speculative decode), kHuffThreads x kHuffCheckpoints
-  int64_t emit_off;        // k_huff1's emission area (emit_reserved images; lane-indexed entry regions)
+  int64_t reserved0;
   int64_t binfo_off;       // uint2 per block (decode order): first sparse entry, (int16 DC << 16) | entry count
   int64_t coef_bytes;      // dense int16 coefficient bytes (host emulator layout)
   int64_t htab_off;        // Huffman decoder tables (6 x HuffTable), built once per image by k_htab

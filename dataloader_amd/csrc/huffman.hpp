@@ -495,23 +495,15 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
 // reaches a block boundary the first decode also passed through (same bit
 // position, same block-in-MCU index), everything after it is what the first
 // decode already found: its end state and remaining block count are reused.
-// `match` (optional): the matched checkpoint's position and first-decode block index
-// ({0xFFFFFFFF, -1}: none; the re-decode ran to the range end).
-struct SyncMatch {
-  uint32_t pos;
-  int32_t m0;
-};
 template <int kWin>
 DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState st, uint32_t end,
-                               const Checkpoint* cps, int cstride, int ncp, RangeOut first,
-                               SyncMatch* match = nullptr) {
+                               const Checkpoint* cps, int cstride, int ncp, RangeOut first) {
   st = sanitize(st, im.blocks_per_mcu);
   int32_t nblk = 0;
   int j = 0;
   BitCursor cur;
   bc_init<kWin>(cur, br, st.pos);
   int32_t blk = st.c, z = st.z;
-  if (match) *match = SyncMatch{0xFFFFFFFFu, -1};
   // the next checkpoint at or after the position, kept in registers: memory is only
   // read when the decode passes one (every kHuffCpStride blocks), not at every block
   Checkpoint cp = ncp > 0 ? cps[0] : Checkpoint{0xFFFFFFFFu, 0u};
@@ -521,7 +513,6 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
       if (cp.pos == cur.pos && (int32_t)(cp.cn & 15u) == blk) {
         RangeOut r = first;
         r.nblk = nblk + first.nblk - (int32_t)(cp.cn >> 4);
-        if (match) *match = SyncMatch{cp.pos, (int32_t)(cp.cn >> 4)};
         return r;
       }
       nblk++;
@@ -596,176 +587,6 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
     }
   }
   return cur.pos;
-}
-
-// The decodes of a range that also emit the range's blocks.
-//
-// decode_emit, the first (speculative) decode: one pass that is decode_range (end state at
-// the first step boundary >= rend, blocks whose DC step starts before rend, checkpoints)
-// and, if `st` turns out to be the true state, decode_write (the blocks opened before wend,
-// values included) at once, so that a lane whose guessed start state the sync rounds
-// confirm never decodes its range again.
-//
-// decode_sync_emit, a sync round's re-decode from a corrected state: decode_range_sync
-// (stops at the first checkpoint the first decode also passed, whose blocks from there on
-// are the first decode's) that also emits the blocks before that checkpoint, or, when none
-// matches, every block of the range as decode_emit does.
-//
-// Blocks go to the sink under local indices 0, 1, .. (their absolute index is only known
-// after the block scan), as long as sink.room(j) holds (kEmitOverflow past that: the lane
-// is then rewritten from its true state).  The insufficient-data rule of decode_write stops
-// the emission with kEmitInsufficient (every later block of the image is zero).  Once the
-// emission has stopped, the decode goes on state-only up to rend.  One step per iteration
-// of the emitting loop (blocks opened and closed inside it, as decode_write's).
-constexpr int32_t kEmitOverflow = 1, kEmitInsufficient = 2;
-struct EmitOut {
-  RangeOut r;       // as decode_range's / decode_range_sync's
-  int32_t nemit;    // blocks emitted (local indices [0, nemit))
-  int32_t flags;    // kEmitOverflow | kEmitInsufficient
-};
-template <int kWin, bool kSync, typename Sink>
-DHD EmitOut decode_emit_t(const BitReader& br, const HuffImage& im, HState st, uint32_t rend, uint32_t wend,
-                          uint32_t avail, Checkpoint* cps, int cstride, int kmax, int32_t* ncp, RangeOut first,
-                          SyncMatch* match, Sink& sink) {
-  st = sanitize(st, im.blocks_per_mcu);
-  EmitOut o;
-  o.nemit = 0;
-  o.flags = 0;
-  int32_t nblk = 0;
-  int n = 0;  // checkpoints recorded (first decode) or passed (sync)
-  bool ended = false;
-  HState endS{0u, 0, 0};
-  BitCursor cur;
-  bc_init<kWin>(cur, br, st.pos);
-  int32_t blk = st.c, z = st.z;
-  Checkpoint cp{0xFFFFFFFFu, 0u};
-  if (kSync) {
-    *match = SyncMatch{0xFFFFFFFFu, -1};
-    if (*ncp > 0) cp = cps[0];
-  }
-  // at a block boundary before the range end: record a checkpoint, or look for a match
-  // (true: the re-decode has joined the first decode)
-  auto boundary = [&]() -> bool {
-    if (kSync) {
-      while (cp.pos < cur.pos) cp = ++n < *ncp ? cps[n * cstride] : Checkpoint{0xFFFFFFFFu, 0u};
-      if (cp.pos == cur.pos && (int32_t)(cp.cn & 15u) == blk) {
-        *match = SyncMatch{cp.pos, (int32_t)(cp.cn >> 4)};
-        o.r = first;
-        o.r.nblk = nblk + first.nblk - (int32_t)(cp.cn >> 4);
-        return true;
-      }
-    } else if (n < kmax && (nblk < kHuffCpDense || (nblk & (kHuffCpStride - 1)) == 0)) {
-      cps[(n++) * cstride] = Checkpoint{cur.pos, ((uint32_t)nblk << 4) | (uint32_t)blk};
-    }
-    nblk++;
-    return false;
-  };
-  // the previous lane's block: state only (decode_write skips it, decode_range passes it)
-  while (z != 0) {
-    if (!ended && cur.pos >= rend) {
-      endS = HState{cur.pos, blk, z};
-      ended = true;
-    }
-    state_step<kWin>(cur, br, im, blk, z);
-  }
-  bool counted = false;  // the emission stopped at a boundary boundary() has already taken
-  if (cur.pos < wend) {
-    bool open = false;
-    for (;;) {
-      if (!open) {  // a block boundary
-        if (!ended && cur.pos >= rend) {
-          endS = HState{cur.pos, blk, z};
-          ended = true;
-        }
-        if (!ended && boundary()) return o;
-        if (blk == 0 && cur.pos > avail) {  // insufficient_data before this MCU: the rest stays zero
-          o.flags |= kEmitInsufficient;
-          counted = true;
-          break;
-        }
-        if (!sink.room(o.nemit)) {
-          o.flags |= kEmitOverflow;
-          counted = true;
-          break;
-        }
-        sink.begin(o.nemit);
-        open = true;
-      }
-      const StepOut so = huff_step<kWin>(cur, br, im, blk, z);
-      if (!ended && cur.pos >= rend && z != 0) {  // the first step boundary >= rend, inside a block
-        endS = HState{cur.pos, blk, z};
-        ended = true;
-      }
-      if (so.kind == 0) sink.dc((int16_t)so.value);
-      else if (so.kind == 1) sink.ac(so.zz, (int16_t)so.value);
-      if (so.block_done) {
-        sink.end();
-        ++o.nemit;
-        open = false;
-        if (cur.pos >= wend) break;
-      }
-    }
-  }
-  // decode_range's remainder (the emission stopped before the range end)
-  while (!ended) {
-    if (cur.pos >= rend) {
-      endS = HState{cur.pos, blk, z};
-      ended = true;
-      break;
-    }
-    if (z == 0 && !counted && boundary()) return o;
-    counted = false;
-    state_step<kWin>(cur, br, im, blk, z);
-  }
-  o.r.end = endS;
-  o.r.nblk = nblk;
-  if (!kSync) *ncp = n;
-  return o;
-}
-template <int kWin, typename Sink>
-DHD EmitOut decode_emit(const BitReader& br, const HuffImage& im, HState st, uint32_t rend, uint32_t wend,
-                        uint32_t avail, Checkpoint* cps, int cstride, int kmax, int32_t* ncp, Sink& sink) {
-  return decode_emit_t<kWin, false>(br, im, st, rend, wend, avail, cps, cstride, kmax, ncp, RangeOut{},
-                                    (SyncMatch*)nullptr, sink);
-}
-template <int kWin, typename Sink>
-DHD EmitOut decode_sync_emit(const BitReader& br, const HuffImage& im, HState st, uint32_t rend, uint32_t wend,
-                             uint32_t avail, const Checkpoint* cps, int cstride, int ncp, RangeOut first,
-                             SyncMatch* match, Sink& sink) {
-  return decode_emit_t<kWin, true>(br, im, st, rend, wend, avail, const_cast<Checkpoint*>(cps), cstride, 0, &ncp,
-                                   first, match, sink);
-}
-
-// decode_write's emission from a true state `st` up to the block boundary at bit position
-// `stop` (exclusive: the block starting there is not emitted), for the prefix of a lane
-// whose first decode joins the true decode at a checkpoint at `stop`.  Returns the blocks
-// emitted (absolute indices first_block, ..).
-template <int kWin, typename Sink>
-DHD int32_t decode_write_prefix(const BitReader& br, const HuffImage& im, HState st, uint32_t stop, int32_t first_block,
-                                int32_t total_blocks, Sink& sink) {
-  st = sanitize(st, im.blocks_per_mcu);
-  BitCursor cur;
-  bc_init<kWin>(cur, br, st.pos);
-  int32_t blk = st.c, z = st.z;
-  while (z != 0) huff_step<kWin>(cur, br, im, blk, z);  // the previous lane's block
-  int32_t b = first_block;
-  bool open = false;
-  while (b < total_blocks) {
-    if (!open) {
-      if (cur.pos >= stop) break;
-      sink.begin(b);
-      open = true;
-    }
-    const StepOut so = huff_step<kWin>(cur, br, im, blk, z);
-    if (so.kind == 0) sink.dc((int16_t)so.value);
-    else if (so.kind == 1) sink.ac(so.zz, (int16_t)so.value);
-    if (so.block_done) {
-      sink.end();
-      ++b;
-      open = false;
-    }
-  }
-  return b - first_block;
 }
 
 // Element offset (int16 units) of absolute block b inside the image's coefficient area.

@@ -126,7 +126,6 @@ __device__ void plan_place(ImgDesc& d, const ChunkSizes& z, int64_t base, int64_
   d.ent_off = base;
   d.rst_off = d.ent_off + z.ent;
   d.coef_off = d.rst_off + z.rst;
-  d.emit_off = d.coef_off + (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;  // (emit_reserved images)
   d.binfo_off = d.coef_off + z.coef;
   d.plane_off = d.binfo_off + z.binfo;
   d.rgb_off = d.plane_off + z.plane;
@@ -564,7 +563,7 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 }
 
 // Entry words a lane buffers in LDS before it stores them as one aligned group: 32-byte
-// groups in k_huff1, 64-byte groups in k_huff3.
+// groups in k_huff1 (its buffers borrow the skip tables' LDS), 64-byte groups in k_huff3.
 // Word w of lane t sits at [w][t], so the lanes' halfword writes never share a bank.
 // (Measured and dropped, DESIGN.md §5: a register shift register instead of LDS, block
 // records buffered and stored in pairs or groups, 64-byte groups in k_huff1.)
@@ -577,10 +576,13 @@ struct HuffLds {     // k_huff1
   RangeOut R[kHuffThreads];
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
-  // SparseSink buffers of the emitting first decode and of the prefix / rewrite writes
-  // (their own LDS: other waves of the item still run state-only decodes on the skip tables)
-  uint32_t sink[kSinkLds * kHuffThreads];
 };
+// k_huff1's write pass (single-segment images) decodes values, not skips: the SparseSink
+// buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
+// (and the range results R, which follow the tables and are read before the write pass)
+static_assert(offsetof(HuffLds, R) == offsetof(HuffLds, tab) + sizeof(HuffTables), "R follows the tables");
+static_assert(sizeof(HuffSkip) + sizeof(RangeOut) * kHuffThreads >= (size_t)kSinkLds * 4 * kHuffThreads,
+              "sink buffers fit the skip tables and R");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
@@ -614,9 +616,7 @@ template <int W>  // entry words buffered per lane in LDS
 struct SparseSinkT {
   static_assert(W % 4 == 0 && W > 0, "whole 16-byte chunks");
   uint32_t* ent;   // image entry area
-  uint2* binfo;    // image block info (emission: the lane's top record, records grow down)
-  int32_t rdir;    // record b at binfo[rdir * b]: 1, or -1 in an emission region
-  uint32_t rlim;   // emission: room(j) holds while entries + a whole block stay below record j
+  uint2* binfo;    // image block info
   uint32_t n;      // halfwords in stored groups (relative to the image entry area), multiple of 2 W
   uint32_t k;      // halfwords buffered in LDS
   uint32_t bstart, dcw, n16, n32;
@@ -634,19 +634,7 @@ struct SparseSinkT {
   __device__ void open(int32_t first_block) {
     n = (uint32_t)first_block * kEntHalfwordsPerBlock;
     k = 0;
-    rdir = 1;
   }
-  // An emission region [base, base + cap) halfwords (decode_emit): entries from its bottom,
-  // record j at halfwords base + cap - 4 (j + 1).
-  __device__ void open_emit(uint32_t base, uint32_t cap) {
-    n = base;
-    k = 0;
-    binfo = (uint2*)(ent + ((base + cap) >> 1)) - 1;
-    rdir = -1;
-    rlim = base + cap - 4 - (kEntHalfwordsPerBlock + 2 * W);
-  }
-  // block j fits: its entries (<= 128 halfwords + the group padding) end below its record
-  __device__ bool room(int32_t j) const { return n + k + 4u * (uint32_t)j <= rlim; }
   __device__ void begin(int32_t blk) {
     b = blk;
     bstart = n + k;
@@ -679,7 +667,7 @@ struct SparseSinkT {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void record(int32_t blk, uint2 r) { binfo[rdir * blk] = r; }
+  __device__ void record(int32_t blk, uint2 r) { binfo[blk] = r; }
   __device__ void end() { record(b, make_uint2(bstart, n16 | (n32 << 7) | dcw)); }
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
@@ -829,7 +817,7 @@ __device__ int huff_item_image(const ImgDesc* desc, int B, int item) {
 // in-segment rounds).  Long ranges stay with k_huff3: in k_huff1 their second
 // decode would double the longest serial chain of the launch.
 __device__ __forceinline__ bool huff_single_segment(const ImgDesc& d) {
-  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= kHuffFuseSubBits && emit_reserved(d);
+  return d.restart_interval == 0 && d.h_items == 1 && d.h_sub <= 3072;
 }
 
 // Loads work item `item`'s image descriptor and tables into LDS; false past the end.
@@ -855,104 +843,22 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
 }
 
 #ifdef DINO_HUFF_PHASES
-// Phase data of k_huff1 work items (instrumented builds only, scripts/huff_phases.py):
-// [item][0] start, [1] the last lane's end of its look-back, [2] after the first decode,
-// [3] after the sync rounds, [4] end (wall_clock64); [5] rounds | single-segment << 32;
-// [6] lanes re-decoded, [7] their summed bits up to the matched checkpoint, [8] the
-// largest such prefix, [9] re-decoded lanes that matched no checkpoint, [10] lanes whose
-// emission region filled, [11] lanes of single-segment items written again whole.
+// Phase timestamps of k_huff1 work items (instrumented builds only, scripts/huff_phases.py):
+// [item][0..4] = start, after the first decode, after the sync rounds, end; [item][4] = rounds.
 constexpr int kPhaseItems = 8192;
-constexpr int kPhaseSlots = 12;
-__device__ uint64_t g_huff_phase[kPhaseItems][kPhaseSlots];
+__device__ uint64_t g_huff_phase[kPhaseItems][5];
 #define HUFF_PHASE(k, v)                                              \
   do {                                                               \
     if (threadIdx.x == 0 && item < kPhaseItems) g_huff_phase[item][k] = (v); \
-  } while (0)
-#define HUFF_PHASE_ADD(k, v)                                                         \
-  do {                                                                              \
-    if (item < kPhaseItems) atomicAdd((unsigned long long*)&g_huff_phase[item][k], (unsigned long long)(v)); \
-  } while (0)
-#define HUFF_PHASE_MAX(k, v)                                                         \
-  do {                                                                              \
-    if (item < kPhaseItems) atomicMax((unsigned long long*)&g_huff_phase[item][k], (unsigned long long)(v)); \
   } while (0)
 #else
 #define HUFF_PHASE(k, v) \
   do {                   \
   } while (0)
-#define HUFF_PHASE_ADD(k, v) \
-  do {                       \
-  } while (0)
-#define HUFF_PHASE_MAX(k, v) \
-  do {                       \
-  } while (0)
 #endif
 
 constexpr int kHuffLookback = 2048;  // bits a lane decodes before its range to guess its start state
 
-// Lane i's emission region in area `a` (0: first decode, 1: re-decodes; halfwords from the
-// image's entry area; see emit_area_bytes).
-__device__ __forceinline__ void emit_region(const ImgDesc& d, int i, int a, uint32_t* base, uint32_t* cap) {
-  const uint32_t c = (uint32_t)emit_lane_cap(d.h_sub);
-  *base = (uint32_t)((d.emit_off - d.coef_off + a * emit_area_bytes(d)) >> 1) + (uint32_t)i * c;
-  *cap = c + (i == d.h_lanes - 1 ? (uint32_t)kEmitLastExtra : 0u);
-}
-// The records of lane i's region in area a: record j at the returned pointer [-j].
-__device__ __forceinline__ const uint2* emit_records(const ImgDesc& d, const uint8_t* ws, int i, int a) {
-  uint32_t base, cap;
-  emit_region(d, i, a, &base, &cap);
-  return (const uint2*)((const uint32_t*)(ws + d.coef_off) + ((base + cap) >> 1)) - 1;
-}
-
-// A lane's blocks in place once its true start state S and first block blk0 are known, from
-// what its decodes emitted: a confirmed guess: the first decode's records; a re-decode that
-// joined the first decode at a checkpoint: the re-decode's records (the blocks before the
-// checkpoint), then the first decode's from there on; a re-decode that joined nothing: its
-// own records.  Only the 8-byte records move (the entries stay where they were emitted).  A
-// lane whose emission is incomplete (region full) writes its range again from S.
-template <typename Sink>
-__device__ void lane_finish(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint8_t* __restrict__ ws, int i,
-                            HState S, bool redone, SyncMatch M, int32_t nemit1, int32_t eflags1, int32_t nemit2,
-                            int32_t eflags2, int32_t blk0, uint32_t nbits, Sink& sink) {
-  uint2* binfo = (uint2*)(ws + d.binfo_off);
-  const int32_t total = d.total_blocks;
-  const bool matched = redone && M.m0 >= 0;
-  const bool ok = !redone ? !(eflags1 & kEmitOverflow)
-                          : (matched ? !(eflags1 & kEmitOverflow) && eflags2 == 0 : !(eflags2 & kEmitOverflow));
-  if (ok) {
-    int32_t b = blk0;
-    if (redone) {
-      const uint2* r2 = emit_records(d, ws, i, 1);
-      for (int32_t j = 0; j < nemit2 && b < total; ++j, ++b) binfo[b] = r2[-j];
-    }
-    if (!redone || matched) {
-      const uint2* r1 = emit_records(d, ws, i, 0);
-      for (int32_t j = matched ? M.m0 : 0; j < nemit1 && b < total; ++j, ++b) binfo[b] = r1[-j];
-    }
-    if ((redone && !matched ? eflags2 : eflags1) & kEmitInsufficient)  // the rest: zero blocks (decode_write)
-      for (; b < total; ++b) binfo[b] = make_uint2(0u, kBinfoAbsDc);
-  } else {
-    sink.binfo = binfo;
-    sink.open(blk0);
-    decode_write<kHuffSrc>(br, im, S, lane_write_end(d, i), blk0, total, (int32_t*)nullptr, nbits, sink);
-    sink.close();
-  }
-}
-
-// k_huff1 per work item: every lane guesses its start state from kHuffLookback bits before
-// its range (decode_lookback), decodes its range from the guess (the first decode, which
-// emits the lane's blocks into its emission region: decode_emit), then sync rounds inside
-// the item re-decode the ranges whose start state changed, stopping at the first checkpoint
-// the first decode also passed.  Items of a multi-segment or a long-range image leave their
-// lane records to k_huff2 / k_huff3.  A single-segment image (huff_single_segment) is
-// finished here: after the rounds and the block scan, lane_finish places each lane's blocks:
-//   * a lane whose guess the rounds confirmed copies its block records into place (its
-//     entries stay where they were emitted);
-//   * a lane re-decoded from its true state that joined its first decode at a checkpoint
-//     writes the blocks up to that checkpoint (decode_write_prefix, into its blk0 region of
-//     the entry area) and copies the records of its first decode from there on;
-//   * any other lane (no checkpoint matched, emission region full) writes its range again
-//     from its true state (decode_write), as every lane did before round 5.
 __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restrict__ desc, int B,
                                                         uint8_t* __restrict__ ws) {
   main_prio();
@@ -972,7 +878,6 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
     const int i = (item - sd.h_item_base) * kHuffThreads + t;  // lane index within the image
     const bool active = i < sd.h_lanes;
-    const bool single = huff_single_segment(sd);
     const uint32_t rend = lane_range_end(sd, i, nbits);
     LaneRec* lr = (LaneRec*)(ws + sd.hlane_off);
     // checkpoint k of lane i at [k][lane]: a wave's lanes write neighbouring words
@@ -986,28 +891,12 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       const uint32_t to = myS.pos, from = to > (uint32_t)kHuffLookback ? to - (uint32_t)kHuffLookback : 0u;
       myS = decode_lookback<kHuffSrc>(br, im, from, to);
     }
-    HUFF_PHASE_MAX(1, wall_clock64());
-    const HState guess = myS;
-    SyncMatch match{0xFFFFFFFFu, -1};
-    SparseSink sink;
-    sink.ent = (uint32_t*)(ws + sd.coef_off);
-    sink.lb = L.sink + t;
-    int32_t nemit = 0, eflags = 0, nemit2 = 0, eflags2 = 0;
-    uint32_t ebase, ecap, ebase2, ecap2;
-    emit_region(sd, i, 0, &ebase, &ecap);
-    emit_region(sd, i, 1, &ebase2, &ecap2);
-    if (active) {  // the first decode emits the lane's blocks into its emission region
-      sink.open_emit(ebase, ecap);
-      const EmitOut e = decode_emit<kHuffSrc>(br, im, myS, rend, lane_write_end(sd, i), nbits, cps, cstride,
-                                              kHuffCheckpoints, &ncp, sink);
-      sink.close();
-      myR1 = e.r;
-      nemit = e.nemit;
-      eflags = e.flags;
+    if (active) {
+      myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
       L.R[t] = myR1;
     }
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
-    HUFF_PHASE(2, wall_clock64());
+    HUFF_PHASE(1, wall_clock64());
     int round = 0;
     for (; round < kHuffThreads + 1; ++round) {
       HState want;
@@ -1017,55 +906,39 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
         redo = !hstate_eq(want, myS);
       }
       __syncthreads();
-      if (redo) {  // from the corrected state, emitting into the lane's re-decode region
+      if (redo) {
         myS = want;
-        sink.open_emit(ebase2, ecap2);
-        const EmitOut e = decode_sync_emit<kHuffSrc>(br, im, want, rend, lane_write_end(sd, i), nbits, cps, cstride, ncp,
-                                                     myR1, &match, sink);
-        sink.close();
-        nemit2 = e.nemit;
-        eflags2 = e.flags;
-        L.R[t] = e.r;
+        L.R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1);
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
     const RangeOut res = L.R[t];
-    HUFF_PHASE(3, wall_clock64());
-    HUFF_PHASE(5, (uint64_t)round | ((uint64_t)(single ? 1 : 0) << 32));
-    const bool confirmed = hstate_eq(guess, myS);
-#ifdef DINO_HUFF_PHASES
-    if (active && !confirmed) {
-      HUFF_PHASE_ADD(6, 1);
-      if (match.m0 >= 0) {
-        HUFF_PHASE_ADD(7, match.pos - myS.pos);
-        HUFF_PHASE_MAX(8, match.pos - myS.pos);
-      } else {
-        HUFF_PHASE_ADD(9, 1);
-      }
-    }
-    if (active && (eflags & kEmitOverflow)) HUFF_PHASE_ADD(10, 1);
-    if (active && single && (((eflags | eflags2) & kEmitOverflow))) HUFF_PHASE_ADD(11, 1);
-#endif
-    if (single) {
-      // the whole image is this segment: its start states are final (k_huff2 and k_huff3 skip it)
+    HUFF_PHASE(2, wall_clock64());
+    HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
+    if (huff_single_segment(sd)) {
+      // the whole image is this segment: its start states are final, so the blocks
+      // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
       uint32_t tot;
       const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)res.nblk : 0u, L.wave, &tot);
-      if (active)
-        lane_finish(br, im, sd, ws, i, myS, !confirmed, match, nemit, eflags, nemit2, eflags2, (int32_t)blk0, nbits,
-                    sink);
+      if (active) {
+        SparseSink sink;
+        sink.ent = (uint32_t*)(ws + sd.coef_off);
+        sink.binfo = (uint2*)(ws + sd.binfo_off);
+        sink.lb = reinterpret_cast<uint32_t*>(&L.tab.skip) + t;
+        sink.open((int32_t)blk0);
+        decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
+                                 nbits, sink);
+        sink.close();
+      }
     } else if (active) {
       LaneRec& o = lr[i];
       o.S = myS;
       o.R = res;
       o.R1 = myR1;
       o.ncp = ncp;
-      o.flags = (confirmed ? 0 : kLaneRedone) | (eflags << 1) | (eflags2 << 3);
-      o.nemit = nemit;
-      o.nemit2 = nemit2;
-      o.M = match;
     }
     __syncthreads();
-    HUFF_PHASE(4, wall_clock64());
+    HUFF_PHASE(3, wall_clock64());
   }
 }
 
@@ -1078,7 +951,6 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
   main_prio();
   __shared__ HuffTables s_tab;
   __shared__ uint32_t s_wave[kHuff2Threads / 64];
-  __shared__ uint32_t s_sink[kSinkLds * kHuff2Threads];
   const ImgDesc& d = desc[blockIdx.x];
   const int t = threadIdx.x;
   if (d.status != DINO_IMG_OK || d.kind != 0 || d.restart_interval > 0 || huff_single_segment(d)) return;
@@ -1096,9 +968,6 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
     const BitReader br{(const uint32_t*)(ws + d.ent_off), (uint32_t)d.ent_len};
     const uint32_t nbits = (uint32_t)d.ent_len * 8u;
     const Checkpoint* cps = (const Checkpoint*)(ws + d.cps_off);
-    SparseSink sink;
-    sink.ent = (uint32_t*)(ws + d.coef_off);
-    sink.lb = s_sink + t;
     for (int round = 0; round <= n; ++round) {
       int any = 0;
       for (int i = 1 + t; i < n; i += kHuff2Threads) {
@@ -1113,17 +982,8 @@ __global__ void __launch_bounds__(kHuff2Threads) k_huff2(const ImgDesc* __restri
         if (lr[i].pad) {
           const HState want = lr[i].W;
           lr[i].S = want;
-          SyncMatch m;
-          uint32_t eb, ec;
-          emit_region(d, i, 1, &eb, &ec);
-          sink.open_emit(eb, ec);
-          const EmitOut e = decode_sync_emit<kHuffSrc>(br, im, want, lane_range_end(d, i, nbits), lane_write_end(d, i),
-                                                       nbits, cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1, &m, sink);
-          sink.close();
-          lr[i].R = e.r;
-          lr[i].M = m;
-          lr[i].nemit2 = e.nemit;
-          lr[i].flags = (lr[i].flags & 7) | kLaneRedone | (e.flags << 3);
+          lr[i].R = decode_range_sync<kHuffSrc>(br, im, want, lane_range_end(d, i, nbits),
+                                             cps + i, d.h_lanes_cap, lr[i].ncp, lr[i].R1);
         }
       }
       __syncthreads();
@@ -1179,11 +1039,13 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff3(const ImgDesc* __restric
           sink.close();
         }
       }
-    } else if (i < sd.h_lanes) {  // the lane's emitted blocks in place (k_huff1's lane_finish)
+    } else if (i < sd.h_lanes) {
       const LaneRec& r = ((const LaneRec*)(ws + sd.hlane_off))[i];
       const BitReader br{words, (uint32_t)sd.ent_len};
-      lane_finish(br, im, sd, ws, i, r.S, (r.flags & kLaneRedone) != 0, r.M, r.nemit, (r.flags >> 1) & 3, r.nemit2,
-                  (r.flags >> 3) & 3, r.blk0, br.nbytes * 8u, sink);
+      sink.open(r.blk0);
+      decode_write<kHuffSrc>(br, im, r.S, lane_write_end(sd, i), r.blk0, sd.total_blocks, (int32_t*)nullptr,
+                               br.nbytes * 8u, sink);
+      sink.close();
     }
     __syncthreads();
   }
@@ -3123,6 +2985,79 @@ __device__ __forceinline__ void final_compute(const uint8_t* __restrict__ tile, 
   }
 }
 
+// Separable form of the same blur for the kernel sizes the DINO sigma range yields: a
+// lane takes 4 columns x kBlurStrip rows of one channel, convolves each tile row it
+// needs once with the 1-D kernel (float fma chain over the taps), then the strip's
+// columns with the 1-D kernel again.  The 2-D kernel of torchvision is the outer
+// product of the same 1-D weights, so the two forms differ only in float rounding
+// (the parity tests hold blurred views to one level on <= 0.5 % of pixels, as for the
+// 2-D form against torch's conv2d); per output it takes 2 KS (KS + kBlurStrip - 1) /
+// kBlurStrip fmas instead of KS^2.  k_final (the large views' bands) takes it: 0.378 ->
+// 0.358 ms per C2 step; k_vfinal keeps the 2-D form, whose registers leave it 7 waves per
+// SIMD instead of 5 (0.466 vs 0.494 ms).
+constexpr int kBlurStrip = 4;
+template <int KS, typename OutT>
+__device__ __forceinline__ void final_compute_sep(const uint8_t* __restrict__ tile, int tp, int64_t tplane, int nr,
+                                                  int y0, int S, const float* __restrict__ k1, bool solarize,
+                                                  const OutT* __restrict__ ntab, OutT* __restrict__ out) {
+  constexpr int R = kBlurStrip, NW = (KS + 3 + 3) / 4, TR = R + KS - 1;
+  float w[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) w[k] = k1[k];
+  const int nq = (S + 3) >> 2, ng = (nr + R - 1) / R;
+  const int last_row = nr + KS - 2;  // the tile's last row (band + halo)
+  const int64_t N = (int64_t)S * S;
+  const bool vec_ok = (S & 3) == 0;
+  const FastDiv dplane((uint32_t)(ng * nq)), dgrp((uint32_t)nq);
+  for (int e = threadIdx.x; e < 3 * ng * nq; e += blockDim.x) {
+    const int ch = (int)dplane.div((uint32_t)e), rem = e - ch * ng * nq;
+    const int gy = (int)dgrp.div((uint32_t)rem), x0 = 4 * (rem - gy * nq);
+    const int ys = gy * R;
+    const uint8_t* pl = tile + ch * tplane + x0;
+    float acc[R][4];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[r][j] = 0.0f;
+#pragma unroll
+    for (int a = 0; a < TR; ++a) {
+      // rows past the band's last only feed outputs past it, which are not stored
+      const uint32_t* row = (const uint32_t*)(pl + min(ys + a, last_row) * tp);
+      uint32_t wv[NW];
+#pragma unroll
+      for (int q = 0; q < NW; ++q) wv[q] = row[q];
+      float h[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int c = 0; c < KS; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int bi = c + j;
+          h[j] = fmaf(w[c], (float)((wv[bi >> 2] >> (8 * (bi & 3))) & 255u), h[j]);
+        }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (a - r < 0 || a - r >= KS) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[r][j] = fmaf(w[a - r], h[j], acc[r][j]);
+      }
+    }
+    const OutT* tb = ntab + 256 * ch;
+    const int n = min(4, S - x0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (ys + r >= nr) break;
+      OutT o4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float rr = rintf(acc[r][j]);
+        const int v = rr <= 0.0f ? 0 : (rr >= 255.0f ? 255 : (int)rr);
+        o4[j] = tb[solarize ? solarize_u8(v) : v];
+      }
+      store_vals4<OutT>(out, ch * N + (int64_t)(y0 + ys + r) * S + x0, o4, n, vec_ok);
+    }
+  }
+}
+
 template <typename OutT>
 __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                const ViewPlan* __restrict__ plan, int nv, int v0, int B,
@@ -3216,10 +3151,10 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
   const bool sol = p.solarize != 0;
   switch (ks) {
     case 1: final_compute<1, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
-    case 3: final_compute<3, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
-    case 5: final_compute<5, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
-    case 7: final_compute<7, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
-    case 9: final_compute<9, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
+    case 3: final_compute_sep<3, OutT>(tile, tp, tplane, nr, y0, S, H.k1, sol, ntab, out); break;
+    case 5: final_compute_sep<5, OutT>(tile, tp, tplane, nr, y0, S, H.k1, sol, ntab, out); break;
+    case 7: final_compute_sep<7, OutT>(tile, tp, tplane, nr, y0, S, H.k1, sol, ntab, out); break;
+    case 9: final_compute_sep<9, OutT>(tile, tp, tplane, nr, y0, S, H.k1, sol, ntab, out); break;
     default: final_compute<0, OutT>(tile, tp, tplane, nr, y0, S, ks, H.k2, sol, ntab, out); break;
   }
 }
@@ -3778,6 +3713,31 @@ hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_
   return hipGetLastError();
 }
 
+// The per-pixel colour operators over all 2^24 inputs (index = a << 16 | b << 8 | c):
+// op 0 RGB -> HSV, op 1 HSV -> RGB, op 2 hue_shift by `param` (the ColorJitter hue op);
+// out[3 * index + k].  For the exhaustive device-side checks against Pillow.
+__global__ void __launch_bounds__(256) k_pixel_ops(int op, int param, uint8_t* __restrict__ out) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  int x = (idx >> 16) & 255, y = (idx >> 8) & 255, z = idx & 255;
+  if (op == 0) {
+    int h, sv, v;
+    rgb_to_hsv(x, y, z, &h, &sv, &v);
+    x = h, y = sv, z = v;
+  } else if (op == 1) {
+    hsv_to_rgb(x, y, z, &x, &y, &z);
+  } else {
+    hue_shift(x, y, z, param);
+  }
+  out[3 * (int64_t)idx] = (uint8_t)x;
+  out[3 * (int64_t)idx + 1] = (uint8_t)y;
+  out[3 * (int64_t)idx + 2] = (uint8_t)z;
+}
+
+hipError_t launch_pixel_ops(int op, int param, uint8_t* out, hipStream_t s) {
+  k_pixel_ops<<<(1 << 24) / 256, 256, 0, s>>>(op, param, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s) {
   k_copy_rgb<<<256, 256, 0, s>>>(desc, idx, ws, dst);
   return hipGetLastError();
@@ -3796,10 +3756,7 @@ hipError_t copy_huff_phases(uint64_t* host, int64_t n_items) {
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return e;
   const int64_t n = n_items < kPhaseItems ? n_items : kPhaseItems;
-  e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_huff_phase), sizeof(uint64_t) * kPhaseSlots * n);
-  if (e != hipSuccess) return e;
-  static uint64_t zeros[kPhaseItems][kPhaseSlots];  // the counters start from zero for the next launches
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_huff_phase), zeros, sizeof(zeros));
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_huff_phase), sizeof(uint64_t) * 5 * n);
 }
 #endif
 

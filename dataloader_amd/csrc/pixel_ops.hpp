@@ -29,76 +29,82 @@ DHD int rgb_to_l(int r, int g, int b) { return (r * 19595 + g * 38470 + b * 7471
 
 DHD int clip8i(int v) { return v <= 0 ? 0 : (v >= 255 ? 255 : v); }
 
-// 1/d (d = 1..255) as correctly rounded doubles.  For integers 0 <= n <= d <= 255,
-// (float)(n * (1/d)) equals the float quotient n / d: the double product is within
-// 2^-52 (relative) of n/d, and a quotient with a denominator <= 255 that is not exact
-// in float lies >= 2^-32 (relative) away from every float rounding midpoint.  The
-// same holds for the rationals k/255 below.  (The exhaustive test of both
-// conversions against Pillow over all 2^24 inputs, tests/test_emu_cpu.py, checks it.)
-struct RcpU8 {
-  double v[256];
-  constexpr RcpU8() : v() {
-    for (int d = 1; d < 256; ++d) v[d] = 1.0 / (double)d;
-  }
-};
-inline constexpr RcpU8 kRcpU8{};
 constexpr double kRcp255 = 1.0 / 255.0;
 
-DHD void rgb_to_hsv(int r, int g, int b, int* oh, int* os, int* ov) {
-  int maxc = r > g ? (r > b ? r : b) : (g > b ? g : b);
-  int minc = r < g ? (r < b ? r : b) : (g < b ? g : b);
-  *ov = maxc;
-  if (minc == maxc) {
-    *oh = 0;
-    *os = 0;
-    return;
-  }
-  // Convert.c rgb2hsv_row: float quotients (via the exact reciprocal products above)
-  const int cri = maxc - minc;
-  const double rcr = kRcpU8.v[cri];
-  float s = (float)((double)cri * kRcpU8.v[maxc]);
-  float rc = (float)((double)(maxc - r) * rcr);
-  float gc = (float)((double)(maxc - g) * rcr);
-  float bc = (float)((double)(maxc - b) * rcr);
-  float h;
-  if (r == maxc) {
-    h = bc - gc;
-  } else if (g == maxc) {
-    h = (float)(2.0 + (double)rc - (double)bc);
-  } else {
-    h = (float)(4.0 + (double)gc - (double)rc);
-  }
-  // fmod(h / 6.0 + 1.0, 1.0): h is in [-1, 5], so the argument is in (0, 2) and the
-  // remainder is the argument minus 1 when >= 1 (exact)
-  const double x = (double)h / 6.0 + 1.0;
-  h = (float)(x >= 1.0 ? x - 1.0 : x);
-  *oh = clip8i((int)((double)h * 255.0));
-  *os = clip8i((int)((double)s * 255.0));
+// 1/d in double: on the GPU the hardware reciprocal (a seed of roughly single
+// precision) refined by one Newton step (relative error ~2^-44), on the host the
+// division.  Used only as n * (1/d) -> float with n <= d <= 255: such a
+// quotient is either exact in float or >= 2^-32 (relative) away from every float
+// rounding midpoint, so both give the correctly rounded float quotient (and the GPU
+// test of all 2^24 inputs against Pillow, tests/test_gpu_round5.py, checks it).
+DHD double rcp_f64(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rcp(d);
+  return fma(y, fma(-d, y, 1.0), y);
+#else
+  return 1.0 / d;
+#endif
 }
 
-DHD void hsv_to_rgb(int h, int s, int v, int* r, int* g, int* b) {
-  if (s == 0) {
-    *r = *g = *b = v;
-    return;
+// Convert.c rgb2hsv_row for one pixel, restated without per-pixel divisions (checked
+// over all 2^24 colours against Pillow, on the host by tests/test_emu_cpu.py and on the
+// GPU by tests/test_gpu_round5.py):
+//  * s = cri / maxc and the channel quotients are float quotients (C's
+//    `cr / (float)maxc` etc.), from the reciprocal above;
+//  * of the three quotients (maxc - x) / cri, the max channel's is 0 and the min
+//    channel's 1 exactly, so h is `a + sign * qm` with qm the middle channel's quotient
+//    and (a, sign) given by the case -- one rounding, as C's float / double expression;
+//  * fmod(h / 6.0 + 1.0, 1.0): h in [-1, 5], so it is h / 6 for h >= 0 and 1 + h / 6
+//    below; h / 6 as a double product with the rounded 1/6 gives the same float.
+DHD void rgb_to_hsv(int r, int g, int b, int* oh, int* os, int* ov) {
+  const int maxc = r > g ? (r > b ? r : b) : (g > b ? g : b);
+  const int minc = r < g ? (r < b ? r : b) : (g < b ? g : b);
+  *ov = maxc;
+  const int cri = maxc - minc;
+  const float s = (float)((double)cri * rcp_f64((double)(maxc > 0 ? maxc : 1)));
+  const int mid = r + g + b - maxc - minc;
+  const float qm = (float)((double)(maxc - mid) * rcp_f64((double)(cri > 0 ? cri : 1)));
+  // r max: g min -> bc - gc = qm - 1, b min -> 1 - qm;  g max: r min -> 2 + 1 - qm,
+  // b min -> 2 + qm - 1;  b max: r min -> 4 + qm - 1, g min -> 4 + 1 - qm
+  float a, sg;
+  if (r == maxc) {
+    a = g == minc ? -1.0f : 1.0f;
+    sg = g == minc ? 1.0f : -1.0f;
+  } else if (g == maxc) {
+    a = r == minc ? 3.0f : 1.0f;
+    sg = r == minc ? -1.0f : 1.0f;
+  } else {
+    a = r == minc ? 3.0f : 5.0f;
+    sg = r == minc ? 1.0f : -1.0f;
   }
-  // Convert.c hsv2rgb: i = floor(h * 6 / 255), f = its fraction (0 exactly when h * 6
-  // is a multiple of 255), fs = s / 255 — the same values without double divisions
+  const float h = fmaf(sg, qm, a);
+  const double y = (double)h * (1.0 / 6.0);
+  const float hf = (float)(h >= 0.0f ? y : y + 1.0);
+  *oh = cri == 0 ? 0 : clip8i((int)((double)hf * 255.0));
+  *os = cri == 0 ? 0 : clip8i((int)((double)s * 255.0));
+}
+
+// Convert.c hsv2rgb: i = floor(h * 6 / 255), f its fraction, fs = s / 255, and the
+// rounded values of v * (1 - fs), v * (1 - fs * f) and v * (1 - fs * (1 - f)), here as
+// floor(v + 0.5 - v * x) by one float fma each (checked over all 2^24 inputs against
+// Pillow, host and GPU).
+DHD void hsv_to_rgb(int h, int s, int v, int* r, int* g, int* b) {
   const int h6 = h * 6;
   const int i = h6 / 255;
-  float f = h6 - 255 * i == 0 ? 0.0f : (float)((double)h6 * kRcp255 - (double)i);
-  float fs = (float)((double)s * kRcp255);
-  int p = (int)round((double)(float)v * (1.0 - (double)fs));
-  int q = (int)round((double)(float)v * (1.0 - (double)(fs * f)));  // fs * f is a float product in C
-  int t = (int)round((double)(float)v * (1.0 - (double)fs * (1.0 - (double)f)));
-  int up = clip8i(p), uq = clip8i(q), ut = clip8i(t);
-  switch (i % 6) {
-    case 0: *r = v;  *g = ut; *b = up; break;
-    case 1: *r = uq; *g = v;  *b = up; break;
-    case 2: *r = up; *g = v;  *b = ut; break;
-    case 3: *r = up; *g = uq; *b = v;  break;
-    case 4: *r = ut; *g = up; *b = v;  break;
-    default: *r = v; *g = up; *b = uq; break;
-  }
+  const float f = (float)((double)(h6 - 255 * i) * kRcp255);
+  const float fs = (float)((double)s * kRcp255);
+  const float vf = (float)v, vh = vf + 0.5f;
+  const int up = clip8i((int)floorf(fmaf(-vf, fs, vh)));
+  const int uq = clip8i((int)floorf(fmaf(-vf, fs * f, vh)));
+  const int ut = clip8i((int)floorf(fmaf(-vf, fmaf(-fs, f, fs), vh)));
+  const int k = i == 6 ? 0 : i;  // i % 6
+  int rr = k == 0 || k == 5 ? v : (k == 1 ? uq : (k == 4 ? ut : up));
+  int gg = k == 1 || k == 2 ? v : (k == 0 ? ut : (k == 3 ? uq : up));
+  int bb = k == 3 || k == 4 ? v : (k == 2 ? ut : (k == 5 ? uq : up));
+  if (s == 0) rr = gg = bb = v;
+  *r = rr;
+  *g = gg;
+  *b = bb;
 }
 
 // torchvision adjust_hue on one pixel: RGB -> HSV, H += delta (uint8 wrap), -> RGB.

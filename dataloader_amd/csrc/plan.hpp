@@ -19,18 +19,8 @@ struct LaneRec {
   int32_t blk0;   // first block the lane emits (k_huff2 scan)
   HState W;       // k_huff2 scratch: wanted start state
   int32_t pad;
-  int32_t flags;  // kLaneRedone | first decode's EmitOut::flags << 1 | last re-decode's << 3
-  int32_t nemit;  // blocks the first decode emitted
-  int32_t nemit2; // blocks the last re-decode emitted
-  SyncMatch M;    // the last re-decode's matched checkpoint
 };
-static_assert(sizeof(LaneRec) == 88, "LaneRec layout");
-constexpr int32_t kLaneRedone = 1;
-
-// Image areas start 256-byte aligned (tail pads each image), and so does the sparse entry
-// area (rst pads ent + rst): a lane's entry region starts at a multiple of 256 bytes in
-// memory too (SparseSink stores groups of up to 64 bytes aligned to their size).
-DHD int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
+static_assert(sizeof(LaneRec) == 68, "LaneRec layout");
 
 // Lanes reserved for the speculative Huffman decode (restart images decode per interval).
 DHD int32_t huff_lanes_cap(const ImgDesc& d) {
@@ -43,26 +33,6 @@ DHD int32_t huff_lanes_cap(const ImgDesc& d) {
 // Sparse entry capacity per block (see SparseSink): 63 u32 entries + 1 alignment halfword.
 constexpr int kEntHalfwordsPerBlock = 128;
 
-// The emission areas of the speculative decode (images without restart intervals).  k_huff1's
-// first decode emits each lane's blocks into a region of its own in area 0 (decode_emit), a
-// sync round's re-decode into one in area 1 (decode_sync_emit): lane i's region is
-// [i cap, (i + 1) cap) halfwords of the area, cap = emit_lane_cap(h_sub) (half a halfword per
-// bit of range + 256: a q85 photo's entries and records take ~0.15 halfwords per bit; a lane
-// that fills its region is written again from its true state), the last lane's region is
-// kEmitLastExtra halfwords longer (the MCU it may decode past the data).  The lane's block
-// records grow down from the top of its region.
-constexpr int kHuffFuseSubBits = 3072;  // single-segment images with ranges up to this are finished by k_huff1
-constexpr int32_t kEmitLastExtra = 2048;
-DHD bool emit_reserved(const ImgDesc& d) { return d.kind == 0 && d.restart_interval == 0; }
-DHD int32_t emit_lane_cap(int32_t sub) { return ((sub >> 1) + 256 + 127) & ~127; }
-// (one area) h_lanes x cap <= (nbits + sub) / 2 + 383 h_lanes halfwords; sub <= kHuffSegBits / kHuffThreads + 32
-DHD int64_t emit_area_bytes(const ImgDesc& d) {
-  if (!emit_reserved(d)) return 0;
-  const int64_t bits = ((int64_t)d.scan_len + 64) * 8;
-  const int64_t sub = kHuffSegBits / kHuffThreads + 32;
-  return align256(2 * ((bits + sub) / 2 + 1 + 383 * (int64_t)huff_lanes_cap(d) + kEmitLastExtra));
-}
-
 // Byte sizes of an image's workspace regions, in chunk order: destuffed entropy
 // bytes, restart offsets, coefficients (baseline: sparse entries, 128 halfwords of
 // capacity per block, see SparseSink; kind 1: the dense int16 buffer), block info
@@ -74,6 +44,10 @@ struct ChunkSizes {
   DHD int64_t total() const { return sum() + tail; }
 };
 
+// Image areas start 256-byte aligned (tail pads each image), and so does the sparse entry
+// area (rst pads ent + rst): a lane's entry region starts at a multiple of 256 bytes in
+// memory too (SparseSink stores groups of up to 64 bytes aligned to their size).
+DHD int64_t align256(int64_t x) { return (x + 255) & ~(int64_t)255; }
 DHD ChunkSizes chunk_finish(ChunkSizes z) {
   z.tail = align256(z.sum()) - z.sum();
   return z;
@@ -104,7 +78,7 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   }
   z.ent = align16((int64_t)d.scan_len + 64);
   z.rst = align256(z.ent + 4 * ((int64_t)d.n_rst_max + 1)) - z.ent;
-  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2 + 2 * emit_area_bytes(d);
+  z.coef = (int64_t)d.total_blocks * kEntHalfwordsPerBlock * 2;
   z.binfo = align16((int64_t)d.total_blocks * 8);
   const int64_t lanes = huff_lanes_cap(d);
   z.cps = lanes * kHuffCheckpoints * (int64_t)sizeof(Checkpoint);

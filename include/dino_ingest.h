@@ -172,6 +172,12 @@ int dino_decode_spans(dino_ctx* ctx, const uint8_t* d_bytes, const int64_t* d_of
 /* Copy decoded image i (HWC uint8 RGB, pitch = width*3) to d_rgb (debug / tests). */
 int dino_copy_rgb(dino_ctx* ctx, int32_t index, uint8_t* d_rgb, void* stream);
 
+/* The per-pixel colour operators of the ColorJitter hue op over all 2^24 inputs
+ * (index = a << 16 | b << 8 | c; d_out: 3 * 2^24 bytes, out[3 * index + k]): op 0 RGB -> HSV
+ * (Pillow convert("HSV")), op 1 HSV -> RGB (convert("RGB")), op 2 the hue shift by
+ * `param` (torchvision adjust_hue's PIL path).  Tests / verification only. */
+int dino_pixel_ops_all(int32_t op, int32_t param, uint8_t* d_out, void* stream);
+
 /* Sample view params on device (counter-based Philox keyed by seed, batch_index,
  * sample, view) for the last decoded batch; writes batch*n_views records. */
 int dino_sample_params(dino_ctx* ctx, const dino_aug_config* cfg, uint64_t seed, uint64_t batch_index,

@@ -176,120 +176,6 @@ inline void model_huffman_spec(const BitReader& br, const HuffImage& im, const I
   }
 }
 
-// ---- k_huff1's emitting first decode (single-segment images) ------------------------
-// Blocks a lane emits under local indices (the emission area + record staging).
-struct BlockListSink {
-  struct Block {
-    int16_t dc = 0;
-    std::vector<std::pair<int, int16_t>> ac;
-  };
-  std::vector<Block> blocks;
-  int32_t cur = -1;
-  int32_t max_rec = 128;
-  bool room(int32_t j) const { return j < max_rec; }
-  void begin(int32_t j) {
-    if ((int32_t)blocks.size() <= j) blocks.resize(j + 1);
-    blocks[j] = Block{};
-    cur = j;
-  }
-  void ac(int zz, int16_t v) { blocks[cur].ac.emplace_back(zz, v); }
-  void dc(int16_t v) { blocks[cur].dc = v; }
-  void end() {}
-  void replay(int32_t j, int32_t b, CoefSink& out) const {
-    out.begin(b);
-    for (auto& e : blocks[j].ac) out.ac(e.first, e.second);
-    out.dc(blocks[j].dc);
-    out.end();
-  }
-};
-
-// k_huff1 on a single-segment image: look-back guess, emitting first decode, sync rounds
-// whose re-decodes emit too (matched checkpoints kept), block scan, then per lane the
-// records placed (kernels.hip lane_finish): the first decode's blocks (guess confirmed), the
-// re-decode's blocks up to the checkpoint where it joined the first decode + the first
-// decode's from there, or the re-decode's blocks alone (no checkpoint joined); a lane whose
-// emission is incomplete is rewritten from its true state.  stats: {rounds, lanes
-// re-decoded, lanes, lanes rewritten whole}.
-template <int kWin>
-inline void model_huffman_emit(const BitReader& br, const HuffImage& im, const ImgDesc& d, uint32_t nbits, int lanes,
-                               int max_rec, CoefSink& sink, int32_t* dcd, int32_t* stats) {
-  const int total_blocks = d.total_blocks;
-  int n = lanes;
-  uint32_t sub = (nbits + n - 1) / n;
-  sub = std::max(32u, (sub + 31) & ~31u);
-  n = std::max(1, std::min(n, (int)((nbits + sub - 1) / sub)));
-  std::vector<HState> S(n), G(n);
-  std::vector<RangeOut> R(n), R1(n);
-  std::vector<EmitOut> E(n), E2(n);
-  std::vector<SyncMatch> M(n, SyncMatch{0xFFFFFFFFu, -1});
-  std::vector<Checkpoint> cps((size_t)n * kHuffCheckpoints);
-  std::vector<int32_t> ncp(n);
-  std::vector<BlockListSink> emit(n), emit2(n);
-  for (auto& e : emit) e.max_rec = max_rec;
-  for (auto& e : emit2) e.max_rec = max_rec;
-  auto rend = [&](int i) -> uint32_t { return i == n - 1 ? nbits : (uint32_t)(i + 1) * sub; };
-  auto wend = [&](int i) -> uint32_t { return i == n - 1 ? 0xFFFFFFFFu : (uint32_t)(i + 1) * sub; };
-  for (int i = 0; i < n; ++i) {
-    G[i] = HState{(uint32_t)i * sub, 0, 0};
-    if (i > 0) G[i] = decode_lookback<kWin>(br, im, G[i].pos > 2048u ? G[i].pos - 2048u : 0u, G[i].pos);
-    S[i] = G[i];
-    E[i] = decode_emit<kWin>(br, im, S[i], rend(i), wend(i), nbits, &cps[(size_t)i * kHuffCheckpoints], 1,
-                             kHuffCheckpoints, &ncp[i], emit[i]);
-    R[i] = R1[i] = E[i].r;
-  }
-  int rounds = 0, redone = 0, whole = 0;
-  for (;;) {
-    std::vector<HState> want(n);
-    std::vector<char> redo(n, 0);
-    for (int i = 1; i < n; ++i) {
-      want[i] = R[i - 1].end;
-      redo[i] = !hstate_eq(want[i], S[i]);
-    }
-    bool any = false;
-    for (int i = 1; i < n; ++i) {
-      if (!redo[i]) continue;
-      S[i] = want[i];
-      emit2[i].blocks.clear();
-      E2[i] = decode_sync_emit<kWin>(br, im, S[i], rend(i), wend(i), nbits, &cps[(size_t)i * kHuffCheckpoints], 1,
-                                     ncp[i], R1[i], &M[i], emit2[i]);
-      R[i] = E2[i].r;
-      any = true;
-    }
-    ++rounds;
-    if (!any) break;
-  }
-  int32_t blk0 = 0;
-  sink.dcd = dcd;
-  for (int i = 0; i < n; ++i) {
-    const bool re = !hstate_eq(S[i], G[i]);
-    redone += re;
-    const bool matched = re && M[i].m0 >= 0;
-    const int32_t f1 = E[i].flags, f2 = re ? E2[i].flags : 0;
-    const bool ok = !re ? !(f1 & kEmitOverflow) : (matched ? !(f1 & kEmitOverflow) && f2 == 0 : !(f2 & kEmitOverflow));
-    if (!ok) {  // rewrite from the true state
-      ++whole;
-      decode_write<kWin>(br, im, S[i], wend(i), blk0, total_blocks, (int32_t*)nullptr, nbits, sink);
-    } else {
-      int32_t b = blk0;
-      if (re)
-        for (int32_t j = 0; j < E2[i].nemit && b < total_blocks; ++j, ++b) emit2[i].replay(j, b, sink);
-      if (!re || matched)
-        for (int32_t j = matched ? M[i].m0 : 0; j < E[i].nemit && b < total_blocks; ++j, ++b) emit[i].replay(j, b, sink);
-      if ((re && !matched ? f2 : f1) & kEmitInsufficient)
-        for (; b < total_blocks; ++b) sink.zero(b);
-    }
-    blk0 += R[i].nblk;
-  }
-  sink.dcd = nullptr;
-  model_dcscan(d, im, dcd, sink.coef);
-  if (stats) {
-    stats[0] = rounds;
-    stats[1] = redone;
-    stats[2] = n;
-    stats[3] = whole;
-  }
-}
-
 struct StageCapture {
   std::vector<uint8_t> ent;
   std::vector<int16_t> coef;
@@ -402,8 +288,6 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     if (mode == 2) {
       BitReader bw{win.data(), (uint32_t)win.size() * 4};
       model_huffman_spec<true>(bw, im, d, (uint32_t)ds.len * 8, lanes, 0, sink, dcd.data(), stats);
-    } else if (mode >= 4) {  // k_huff1's emitting decode; mode 5: record cap 3 (the rewrite fallback)
-      model_huffman_emit<kHuffSrc>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 5 ? 3 : 128, sink, dcd.data(), stats);
     } else {
       model_huffman_spec<kHuffSrc>(br, im, d, (uint32_t)ds.len * 8, lanes, mode == 3 ? 16 : 0, sink, dcd.data(),
                                 stats);

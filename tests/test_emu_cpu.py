@@ -95,8 +95,7 @@ def _zoo():
     return out
 
 
-@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024),
-                                        (4, 3), (4, 64), (4, 256), (5, 64)])
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 3), (1, 64), (1, 256), (2, 7), (2, 512), (3, 100), (3, 1024)])
 def test_decode_bit_exact_vs_pillow(emu, mode, lanes):
     for j in _zoo():
         r, out, _ = emu_decode(emu, j, mode, lanes)
@@ -143,7 +142,7 @@ def _damaged_streams(rng):
     return out
 
 
-@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 64), (1, 300), (3, 1000), (4, 64), (4, 300), (5, 100)])
+@pytest.mark.parametrize("mode,lanes", [(0, 1), (1, 64), (1, 300), (3, 1000)])
 def test_damaged_streams_bit_exact_vs_pillow(emu, mode, lanes):
     for name, j in _damaged_streams(np.random.default_rng(1)):
         ref = cpu_ref.decode_rgb(j)
@@ -170,8 +169,7 @@ def test_corrupt_bytes_all_decode_modes_vs_pillow(emu):
                 b[p] = v
         j = bytes(b)
         ref = cpu_ref.decode_rgb(j)
-        outs = [emu_decode(emu, j, m, lanes) for m, lanes in ((0, 1), (1, 200), (1, 77), (3, 513), (4, 200), (4, 77),
-                                                              (5, 130))]
+        outs = [emu_decode(emu, j, m, lanes) for m, lanes in ((0, 1), (1, 200), (1, 77), (3, 513))]
         for r, out, _ in outs:
             assert r == outs[0][0]
             np.testing.assert_array_equal(out, outs[0][1])

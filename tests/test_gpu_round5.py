@@ -189,3 +189,27 @@ def test_concurrent_pipelines_take_separate_role_streams(gpu_device):
     d = MI355XAugPipeline(lambda: [], cfg, 4, depth=3)
     assert [sl.engine.stream.cuda_stream for sl in d._slots] == sa
     d.close()
+
+
+def test_pixel_ops_all_inputs_match_pillow(gpu_device):
+    """The ColorJitter hue op's colour conversions on the device (division-free restatement,
+    pixel_ops.hpp) over all 2^24 inputs: RGB -> HSV and HSV -> RGB equal Pillow's Convert.c,
+    and the whole hue shift equals ``cpu_ref.adjust_hue`` (torchvision's PIL path) for
+    shifts of both signs."""
+    from PIL import Image
+    from dataloader_amd import _lib
+    lib = _lib.load()
+    idx = np.arange(1 << 24, dtype=np.uint32)
+    allc = np.stack([(idx >> 16) & 255, (idx >> 8) & 255, idx & 255], -1).astype(np.uint8).reshape(4096, 4096, 3)
+    im = Image.fromarray(allc, "RGB")
+    out = torch.empty(3 << 24, dtype=torch.uint8, device=gpu_device)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def run(op, param=0):
+        _lib.check(lib.dino_pixel_ops_all(op, param, out.data_ptr(), stream), "dino_pixel_ops_all")
+        return out.cpu().numpy().reshape(4096, 4096, 3)
+
+    np.testing.assert_array_equal(run(0), np.asarray(im.convert("HSV")))
+    np.testing.assert_array_equal(run(1), np.asarray(Image.fromarray(allc, "HSV").convert("RGB")))
+    for f in (-0.5, -0.1, 0.037, 0.25):
+        np.testing.assert_array_equal(run(2, int(f * 255) & 0xFF), np.asarray(cpu_ref.adjust_hue(im, f)), err_msg=str(f))
