@@ -18,45 +18,58 @@
 
 namespace dino {
 
-// Derived decoding table for one Huffman table (jpeg_make_d_derived_tbl).
-// Lookahead entry for each LB-bit prefix: (symbol << 5) | code length, 0 when the
-// code is longer than LB.  AC tables look ahead kLookBits = 11 bits; DC tables
-// kDcLookBits = 9 (the standard DC codes are <= 9 bits for luma and only the rare
-// categories >= 10 of chroma need the slow path), which keeps an image's six tables
-// at 17.3 KiB of LDS (32.7 KiB with the skip entries).
+// Derived decoding table for one Huffman table (jpeg_make_d_derived_tbl), what the
+// long-code path reads, and the same with its LB-bit lookahead (the progressive
+// decoder's tables).  Lookahead entry for each LB-bit prefix: (symbol << 5) | code
+// length, 0 when the code is longer than LB.  AC tables look ahead kLookBits = 11
+// bits; DC tables kDcLookBits = 9 (the standard DC codes are <= 9 bits for luma and
+// only the rare categories >= 10 of chroma need the slow path).
 constexpr int kDcLookBits = 9;
+struct HuffDerived {
+  int32_t maxcode[18];     // maxcode[l], -1 if no codes of length l; [17] sentinel
+  int32_t valoffset[18];
+  uint8_t huffval[256];
+};
 template <int LB>
 struct HuffTableT {
-  int32_t maxcode[18];     // maxcode[l], -1 if no codes of length l; [17] sentinel
+  int32_t maxcode[18];
   int32_t valoffset[18];
   uint8_t huffval[256];
   uint16_t look[1 << LB];
 };
-using HuffTable = HuffTableT<kLookBits>;
-using DcTable = HuffTableT<kDcLookBits>;
 
-// Skip entries of the state-only decodes (first decode and sync re-decodes): what a
-// step does to the decoder state without its coefficient value, indexed like `look`:
-// bits consumed (code + extra bits) | zigzag advance << 5 (DC 1; AC: r + 1, ZRL 16,
-// EOB 64), 0 when the code is longer than the lookahead.
+// Skip entries of the state-only decodes (look-back, first decode, sync re-decodes):
+// what a step does to the decoder state without its coefficient value, indexed like
+// `look`: bits consumed (code + extra bits) | zigzag advance << 5 (DC 1; AC: r + 1,
+// ZRL 16, EOB 64), 0 when the code is longer than the lookahead.  An AC entry whose
+// second symbol's code also lies inside the lookahead carries that symbol too: its
+// bits << 12 | its advance << 17 | 1 << 24 (skip_step takes both while the first leaves
+// the block open): ~1.7 symbols per lookup on the bench streams instead of 1.
 struct HuffSkip {
-  uint16_t ac[3][1 << kLookBits];
-  uint16_t dc[3][1 << kDcLookBits];
+  uint32_t ac[3][1 << kLookBits];
+  uint32_t dc[3][1 << kDcLookBits];
 };
+constexpr uint32_t kSkipPair = 1u << 24;
 
-// The six tables of an image: AC tables of components 0..2, then DC tables.  Both
-// kinds share the layout up to `look`, so the slow path reads either through one type.
+// The tables of an image (AC of components 0..2, DC of components 0..2): derived
+// tables, value lookaheads, skip entries.  The lookaheads and the skip entries are
+// separate arrays so that k_huff1 can hold only the skip entries while it runs the
+// state-only decodes and load the lookaheads over them for its write pass.
 struct HuffTables {
-  HuffTable ac[3];
-  DcTable dc[3];
+  HuffDerived ac[3];
+  HuffDerived dc[3];
+  uint16_t ac_look[3][1 << kLookBits];
+  uint16_t dc_look[3][1 << kDcLookBits];
   HuffSkip skip;
 };
 static_assert(sizeof(HuffTables) % 16 == 0, "HuffTables is copied in 16-byte words");
+static_assert(offsetof(HuffTables, ac_look) % 16 == 0 && offsetof(HuffTables, skip) % 16 == 0, "16-byte parts");
+constexpr int kHuffLookBytes = (int)(offsetof(HuffTables, skip) - offsetof(HuffTables, ac_look));
 
 // Build maxcode/valoffset/huffval (not the lookahead) from BITS[16] + HUFFVAL.
 // Returns false on an invalid table (libjpeg JERR_BAD_HUFF_TABLE).
-template <int LB>
-DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTableT<LB>* t) {
+template <typename T>
+DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, T* t) {
   int p = 0;
   int code = 0;
   for (int l = 1; l <= 16; ++l) {
@@ -95,8 +108,8 @@ DHD bool huff_build_derived(const uint8_t* bits16, bool is_dc, HuffTableT<LB>* t
 DHD int huff_extend(int x, int s) { return x < (1 << (s - 1)) ? x + (int)(((unsigned)-1) << s) + 1 : x; }
 
 // Lookahead entry for the LB-bit prefix `idx` (computable independently per entry).
-template <int LB>
-DHD uint16_t huff_look_entry(const HuffTableT<LB>* t, int idx) {
+template <int LB, typename T>
+DHD uint16_t look_entry_of(const T* t, int idx) {
   for (int l = 1; l <= LB; ++l) {
     const int code = idx >> (LB - l);
     if (code <= t->maxcode[l]) {  // canonical code: first length whose maxcode covers the prefix
@@ -105,6 +118,10 @@ DHD uint16_t huff_look_entry(const HuffTableT<LB>* t, int idx) {
     }
   }
   return 0;
+}
+template <int LB>
+DHD uint16_t huff_look_entry(const HuffTableT<LB>* t, int idx) {
+  return look_entry_of<LB>(t, idx);
 }
 
 // Skip entry of a decoded symbol (see HuffSkip); len 17 is libjpeg's fake zero.
@@ -115,8 +132,23 @@ DHD uint32_t skip_from_sym(int sym, int len, bool dc) {
 }
 
 // Skip entry for a lookahead entry (0 stays 0: the long-code path).
-DHD uint16_t skip_entry(uint32_t look, bool dc) {
-  return look ? (uint16_t)skip_from_sym((int)(look >> 5), (int)(look & 31u), dc) : (uint16_t)0;
+DHD uint32_t skip_entry(uint32_t look, bool dc) {
+  return look ? skip_from_sym((int)(look >> 5), (int)(look & 31u), dc) : 0u;
+}
+
+// AC skip entry of lookahead index idx (look: the table's LB-bit lookahead) with the
+// second symbol when its code is decided by the index's remaining bits and both symbols
+// fit the 32 bits a step may consume.
+template <int LB>
+DHD uint32_t skip_pair_entry(const uint16_t* look, int idx) {
+  const uint32_t e = skip_entry(look[idx], false);
+  const int len1 = (int)(e & 31u);
+  if (!e || len1 >= LB) return e;
+  const uint32_t l2 = look[(idx << len1) & ((1 << LB) - 1)];
+  if (!l2 || (int)(l2 & 31u) > LB - len1) return e;
+  const uint32_t e2 = skip_entry(l2, false);
+  if (len1 + (int)(e2 & 31u) > 32) return e;
+  return e | ((e2 & 31u) << 12) | ((e2 >> 5) << 17) | kSkipPair;
 }
 
 // Bit reader over a destuffed, zero-padded big-endian byte stream.
@@ -264,8 +296,8 @@ DHD void huff_slow_bits(uint32_t p17, TabPtr t, int* sym, int* len) {
   *len = l;
 }
 
-template <int LB>
-DHD void huff_slow(const BitCursor& c, const HuffTableT<LB>* t, int* sym, int* len) {
+template <int LB, typename T>
+DHD void huff_slow(const BitCursor& c, const T* t, int* sym, int* len) {
   huff_slow_bits<LB>(bc_peek(c, 17), t, sym, len);
 }
 
@@ -282,13 +314,19 @@ DHD bool hstate_eq(const HState& a, const HState& b) { return a.pos == b.pos && 
 // Everything a lane indexes per step is a base pointer or a packed word, so that
 // no per-lane array is dynamically indexed (which would spill it to scratch).
 struct HuffImage {
-  const HuffTables* tabs;
-  uint32_t mcu_comp;       // component of block b of the MCU in bits [2b, 2b+2)
+  const HuffTables* tabs;      // derived tables and value lookaheads as in HuffTables
+  uint32_t skip_off;           // byte offset of the HuffSkip entries from tabs
+  uint32_t mcu_comp;           // component of block b of the MCU in bits [2b, 2b+2)
   int32_t blocks_per_mcu;
 };
 
+DHD const uint32_t* hi_skip(const HuffImage& im) {
+  return reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(im.tabs) + im.skip_off);
+}
+
 DHD void hi_init(HuffImage& im, const HuffTables* tabs, const uint8_t* mcu_comp, int blocks_per_mcu) {
   im.tabs = tabs;
+  im.skip_off = (uint32_t)offsetof(HuffTables, skip);
   im.mcu_comp = 0;
   for (int i = 0; i < blocks_per_mcu && i < kMaxBlocksPerMcu; ++i) im.mcu_comp |= (uint32_t)(mcu_comp[i] & 3) << (2 * i);
   im.blocks_per_mcu = blocks_per_mcu;
@@ -337,18 +375,18 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
   bc_fill<kWin>(cur, br);
   const int comp = hi_comp(im, blk);
   const bool dc = z == 0;
-  // both table kinds keep `look` at the same offset: one pointer, one shift select
-  const HuffTable* t = dc ? reinterpret_cast<const HuffTable*>(im.tabs->dc + comp) : im.tabs->ac + comp;
+  // AC lookaheads first, then DC: one base, one shift select
+  const uint16_t* look = dc ? im.tabs->dc_look[comp] : im.tabs->ac_look[comp];
   const uint32_t hi32 = (uint32_t)(cur.buf >> 32);  // >= 32 valid bits after bc_fill
-  const uint32_t e = t->look[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
+  const uint32_t e = look[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
   int sym, len;
   if (e) {
     sym = (int)(e >> 5);
     len = (int)(e & 31u);
   } else if (dc) {
-    huff_slow(cur, reinterpret_cast<const DcTable*>(t), &sym, &len);
+    huff_slow<kDcLookBits>(cur, im.tabs->dc + comp, &sym, &len);
   } else {
-    huff_slow(cur, t, &sym, &len);
+    huff_slow<kLookBits>(cur, im.tabs->ac + comp, &sym, &len);
   }
   const int s = dc ? sym : sym & 15;  // s <= 15 (DC tables are validated), len <= 17: len + s < 32
   const int r = dc ? 0 : sym >> 4;
@@ -388,24 +426,34 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
 // only look for block boundaries and end states: one HuffSkip lookup gives the bits
 // and the zigzag advance, so no extra-bit value is extracted.  Same state sequence as
 // huff_step (checked by the emulator tests, which run both on the same streams).
+// With a two-symbol entry both are taken when the first leaves the block open and ends
+// before `lim`: the decodes stop at the first step boundary >= their end, which must
+// stay a boundary they visit (the sync rounds compare end and start states), and
+// block boundaries (checkpoints) are never stepped over.
 template <int kWin>
-DHD void skip_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
+DHD void skip_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z, uint32_t lim) {
   bc_fill<kWin>(cur, br);
   const int comp = hi_comp(im, blk);
   const bool dc = z == 0;
   const uint32_t hi32 = (uint32_t)(cur.buf >> 32);
-  const uint16_t* tab = dc ? im.tabs->skip.dc[comp] : im.tabs->skip.ac[comp];
+  const uint32_t* tab = hi_skip(im) + (dc ? 3 * (1 << kLookBits) + comp * (1 << kDcLookBits) : comp * (1 << kLookBits));
   uint32_t e = tab[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
   if (!e) {
     int sym, len;
     if (dc)
-      huff_slow(cur, im.tabs->dc + comp, &sym, &len);
+      huff_slow<kDcLookBits>(cur, im.tabs->dc + comp, &sym, &len);
     else
-      huff_slow(cur, im.tabs->ac + comp, &sym, &len);
+      huff_slow<kLookBits>(cur, im.tabs->ac + comp, &sym, &len);
     e = skip_from_sym(sym, len, dc);
   }
-  bc_skip(cur, (int)(e & 31u));
-  z += (int32_t)(e >> 5);
+  uint32_t len = e & 31u;
+  int32_t zi = (int32_t)((e >> 5) & 127u);
+  if ((e & kSkipPair) && z + zi < 64 && cur.pos + len < lim) {
+    len += (e >> 12) & 31u;
+    zi += (int32_t)((e >> 17) & 127u);
+  }
+  bc_skip(cur, (int)len);
+  z += zi;
   if (z >= 64) {
     z = 0;
     blk = blk + 1 == im.blocks_per_mcu ? 0 : blk + 1;
@@ -418,8 +466,8 @@ DHD void skip_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int
 
 // The step of the state-only decodes (skip_step; huff_step there measured slower).
 template <int kWin>
-DHD void state_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
-  skip_step<kWin>(cur, br, im, blk, z);
+DHD void state_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z, uint32_t lim) {
+  skip_step<kWin>(cur, br, im, blk, z, lim);
 }
 
 // A guessed start state for the range starting at bit `to`: decode state-only from an
@@ -432,7 +480,7 @@ DHD HState decode_lookback(const BitReader& br, const HuffImage& im, uint32_t fr
   BitCursor cur;
   bc_init<kWin>(cur, br, from);
   int32_t blk = 0, z = 0;
-  while (cur.pos < to) state_step<kWin>(cur, br, im, blk, z);
+  while (cur.pos < to) state_step<kWin>(cur, br, im, blk, z, to);
   return HState{cur.pos, blk, z};
 }
 
@@ -482,7 +530,7 @@ DHD RangeOut decode_range(const BitReader& br, const HuffImage& im, HState st, u
         cps[(n++) * cstride] = Checkpoint{cur.pos, ((uint32_t)r.nblk << 4) | (uint32_t)blk};
       r.nblk++;
     }
-    state_step<kWin>(cur, br, im, blk, z);
+    state_step<kWin>(cur, br, im, blk, z, end);
   }
   r.end.pos = cur.pos;
   r.end.c = blk;
@@ -517,7 +565,7 @@ DHD RangeOut decode_range_sync(const BitReader& br, const HuffImage& im, HState 
       }
       nblk++;
     }
-    state_step<kWin>(cur, br, im, blk, z);
+    state_step<kWin>(cur, br, im, blk, z, end);
   }
   RangeOut r;
   r.end.pos = cur.pos;

@@ -570,19 +570,23 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 constexpr int kSinkLds = 8;
 constexpr int kSinkLds3 = 16;
 
+// k_huff1's tables in LDS: a HuffTables up to its lookaheads (the derived tables), then
+// one region that holds the skip entries during the state-only decodes and the value
+// lookaheads + the SparseSink buffers (kSinkLds words per lane) during the write pass of
+// a single-segment image (loaded over the skip entries once the rounds are done; the
+// next item reloads its skip entries).  38 KiB in all: 4 items per CU.
+constexpr int kHuffLookOff = (int)offsetof(HuffTables, ac_look);
+constexpr int kHuffSinkOff = kHuffLookOff + kHuffLookBytes;
+constexpr int kHuff1TabBytes =
+    kHuffLookOff + ((int)sizeof(HuffSkip) > kHuffLookBytes + kSinkLds * 4 * kHuffThreads
+                        ? (int)sizeof(HuffSkip) : kHuffLookBytes + kSinkLds * 4 * kHuffThreads);
 struct HuffLds {     // k_huff1
   ImgDesc sd;
-  HuffTables tab;
+  alignas(16) uint8_t tab[kHuff1TabBytes];
   RangeOut R[kHuffThreads];
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
-// k_huff1's write pass (single-segment images) decodes values, not skips: the SparseSink
-// buffers (kSinkLds) take the skip tables' LDS then (reloaded with the next item's tables)
-// (and the range results R, which follow the tables and are read before the write pass)
-static_assert(offsetof(HuffLds, R) == offsetof(HuffLds, tab) + sizeof(HuffTables), "R follows the tables");
-static_assert(sizeof(HuffSkip) + sizeof(RangeOut) * kHuffThreads >= (size_t)kSinkLds * 4 * kHuffThreads,
-              "sink buffers fit the skip tables and R");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
@@ -731,20 +735,20 @@ __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict
   }
   for (int e = t; e < 3 * (1 << kLookBits); e += kHuffThreads) {
     const int c = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
-    if (c < d.ncomp) s_tab.ac[c].look[idx] = huff_look_entry(&s_tab.ac[c], idx);
+    if (c < d.ncomp) s_tab.ac_look[c][idx] = look_entry_of<kLookBits>(&s_tab.ac[c], idx);
   }
   for (int e = t; e < 3 * (1 << kDcLookBits); e += kHuffThreads) {
     const int c = e >> kDcLookBits, idx = e & ((1 << kDcLookBits) - 1);
-    if (c < d.ncomp) s_tab.dc[c].look[idx] = huff_look_entry(&s_tab.dc[c], idx);
+    if (c < d.ncomp) s_tab.dc_look[c][idx] = look_entry_of<kDcLookBits>(&s_tab.dc[c], idx);
   }
   __syncthreads();
   for (int e = t; e < 3 * (1 << kLookBits); e += kHuffThreads) {
     const int c = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
-    if (c < d.ncomp) s_tab.skip.ac[c][idx] = skip_entry(s_tab.ac[c].look[idx], false);
+    if (c < d.ncomp) s_tab.skip.ac[c][idx] = skip_pair_entry<kLookBits>(s_tab.ac_look[c], idx);
   }
   for (int e = t; e < 3 * (1 << kDcLookBits); e += kHuffThreads) {
     const int c = e >> kDcLookBits, idx = e & ((1 << kDcLookBits) - 1);
-    if (c < d.ncomp) s_tab.skip.dc[c][idx] = skip_entry(s_tab.dc[c].look[idx], true);
+    if (c < d.ncomp) s_tab.skip.dc[c][idx] = skip_entry(s_tab.dc_look[c][idx], true);
   }
   __syncthreads();
   uint4* dst = (uint4*)(ws + d.htab_off);
@@ -837,7 +841,17 @@ __device__ bool huff_load_item(LdsT& L, const ImgDesc* desc, int B, const uint8_
   if (L.img == -2) return true;
   const uint4* src = (const uint4*)(ws + L.sd.htab_off);
   uint4* dst = (uint4*)&L.tab;
-  for (int k = threadIdx.x; k < tab_bytes / 16; k += kHuffThreads) dst[k] = src[k];
+  if (tab_bytes < 0) {  // k_huff1: the derived tables, then the skip entries at the lookaheads' offset
+#pragma unroll 1
+    for (int k = threadIdx.x; k < kHuffLookOff / 16; k += kHuffThreads) dst[k] = src[k];
+    const uint4* ss = (const uint4*)(ws + L.sd.htab_off + offsetof(HuffTables, skip));
+    uint4* sd = (uint4*)((uint8_t*)&L.tab + kHuffLookOff);
+#pragma unroll 1
+    for (int k = threadIdx.x; k < (int)(sizeof(HuffSkip) / 16); k += kHuffThreads) sd[k] = ss[k];
+  } else {
+#pragma unroll 1
+    for (int k = threadIdx.x; k < tab_bytes / 16; k += kHuffThreads) dst[k] = src[k];
+  }
   __syncthreads();
   return true;
 }
@@ -866,14 +880,15 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
   HuffLds& L = *reinterpret_cast<HuffLds*>(smem);
   const int t = threadIdx.x;
   for (int item = blockIdx.x;; item += gridDim.x) {
-    if (!huff_load_item(L, desc, B, ws, item)) return;
+    if (!huff_load_item(L, desc, B, ws, item, false, -1)) return;
     const ImgDesc& sd = L.sd;
     if (sd.restart_interval > 0) {
       __syncthreads();
       continue;
     }
     HuffImage im;
-    hi_init(im, &L.tab, sd.mcu_comp, sd.blocks_per_mcu);
+    hi_init(im, reinterpret_cast<const HuffTables*>(L.tab), sd.mcu_comp, sd.blocks_per_mcu);
+    im.skip_off = (uint32_t)kHuffLookOff;  // the skip entries sit where the value lookaheads come later
     const BitReader br{(const uint32_t*)(ws + sd.ent_off), (uint32_t)sd.ent_len};
     const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
     const int i = (item - sd.h_item_base) * kHuffThreads + t;  // lane index within the image
@@ -917,14 +932,22 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
     if (huff_single_segment(sd)) {
       // the whole image is this segment: its start states are final, so the blocks
-      // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it)
+      // are written here while the stream is still in cache (k_huff2 and k_huff3 skip it);
+      // the value lookaheads replace the skip entries (no lane reads those any more)
+      {
+        const uint4* ls = (const uint4*)(ws + sd.htab_off + kHuffLookOff);
+        uint4* ld = (uint4*)(L.tab + kHuffLookOff);
+#pragma unroll 1
+        for (int k = t; k < kHuffLookBytes / 16; k += kHuffThreads) ld[k] = ls[k];
+      }
+      __syncthreads();
       uint32_t tot;
       const uint32_t blk0 = block_excl_scan<kHuffThreads>(active ? (uint32_t)res.nblk : 0u, L.wave, &tot);
       if (active) {
         SparseSink sink;
         sink.ent = (uint32_t*)(ws + sd.coef_off);
         sink.binfo = (uint2*)(ws + sd.binfo_off);
-        sink.lb = reinterpret_cast<uint32_t*>(&L.tab.skip) + t;
+        sink.lb = reinterpret_cast<uint32_t*>(L.tab + kHuffSinkOff) + t;
         sink.open((int32_t)blk0);
         decode_write<kHuffSrc>(br, im, myS, lane_write_end(sd, i), (int32_t)blk0, sd.total_blocks, (int32_t*)nullptr,
                                  nbits, sink);

@@ -104,10 +104,10 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTables* tabs, H
   for (int c = 0; c < d.ncomp; ++c) {
     if (!huff_build_derived(p + d.huff_off[d.comp[c].td], true, &tabs->dc[c])) return false;
     if (!huff_build_derived(p + d.huff_off[4 + d.comp[c].ta], false, &tabs->ac[c])) return false;
-    for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->dc[c].look[i] = huff_look_entry(&tabs->dc[c], i);
-    for (int i = 0; i < (1 << kLookBits); ++i) tabs->ac[c].look[i] = huff_look_entry(&tabs->ac[c], i);
-    for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->skip.dc[c][i] = skip_entry(tabs->dc[c].look[i], true);
-    for (int i = 0; i < (1 << kLookBits); ++i) tabs->skip.ac[c][i] = skip_entry(tabs->ac[c].look[i], false);
+    for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->dc_look[c][i] = look_entry_of<kDcLookBits>(&tabs->dc[c], i);
+    for (int i = 0; i < (1 << kLookBits); ++i) tabs->ac_look[c][i] = look_entry_of<kLookBits>(&tabs->ac[c], i);
+    for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->skip.dc[c][i] = skip_entry(tabs->dc_look[c][i], true);
+    for (int i = 0; i < (1 << kLookBits); ++i) tabs->skip.ac[c][i] = skip_pair_entry<kLookBits>(tabs->ac_look[c], i);
   }
   hi_init(im, tabs, d.mcu_comp, d.blocks_per_mcu);
   return true;
