@@ -648,9 +648,15 @@ struct SparseSinkT {
   }
   // a lane's region starts 256-byte aligned, so a group of W words is aligned too
   __device__ void put(uint32_t h) {
+#ifdef DINO_DIAG_NOSINK
+    if (h == 0x12345u) lb[0] = h;
+    return;
+#endif
     ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[k & 1] = (uint16_t)h;
     if (++k == 2 * W) {
+#ifndef DINO_DIAG_NOFLUSH
       lds_flush(W);
+#endif
       n += 2 * W;
       k = 0;
     }
@@ -671,7 +677,13 @@ struct SparseSinkT {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void record(int32_t blk, uint2 r) { binfo[blk] = r; }
+  __device__ void record(int32_t blk, uint2 r) {
+#ifdef DINO_DIAG_NOREC
+    if (r.x == 0x12345u) binfo[blk] = r;
+    return;
+#endif
+    binfo[blk] = r;
+  }
   __device__ void end() { record(b, make_uint2(bstart, n16 | (n32 << 7) | dcw)); }
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
