@@ -705,6 +705,22 @@ class _ProgMixSource:
         return out
 
 
+def _side_stats(pipe) -> dict | None:
+    """The side decoder's launches: pools, images, host seconds per phase on its launcher
+    thread, and (DINO_SIDE_TIMING=1) each launch's GPU span."""
+    sd = getattr(pipe, "_side", None)
+    if sd is None:
+        return None
+    out = {"launches": sd.launches, "images": sd.images, "urgent_flushes": pipe.stats.get("side_urgent", 0),
+           "launcher_s": {k: round(v, 3) for k, v in sd.phase_seconds.items()},
+           "per_batch_ms": {k: round(v * 1e3 / max(1, sd.lead["jobs"]), 2) for k, v in sd.lead.items() if k != "jobs"}}
+    if sd.timing:
+        ms = sd.launch_ms()
+        out["gpu_ms_per_launch"] = [m for m, _ in ms][:64]
+        out["images_per_launch"] = [n for _, n in ms][:64]
+    return out
+
+
 def run_prog_leg(args, uniq, uniq_prog, rank: int, world: int, cfg, B: int, dist) -> dict:
     """Progressive mix through the drop-in path: ``MI355XBackend.build_pipeline``
     + ``build_pipeline_iterator`` with the backend's default routing, on C2 batches in which one
@@ -753,6 +769,7 @@ def run_prog_leg(args, uniq, uniq_prog, rank: int, world: int, cfg, B: int, dist
                 "side_decoded": int(st["side_decoded"]), "host_decoded": int(st["host_decoded"]),
                 "progressive_handed_over": prog_handed,
                 "host_ms_per_batch": {k: round(v * 1e3 / max(1, handed), 3) for k, v in pipe.host_seconds.items()},
+                "side": _side_stats(pipe),
                 "workload": f"C2 (640x480 q85, B = {B}) with one image in {src._every} a progressive encode "
                             f"({len(uniq_prog)} distinct), host-fed through MI355XBackend.build_pipeline "
                             "(default route) + build_pipeline_iterator"}

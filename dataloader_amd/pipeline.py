@@ -80,12 +80,12 @@ def _calibrate_refs() -> int:
 _REFS_PIPELINE_ONLY = _calibrate_refs()
 
 
-def _all_unshared(views) -> bool:
+def _all_unshared(views, in_dicts: list[int]) -> bool:
     """Nothing outside the pipeline holds any tensor of ``views`` or its memory: each tensor
-    object is referenced only by the slot's view cache list and outputs dict, and its storage
-    only by the tensor (a view, slice or chunk the caller kept shares the storage and raises
-    its use count)."""
-    if any(n > _REFS_PIPELINE_ONLY for n in _refcounts(views)):
+    object is referenced only by the output ring's list and the ``in_dicts[i]`` slot outputs
+    dicts that hold it (one reference each), and its storage only by the tensor (a view,
+    slice or chunk the caller kept shares the storage and raises its use count)."""
+    if any(n > _REFS_PIPELINE_ONLY - 1 + k for n, k in zip(_refcounts(views), in_dicts)):
         return False
     use_count = getattr(torch._C, "_storage_Use_Count", None)
     if use_count is None:  # no way to see views: never reuse
@@ -115,8 +115,7 @@ class _Slot:
         self.d_offs: list = [None, None]
         self.buf_done: list = [None, None]            # event after the last batch that read each buffer
         self.buf_next = 0
-        self.view_cache = None                        # (shape key, output tensors) reused once the caller drops them
-        self.consumer: torch.cuda.Stream | None = None  # the stream the last outputs were handed to
+        self.view_set = -1                            # the output set (pipeline ring) of the slot's batch
 
 
 class _Staging:
@@ -386,6 +385,9 @@ class MI355XAugPipeline:
         self._prefetcher: _Prefetcher | None = None
         # the side look-ahead holds its batches in HBM (``_stage_on_device``), not in staging
         self._ring = _StagingRing(self.depth + self.prefetch_ahead + (4 if self._side_ahead else 0) + 2)
+        # copier threads of the host half's pack (dino_gather_probe): the source's own count
+        # (the native feeds) or DINO_GATHER_THREADS (default 8)
+        self._gather_threads = int(getattr(source, "nthreads", 0) or os.environ.get("DINO_GATHER_THREADS", 8))
         self._native = hasattr(source, "next_spans")
         # the feed can hand batches over where they lie (page-locked shard ranges, DMA'd as they are)
         self._spans_feed = hasattr(source, "next_batch_spans")
@@ -412,6 +414,8 @@ class MI355XAugPipeline:
                                    workspace_bytes=workspace_bytes, stream=stream)
             self._slots.append(_Slot(eng))
         self._last: _Slot = self._slots[0]          # the last launched batch
+        # output sets (shape key, tensors, consumer stream), batch n -> set n % (depth + 1)
+        self._view_ring: list = [None] * (self.depth + 1)
         self._handed: _Slot | None = None            # the last batch handed over (iterator / run_one_batch)
         self._closed = False
         _LIVE.add(self)
@@ -527,21 +531,29 @@ class MI355XAugPipeline:
         return sl.outputs
 
     def _views_for(self, sl: _Slot, cfg, batch: int) -> list[torch.Tensor]:
-        """Output tensors for the slot's next batch: the slot's previous ones when nothing but
-        the slot still references them (the caller dropped that batch, as DALI's iterator
-        expects before its buffers are refilled), else new ones.  A reused set is written
-        only after the work the caller had queued on its stream by now (the caching
-        allocator's record_stream rule, applied at reuse)."""
+        """Output tensors for the slot's next batch.  Batch n takes output set n % (depth + 1)
+        of a ring: with ``depth`` batches in flight, the set's previous batch (n - depth - 1)
+        is one the caller has replaced by a later one in ``for batch in loader`` (whose loop
+        variable still holds batch n - depth while batch n launches, so a set per slot was
+        never free then: every batch allocated its outputs anew, ~1.3 ms of the host thread
+        per batch).  The set is reused when nothing but the pipeline references it, else new
+        tensors are made; a reused set is written only after the work the caller had queued
+        on its stream by now (the caching allocator's record_stream rule, applied at reuse)."""
         key = (batch, cfg.n_global, cfg.n_local, cfg.global_size, cfg.local_size, cfg.out_dtype)
-        vc = sl.view_cache
-        if vc is not None and vc[0] == key and _all_unshared(vc[1]):
-            if sl.consumer is not None and sl.engine.stream is not None:
-                ev = torch.cuda.Event()
-                ev.record(sl.consumer)
-                sl.engine.stream.wait_event(ev)
-            return vc[1]
+        j = self._batch_index % len(self._view_ring)
+        sl.view_set = j
+        vc = self._view_ring[j]
+        if vc is not None and vc[0] == key:
+            in_dicts = [sum(1 for s in self._slots if s.outputs is not None and any(o is t for o in s.outputs.values()))
+                        for t in vc[1]]
+            if _all_unshared(vc[1], in_dicts):
+                if vc[2] is not None and sl.engine.stream is not None:
+                    ev = torch.cuda.Event()
+                    ev.record(vc[2])
+                    sl.engine.stream.wait_event(ev)
+                return vc[1]
         views = sl.engine.alloc_views(cfg, batch)
-        sl.view_cache = (key, views)
+        self._view_ring[j] = [key, views, None]
         return views
 
     # ------------------------------------------------------------------ host half
@@ -584,9 +596,10 @@ class MI355XAugPipeline:
                     hs["probe"] += time.perf_counter() - t1
                     return _Prepared(st, None, bs.offsets, info, ws, aws, sizes, {}, spans=bs)
             st = self._ring.acquire()
+            hs["staging"] = hs.get("staging", 0.0) + time.perf_counter() - t1  # waiting for a free staging buffer
             try:
                 st.fit(int(lens.sum()), B)
-                off, info, ws, aws = fallback.gather_probe(ptrs, lens, st.buf, getattr(self._source, "nthreads", 8),
+                off, info, ws, aws = fallback.gather_probe(ptrs, lens, st.buf, self._gather_threads,
                                                            self._max_image_dim, cfg)
                 st.off.numpy()[: B + 1] = off
                 t2 = time.perf_counter()
@@ -757,8 +770,13 @@ class MI355XAugPipeline:
         try:
             while not self._source_end and (not self._ahead or
                                             (self._side_hot > 0 and len(self._ahead) < self._side_ahead)):
+                # a head batch whose side decode is still running waits for it behind further
+                # batches (pulled blocking) rather than at its launch: when the host half is the
+                # bottleneck the look-ahead never fills otherwise, every pool is flushed small and
+                # late, and each launch waits out a whole side decode (~30 ms of k_pscan latency)
+                head_busy = bool(self._ahead) and self._ahead[0].side is not None and not self._ahead[0].side.done()
                 try:
-                    pb = self._pull_one(block=not self._ahead)
+                    pb = self._pull_one(block=not self._ahead or head_busy)
                 except StopIteration:
                     self._source_end = True
                     break
@@ -1036,7 +1054,8 @@ class MI355XAugPipeline:
             cur.wait_event(sl.event)
             for t in sl.outputs.values():
                 t.record_stream(cur)
-            sl.consumer = cur
+            if sl.view_set >= 0 and self._view_ring[sl.view_set] is not None:
+                self._view_ring[sl.view_set][2] = cur  # the stream the set was handed to
         self._handed = sl
         return dict(sl.outputs)  # the caller's own dict: its references keep the tensors from reuse
 

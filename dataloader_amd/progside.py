@@ -23,6 +23,7 @@ route (``tests/test_gpu_round3.py``).
 from __future__ import annotations
 
 import ctypes
+import queue
 import threading
 import time
 
@@ -37,22 +38,43 @@ class SideJob:
     """One batch's share of the side path: device containers by batch index, ready after
     ``event`` (None until the pool holding its images is launched)."""
 
-    __slots__ = ("containers", "event", "status", "rows", "pending")
+    __slots__ = ("containers", "event", "status", "rows", "pending", "launched", "error", "t_add", "t_launch",
+                 "owner")
 
     def __init__(self):
         self.containers: dict = {}
         self.event: torch.cuda.Event | None = None
         self.status: torch.Tensor | None = None   # pinned int32[n][4] of the mini-batch
         self.rows: dict = {}                      # batch index -> mini-batch row
-        self.pending = True
+        self.pending = True                       # still in the pool (not handed to the launcher)
+        self.launched = threading.Event()         # the launcher thread has enqueued its decode
+        self.error: BaseException | None = None
+        self.t_add = time.perf_counter()          # host clock: joined the pool / its decode enqueued
+        self.t_launch = 0.0
+        self.owner = None                         # the DeviceSideDecoder (lead-time statistics)
+
+    def done(self) -> bool:
+        """Its side decode has been launched and has finished (ready() would not wait)."""
+        return self.launched.is_set() and (self.event is None or self.event.query())
 
     def ready(self) -> dict:
-        """The containers of images the side decode finished (waits for it; normally long
-        done).  An image the device decoder failed on is left out: its batch decodes it
-        again and reaches the same outcome (zero-filled views where Pillow raises)."""
+        """The containers of images the side decode finished (waits for its launch and for
+        the decode; normally long done).  An image the device decoder failed on is left out:
+        its batch decodes it again and reaches the same outcome (zero-filled views where
+        Pillow raises)."""
+        t0 = time.perf_counter()
+        self.launched.wait()
+        if self.error is not None:
+            raise RuntimeError("side decode launch failed") from self.error
         if self.event is None:
             return {}
         self.event.synchronize()
+        if self.owner is not None:
+            lt = self.owner.lead
+            lt["jobs"] += 1
+            lt["wait_s"] += time.perf_counter() - t0
+            lt["since_add_s"] += t0 - self.t_add
+            lt["since_launch_s"] += t0 - self.t_launch
         st = self.status.numpy()[:, 0]
         return {i: c for i, c in self.containers.items() if st[self.rows[i]] == 0}
 
@@ -124,9 +146,12 @@ class _SideEngine:
 
 class DeviceSideDecoder:
     """Pending pool + ``engines`` side contexts (created on demand).  ``add`` queues a
-    batch's images and launches the pool once it holds ``min_images``; ``flush`` launches
-    it now (a batch holding pending images is about to launch).  A launch waits only when
-    every context still has a mini-batch in flight (backpressure)."""
+    batch's images and hands the pool to the launcher once it holds ``min_images``;
+    ``flush`` hands it over now (a batch holding pending images is about to launch).
+    The launches (pack, probe, H2D, the decode and container copies, ~30 ms of host time
+    for a pool of 512 images, and the wait for a free context when every one still has a
+    mini-batch in flight) run on a launcher thread of their own: on the pipeline's launch
+    thread they cost the c2_prog leg ~3 ms per batch (``scripts/prof_leg.py``)."""
 
     def __init__(self, device: torch.device, max_images: int = 512, min_images: int | None = None,
                  engines: int | None = None, max_image_dim: int = 0, stream_set: int = 0):
@@ -156,13 +181,20 @@ class DeviceSideDecoder:
         self.images = 0
         self.host_seconds = 0.0   # spent in _launch (pack, probe, launches; waits for a free context)
         self.phase_seconds = {"engine": 0.0, "pack": 0.0, "probe": 0.0, "decode": 0.0, "containers": 0.0}
+        # per batch handed out: waits in ready(), time since its images joined the pool and
+        # since their decode was enqueued (host clock)
+        self.lead = {"jobs": 0, "wait_s": 0.0, "since_add_s": 0.0, "since_launch_s": 0.0}
         # add (the prefetch thread) and flush (also the launch thread, for a batch about to launch)
         self._lock = threading.RLock()
+        self._parts: "queue.Queue" = queue.Queue()   # pools handed to the launcher thread
+        self._launcher = threading.Thread(target=self._run, name="dino-side-launcher", daemon=True)
+        self._launcher.start()
 
     def add(self, imgs: dict) -> SideJob | None:
         if not imgs:
             return None
         job = SideJob()
+        job.owner = self
         with self._lock:
             for i in sorted(imgs):
                 self._pool.append((job, int(i), imgs[i]))
@@ -185,11 +217,29 @@ class DeviceSideDecoder:
         return e
 
     def flush(self) -> None:
-        """Decode the pending pool now (in mini-batches of at most ``max_images``)."""
-        with self._lock, torch.cuda.device(self.device):
+        """Hand the pending pool to the launcher now (in mini-batches of at most
+        ``max_images``); returns at once."""
+        with self._lock:
             while self._pool:
                 part, self._pool = self._pool[: self.max_images], self._pool[self.max_images:]
-                self._launch(part)
+                for job, _, _ in part:
+                    job.pending = False
+                self._parts.put(part)
+
+    def _run(self) -> None:
+        while True:
+            part = self._parts.get()
+            if part is None:
+                return
+            try:
+                with torch.cuda.device(self.device):
+                    self._launch(part)
+            except BaseException as e:  # noqa: BLE001 -- the batches waiting on it re-raise
+                for job, _, _ in part:
+                    job.error = e
+            finally:
+                for job, _, _ in part:
+                    job.launched.set()
 
     def _launch(self, part: list) -> None:
         t_start = time.perf_counter()
@@ -250,20 +300,24 @@ class DeviceSideDecoder:
                 _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(big.data_ptr() + o + 16), eng._s()),
                            "dino_copy_rgb")
                 job.containers[i] = big[o:o + 16 + w * h * 3]
-            done = torch.cuda.Event()
-            done.record(es)
-            cs.wait_event(done)  # back on the torch stream: status copy, consumers wait for ev
+            # the status copy and the completion event on the decode's own stream: a torch stream
+            # made to wait for the decode would hold its hardware queue (shared with other
+            # streams, GPU_MAX_HW_QUEUES) for the whole decode -- the batches' H2D copies
+            # queued behind it, their staging buffers stayed busy and the host half stalled
+            # (c2_prog: 3.3 ms per batch waiting for staging)
             status = torch.empty((len(items), 4), dtype=torch.int32, pin_memory=True)
-            status.copy_(d_info, non_blocking=True)
+            with torch.cuda.stream(es):
+                status.copy_(d_info, non_blocking=True)
             ph["containers"] += time.perf_counter() - t4
             ev = torch.cuda.Event(enable_timing=self.timing)
-            ev.record(cs)
+            ev.record(es)
             if self.timing:
                 self.spans.append((t0, ev, len(part)))
+        t_end = time.perf_counter()
         for job, _, _ in part:
-            job.event, job.status, job.pending = ev, status, False
+            job.event, job.status, job.t_launch = ev, status, t_end
         se.last = ev
-        se.keep = (hb, off, d_bytes, d_off, heads)
+        se.keep = (hb, off, d_bytes, d_off, heads, d_info, big)
         self.launches += 1
         self.images += len(part)
         self.host_seconds += time.perf_counter() - t_start
@@ -277,6 +331,9 @@ class DeviceSideDecoder:
         return out
 
     def close(self) -> None:
+        if self._launcher.is_alive():
+            self._parts.put(None)
+            self._launcher.join()
         if self.timing:
             import sys
             print("side launches (ms, images):", self.launch_ms(), file=sys.stderr)

@@ -249,8 +249,14 @@ def test_side_look_ahead_engages_only_with_coefficient_buffer_images():
         pulled.append(k)
         return PB(k, k in prog_at)
 
+    class Job:  # a side decode already finished
+        pending = False
+
+        def done(self):
+            return True
+
     def side_submit(pb):
-        pb.side = object() if pb.prog else None
+        pb.side = Job() if pb.prog else None
 
     def stage(pb):
         pb.staged = True
@@ -265,3 +271,44 @@ def test_side_look_ahead_engages_only_with_coefficient_buffer_images():
     assert {5, 6, 7, 8, 9} <= staged and max(staged) <= 6 + 4
     assert not staged & set(range(11, 16))
     assert pulled[:6] == [0, 1, 2, 3, 4, 5]
+
+
+def test_side_look_ahead_fills_behind_a_running_side_decode():
+    """A head batch whose side decode has not finished is not handed out while the look-ahead
+    has room: further batches are pulled (blocking) behind it, so when the host half is the
+    bottleneck the decode's latency is covered by later batches instead of stalling the launch."""
+    from collections import deque
+
+    from dataloader_amd.pipeline import MI355XAugPipeline
+
+    class Job:
+        pending = False
+
+        def __init__(self):
+            self.finished = False
+
+        def done(self):
+            return self.finished
+
+    class PB:
+        def __init__(self, k):
+            self.k, self.side, self.staged = k, Job() if k == 0 else None, False
+
+    src = iter(range(40))
+    p = MI355XAugPipeline.__new__(MI355XAugPipeline)
+    p._side_ahead, p._side_hot, p._ahead, p._source_end = 6, 0, deque(), False
+    p._side = None
+    p.host_seconds = {"wait": 0.0}
+    p.stats = {}
+    blocking = []
+
+    def pull_one(block):
+        blocking.append(block)
+        return PB(next(src))
+
+    p._pull_one, p._side_submit, p._stage_on_device = pull_one, lambda pb: None, lambda pb: None
+    first = p._pull_side()
+    assert first.k == 0 and len(p._ahead) == 5           # batches 1-5 pulled behind the busy head
+    assert all(blocking)                                  # each of them waited for the host half
+    first.side.finished = True
+    assert [p._pull_side().k for _ in range(3)] == [1, 2, 3]
