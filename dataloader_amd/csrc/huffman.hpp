@@ -58,7 +58,7 @@ constexpr uint32_t kSkipPair = 1u << 24;
 struct HuffTables {
   HuffDerived ac[3];
   HuffDerived dc[3];
-  uint16_t ac_look[3][1 << kLookBits];
+  uint32_t ac_look[3][1 << kLookBits];   // value lookahead with the second symbol (look_pair_entry)
   uint16_t dc_look[3][1 << kDcLookBits];
   HuffSkip skip;
 };
@@ -124,6 +124,26 @@ DHD uint16_t huff_look_entry(const HuffTableT<LB>* t, int idx) {
   return look_entry_of<LB>(t, idx);
 }
 
+// AC value lookahead entry of index idx: the single-symbol entry (symbol << 5 | code
+// length, bits 0-12) and, when the next symbol's code is decided by the index's remaining
+// bits after the first symbol's code and extra bits, that symbol too: its code length
+// << 13 | its symbol << 17 | kLookPair.  decode_write then takes two coefficients per
+// step (the write pass of the speculative decode: ~1.7 symbols per lookup on the bench
+// streams).
+constexpr uint32_t kLookPair = 1u << 25;
+// look: the table's single-symbol entries (bits 0-12 of each word; any pair bits above
+// are ignored, so the entries can be completed in place, each by its own thread).
+template <int LB>
+DHD uint32_t look_pair_entry(const uint32_t* look, int idx) {
+  const uint32_t e = look[idx] & 0x1FFFu;
+  if (!e) return 0u;
+  const int used = (int)(e & 31u) + (int)((e >> 5) & 15u);
+  if (used >= LB) return e;
+  const uint32_t l2 = look[(idx << used) & ((1 << LB) - 1)] & 0x1FFFu;
+  if (!l2 || (int)(l2 & 31u) > LB - used) return e;
+  return e | ((l2 & 31u) << 13) | ((l2 >> 5) << 17) | kLookPair;
+}
+
 // Skip entry of a decoded symbol (see HuffSkip); len 17 is libjpeg's fake zero.
 DHD uint32_t skip_from_sym(int sym, int len, bool dc) {
   const int s = dc ? sym : sym & 15, r = dc ? 0 : sym >> 4;
@@ -136,15 +156,15 @@ DHD uint32_t skip_entry(uint32_t look, bool dc) {
   return look ? skip_from_sym((int)(look >> 5), (int)(look & 31u), dc) : 0u;
 }
 
-// AC skip entry of lookahead index idx (look: the table's LB-bit lookahead) with the
-// second symbol when its code is decided by the index's remaining bits and both symbols
-// fit the 32 bits a step may consume.
+// AC skip entry of lookahead index idx (look: the table's LB-bit value lookahead, its
+// single-symbol part) with the second symbol when its code is decided by the index's
+// remaining bits and both symbols fit the 32 bits a step may consume.
 template <int LB>
-DHD uint32_t skip_pair_entry(const uint16_t* look, int idx) {
-  const uint32_t e = skip_entry(look[idx], false);
+DHD uint32_t skip_pair_entry(const uint32_t* look, int idx) {
+  const uint32_t e = skip_entry(look[idx] & 0x1FFFu, false);
   const int len1 = (int)(e & 31u);
   if (!e || len1 >= LB) return e;
-  const uint32_t l2 = look[(idx << len1) & ((1 << LB) - 1)];
+  const uint32_t l2 = look[(idx << len1) & ((1 << LB) - 1)] & 0x1FFFu;
   if (!l2 || (int)(l2 & 31u) > LB - len1) return e;
   const uint32_t e2 = skip_entry(l2, false);
   if (len1 + (int)(e2 & 31u) > 32) return e;
@@ -351,6 +371,9 @@ struct StepOut {
   int32_t kind;    // 0 = DC (value = diff), 1 = AC coefficient (value, zz index), 2 = no coefficient
   int32_t value;
   int32_t zz;
+  int32_t ac2;     // a second AC coefficient in the same step (value2, zz2)
+  int32_t value2;
+  int32_t zz2;
   int32_t block_done;
 };
 
@@ -367,21 +390,23 @@ DHD uint32_t ubfe(uint32_t x, uint32_t off, uint32_t width) {
 // read gives the symbol and code length of every code of <= kLookBits bits; the
 // extra bits are then extracted from the same 32-bit view of the window, so
 // short and long (code + extra) steps take one branch-free path and the lanes of
-// a wave only diverge for codes longer than kLookBits.
+// a wave only diverge for codes longer than kLookBits.  An AC entry carrying a second
+// symbol (look_pair_entry) completes it in the same step while the first leaves the
+// block open (ac2 = 1: a second coefficient; a second ZRL or EOB only moves z).
 template <int kWin>
 DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, int32_t& blk, int32_t& z) {
   StepOut o;
   o.block_done = 0;
+  o.ac2 = 0;
   bc_fill<kWin>(cur, br);
   const int comp = hi_comp(im, blk);
   const bool dc = z == 0;
-  // AC lookaheads first, then DC: one base, one shift select
-  const uint16_t* look = dc ? im.tabs->dc_look[comp] : im.tabs->ac_look[comp];
   const uint32_t hi32 = (uint32_t)(cur.buf >> 32);  // >= 32 valid bits after bc_fill
-  const uint32_t e = look[hi32 >> (dc ? 32 - kDcLookBits : 32 - kLookBits)];
+  const uint32_t e = dc ? (uint32_t)im.tabs->dc_look[comp][hi32 >> (32 - kDcLookBits)]
+                        : im.tabs->ac_look[comp][hi32 >> (32 - kLookBits)];
   int sym, len;
   if (e) {
-    sym = (int)(e >> 5);
+    sym = (int)((e >> 5) & 255u);
     len = (int)(e & 31u);
   } else if (dc) {
     huff_slow<kDcLookBits>(cur, im.tabs->dc + comp, &sym, &len);
@@ -392,7 +417,7 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
   const int r = dc ? 0 : sym >> 4;
   const uint32_t x = ubfe(hi32, (uint32_t)(32 - len - s), (uint32_t)s);
   const int v = s ? huff_extend((int)x, s) : 0;
-  bc_skip(cur, len + s);
+  int used = len + s;
   if (dc) {
     o.kind = 0;
     o.value = v;
@@ -414,6 +439,24 @@ DHD StepOut huff_step(BitCursor& cur, const BitReader& br, const HuffImage& im, 
     else
       z = 64;  // EOB
   }
+  if ((e & kLookPair) && z < 64) {  // (AC entries only) the second symbol, inside the same 32-bit view
+    const int len2 = (int)((e >> 13) & 15u), sym2 = (int)((e >> 17) & 255u);
+    const int s2 = sym2 & 15, r2 = sym2 >> 4;
+    const uint32_t x2 = ubfe(hi32, (uint32_t)(32 - used - len2 - s2), (uint32_t)s2);
+    used += len2 + s2;
+    if (s2) {
+      z += r2;
+      o.ac2 = 1;
+      o.value2 = huff_extend((int)x2, s2);
+      o.zz2 = z > 79 ? 79 : z;
+      z += 1;
+    } else if (r2 == 15) {
+      z += 16;
+    } else {
+      z = 64;
+    }
+  }
+  bc_skip(cur, used);
   if (z >= 64) {
     z = 0;
     blk = blk + 1 == im.blocks_per_mcu ? 0 : blk + 1;
@@ -627,6 +670,7 @@ DHD uint32_t decode_write(const BitReader& br, const HuffImage& im, HState st, u
     } else if (o.kind == 1) {
       sink.ac(o.zz, (int16_t)o.value);
     }
+    if (o.ac2) sink.ac(o.zz2, (int16_t)o.value2);
     if (o.block_done) {
       sink.end();
       ++b;

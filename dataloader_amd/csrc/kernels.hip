@@ -568,25 +568,28 @@ __device__ __forceinline__ int huff_segments(int64_t nbits) {
 // (Measured and dropped, DESIGN.md §5: a register shift register instead of LDS, block
 // records buffered and stored in pairs or groups, 64-byte groups in k_huff1.)
 constexpr int kSinkLds = 8;
-constexpr int kSinkLds3 = 16;
+constexpr int kSinkLds3 = 8;  // (16: 64-byte groups, but 47 KiB of LDS per item with the pair lookaheads: slower)
 
 // k_huff1's tables in LDS: a HuffTables up to its lookaheads (the derived tables), then
-// one region that holds the skip entries during the state-only decodes and the value
-// lookaheads + the SparseSink buffers (kSinkLds words per lane) during the write pass of
-// a single-segment image (loaded over the skip entries once the rounds are done; the
-// next item reloads its skip entries).  38 KiB in all: 4 items per CU.
+// one region that holds the skip entries and the lanes' range results R during the
+// state-only decodes and the value lookaheads + the SparseSink buffers (kSinkLds words per
+// lane) during the write pass of a single-segment image (loaded over the skip entries
+// once the rounds are done and R is read; the next item reloads its skip entries).
+// 39 KiB in all: 4 items per CU.
 constexpr int kHuffLookOff = (int)offsetof(HuffTables, ac_look);
 constexpr int kHuffSinkOff = kHuffLookOff + kHuffLookBytes;
+constexpr int kHuffROff = kHuffLookOff + (int)sizeof(HuffSkip);
+constexpr int kHuffSkipPhaseBytes = (int)sizeof(HuffSkip) + (int)sizeof(RangeOut) * kHuffThreads;
+constexpr int kHuffWritePhaseBytes = kHuffLookBytes + kSinkLds * 4 * kHuffThreads;
 constexpr int kHuff1TabBytes =
-    kHuffLookOff + ((int)sizeof(HuffSkip) > kHuffLookBytes + kSinkLds * 4 * kHuffThreads
-                        ? (int)sizeof(HuffSkip) : kHuffLookBytes + kSinkLds * 4 * kHuffThreads);
+    kHuffLookOff + (kHuffSkipPhaseBytes > kHuffWritePhaseBytes ? kHuffSkipPhaseBytes : kHuffWritePhaseBytes);
 struct HuffLds {     // k_huff1
   ImgDesc sd;
   alignas(16) uint8_t tab[kHuff1TabBytes];
-  RangeOut R[kHuffThreads];
   uint32_t wave[kHuffThreads / 64];
   int32_t img, item;
 };
+static_assert(sizeof(HuffLds) <= 40 * 1024, "4 k_huff1 items per CU");
 // k_huff3 writes coefficients (huff_step): the skip entries stay in global memory
 constexpr int kHuffTabBytesNoSkip = (int)offsetof(HuffTables, skip);
 static_assert(kHuffTabBytesNoSkip % 16 == 0, "HuffTables::skip is 16-byte aligned");
@@ -648,15 +651,9 @@ struct SparseSinkT {
   }
   // a lane's region starts 256-byte aligned, so a group of W words is aligned too
   __device__ void put(uint32_t h) {
-#ifdef DINO_DIAG_NOSINK
-    if (h == 0x12345u) lb[0] = h;
-    return;
-#endif
     ((uint16_t*)(lb + (k >> 1) * kHuffThreads))[k & 1] = (uint16_t)h;
     if (++k == 2 * W) {
-#ifndef DINO_DIAG_NOFLUSH
       lds_flush(W);
-#endif
       n += 2 * W;
       k = 0;
     }
@@ -677,13 +674,7 @@ struct SparseSinkT {
     ++n32;
   }
   __device__ void dc(int16_t v) { dcw = (uint32_t)(uint16_t)v << 16; }
-  __device__ void record(int32_t blk, uint2 r) {
-#ifdef DINO_DIAG_NOREC
-    if (r.x == 0x12345u) binfo[blk] = r;
-    return;
-#endif
-    binfo[blk] = r;
-  }
+  __device__ void record(int32_t blk, uint2 r) { binfo[blk] = r; }
   __device__ void end() { record(b, make_uint2(bstart, n16 | (n32 << 7) | dcw)); }
   // an all-zero block with absolute DC 0 (kBinfoAbsDc: k_dcscan does not add it up)
   __device__ void zero(int32_t blk) { record(blk, make_uint2(n + k, kBinfoAbsDc)); }
@@ -756,7 +747,10 @@ __global__ void __launch_bounds__(kHuffThreads) k_htab(const uint8_t* __restrict
   __syncthreads();
   for (int e = t; e < 3 * (1 << kLookBits); e += kHuffThreads) {
     const int c = e >> kLookBits, idx = e & ((1 << kLookBits) - 1);
-    if (c < d.ncomp) s_tab.skip.ac[c][idx] = skip_pair_entry<kLookBits>(s_tab.ac_look[c], idx);
+    if (c < d.ncomp) {  // (both read only the entries' single-symbol bits, which stay as they are)
+      s_tab.skip.ac[c][idx] = skip_pair_entry<kLookBits>(s_tab.ac_look[c], idx);
+      s_tab.ac_look[c][idx] = look_pair_entry<kLookBits>(s_tab.ac_look[c], idx);
+    }
   }
   for (int e = t; e < 3 * (1 << kDcLookBits); e += kHuffThreads) {
     const int c = e >> kDcLookBits, idx = e & ((1 << kDcLookBits) - 1);
@@ -901,6 +895,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     HuffImage im;
     hi_init(im, reinterpret_cast<const HuffTables*>(L.tab), sd.mcu_comp, sd.blocks_per_mcu);
     im.skip_off = (uint32_t)kHuffLookOff;  // the skip entries sit where the value lookaheads come later
+    RangeOut* const R = reinterpret_cast<RangeOut*>(L.tab + kHuffROff);  // lane results (skip phase)
     const BitReader br{(const uint32_t*)(ws + sd.ent_off), (uint32_t)sd.ent_len};
     const uint32_t nbits = (uint32_t)sd.ent_len * 8u;
     const int i = (item - sd.h_item_base) * kHuffThreads + t;  // lane index within the image
@@ -920,7 +915,7 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
     }
     if (active) {
       myR1 = decode_range<kHuffSrc>(br, im, myS, rend, cps, cstride, kHuffCheckpoints, &ncp);
-      L.R[t] = myR1;
+      R[t] = myR1;
     }
     __syncthreads();  // lane t-1's first decode (another wave) is visible before round 0
     HUFF_PHASE(1, wall_clock64());
@@ -929,17 +924,17 @@ __global__ void __launch_bounds__(kHuffThreads) k_huff1(const ImgDesc* __restric
       HState want;
       bool redo = false;
       if (active && t >= 1) {
-        want = L.R[t - 1].end;
+        want = R[t - 1].end;
         redo = !hstate_eq(want, myS);
       }
       __syncthreads();
       if (redo) {
         myS = want;
-        L.R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1);
+        R[t] = decode_range_sync<kHuffSrc>(br, im, want, rend, cps, cstride, ncp, myR1);
       }
       if (!__syncthreads_or(redo ? 1 : 0)) break;
     }
-    const RangeOut res = L.R[t];
+    const RangeOut res = R[t];
     HUFF_PHASE(2, wall_clock64());
     HUFF_PHASE(4, (uint64_t)round | ((uint64_t)(huff_single_segment(sd) ? 1 : 0) << 32));
     if (huff_single_segment(sd)) {

@@ -108,6 +108,7 @@ inline bool model_tables(const uint8_t* p, const ImgDesc& d, HuffTables* tabs, H
     for (int i = 0; i < (1 << kLookBits); ++i) tabs->ac_look[c][i] = look_entry_of<kLookBits>(&tabs->ac[c], i);
     for (int i = 0; i < (1 << kDcLookBits); ++i) tabs->skip.dc[c][i] = skip_entry(tabs->dc_look[c][i], true);
     for (int i = 0; i < (1 << kLookBits); ++i) tabs->skip.ac[c][i] = skip_pair_entry<kLookBits>(tabs->ac_look[c], i);
+    for (int i = 0; i < (1 << kLookBits); ++i) tabs->ac_look[c][i] = look_pair_entry<kLookBits>(tabs->ac_look[c], i);
   }
   hi_init(im, tabs, d.mcu_comp, d.blocks_per_mcu);
   return true;
