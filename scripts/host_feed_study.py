@@ -22,10 +22,12 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 
-def _rank(rank: int, world: int, job: str, paths: list, B: int, threads: int, seconds: float, gpu: bool, q) -> None:
+def _rank(rank: int, world: int, job: str, paths: list, B: int, threads: int, seconds: float, gpu: bool, q,
+          lookahead: int = 2) -> None:
     from dataloader_amd import tario
     cache = tario.ShmShardCache(job_id=job, node_master=False, shard_timeout_s=60.0)
-    feed = tario.NativeShardFeed(cache, paths, B, rank=rank, world=world, nthreads=threads, slots=6)
+    feed = tario.NativeShardFeed(cache, paths, B, rank=rank, world=world, nthreads=threads, slots=6,
+                                 lookahead=lookahead)
     n_img = n_bytes = 0
     t_end = None
     if gpu:
@@ -83,6 +85,7 @@ def main() -> None:
     ap.add_argument("--per-rank", type=int, default=4000, help="images per rank (one epoch)")
     ap.add_argument("--shard", type=int, default=500)
     ap.add_argument("--gpu-rank", action="store_true", help="rank 0 runs the GPU pipeline")
+    ap.add_argument("--lookahead", type=int, default=2, help="shards opened ahead per feed (= opener threads, <= 4)")
     a = ap.parse_args()
     from bench import _cpu_model, make_shards, make_unique
     from dataloader_amd import tario
@@ -100,7 +103,7 @@ def main() -> None:
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_rank, args=(r, a.ranks, job, paths, a.batch, a.threads, a.seconds,
-                                             a.gpu_rank and r == 0, q)) for r in range(a.ranks)]
+                                             a.gpu_rank and r == 0, q, a.lookahead)) for r in range(a.ranks)]
     try:
         for p in procs:
             p.start()
@@ -113,7 +116,8 @@ def main() -> None:
         master.close(remove=True)
     host = [r for r in res if not r["gpu"]]
     print(json.dumps({
-        "ranks": a.ranks, "threads_per_feed": a.threads, "batch": a.batch, "seconds": a.seconds,
+        "ranks": a.ranks, "threads_per_feed": a.threads, "lookahead": a.lookahead, "batch": a.batch,
+        "seconds": a.seconds,
         "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": _cpu_model(),
         "mean_jpeg_bytes": round(shard_bytes / total),
         "per_rank": res,
