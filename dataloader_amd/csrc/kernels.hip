@@ -2452,10 +2452,19 @@ __device__ __forceinline__ int hresize_pitch(int S, int cw, int kh, int sw) {
   const int span = min(cw, (int)(((int64_t)sw * cw + S - 1) / S) + kh + 2) + 4;
   return ((span + 3) & ~3) + 8;  // + slack for the last group's upper word
 }
-// LDS bytes of a band of R rows: (pitch / 4) source words x (3 R + 2) row-channel words,
+// Words per staged source group: 3 R row-channel words + 2, rounded to 2 mod 4.  Even, so
+// a row pair's six words are one 8-byte-aligned run; 2 mod 4, so the row pairs that the
+// lanes of a ds_read_b64 group read at distinct source groups k fall on distinct bank
+// pairs (k R3p mod 64): with R = 10 or 14 (R3p 32 / 44) up to 16-way conflicts, 52 % of
+// the kernel's LDS cycles (SQ_LDS_BANK_CONFLICT, profiles/r05_c2_lds.txt).
+__host__ __device__ __forceinline__ int hresize_r3p(int R) {
+  const int r = 3 * R + 2;
+  return (r & 3) == 0 ? r + 2 : r;
+}
+// LDS bytes of a band of R rows: (pitch / 4) source words x R3p row-channel words,
 // plus room for the over-read of the last output's zero-tap groups (ng_max words).
 __device__ __forceinline__ int hresize_rows_bytes(int pitch, int R, int ng_max) {
-  return (pitch / 4 + ng_max + 1) * (3 * R + 2) * 4;
+  return (pitch / 4 + ng_max + 1) * hresize_r3p(R) * 4;
 }
 __device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
   const int ng_max = (kh + 3) / 4;
@@ -2471,7 +2480,7 @@ __device__ __forceinline__ HrTile hresize_tile(int S, int cw, int kh) {
   int R = 16;
   while (R > kHresizeMinRows && tap_bytes * sw + hresize_rows_bytes(t.pitch, R, ng_max) > kHresizeLds) R -= 2;
   t.R = R;
-  t.R3p = 3 * R + 2;
+  t.R3p = hresize_r3p(R);
   return t;
 }
 
@@ -2511,7 +2520,7 @@ __device__ __forceinline__ int hr_find_view(const ViewPlan* __restrict__ plan, i
 // accumulates three signed-dot4 digit products per row, channel and group of 4 taps.
 // Rows are staged with the sign bit flipped (p - 128 as int8) from source column c0,
 // word-interleaved: word (gw, r, c) = 4 pixels gw of row r, channel c at gw * R3p + 3 r + c
-// (R3p = 3 R + 2: even, so a row pair's six words are one 8-byte-aligned run: three
+// (R3p = hresize_r3p(R): even, so a row pair's six words are one 8-byte-aligned run: three
 // ds_read_b64 per group and one address for all of them).  The taps' pixels start at xmin,
 // so each group's 4 pixels are one v_alignbyte of a word and the next group's (carried).
 // The group loop runs the view's ng_max groups for every lane (taps past an output's own
