@@ -54,12 +54,18 @@ struct JitterPlan {
   int32_t has_contrast; // contrast op present (then it is the first op of stage 1)
   int32_t n_post;       // ops after contrast
   uint32_t pre, post;   // op codes, one per byte (packed so that lanes keep them in registers)
+  // Optional 256-entry tables of the view's brightness and contrast blends (LDS on the
+  // GPU, jitter_tables): both ops are one function of the channel value per view, so a
+  // lookup replaces the float blend (same values: the table holds blend_u8 itself).
+  const uint8_t* tb;
+  const uint8_t* tc;
 };
 
 DHD JitterPlan make_jitter_plan(const dino_view_params& p) {
   JitterPlan j;
   j.n_pre = j.n_post = j.has_contrast = 0;
   j.pre = j.post = 0;
+  j.tb = j.tc = nullptr;
   if (!p.jitter) return j;
   const uint32_t ord = (uint32_t)p.order[0] | ((uint32_t)p.order[1] << 8) | ((uint32_t)p.order[2] << 16) |
                        ((uint32_t)p.order[3] << 24);
@@ -73,15 +79,24 @@ DHD JitterPlan make_jitter_plan(const dino_view_params& p) {
 }
 
 // One ColorJitter op on one pixel (torchvision ColorJitter.forward -> Pillow).
-DHD void jitter_op(int op, int& r, int& g, int& b, const dino_view_params& p, int contrast_mean, int hue_d) {
+DHD void jitter_op(int op, int& r, int& g, int& b, const dino_view_params& p, int contrast_mean, int hue_d,
+                   const uint8_t* tb = nullptr, const uint8_t* tc = nullptr) {
   switch (op) {
     case 0: {  // brightness: blend(black, img, f)
+      if (tb) {
+        r = tb[r], g = tb[g], b = tb[b];
+        break;
+      }
       r = blend_u8(0, r, p.brightness);
       g = blend_u8(0, g, p.brightness);
       b = blend_u8(0, b, p.brightness);
       break;
     }
     case 1: {  // contrast: blend(mean(L) grey, img, f)
+      if (tc) {
+        r = tc[r], g = tc[g], b = tc[b];
+        break;
+      }
       r = blend_u8(contrast_mean, r, p.contrast);
       g = blend_u8(contrast_mean, g, p.contrast);
       b = blend_u8(contrast_mean, b, p.contrast);
@@ -101,14 +116,14 @@ DHD void jitter_op(int op, int& r, int& g, int& b, const dino_view_params& p, in
 }
 
 DHD void jitter_stage0(const JitterPlan& j, int& r, int& g, int& b, const dino_view_params& p, int hue_d) {
-  for (int k = 0; k < j.n_pre; ++k) jitter_op((j.pre >> (8 * k)) & 0xFF, r, g, b, p, 0, hue_d);
+  for (int k = 0; k < j.n_pre; ++k) jitter_op((j.pre >> (8 * k)) & 0xFF, r, g, b, p, 0, hue_d, j.tb, nullptr);
 }
 
 // Contrast (if any), later ops, then grayscale.
 DHD void jitter_stage1(const JitterPlan& j, int& r, int& g, int& b, const dino_view_params& p, int contrast_mean,
                        int hue_d) {
-  if (j.has_contrast) jitter_op(1, r, g, b, p, contrast_mean, hue_d);
-  for (int k = 0; k < j.n_post; ++k) jitter_op((j.post >> (8 * k)) & 0xFF, r, g, b, p, contrast_mean, hue_d);
+  if (j.has_contrast) jitter_op(1, r, g, b, p, contrast_mean, hue_d, j.tb, j.tc);
+  for (int k = 0; k < j.n_post; ++k) jitter_op((j.post >> (8 * k)) & 0xFF, r, g, b, p, contrast_mean, hue_d, j.tb, j.tc);
   if (p.gray) {
     int l = rgb_to_l(r, g, b);
     r = g = b = l;

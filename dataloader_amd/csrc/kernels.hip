@@ -2885,6 +2885,30 @@ __device__ __forceinline__ uint32_t wg_sum(uint32_t v, uint32_t* s_part) {
   return t;
 }
 
+// The view's brightness / contrast blends as 256-entry LDS tables (JitterPlan::tb / tc):
+// filled by the workgroup's first 256 lanes, read after the caller's next barrier
+// (brightness, contrast and saturation together were 4.6 % of a C2 step, diagnosis build
+// without them: 175.8k -> 183.8k img/s; the tables: k_final 0.345 -> 0.324 ms).
+// stages: bit 0 = stage 0 (the ops before contrast), bit 1 = stage 1 (contrast and after);
+// a table is made only when a stage the caller runs holds its op.
+__device__ __forceinline__ bool jitter_has(uint32_t ops, int n, int op) {
+  bool f = false;
+  for (int k = 0; k < n; ++k) f |= (int)((ops >> (8 * k)) & 0xFFu) == op;
+  return f;
+}
+__device__ __forceinline__ void jitter_tables(JitterPlan& jp, const dino_view_params& p, uint8_t* tb, uint8_t* tc,
+                                              int contrast_mean, int stages) {
+  if (!p.jitter) return;
+  const bool b = ((stages & 1) && jitter_has(jp.pre, jp.n_pre, 0)) || ((stages & 2) && jitter_has(jp.post, jp.n_post, 0));
+  const bool c = tc && (stages & 2) && jp.has_contrast;
+  if (threadIdx.x < 256) {
+    if (b) tb[threadIdx.x] = blend_u8(0, (int)threadIdx.x, p.brightness);
+    if (c) tc[threadIdx.x] = blend_u8(contrast_mean, (int)threadIdx.x, p.contrast);
+  }
+  if (b) jp.tb = tb;
+  if (c) jp.tc = tc;
+}
+
 __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                               ViewPlan* __restrict__ plan, int nv, int v0, int B,
                                               const uint8_t* __restrict__ ws, const uint8_t* __restrict__ aws,
@@ -2898,6 +2922,8 @@ __global__ void __launch_bounds__(256) k_vert(const ImgDesc* __restrict__ desc, 
   const dino_view_params p = prm[i];
   const int64_t N = (int64_t)S * S;
   uint8_t* crop = gcrop + crop_slot(cfg, B, b, v);  // (256 lanes: s_part holds 4 waves)
+  // (no blend tables here: a band of 8 rows is too short to repay making one, k_vert 0.272
+  // -> 0.288 ms per C2 step with them)
   const JitterPlan jp = make_jitter_plan(p);
   const int y0 = bk.x * vert_rows(S);
   const int nr = min(vert_rows(S), S - y0);
@@ -3186,9 +3212,12 @@ __global__ void __launch_bounds__(256) k_final(const ImgDesc* __restrict__ desc,
     const int c = e >> 8;
     ntab[e] = out_cast<OutT>(u8_normalize(e & 255, nb ? nb[c] : cfg.mean[c], nb ? nb[3 + c] : cfg.std[c]));
   }
-  const JitterPlan jp = make_jitter_plan(p);
+  JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
   const int cmean = contrast_mean_from_sum(vp.lsum, N);
+  __shared__ uint8_t s_tb[256], s_tc[256];
+  jitter_tables(jp, p, s_tb, s_tc, cmean, 2);
+  if (jp.tb || jp.tc) __syncthreads();
   auto stage_px = [&](int lr, int tc, int r, int g, int bb) {
     jitter_stage1(jp, r, g, bb, p, cmean, hd);
     const int to = lr * tp + tc;
@@ -3288,8 +3317,11 @@ __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __rest
     const int c = e >> 8;
     ntab[e] = out_cast<OutT>(u8_normalize(e & 255, nb ? nb[c] : cfg.mean[c], nb ? nb[3 + c] : cfg.std[c]));
   }
-  const JitterPlan jp = make_jitter_plan(p);
+  JitterPlan jp = make_jitter_plan(p);
   const int hd = hue_delta(p.hue);
+  __shared__ uint8_t s_tb[256], s_tc[256];
+  jitter_tables(jp, p, s_tb, nullptr, 0, 3);  // the contrast table once the view's mean is known
+  if (jp.tb) __syncthreads();
   uint8_t* in0 = tile + (int64_t)pad * tp + pad;  // interior (0, 0)
   const uint32_t lsum = vert_apply(
       desc[b], p, vp, ws, aws, S, 0, S, jp, hd,
@@ -3310,6 +3342,10 @@ __global__ void __launch_bounds__(kVFinalThreads) k_vfinal(const ImgDesc* __rest
       });
   __syncthreads();
   const int cmean = jp.has_contrast ? contrast_mean_from_sum(wg_sum(lsum, s_part), N) : 0;
+  if (jp.has_contrast) {
+    jitter_tables(jp, p, s_tb, s_tc, cmean, 2);
+    __syncthreads();
+  }
   // the ops after contrast, in place on the interior (none: no jitter and no grayscale)
   const FastDiv ds((uint32_t)S);
   const bool stage1 = jp.has_contrast || jp.n_post > 0 || p.gray;
