@@ -646,6 +646,9 @@ def run_e2e(args, uniq, rank: int, world: int, cfg, B: int, dist) -> dict:
             print(json.dumps({"gil_sampler": sampler.stop()}), file=sys.stderr, flush=True)
         assert len(out) == 1 and len(out[0]) == cfg.n_views
         st = pipe.flush_stats()
+        if os.environ.get("DINO_TIMELINE") == "1":  # study: per-batch host / device timeline
+            Path("gpurun_out").mkdir(exist_ok=True)
+            Path("gpurun_out/timeline_e2e.json").write_text(json.dumps(pipe.timeline()))
         bad = {k: v for k, v in st["status"].items() if k != 0}
         if bad:
             raise RuntimeError(f"e2e decode failures: {bad}")

@@ -432,6 +432,23 @@ int dino_stream_create(int device, int32_t cu_count, void** stream) {
   *stream = nullptr;
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  if (cu_count < 0) {  // a non-blocking stream from the least priority's pool of hardware queues
+    int least = 0, greatest = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    if ((e = hipDeviceGetStreamPriorityRange(&least, &greatest)) == hipSuccess &&
+        (e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, least)) == hipSuccess &&
+        (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) == hipSuccess &&
+        (e = hipEventRecord(ev, s)) == hipSuccess)  // first use: HIP picks the stream's queue now
+      e = hipEventSynchronize(ev);
+    if (ev) (void)hipEventDestroy(ev);
+    if (e != hipSuccess) {
+      if (s) (void)hipStreamDestroy(s);
+      return hip_fail(e, "dino_stream_create");
+    }
+    *stream = (void*)s;
+    return DINO_OK;
+  }
   int n = 0;
   if ((e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device)) != hipSuccess)
     return hip_fail(e, "dino_stream_create");

@@ -243,15 +243,32 @@ def release_stream_set(device, s: int) -> None:
         _SETS_BUSY.get(_dev_index(device), set()).discard(s)
 
 
+def _new_role_stream(idx: int, role: str) -> torch.cuda.Stream:
+    """A role's stream.  The batch slots and the copy stream come from the least priority's
+    pool of hardware queues (``dino_stream_create(-1)``), the other roles from torch's pool
+    (DINO_ROLE_STREAMS=torch: all of them).  HIP multiplexes streams onto GPU_MAX_HW_QUEUES
+    = 4 queues per priority; from torch's pool two of the three slots shared one and ran one
+    after the other (their batches queue in one FIFO: 128 of 198 e2e batches started on the
+    other slot's end), e2e 156.3k img/s; on queues of their own 172.9k (C2 177.2k,
+    ``scripts/rolestream_study.sh``).  The streams live as long as the process, as torch's
+    pool streams do."""
+    if role in ("slot", "copy") and os.environ.get("DINO_ROLE_STREAMS", "low") == "low":
+        from . import _lib
+        h = ctypes.c_void_p()
+        _lib.check(_lib.load().dino_stream_create(idx, -1, ctypes.byref(h)), "dino_stream_create")
+        return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", idx))
+    return torch.cuda.Stream(device=idx)
+
+
 def role_stream(device, role: str, k: int = 0, stream_set: int = 0) -> torch.cuda.Stream:
     idx = _dev_index(device)
     with _ROLE_LOCK:
         if not any(key[:2] == (idx, stream_set) for key in _ROLE_STREAMS):
             for r, j in _ROLE_ORDER:
-                _ROLE_STREAMS[(idx, stream_set, r, j)] = torch.cuda.Stream(device=idx)
+                _ROLE_STREAMS[(idx, stream_set, r, j)] = _new_role_stream(idx, r)
         st = _ROLE_STREAMS.get((idx, stream_set, role, k))
         if st is None:
-            st = _ROLE_STREAMS[(idx, stream_set, role, k)] = torch.cuda.Stream(device=idx)
+            st = _ROLE_STREAMS[(idx, stream_set, role, k)] = _new_role_stream(idx, role)
         return st
 
 
@@ -418,6 +435,9 @@ class MI355XAugPipeline:
         self._view_ring: list = [None] * (self.depth + 1)
         self._handed: _Slot | None = None            # the last batch handed over (iterator / run_one_batch)
         self._closed = False
+        # study hook (DINO_TIMELINE=1): per batch, host stamps and timing events on the copy and
+        # slot streams (``timeline()``); off, nothing is recorded
+        self._timeline: list | None = [] if os.environ.get("DINO_TIMELINE") == "1" else None
         _LIVE.add(self)
         if self._feed:
             sizes = self._sizes()
@@ -888,6 +908,7 @@ class MI355XAugPipeline:
         staging on the slot's stream, then the kernels (``dino_run_batch``)."""
         if self._closed:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
+        self._tl_pull = time.perf_counter()
         return self._enqueue_prepared(self._pull())
 
     def _enqueue_prepared(self, pb: _Prepared) -> _Slot:
@@ -896,6 +917,7 @@ class MI355XAugPipeline:
             raise RuntimeError("MI355XAugPipeline.run_one_batch() called after close()")
         st = pb.staging
         t0 = time.perf_counter()
+        tl = {"t0": t0, "pull": getattr(self, "_tl_pull", t0)} if self._timeline is not None else None
         copied = None
         buf_j = None  # the native feed's input buffer of the slot this batch reads
         try:
@@ -930,8 +952,15 @@ class MI355XAugPipeline:
                     try:
                         if cs is not sl.engine.stream and sl.buf_done[j] is not None:
                             cs.wait_event(sl.buf_done[j])
+                        if tl is not None:
+                            tl["issue"] = time.perf_counter()
+                            tl["c0"] = torch.cuda.Event(enable_timing=True)
+                            tl["c0"].record(cs)
                         self._source.copy(fb, sl.d_ins[j].data_ptr(), sl.d_offs[j].data_ptr(),
                                           cs.cuda_stream if cs is not None else 0)
+                        if tl is not None:
+                            tl["c1"] = torch.cuda.Event(enable_timing=True)
+                            tl["c1"].record(cs)
                     except BaseException:
                         self._source.release(fb)
                         raise
@@ -975,8 +1004,17 @@ class MI355XAugPipeline:
                         self.host_seconds["merge"] = self.host_seconds.get("merge", 0.0) + time.perf_counter() - tm
                 copied = torch.cuda.Event()
                 copied.record()
+            if tl is not None:
+                tl["k0"] = torch.cuda.Event(enable_timing=True)
+                tl["k0"].record(sl.engine.stream)
             self._launch(sl, d_bytes, d_offsets, B, None, cfg=cfg, account=True, raw_mask=d_raw, sizes=sizes,
                          probe=pb.info, lengths=d_lens)
+            if tl is not None:
+                tl["k1"] = torch.cuda.Event(enable_timing=True)
+                tl["k1"].record(sl.engine.stream)
+                tl["t1"] = time.perf_counter()
+                tl["slot"] = self._slots.index(sl)
+                self._timeline.append(tl)
             if buf_j is not None:
                 sl.buf_done[buf_j] = sl.event
             sl.inflight = (d_bytes, d_offsets, d_raw, d_lens, side)  # device copies live until the slot's next batch
@@ -1058,6 +1096,26 @@ class MI355XAugPipeline:
                 self._view_ring[sl.view_set][2] = cur  # the stream the set was handed to
         self._handed = sl
         return dict(sl.outputs)  # the caller's own dict: its references keep the tensors from reuse
+
+    def timeline(self) -> list[dict]:
+        """The DINO_TIMELINE=1 records (after a synchronize): per batch, host seconds of the
+        launch start / copy issue / launch end and device ms of copy start / end and kernel
+        start / end, both relative to the first record."""
+        if not self._timeline:
+            return []
+        torch.cuda.synchronize(self.device)
+        ref = self._timeline[0]
+        e0 = ref.get("c0") or ref["k0"]
+        out = []
+        for r in self._timeline:
+            d = {"slot": r["slot"], "pull": r["pull"] - ref["t0"], "t0": r["t0"] - ref["t0"], "t1": r["t1"] - ref["t0"]}
+            if "issue" in r:
+                d["issue"] = r["issue"] - ref["t0"]
+            for k in ("c0", "c1", "k0", "k1"):
+                if k in r:
+                    d[k] = e0.elapsed_time(r[k]) / 1e3
+            out.append(d)
+        return out
 
     def wait(self) -> None:
         """Make the caller's stream wait for the last enqueued batch."""

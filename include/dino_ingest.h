@@ -258,7 +258,11 @@ int dino_copy_h2d(void* d_dst, const void* host_src, int64_t nbytes, void* strea
 /* A stream on its own hardware queue (a CU-masked stream: the runtime never shares
  * its queue with other streams), for work that must not queue behind, or hold up,
  * the batch streams: the progressive side decode (dataloader_amd/progside.py).
- * cu_count <= 0 or >= the device's CUs: every CU; else cu_count CUs spread evenly. */
+ * cu_count == 0 or >= the device's CUs: every CU; else cu_count CUs spread evenly.
+ * cu_count < 0: instead a non-blocking stream of the least priority (HIP keeps a pool of
+ * GPU_MAX_HW_QUEUES queues per priority; torch's streams use the normal and high pools),
+ * used once at creation so that streams made in a row take different queues: the
+ * pipeline's batch slots and its H2D copy stream (DINO_ROLE_STREAMS=low). */
 int dino_stream_create(int device, int32_t cu_count, void** stream);
 int dino_stream_destroy(void* stream);
 
