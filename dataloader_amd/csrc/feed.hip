@@ -16,7 +16,8 @@
 //   packer thread   takes the next B samples (a batch may straddle shards; the last partial
 //                   batch of an epoch is dropped, dali_backend.py:187), packs them into a
 //                   pinned slot with `nthreads` copier threads and probes each image right
-//                   after its copy (status, kind, workspace bytes), unmaps consumed shards;
+//                   after its copy (status, kind, workspace bytes), hands consumed shards to
+//                   the openers, which unmap them outside the feed's lock;
 //   caller          dino_feed_next (blocks with the GIL released: ctypes), then
 //                   dino_feed_copy (H2D of the slot on the caller's stream; the slot returns
 //                   to the packer when that copy retires) or dino_feed_release.
@@ -37,6 +38,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -332,6 +334,10 @@ struct dino_feed {
   int64_t open_next = 0;               // push-order ticket of the next shard an opener takes
   int64_t open_done = 0;               // ticket of the next shard to append to `opened`
   std::map<int64_t, std::shared_ptr<Shard>> parked;  // finished out of order (null: failed)
+  // packed shards whose mappings the openers unmap: an unmap of a populated shard (a TLB
+  // shootdown across the process's threads) ran on the packer under this feed's lock, where
+  // the caller's dino_feed_next waits; the openers do it outside the lock
+  std::vector<std::shared_ptr<Shard>> retired;
   bool epoch_end = false;              // no more pushes this epoch
   bool epoch_done = false;             // the packer found fewer than B samples left after epoch_end
   bool stop = false;
@@ -342,6 +348,10 @@ struct dino_feed {
   double t_open = 0, t_pack = 0, t_slot_wait = 0, t_sample_wait = 0;
   std::vector<std::thread> openers;
   std::thread packer;
+  // study trace (DINO_FEED_TRACE=path, written at destroy): per packed batch the packer's
+  // loop start / slot / samples / pack end / ready stamps, per dino_feed_next its entry / return
+  std::vector<std::array<double, 6>> trace_pack, trace_next;
+  bool trace = getenv("DINO_FEED_TRACE") != nullptr;
 
   void opener_loop();
   void packer_loop();
@@ -352,9 +362,18 @@ void dino_feed::opener_loop() {
   std::unique_lock<std::mutex> lk(m);
   for (;;) {
     cv.wait(lk, [&] {
-      return stop || (!pending.empty() && (int)(opened.size() + parked.size()) + opening < lookahead + 1);
+      return stop || !retired.empty() ||
+             (!pending.empty() && (int)(opened.size() + parked.size()) + opening < lookahead + 1);
     });
     if (stop) return;
+    if (!retired.empty()) {
+      std::vector<std::shared_ptr<Shard>> done;
+      done.swap(retired);
+      lk.unlock();
+      done.clear();  // munmap, outside the lock
+      lk.lock();
+      continue;
+    }
     auto sh = std::make_shared<Shard>();
     sh->path = pending.front();
     pending.pop_front();
@@ -425,9 +444,11 @@ void dino_feed::packer_loop() {
   std::unique_lock<std::mutex> lk(m);
   for (;;) {
     double t0 = now_s();
+    std::array<double, 6> tr{t0, 0, 0, 0, 0, 0};
     const int k = free_slot_locked(lk);
     if (k < 0) return;
     t_slot_wait += now_s() - t0;
+    tr[1] = now_s();
     // wait for B samples (or the end of the epoch)
     t0 = now_s();
     int64_t avail = 0;
@@ -445,6 +466,7 @@ void dino_feed::packer_loop() {
       cv.wait(lk);
     }
     t_sample_wait += now_s() - t0;
+    tr[2] = now_s();
     const int64_t gen = generation;
     Slot& sl = slots[k];
     sl.state = kFilling;
@@ -487,14 +509,20 @@ void dino_feed::packer_loop() {
       memcpy(sl.offs_pinned, sl.offs.data(), sizeof(int64_t) * (batch + 1));
     }
     const double dt = now_s() - t0;
+    tr[3] = now_s();
     lk.lock();
-    used.clear();
+    tr[4] = now_s();
     t_pack += dt;
-    // unmap the shards every sample of which is packed (their bytes now live in slots)
+    // the shards every sample of which is packed (their bytes now live in slots) go to the
+    // openers to unmap
     while (!opened.empty() && opened.front()->next >= opened.front()->samples.size()) {
+      retired.push_back(std::move(opened.front()));
       opened.pop_front();
       ++shards_done;
     }
+    for (auto& u : used)
+      if (u.use_count() == 1) retired.push_back(std::move(u));  // a shard reset() dropped meanwhile
+    used.clear();
     if (!ok) {
       sl.state = kFree;
       if (error.empty()) error = "dino_feed: allocation of a pinned slot failed";
@@ -510,6 +538,10 @@ void dino_feed::packer_loop() {
     sl.seq = next_seq++;
     sl.state = kReady;
     ++batches;
+    if (trace) {
+      tr[5] = now_s();
+      trace_pack.push_back(tr);
+    }
     cv.notify_all();
   }
 }
@@ -562,6 +594,13 @@ int dino_feed_destroy(dino_feed* f) {
   for (auto& t : f->openers)
     if (t.joinable()) t.join();
   if (f->packer.joinable()) f->packer.join();
+  if (f->trace) {
+    if (FILE* fp = fopen(getenv("DINO_FEED_TRACE"), "w")) {
+      for (auto& r : f->trace_pack) fprintf(fp, "P %.6f %.6f %.6f %.6f %.6f %.6f\n", r[0], r[1], r[2], r[3], r[4], r[5]);
+      for (auto& r : f->trace_next) fprintf(fp, "N %.6f %.6f %.6f %.0f %.0f\n", r[0], r[1], r[2], r[3], r[4]);
+      fclose(fp);
+    }
+  }
   for (auto& s : f->slots) {  // copies still reading a slot finish first
     if (s.state == kCopying) (void)hipEventSynchronize(s.ev);
     if (s.ev) (void)hipEventDestroy(s.ev);
@@ -625,7 +664,9 @@ int dino_feed_set_epoch(dino_feed* f, uint64_t epoch) {
 
 int dino_feed_next(dino_feed* f, int32_t timeout_ms, dino_feed_batch* out) {
   if (!f || !out) return feed_fail(DINO_EINVAL, "dino_feed_next: bad arguments");
+  const double t_in = now_s();
   std::unique_lock<std::mutex> lk(f->m);
+  const double t_lock = now_s();
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms < 0 ? 0 : timeout_ms);
   for (;;) {
     if (!f->error.empty()) {  // one shard failed: report it once, the feed goes on without it
@@ -648,6 +689,7 @@ int dino_feed_next(dino_feed* f, int32_t timeout_ms, dino_feed_batch* out) {
         out->ws_need = s.ws;
         out->aws_need = s.aws;
         out->seq = s.seq;
+        if (f->trace) f->trace_next.push_back({t_in, t_lock, now_s(), (double)s.seq, (double)timeout_ms, 0});
         return DINO_OK;
       }
     }
