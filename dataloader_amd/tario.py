@@ -762,7 +762,7 @@ class NativeShardFeed:
         self._B = int(batch_size)
         self.nthreads = int(nthreads)
         self._slots = max(2, int(slots))
-        self._lookahead = max(1, int(lookahead))
+        self._lookahead = max(1, int(os.environ.get("DINO_FEED_LOOKAHEAD", lookahead)))
         self._max_dim = 0
         self._cfg = None
         self._feed = ctypes.c_void_p()
