@@ -181,7 +181,8 @@ std::string open_shard(Shard& s) {
   if ((int64_t)hdr[0] > st.st_size - 16) return "shard " + s.path + ": data length past the file";
   s.tar = (const uint8_t*)m + 16;
   s.tar_len = (int64_t)hdr[0];
-  if (madvise(m, s.map_len, MADV_POPULATE_READ) != 0) {  // Linux >= 5.14; else touch every page
+  static const bool populate = !getenv("DINO_FEED_POPULATE") || getenv("DINO_FEED_POPULATE")[0] != '0';
+  if (populate && madvise(m, s.map_len, MADV_POPULATE_READ) != 0) {  // Linux >= 5.14; else touch every page
     volatile uint8_t sink = 0;
     for (size_t o = 0; o < s.map_len; o += 4096) sink ^= ((const uint8_t*)m)[o];
     (void)sink;

@@ -312,3 +312,29 @@ def test_side_look_ahead_fills_behind_a_running_side_decode():
     assert all(blocking)                                  # each of them waited for the host half
     first.side.finished = True
     assert [p._pull_side().k for _ in range(3)] == [1, 2, 3]
+
+
+def test_output_set_reuse_check_sees_every_outside_reference():
+    """The output ring reuses a set only when nothing outside the pipeline holds a tensor
+    of it or its memory (pipeline._all_unshared; ADVICE r4: no assumed interpreter
+    reference counts).  CPU tensors, same reference structure as a slot's."""
+    from dataloader_amd import pipeline as P
+
+    views = [torch.empty(4), torch.empty(4)]
+    ring = [("key", views, None)]  # the ring's list holds the tensors
+    outputs = {"a": views[0], "b": views[1]}  # one slot's outputs dict
+    assert P._all_unshared(views, [1, 1])
+    held = views[0]  # a direct reference kept by the caller
+    assert not P._all_unshared(views, [1, 1])
+    del held
+    assert P._all_unshared(views, [1, 1])
+    part = views[1][:2]  # a view of the memory
+    assert not P._all_unshared(views, [1, 1])
+    del part
+    caller = dict(outputs)  # the caller's own dict of the batch
+    assert not P._all_unshared(views, [1, 1])
+    del caller
+    assert P._all_unshared(views, [1, 1])
+    del outputs  # no slot dict holds them any more
+    assert P._all_unshared(views, [0, 0])
+    assert ring
