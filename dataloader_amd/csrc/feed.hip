@@ -7,7 +7,7 @@
 // arrays per batch; here a batch never becomes Python objects:
 //
 //   opener threads  mmap a shard-cache file ([data_len:u64][magic:u64] + tar, reference
-//                   shard_cache.py:83-85, 584-609), fault its pages in, index the tar
+//                   shard_cache.py:83-85, 584-609), index the tar
 //                   (dino_tar_index), up to `lookahead` shards ahead of the packer; one
 //                   thread per shard of the look-ahead (at most kMaxOpeners), so that two
 //                   shards' page population overlaps (measured at 8 ranks per node: the
@@ -181,7 +181,12 @@ std::string open_shard(Shard& s) {
   if ((int64_t)hdr[0] > st.st_size - 16) return "shard " + s.path + ": data length past the file";
   s.tar = (const uint8_t*)m + 16;
   s.tar_len = (int64_t)hdr[0];
-  static const bool populate = !getenv("DINO_FEED_POPULATE") || getenv("DINO_FEED_POPULATE")[0] != '0';
+  // No pre-fault by default: the copier threads fault the pages in as they pack (the kernel
+  // maps 16 pages per fault around the address), spread over `nthreads` threads, where the
+  // openers' MADV_POPULATE_READ of every page of a shard made them the feed's bottleneck
+  // (e2e, same box, alternated: 151.0k / 172.0k / 168.9k img/s with it, 173.5k / 174.3k /
+  // 175.4k without; scripts/populate_study.sh).  DINO_FEED_POPULATE=1 restores it.
+  static const bool populate = getenv("DINO_FEED_POPULATE") && getenv("DINO_FEED_POPULATE")[0] == '1';
   if (populate && madvise(m, s.map_len, MADV_POPULATE_READ) != 0) {  // Linux >= 5.14; else touch every page
     volatile uint8_t sink = 0;
     for (size_t o = 0; o < s.map_len; o += 4096) sink ^= ((const uint8_t*)m)[o];
