@@ -493,33 +493,54 @@ def summarize(leg: dict, ab: dict, B: int, steps: int, world: int, tag: str) -> 
            "mean_jpeg_bytes": round(ab["s_jpeg"]), "mean_pixels": round(ab["pixels"]),
            "statuses_checked": leg.get("statuses_checked"), "statuses_checked_total": leg.get("statuses_checked_total")}
     if per_kernel:
-        dom = max(per_kernel, key=lambda k: per_kernel[k]["total_ms"])
+        # per step: a kernel launched once per view class (k_hresize, k_rcoeffs: twice per step)
+        # is charged all its launches of the step, never one launch
+        lps = {k: v["launches"] / max(steps, 1) for k, v in per_kernel.items()}
+        step_ms = {k: v["total_ms"] / max(steps, 1) for k, v in per_kernel.items()}
+        dom = max(per_kernel, key=lambda k: step_ms[k])
         # algorithmic bytes per image = S_jpeg + sum over views of 3 S^2 x out bytes;
-        # one launch of any Stage-3 kernel processes the batch of B images
-        bytes_launch = ab["path"] * B
-        achieved = bytes_launch / (per_kernel[dom]["avg_ms"] * 1e-3) / 1e9
+        # a step processes the batch of B images, its launches of the dominant kernel share them
+        bytes_step = ab["path"] * B
+        bytes_launch = bytes_step / max(lps[dom], 1e-9)
+        achieved = bytes_step / (step_ms[dom] * 1e-3) / 1e9
         dom_traffic = traffic.get(dom)
+        dom_iface = ab.get(dom, 0.0) * B / max(lps[dom], 1e-9)   # the kernel's own interface bytes per launch
+        path_gbs = ab["path"] * B * world / (dt / steps) / 1e9
+        path_frac = round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5)
         out["roofline"] = {
             "bound": "hbm", "achieved": round(achieved, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
             "frac": round(achieved / PEAK_HBM_GBS, 5), "traffic": dom_traffic, "kernel": dom,
             "algorithmic_bytes_per_launch": int(bytes_launch), "avg_launch_ms": round(per_kernel[dom]["avg_ms"], 4),
-            "definition": "SURVEY 8(d) bytes per image (S_jpeg + 3*sum(S_v^2)*out_bytes) x batch / dominant "
-                          "kernel's mean launch time (HIP events on its stream, serialized pass after the timed region)",
+            "launches_per_step": round(lps[dom], 3), "kernel_ms_per_step": round(step_ms[dom], 4),
+            "interface_bytes_per_launch": int(dom_iface) if dom_iface else None,
+            "traffic_over_interface": round(dom_traffic / dom_iface, 3) if dom_traffic and dom_iface else None,
+            "path_frac": path_frac,
+            "definition": "SURVEY 8(d) bytes per image (S_jpeg + 3*sum(S_v^2)*out_bytes) x batch (bytes of a "
+                          "step) / the dominant kernel's time per step (sum of its launches' HIP-event times on "
+                          "its stream, serialized pass after the timed region); per launch: bytes / launches "
+                          "per step over the mean launch time (the same ratio). path_frac: the whole timed step "
+                          "against the same bytes. traffic: PMC HBM bytes per launch (rocprofv3, "
+                          "traffic_source); traffic_over_interface: that over the kernel's own interface bytes",
             "traffic_source": f"profiles/{traffic_src}" if traffic_src else None}
         roof_all = {}
         for k, v in per_kernel.items():
             if ab.get(k) and v["avg_ms"] > 0:
-                gbs = ab[k] * B / (v["avg_ms"] * 1e-3) / 1e9
+                gbs = ab[k] * B / (step_ms[k] * 1e-3) / 1e9
+                iface_launch = ab[k] * B / max(lps[k], 1e-9)
+                tr = traffic.get(k)
                 roof_all[k] = {"achieved_GBs": round(gbs, 1), "frac": round(gbs / PEAK_HBM_GBS, 4),
-                               "avg_ms": round(v["avg_ms"], 4), "interface_bytes_per_launch": int(ab[k] * B),
-                               "traffic_bytes_per_launch": traffic.get(k)}
+                               "avg_ms": round(v["avg_ms"], 4), "launches_per_step": round(lps[k], 3),
+                               "ms_per_step": round(step_ms[k], 4),
+                               "interface_bytes_per_step": int(ab[k] * B),
+                               "interface_bytes_per_launch": int(iface_launch),
+                               "traffic_bytes_per_launch": tr,
+                               "traffic_over_interface": round(tr / iface_launch, 3) if tr else None}
         out["roofline_kernels"] = roof_all
         out["kernels_ms_per_step"] = {k: round(v["total_ms"] / steps, 4) for k, v in per_kernel.items() if v["launches"]}
         step_traffic = sum((traffic.get(k) or 0) * v["launches"] / max(steps, 1) for k, v in per_kernel.items()) \
             if traffic else None
-        path_gbs = ab["path"] * B * world / (dt / steps) / 1e9
         out["path_roofline"] = {"algorithmic_bytes_per_image": int(ab["path"]), "achieved_GBs": round(path_gbs, 2),
-                                "frac": round(path_gbs / PEAK_HBM_GBS / max(world, 1), 5),
+                                "frac": path_frac,
                                 "pmc_traffic_bytes_per_step": int(step_traffic) if step_traffic else None,
                                 "algorithmic_bytes_per_step": int(ab["path"] * B)}
     if leg.get("t_ser") is not None:

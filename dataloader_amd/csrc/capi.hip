@@ -572,6 +572,10 @@ int dino_debug_region(dino_ctx* c, int32_t index, int32_t region, void* d_dst, i
       src = c->d_ws + d.hlane_off;
       n = d.restart_interval > 0 ? 0 : (int64_t)d.h_lanes * 68;
       break;
+    case 6:  // kind 1: the scan list header (PHdr: levels, lane-decoder flag and slots)
+      src = c->d_ws + d.htab_off;
+      n = d.kind == 1 ? (int64_t)sizeof(PHdr) : 0;
+      break;
     default: return fail(DINO_EINVAL, "dino_debug_region: region %s%lld", "", region);
   }
   if (d.status != 0 && region != 0) return fail(DINO_EINVAL, "dino_debug_region: image status %s%lld", "", d.status);

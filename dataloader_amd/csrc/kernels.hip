@@ -22,6 +22,7 @@
 #include "idct.hpp"
 #include "jpeg_parse.hpp"
 #include "kernels.hpp"
+#include "lscan.hpp"
 #include "mask.hpp"
 #include "plan.hpp"
 #include "progressive.hpp"
@@ -146,10 +147,14 @@ __global__ void __launch_bounds__(1024) k_plan(ImgDesc* __restrict__ desc, int B
   __shared__ int64_t part[1024];
   __shared__ int32_t dpart[1024];
   const int t = threadIdx.x;
-  if (t == 0) {  // the batch's coefficient-buffer registry (k_pwalk, k_pscan)
+  if (t == 0) {  // the batch's coefficient-buffer registry (k_pwalk, k_pscan, k_plscan)
     pctl->ticket = 0;
     pctl->nprog = 0;
     pctl->max_scans = 0;
+    pctl->cap = (uint32_t)B;
+    pctl->lticket = 0;
+    pctl->nlane = 0;
+    pctl->lmax_scans = 0;
   }
   const int per = (B + 1023) / 1024;
   int64_t local = 0;
@@ -1140,13 +1145,17 @@ struct PWalkLds {
   uint8_t slot_dc[kPMaxTabs];
   ProgTable tab[kPMaxTabs];
   int32_t ntab, bad;
+  int32_t lslot[kMaxScans];  // lane_plan
+  LanePlan lp;
+  int32_t lane;
 };
+__device__ __forceinline__ uint32_t wave_destuff(const uint8_t* img, int64_t len, int64_t from, uint8_t* dst, int lane);
 
 __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restrict__ bytes,
                                                          const int64_t* __restrict__ offsets,
                                                          const int64_t* __restrict__ lengths,
                                                          ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
-                                                         PCtl* __restrict__ pctl) {
+                                                         PCtl* __restrict__ pctl, int lane_ok) {
   __shared__ PWalkLds L;
   const int img = blockIdx.x, t = threadIdx.x;
   if (desc[img].status != DINO_IMG_OK || desc[img].kind != 1) return;
@@ -1166,6 +1175,10 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
     L.ntab = prog_table_slots(L.scans, dl.n_scans, L.slot_off, L.slot_dc, L.ts,
                               ptab_capacity(dl.hlane_off - dl.htab_off));
     L.bad = 0;
+    // the lane decoder (lscan.hpp) when the script allows deferring the refinements and the
+    // side records were planned (kind 1 from the parse: a restart image k_htab switched is not)
+    L.lane = lane_plan(L.scans, dl.n_scans, dl.progressive != 0, L.lslot, &L.lp) &&
+             dl.plane_off - dl.binfo_off >= (dl.coef_bytes / 128) * kLSideBytes && lane_ok;
   }
   __syncthreads();
   if (dl.status != DINO_IMG_OK || L.ntab < 0) {
@@ -1190,7 +1203,8 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
     o.sr = L.scans[t];
     o.tslots = L.ts[t];
     o.pipe = prog_pipelined(L.scans, n, t, dl.progressive != 0, &o.deps) ? 1 : 0;
-    o.pad = 0;
+    o.dlen = 0;
+    o.slot = L.lane ? L.lslot[t] : -1;
     ps[prog_level_rank(L.scans, n, t)] = o;
   }
   int nlev = 0;
@@ -1205,19 +1219,41 @@ __global__ void __launch_bounds__(kPWalkThreads) k_pwalk(const uint8_t* __restri
   if (t == 0) {
     hd->n_scans = n;
     hd->n_levels = nlev;
-    hd->pad[0] = 0;
+    hd->lane = L.lane;
+    lane_pack(L.lp, &hd->lane_nac, &hd->lane_al_ac, hd->lane_band, &hd->lane_ndc, &hd->lane_al_dc);
   }
-  // libjpeg's zeroed coefficient arrays
+  // libjpeg's zeroed coefficient arrays (+ the lane decoder's side records)
   {
     uint4* c4 = (uint4*)(ws + dl.coef_off);
     const int64_t nq = dl.coef_bytes >> 4;
     for (int64_t q = t; q < nq; q += kPWalkThreads) c4[q] = make_uint4(0u, 0u, 0u, 0u);
+    if (L.lane) {
+      uint4* s4 = (uint4*)(ws + dl.binfo_off);
+      const int64_t ns = (dl.coef_bytes / 128) * (kLSideBytes / 16);
+      for (int64_t q = t; q < ns; q += kPWalkThreads) s4[q] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  if (L.lane) {  // every scan destuffed here, a wave per scan (k_pscan does it per scan wave)
+    __syncthreads();  // the PScan records (dlen) are complete
+    const int w = t >> 6, ln = t & 63;
+    for (int i = w; i < n; i += kPWalkThreads / 64) {
+      const ScanRec& sr = L.scans[i];
+      uint8_t* clean = ws + dl.ent_off + ((sr.data_off - dl.scan_off + 3) & ~3);
+      const uint32_t dlen = wave_destuff(p, len, sr.data_off, clean, ln);
+      if (ln == 0) ps[prog_level_rank(L.scans, n, i)].dlen = (int32_t)dlen;
+    }
   }
   if (t == 0) {
     desc[img].n_scans = n;
-    const uint32_t k = atomicAdd(&pctl->nprog, 1u);
-    pctl->pimg[k] = img;
-    atomicMax(&pctl->max_scans, (uint32_t)n);
+    if (L.lane) {
+      const uint32_t k = atomicAdd(&pctl->nlane, 1u);
+      pctl->pimg[pctl->cap - 1 - k] = img;
+      atomicMax(&pctl->lmax_scans, (uint32_t)n);
+    } else {
+      const uint32_t k = atomicAdd(&pctl->nprog, 1u);
+      pctl->pimg[k] = img;
+      atomicMax(&pctl->max_scans, (uint32_t)n);
+    }
   }
 }
 
@@ -1697,8 +1733,9 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
                                                          const int64_t* __restrict__ offsets,
                                                          const int64_t* __restrict__ lengths,
                                                          const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
-                                                         PCtl* __restrict__ pctl) {
+                                                         PCtl* __restrict__ pctl, int prio) {
   __shared__ int16_t s_stage[4][16 * 64];
+  if (prio) __builtin_amdgcn_s_setprio(3);
   const int lane = threadIdx.x & 63;
   const DINO_CONST PCtl* cc = (const DINO_CONST PCtl*)pctl;
   const uint32_t nprog = cc->nprog;
@@ -1777,6 +1814,369 @@ __global__ void __launch_bounds__(kPScanThreads) k_pscan(const uint8_t* __restri
 #endif
     __threadfence();  // this scan's coefficient stores before its completion count
     if (lane == 0) __hip_atomic_fetch_add(&((PHdr*)region)->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_plscan + k_papply: the lane decoder of progressive images (lscan.hpp).  A one-wave
+// workgroup takes tickets (scan index j, group of 64 lane images): lane i decodes scan j
+// of image i of the group once every lane's image has finished the scans of the level
+// before (earlier tickets, so no wait is ever on a later one).  k_papply then applies the
+// deferred refinements, a lane per coefficient.
+// ---------------------------------------------------------------------------
+constexpr int kLLookBits = 8;                               // LDS lookahead of the scan's main table
+// A lane's LDS table row: the lookahead (u16 entries), maxcode / valoffset of the lengths
+// kLLookBits + 1 .. 16 and the 256 symbol bytes (the slow path of the same table); 16-byte
+// aligned rows of 212 words (212 mod 64 = 20: the 64 rows start on different banks).
+constexpr int kLSlowLens = 16 - kLLookBits;
+constexpr int kLRowMc = (1 << kLLookBits) / 2;
+constexpr int kLRowVo = kLRowMc + kLSlowLens;
+constexpr int kLRowHv = kLRowVo + kLSlowLens;
+constexpr int kLLookWords = 212;
+static_assert(kLRowHv + 64 <= kLLookWords && kLSlowLens == 8, "lane table row");
+// Per lane, in LDS as [entry][lane] (conflict-free): a ring of the scan's destuffed dwords
+// and a ring of the next blocks' history masks.  Rings are refilled in wave-wide phases
+// (all lanes that have room load a chunk at once, one memory wait per phase), so the decode
+// steps themselves never wait on global memory: on gfx9 a load's wait also waits for every
+// store issued before it, and the lanes' triggers would otherwise never line up.
+constexpr int kLRing = 128, kLChunk = 32, kLLow = 16;   // dwords (kLLow: > a DC MCU's 10 blocks x 32 bits)
+constexpr int kLMRing = 32, kLMChunk = 16, kLMLow = 4;  // masks
+constexpr int kPLscanLds = 64 * kLLookWords * 4 + kLRing * 64 * 4 + kLMRing * 64 * 8 + 80;
+
+struct LaneReader {
+  const DINO_GLOBAL uint32_t* src;
+  DINO_LDS uint32_t* ring;  // this lane's column: dword i at ring[(i % kLRing) * 64]
+  uint32_t nw, nbits, pos, wi, tail;
+  uint32_t a0, a1, a2;      // dwords wi, wi + 1, wi + 2
+  __device__ __forceinline__ void fill_chunk() {
+    uint32_t v[kLChunk];
+#pragma unroll
+    for (int q = 0; q < kLChunk; ++q) v[q] = src[tail + q < nw ? tail + q : 0u];  // (always a valid address)
+#pragma unroll
+    for (int q = 0; q < kLChunk; ++q)
+      ring[((tail + q) % kLRing) * 64] = tail + q < nw ? __builtin_bswap32(v[q]) : 0u;
+    tail += kLChunk;
+  }
+  __device__ __forceinline__ void init(const uint32_t* s, uint32_t nbytes, DINO_LDS uint32_t* rg) {
+    src = gmem(s);
+    ring = rg;
+    nw = (nbytes + 3) >> 2;
+    nbits = nbytes * 8;
+    pos = wi = tail = 0;
+    fill_chunk();
+    fill_chunk();
+    a0 = ring[0];
+    a1 = ring[64];
+    a2 = ring[128];
+  }
+  __device__ __forceinline__ void maintain() {
+    if (__ballot(tail - wi < (uint32_t)kLLow)) {  // a refill phase (the wave's active lanes)
+      if (kLRing - (tail - wi) >= (uint32_t)kLChunk) fill_chunk();
+    }
+  }
+  __device__ __forceinline__ uint32_t peek() const {
+    const uint64_t x = ((uint64_t)a0 << 32 | a1) << (pos & 31);
+    return (uint32_t)(x >> 32);
+  }
+  __device__ __forceinline__ void skip(int n) {  // n <= 32: at most one dword boundary
+    pos += (uint32_t)n;
+    if ((pos >> 5) != wi) {
+      ++wi;
+      a0 = a1;
+      a1 = a2;
+      a2 = ring[((wi + 2) % kLRing) * 64];
+    }
+  }
+  __device__ __forceinline__ bool insuff() const { return pos > nbits; }
+};
+
+// Codes longer than the lookahead: the canonical-code search over lengths from .. 16 in
+// the image's PTab (global), libjpeg's l = 17 fake zero when none matches.
+__device__ __forceinline__ void lane_slow(const DINO_GLOBAL PTab* t, uint32_t p, int from, int* sym, int* len) {
+  const uint32_t p17 = p >> 15;
+  int32_t mc[8], vo[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {  // lengths 9 .. 16, loaded together
+    mc[q] = t->maxcode[9 + q];
+    vo[q] = t->valoffset[9 + q];
+  }
+  int l = 17, off = 0;
+#pragma unroll
+  for (int q = 7; q >= 0; --q) {  // the shortest matching length wins
+    if (9 + q >= from && (int32_t)(p17 >> (17 - (9 + q))) <= mc[q]) {
+      l = 9 + q;
+      off = vo[q];
+    }
+  }
+  *len = l;
+  if (l > 16) {
+    *sym = 0;  // JWRN_HUFF_BAD_CODE
+    return;
+  }
+  const int ix = ((int)(p17 >> (17 - l)) + off) & 255;
+  *sym = (int)((t->huffval[ix >> 2] >> (8 * (ix & 3))) & 0xFFu);
+}
+
+// The same on the lane's LDS row (its main table's codes longer than the lookahead).
+__device__ __forceinline__ void lane_slow_lds(const DINO_LDS uint32_t* row, uint32_t p, int* sym, int* len) {
+  const DINO_LDS uint4* r4 = (const DINO_LDS uint4*)(row + kLRowMc);
+  const uint4 m0 = r4[0], m1 = r4[1], v0 = r4[2], v1 = r4[3];  // loaded together
+  const int32_t mc[8] = {(int32_t)m0.x, (int32_t)m0.y, (int32_t)m0.z, (int32_t)m0.w,
+                         (int32_t)m1.x, (int32_t)m1.y, (int32_t)m1.z, (int32_t)m1.w};
+  const int32_t vo[8] = {(int32_t)v0.x, (int32_t)v0.y, (int32_t)v0.z, (int32_t)v0.w,
+                         (int32_t)v1.x, (int32_t)v1.y, (int32_t)v1.z, (int32_t)v1.w};
+  const uint32_t p17 = p >> 15;
+  int l = 17, off = 0;
+#pragma unroll
+  for (int q = kLSlowLens - 1; q >= 0; --q) {  // the shortest matching length wins
+    if ((int32_t)(p17 >> (17 - (kLLookBits + 1 + q))) <= mc[q]) {
+      l = kLLookBits + 1 + q;
+      off = vo[q];
+    }
+  }
+  *len = l;
+  const int ix = ((int)(p17 >> (17 - (l > 16 ? 16 : l))) + off) & 255;
+  const uint32_t h = (row[kLRowHv + (ix >> 2)] >> (8 * (ix & 3))) & 0xFFu;
+  *sym = l > 16 ? 0 : (int)h;  // (l = 17: JWRN_HUFF_BAD_CODE)
+}
+
+struct LaneTabs {
+  const DINO_LDS uint32_t* look;  // this lane's row: the main table (lpos) and its slow path
+  int lpos;
+  const PTab* tabs;
+  uint64_t ts;
+  const DINO_LDS uint8_t* natl;
+  __device__ __forceinline__ void lookup_ac(uint32_t p, int* sym, int* len) const {  // position 4, always the row
+    const uint32_t i = p >> (32 - kLLookBits);
+    const uint32_t w = look[i >> 1];
+    const uint32_t e = (i & 1) ? w >> 16 : w & 0xFFFFu;
+    if (e) {
+      *sym = (int)(e >> 4);
+      *len = (int)(e & 15u);
+    } else {
+      lane_slow_lds(look, p, sym, len);
+    }
+  }
+  __device__ __forceinline__ void lookup(int k, uint32_t p, int* sym, int* len) const {
+    if (k == lpos) {
+      lookup_ac(p, sym, len);
+      return;
+    }
+    const DINO_GLOBAL PTab* t = gmem(tabs + pbyte64(ts, k));
+    const uint32_t e = t->look[p >> (32 - kPLookBits)];
+    if (e) {
+      *sym = (int)(e >> 4);
+      *len = (int)(e & 15u);
+    } else {
+      lane_slow(t, p, kPLookBits + 1, sym, len);
+    }
+  }
+  __device__ __forceinline__ int nat(int k) const { return natl[k < 79 ? k : 79]; }
+};
+
+// Stores of a lane's scan: coefficients (first scans), the history masks (fire-and-forget
+// atomic ORs), the deferred refinements (side records).  A refinement reads the next blocks'
+// histories from its LDS ring.
+struct LaneOut {
+  DINO_GLOBAL int16_t* coef;
+  uint8_t* side;
+  int32_t slot;
+  DINO_LDS uint2* mring;  // this lane's column: mask of block m at mring[(m % kLMRing) * 64]
+  int64_t blk0;
+  int32_t bw, mcx, nblk, mtail, mtx, mty;
+  bool refine;
+  __device__ __forceinline__ void set(int64_t e, int16_t v) { coef[e] = v; }
+  __device__ __forceinline__ void fill_masks() {
+    uint2 v[kLMChunk];
+    int32_t x = mtx, y = mty;
+#pragma unroll
+    for (int q = 0; q < kLMChunk; ++q) {
+      const int64_t b = mtail + q < nblk ? blk0 + (int64_t)y * bw + x : blk0;  // (always a valid address)
+      v[q] = *gmem((const uint2*)(side + b * kLSideBytes));
+      if (++x == mcx) {
+        x = 0;
+        ++y;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kLMChunk; ++q) mring[((mtail + q) % kLMRing) * 64] = v[q];
+    mtx = x;
+    mty = y;
+    mtail += kLMChunk;
+  }
+  __device__ __forceinline__ void begin_ac(int64_t b0, int32_t w, int32_t mx, int32_t n, bool ref) {
+    blk0 = b0;
+    bw = w;
+    mcx = mx;
+    nblk = n;
+    refine = ref;
+    mtail = mtx = mty = 0;
+    if (refine) {
+      fill_masks();
+      fill_masks();
+    }
+  }
+  __device__ __forceinline__ void maintain(int32_t m) {
+    const bool low = refine && mtail < nblk && mtail - m < kLMLow;
+    if (__ballot(low)) {  // a refill phase
+      if (refine && mtail < nblk && kLMRing - (mtail - m) >= kLMChunk) fill_masks();
+    }
+  }
+  __device__ __forceinline__ uint64_t mask(int32_t m) const {
+    const uint2 v = mring[(m % kLMRing) * 64];
+    return (uint64_t)v.y << 32 | v.x;
+  }
+  __device__ __forceinline__ void mask_or(int64_t b, uint64_t bits) {
+    __hip_atomic_fetch_or((uint64_t*)(side + b * kLSideBytes), bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __device__ __forceinline__ void ac_ops(int64_t b, uint64_t seq, uint64_t nzn, uint64_t neg) {
+    DINO_GLOBAL uint64_t* tr = gmem((uint64_t*)(side + b * kLSideBytes + kLTripleOff + 24 * slot));
+    tr[0] = seq;
+    tr[1] = nzn;
+    tr[2] = neg;
+  }
+  __device__ __forceinline__ void dc_op(int64_t b) { *gmem(side + b * kLSideBytes + kLDcOff + slot) = 1; }
+};
+
+__global__ void __launch_bounds__(64) k_plscan(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
+                                               PCtl* __restrict__ pctl, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(3);
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  DINO_LDS uint32_t* s_look = (DINO_LDS uint32_t*)smem;
+  DINO_LDS uint32_t* s_ring = s_look + 64 * kLLookWords;
+  DINO_LDS uint2* s_mring = (DINO_LDS uint2*)(s_ring + kLRing * 64);
+  DINO_LDS uint8_t* s_nat = (DINO_LDS uint8_t*)(s_mring + kLMRing * 64);
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 80; i += 64) s_nat[i] = kNaturalOrder[i];
+  __syncthreads();
+  const uint32_t nlane = pctl->nlane, cap = pctl->cap;
+  if (nlane == 0) return;
+  const uint32_t ngroups = (nlane + 63) / 64;
+  const uint32_t total = ngroups * pctl->lmax_scans;
+  DINO_LDS uint32_t* row = s_look + lane * kLLookWords;
+  for (;;) {
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(&pctl->lticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)__shfl(tk, 0));
+    if (tk >= total) break;
+    const uint32_t j = tk / ngroups, g = tk - j * ngroups;
+    const uint32_t li = g * 64 + (uint32_t)lane;
+    const int img = li < nlane ? pctl->pimg[cap - 1 - li] : -1;
+    const ImgDesc* d = desc + (img >= 0 ? img : 0);
+    uint8_t* region = ws + d->htab_off;
+    PHdr* hd = (PHdr*)region;
+    const bool act = img >= 0 && (int)j < hd->n_scans;
+    PScan ps;
+    if (act) ps = ((const PScan*)(region + kPScanOff))[j];
+    const ScanRec& sr = ps.sr;
+    const PTab* tabs = (const PTab*)(region + kPTabOff);
+    // the scan's main table (AC: position 4, DC: position 0) into the lane's LDS row, as
+    // kLLookBits-bit entries (codes of <= kLLookBits bits, else 0) + its slow-path arrays
+    const int lpos = act && sr.ss > 0 ? 4 : 0;
+    const int tsl = act ? pbyte64(ps.tslots, lpos) : 0xFF;
+    if (tsl != 0xFF) {
+      const DINO_GLOBAL uint4* src = gmem((const uint4*)tabs[tsl].look);
+#pragma unroll 8
+      for (int q = 0; q < (1 << kPLookBits) / 8; ++q) {  // 8 entries of the 9-bit table -> 4 of ours
+        const uint4 v = src[q];
+        uint32_t e[4] = {v.x & 0xFFFFu, v.y & 0xFFFFu, v.z & 0xFFFFu, v.w & 0xFFFFu};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) e[k] = (e[k] & 15u) <= (uint32_t)kLLookBits ? e[k] : 0u;
+        row[2 * q] = e[0] | e[1] << 16;
+        row[2 * q + 1] = e[2] | e[3] << 16;
+      }
+      const DINO_GLOBAL PTab* tg = gmem(tabs + tsl);
+#pragma unroll
+      for (int q = 0; q < kLSlowLens; ++q) {
+        row[kLRowMc + q] = (uint32_t)tg->maxcode[kLLookBits + 1 + q];
+        row[kLRowVo + q] = (uint32_t)tg->valoffset[kLLookBits + 1 + q];
+      }
+#pragma unroll 8
+      for (int q = 0; q < 64; ++q) row[kLRowHv + q] = tg->huffval[q];
+    }
+    // wait for the previous level of every lane's image (earlier tickets)
+    for (;;) {
+      bool ready = true;
+      if (act && sr.level > 0)
+        ready = __hip_atomic_load(&hd->done[sr.level - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >=
+                hd->cnt[sr.level - 1];
+      if (!__ballot(!ready)) break;
+      __builtin_amdgcn_s_sleep(8);
+    }
+#ifdef DINO_PROG_PHASES
+    const uint64_t t0 = wall_clock64();
+#endif
+    if (act) {
+      LaneReader r;
+      r.init((const uint32_t*)(ws + d->ent_off + ((sr.data_off - d->scan_off + 3) & ~3)), (uint32_t)ps.dlen,
+             s_ring + lane);
+      LaneTabs t{(const DINO_LDS uint32_t*)row, tsl != 0xFF ? lpos : -1, tabs, ps.tslots,
+                 (const DINO_LDS uint8_t*)s_nat};
+      LaneOut o;
+      o.coef = gmem((int16_t*)(ws + d->coef_off));
+      o.side = ws + d->binfo_off;
+      o.slot = ps.slot;
+      o.mring = s_mring + lane;
+      o.refine = false;
+      lane_scan_decode(r, t, d, sr, o);
+#ifdef DINO_PROG_PHASES
+      if (img < kProgPhaseImgs) {
+        g_prog_phase[img][j][0] = t0;
+        g_prog_phase[img][j][1] = wall_clock64();
+        g_prog_phase[img][j][2] = (uint64_t)sr.level | ((uint64_t)sr.ss << 8) | ((uint64_t)sr.se << 16) |
+                                  ((uint64_t)sr.ah << 24) | ((uint64_t)sr.al << 28) | ((uint64_t)sr.ns << 32);
+      }
+#endif
+      __threadfence();  // this scan's stores before its completion count
+      __hip_atomic_fetch_add(&hd->done[sr.level], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// The deferred refinements (lane_apply_block), data-parallel: a wave per block, lane k =
+// zigzag coefficient k.  Grid (x, lane image).
+constexpr int kPApplyWgs = 16;
+__global__ void __launch_bounds__(256) k_papply(const ImgDesc* __restrict__ desc, uint8_t* __restrict__ ws,
+                                                const PCtl* __restrict__ pctl) {
+  const uint32_t k = blockIdx.y;
+  if (k >= pctl->nlane) return;
+  const int img = pctl->pimg[pctl->cap - 1 - k];
+  const ImgDesc& d = desc[img];
+  const PHdr* hd = (const PHdr*)(ws + d.htab_off);
+  const uint32_t nac = hd->lane_nac, ndc = hd->lane_ndc, al_dc = hd->lane_al_dc;
+  const uint64_t al_ac = hd->lane_al_ac;
+  const uint64_t band_ac[3] = {hd->lane_band[0], hd->lane_band[1], hd->lane_band[2]};
+  if (nac == 0 && ndc == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int pos = kNaturalOrder[lane];
+  const int64_t nb0 = (int64_t)d.comp[0].bw * d.comp[0].bh;
+  const int64_t nb1 = d.ncomp > 1 ? (int64_t)d.comp[1].bw * d.comp[1].bh : 0;
+  const int64_t nblk = d.coef_bytes / 128;
+  int16_t* coef = (int16_t*)(ws + d.coef_off);
+  const uint8_t* side = ws + d.binfo_off;
+  const int64_t step = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < nblk; b += step) {
+    const int c = b < nb0 ? 0 : (b < nb0 + nb1 ? 1 : 2);
+    const int na = (int)((nac >> (4 * c)) & 15u);
+    const uint8_t* sd = side + b * kLSideBytes;
+    const int16_t v0 = coef[b * 64 + pos];
+    int16_t v = v0;
+    const uint64_t bw = c == 0 ? band_ac[0] : (c == 1 ? band_ac[1] : band_ac[2]);
+    for (int s = 0; s < na; ++s) {
+      const uint64_t* tr = (const uint64_t*)(sd + kLTripleOff + 24 * s);
+      const uint64_t seq = tr[0], nzn = tr[1], neg = tr[2];
+      const int bd = (int)((bw >> (12 * s)) & 0xFFFu), ss = bd & 63, se = bd >> 6;
+      // correction bit j of the sequence -> the band's j-th coefficient non-zero so far
+      const bool hist = v != 0 && lane >= ss && lane <= se;
+      const uint64_t hm = __ballot(hist);
+      const uint32_t j = lane_rank(hm);
+      const bool corr = hist && ((seq >> ((63 - j) & 63)) & 1u);
+      v = ac_refine_value(v, corr, (nzn >> lane) & 1u, (neg >> lane) & 1u, (int)((al_ac >> (16 * c + 4 * s)) & 15u));
+    }
+    if (lane == 0)
+      for (int s = 0; s < (int)ndc; ++s)
+        if (sd[kLDcOff + s]) v = (int16_t)(v | (1 << ((al_dc >> (4 * s)) & 15u)));
+    if (v != v0) coef[b * 64 + pos] = v;
   }
 }
 
@@ -3691,7 +4091,8 @@ static const char* const kKernelNames[kKNumKernels] = {"k_parse", "k_plan", "k_d
                                                        "k_color", "k_params", "k_vplan", "k_rcoeffs", "k_hresize",
                                                        "k_final_global", "k_final_local", "k_vert_global",
                                                        "k_vert_local", "k_dcscan", "k_htab", "k_hseg", "k_huff2",
-                                                       "k_huff3", "k_prog", "k_pwalk"};
+                                                       "k_huff3", "k_prog", "k_pwalk", "k_plscan",
+                                                       "k_papply"};
 const char* g_failed_kernel = "";
 
 #define TIMED(tm, kid, s, launch)                          \
@@ -3736,12 +4137,25 @@ hipError_t init_launch_geom(int device, LaunchGeom* g) {
                                kHresizeLds)) != hipSuccess)
     return e;
   g->grid_hr = persistent_grid(reinterpret_cast<const void*>(&k_hresize), kHresizeLds, cus);
+  if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_plscan), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               kPLscanLds)) != hipSuccess)
+    return e;
   // scan waves: one per CU by default.  A scan's serial decode runs on the CU's one scalar
   // unit, which the CU's waves share: two scan waves on a CU each run at about half speed
   // (DINO_PSCAN_PER_CU: waves per CU, measured in profiles/r03_prog_*).
   const char* pc = getenv("DINO_PSCAN_PER_CU");
   const int per_cu = pc && atoi(pc) > 0 ? atoi(pc) : 1;
   g->grid_ps = per_cu * cus;
+  // lane scan waves: one ticket each (a 512-image pool of libjpeg-default files: 80); the rest exit
+  const char* ls = getenv("DINO_PLSCAN_WAVES");
+  g->grid_ls = ls && atoi(ls) > 0 ? atoi(ls) : 2 * cus;
+  // the scan waves' issue priority: 0 below the batch kernels (s_setprio 3, main_prio), 1 level
+  const char* sp = getenv("DINO_SCAN_PRIO");
+  g->scan_prio = sp ? atoi(sp) : 0;
+  // the lane decoder is opt-in (DINO_PROG_LANE=1): its throughput is higher but a scan's latency
+  // is ~3x a scan wave's, more than the side route's look-ahead covers
+  const char* pl = getenv("DINO_PROG_LANE");
+  g->prog_lane = pl ? (atoi(pl) != 0) : 0;
   return hipSuccess;
 }
 
@@ -3755,8 +4169,12 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
   TIMED(tm, kKDestuff, s, (k_destuff_write<<<grid_ds, kDestuffThreads, 0, s>>>(a.bytes, a.offsets, B, a.desc, a.ws)));
   TIMED(tm, kKHtab, s, (k_htab<<<B, kHuffThreads, 0, s>>>(a.bytes, a.offsets, a.desc, a.ws)));
   // after k_htab's kind switch
-  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
-  TIMED(tm, kKProg, s, (k_pscan<<<a.geom.grid_ps, kPScanThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl)));
+  TIMED(tm, kKPwalk, s, (k_pwalk<<<B, kPWalkThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl,
+                                                               a.geom.prog_lane)));
+  TIMED(tm, kKProg, s, (k_pscan<<<a.geom.grid_ps, kPScanThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl,
+                                                                             a.geom.scan_prio)));
+  TIMED(tm, kKPlscan, s, (k_plscan<<<a.geom.grid_ls, 64, kPLscanLds, s>>>(a.desc, a.ws, a.pctl, a.geom.scan_prio)));
+  TIMED(tm, kKPapply, s, (k_papply<<<dim3(kPApplyWgs, B), 256, 0, s>>>(a.desc, a.ws, a.pctl)));
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));

@@ -31,7 +31,7 @@ struct ViewPlan {
 enum KernelId : int {
   kKParse = 0, kKPlan, kKDestuff, kKHuff1, kKIdct, kKColor, kKParams, kKVplan, kKRcoeffs, kKHresize,
   kKFinalGlobal, kKFinalLocal, kKVertGlobal, kKVertLocal, kKDcscan, kKHtab, kKHseg, kKHuff2, kKHuff3, kKProg,
-  kKPwalk, kKNumKernels
+  kKPwalk, kKPlscan, kKPapply, kKNumKernels
 };
 
 struct KernelTimer {
@@ -56,17 +56,23 @@ struct LaunchGeom {
   int32_t grid1;     // persistent k_huff1 grid (occupancy x CUs)
   int32_t grid3;     // persistent k_huff3 grid
   int32_t grid_ps;   // persistent k_pscan grid (waves)
+  int32_t grid_ls;   // persistent k_plscan grid (one-wave workgroups)
+  int32_t prog_lane; // 1: eligible progressive images take k_plscan (DINO_PROG_LANE=0: all k_pscan)
+  int32_t scan_prio; // 1: scan waves at the batch kernels' issue priority (DINO_SCAN_PRIO)
   int32_t grid_hr;   // persistent k_hresize grid (occupancy x CUs)
 };
 
 // Coefficient-buffer images of a batch (k_plan zeroes, k_pwalk registers, k_pscan
 // takes tickets): ticket t = scan t / nprog of image pimg[t % nprog] (each image's scans
 // in dependency-level order, so a scan only ever waits for scans with earlier tickets).
+// Lane images (k_plscan, lscan.hpp) register from the other end: limg(k) = pimg[cap - 1 - k];
+// lticket t = scan t / ngroups of the 64-image group t % ngroups.
 struct PCtl {
-  uint32_t ticket, nprog, max_scans, pad;
+  uint32_t ticket, nprog, max_scans, cap;
+  uint32_t lticket, nlane, lmax_scans, pad;
   int32_t pimg[1];  // [max_batch]
 };
-DHD int64_t pctl_bytes(int max_batch) { return 16 + 4 * (int64_t)(max_batch > 0 ? max_batch : 1); }
+DHD int64_t pctl_bytes(int max_batch) { return 32 + 4 * (int64_t)(max_batch > 0 ? max_batch : 1); }
 hipError_t init_launch_geom(int device, LaunchGeom* g);
 
 struct DecodeArgs {

@@ -6,6 +6,7 @@
 #include "kernels.hpp"
 #include "progressive.hpp"
 #include "pscan.hpp"
+#include "lscan.hpp"
 #include "resize.hpp"
 
 namespace dino {
@@ -73,6 +74,7 @@ DHD ChunkSizes image_chunk_bytes(const ImgDesc& d) {
   if (d.kind == 1) {
     z.ent = align16((int64_t)d.scan_len + 64);  // each scan's destuffed bytes (k_pscan)
     z.coef = align16(d.coef_bytes);
+    z.binfo = (d.coef_bytes / 128) * kLSideBytes;  // side records of the lane decoder (lscan.hpp)
     z.htab = kPRegionBytes;  // scan list + decoder tables (k_pwalk -> k_pscan)
     return chunk_finish(z);
   }

@@ -108,6 +108,18 @@ DHD int next_marker_at(const uint8_t* p, int64_t len, int64_t pos, int64_t* afte
   }
 }
 
+// The last coefficient (zigzag index) a scan may write.  On a corrupt stream an AC first
+// scan's run moves k up to se + 15 before the store and an AC refinement puts a new
+// coefficient at se + 1 (libjpeg's natural-order safety entries map k > 63 to 63), so
+// scans of adjacent bands of one component can write the same coefficient; ordering them
+// by these ranges keeps libjpeg's file order for every stream, not only valid ones.
+DHD int scan_write_end(const ScanRec& sr, bool progressive) {
+  if (!progressive) return 63;
+  if (sr.ss == 0) return sr.se;
+  const int e = sr.se + (sr.ah == 0 ? 15 : 1);
+  return e < 63 ? e : 63;
+}
+
 // Walk the scans of a kind-1 image (d->first_sos is the FF of its first SOS), filling
 // scans[0..n) and d->n_scans; updates d->status on error.  Every lane of a wave may
 // run it (all values are wave-uniform); `find` is the entropy-data end finder.
@@ -239,13 +251,15 @@ DHD int prog_walk(const uint8_t* p, int64_t len, ImgDesc* d, ScanRec* scans, Fin
           latched[ci] = true;
         }
       }
-      // dependency level: after every earlier scan that wrote one of its coefficients
+      // dependency level: after every earlier scan that wrote (or, on a corrupt stream, may
+      // have written) one of the coefficients it may write
+      const int wend = scan_write_end(sr, d->progressive != 0);
       int lv = -1;
       for (int k = 0; k < ns; ++k)
-        for (int cf = sr.ss; cf <= sr.se; ++cf) lv = level_of[sr.comp[k]][cf] > lv ? level_of[sr.comp[k]][cf] : lv;
+        for (int cf = sr.ss; cf <= wend; ++cf) lv = level_of[sr.comp[k]][cf] > lv ? level_of[sr.comp[k]][cf] : lv;
       sr.level = lv + 1;
       for (int k = 0; k < ns; ++k)
-        for (int cf = sr.ss; cf <= sr.se; ++cf) level_of[sr.comp[k]][cf] = (int8_t)sr.level;
+        for (int cf = sr.ss; cf <= wend; ++cf) level_of[sr.comp[k]][cf] = (int8_t)sr.level;
       // entropy data: up to the first marker that is not RSTn
       sr.data_off = (int32_t)next_pos;
       const int64_t e = find(p, next_pos, len);

@@ -115,10 +115,11 @@ DHD int prog_level_rank(const ScanRec* scans, int n, int i) {
 
 struct PScan {
   ScanRec sr;
+  int32_t dlen;     // lane images: the scan's destuffed bytes (k_pwalk)
   uint64_t tslots;  // byte k: table slot of DC table k (k < 4) / AC table k - 4; 0xFF none
   uint64_t deps;    // pipelined scans: byte k = sorted index of an earlier scan it reads after, 0xFF none
   int32_t pipe;     // 1: follows its dependencies block by block (prog_pipelined), 0: waits for its level
-  int32_t pad;
+  int32_t slot;     // lane images: the refinement slot it records into (lane_plan), -1 none
 };
 static_assert(sizeof(PScan) == 112, "PScan layout");
 struct PHdr {
@@ -126,13 +127,18 @@ struct PHdr {
   int32_t cnt[kMaxScans];   // scans per level
   int32_t done[kMaxScans];  // scans of each level completed (k_pscan)
   int32_t prog[kMaxScans];  // blocks each scan (sorted index) has finished and published
-  int32_t pad[14];
+  int32_t lane;             // 1: decoded by k_plscan + k_papply (lscan.hpp), 0: by k_pscan
+  uint32_t lane_nac, lane_ndc, lane_al_dc;  // lane_pack
+  uint64_t lane_al_ac;
+  uint64_t lane_band[3];
+  int32_t pad[2];
 };
 static_assert(sizeof(PHdr) == 832, "PHdr layout");
 
-// Scans whose coefficient sets intersect (a shared component and overlapping bands).
+// Scans whose coefficient sets intersect (a shared component and overlapping write ranges,
+// scan_write_end; AC scans only, which are progressive).
 DHD bool scans_overlap(const ScanRec& a, const ScanRec& b) {
-  if (a.se < b.ss || b.se < a.ss) return false;
+  if (scan_write_end(a, true) < b.ss || scan_write_end(b, true) < a.ss) return false;
   for (int i = 0; i < a.ns && i < 4; ++i)
     for (int j = 0; j < b.ns && j < 4; ++j)
       if (a.comp[i] == b.comp[j]) return true;

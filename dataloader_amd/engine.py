@@ -118,7 +118,8 @@ class IngestEngine:
 
     KERNEL_NAMES = ["k_parse", "k_plan", "k_destuff", "k_huff1", "k_idct", "k_color", "k_params", "k_vplan",
                     "k_rcoeffs", "k_hresize", "k_final_global", "k_final_local", "k_vert_global", "k_vert_local",
-                    "k_dcscan", "k_htab", "k_hseg", "k_huff2", "k_huff3", "k_prog", "k_pwalk"]
+                    "k_dcscan", "k_htab", "k_hseg", "k_huff2", "k_huff3", "k_prog", "k_pwalk", "k_plscan",
+                    "k_papply"]
 
     def set_timing(self, enable: bool) -> None:
         _lib.check(self.lib.dino_set_timing(self._ctx, int(enable)), "dino_set_timing")

@@ -414,13 +414,25 @@ class MI355XAugPipeline:
         # H2D copies of the native feed's batches, off the slots' streams (DINO_COPY_STREAM=0: on them)
         self._copy_stream = None
         self._device_arg = device
+        self._closed = True  # until the end of __init__: close() must not run on a half-built pipeline
+        self._slots: list[_Slot] = []
         self._stream_set = acquire_stream_set(device)
+        try:
+            self._init_device(aug_cfg, device, depth, engine, max_image_dim, workspace_bytes)
+        except BaseException:  # a failed construction hands its stream set back
+            for sl in self._slots:
+                if sl.engine is not engine:
+                    sl.engine.close()
+            self._host.close()
+            release_stream_set(device, self._stream_set)
+            raise
+
+    def _init_device(self, aug_cfg, device, depth, engine, max_image_dim, workspace_bytes) -> None:
         if (self._feed and depth > 1 and os.environ.get("DINO_COPY_STREAM", "1") != "0") or self._side_ahead:
             self._copy_stream = role_stream(device, "copy", 0, self._stream_set)
         max_crop = max(int(aug_cfg.max_global_crop_size or aug_cfg.global_crop_size),
                        int(aug_cfg.max_local_crop_size or aug_cfg.local_crop_size),
                        aug_cfg.global_crop_size, aug_cfg.local_crop_size)
-        self._slots: list[_Slot] = []
         for k in range(self.depth):
             if k == 0 and engine is not None:
                 eng = engine
@@ -434,15 +446,15 @@ class MI355XAugPipeline:
         # output sets (shape key, tensors, consumer stream), batch n -> set n % (depth + 1)
         self._view_ring: list = [None] * (self.depth + 1)
         self._handed: _Slot | None = None            # the last batch handed over (iterator / run_one_batch)
-        self._closed = False
         # study hook (DINO_TIMELINE=1): per batch, host stamps and timing events on the copy and
         # slot streams (``timeline()``); off, nothing is recorded
         self._timeline: list | None = [] if os.environ.get("DINO_TIMELINE") == "1" else None
-        _LIVE.add(self)
         if self._feed:
             sizes = self._sizes()
             self._feed_sizes = sizes
             self._source.configure(max_image_dim=self._max_image_dim, cfg=self._cfg(*sizes))
+        self._closed = False
+        _LIVE.add(self)
 
     @staticmethod
     def side_queue(prefetch_ahead: int, side_ahead: int) -> int:
@@ -526,6 +538,8 @@ class MI355XAugPipeline:
             eng.set_norm(sl.norm)
         if views is None:
             views = self._views_for(sl, cfg, batch)
+        else:
+            sl.view_set = -1  # the caller's own tensors, not a set of the ring
         views, info = eng.run_batch(d_bytes, d_offsets, batch, cfg, self._seed, self._batch_index,
                                     views=views, params_out=sl.params, raw_mask=raw_mask, lengths=lengths)
         sl.info = info
@@ -545,6 +559,8 @@ class MI355XAugPipeline:
         if eng.stream is not None:
             sl.event = torch.cuda.Event()
             sl.event.record(eng.stream)
+            if sl.view_set >= 0 and self._view_ring[sl.view_set] is not None:
+                self._view_ring[sl.view_set][3] = sl.event  # a later batch reusing the set waits for it
         self._last = sl
         self._handed = None
         self._batch_index += 1
@@ -567,13 +583,17 @@ class MI355XAugPipeline:
             in_dicts = [sum(1 for s in self._slots if s.outputs is not None and any(o is t for o in s.outputs.values()))
                         for t in vc[1]]
             if _all_unshared(vc[1], in_dicts):
-                if vc[2] is not None and sl.engine.stream is not None:
-                    ev = torch.cuda.Event()
-                    ev.record(vc[2])
-                    sl.engine.stream.wait_event(ev)
+                if sl.engine.stream is not None:
+                    if vc[2] is not None:  # the caller's work on the set's last hand-over
+                        ev = torch.cuda.Event()
+                        ev.record(vc[2])
+                        sl.engine.stream.wait_event(ev)
+                    if vc[3] is not None:  # the set's last writer, a batch of another slot
+                        sl.engine.stream.wait_event(vc[3])
                 return vc[1]
         views = sl.engine.alloc_views(cfg, batch)
-        self._view_ring[j] = [key, views, None]
+        # [shape key, tensors, consumer stream of the last hand-over, completion of the last writer]
+        self._view_ring[j] = [key, views, None, None]
         return views
 
     # ------------------------------------------------------------------ host half
@@ -1076,6 +1096,7 @@ class MI355XAugPipeline:
         eng.batch_info(sl.info)
         sl.outputs = {self._names[i]: v for i, v in enumerate(views)}
         sl.sizes = sizes
+        sl.view_set = -1  # fresh tensors at the new sizes: not a set of the ring
         if eng.stream is not None:
             sl.event = torch.cuda.Event()
             sl.event.record(eng.stream)

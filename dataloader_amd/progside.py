@@ -26,6 +26,7 @@ import ctypes
 import queue
 import threading
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -63,6 +64,8 @@ class SideJob:
         its batch decodes it again and reaches the same outcome (zero-filled views where
         Pillow raises)."""
         t0 = time.perf_counter()
+        if self.pending and self.owner is not None:  # still in the pool: hand it to the launcher now
+            self.owner.flush()
         self.launched.wait()
         if self.error is not None:
             raise RuntimeError("side decode launch failed") from self.error
@@ -187,8 +190,14 @@ class DeviceSideDecoder:
         # add (the prefetch thread) and flush (also the launch thread, for a batch about to launch)
         self._lock = threading.RLock()
         self._parts: "queue.Queue" = queue.Queue()   # pools handed to the launcher thread
-        self._launcher = threading.Thread(target=self._run, name="dino-side-launcher", daemon=True)
+        # the thread holds only a weak reference: a decoder nobody closes can still be collected
+        self._launcher = threading.Thread(target=_launcher_loop, args=(weakref.ref(self), self._parts),
+                                          name="dino-side-launcher", daemon=True)
         self._launcher.start()
+
+    def __del__(self):
+        if getattr(self, "_parts", None) is not None:
+            self._parts.put(None)
 
     def add(self, imgs: dict) -> SideJob | None:
         if not imgs:
@@ -226,20 +235,16 @@ class DeviceSideDecoder:
                     job.pending = False
                 self._parts.put(part)
 
-    def _run(self) -> None:
-        while True:
-            part = self._parts.get()
-            if part is None:
-                return
-            try:
-                with torch.cuda.device(self.device):
-                    self._launch(part)
-            except BaseException as e:  # noqa: BLE001 -- the batches waiting on it re-raise
-                for job, _, _ in part:
-                    job.error = e
-            finally:
-                for job, _, _ in part:
-                    job.launched.set()
+    def _run_part(self, part: list) -> None:
+        try:
+            with torch.cuda.device(self.device):
+                self._launch(part)
+        except BaseException as e:  # noqa: BLE001 -- the batches waiting on it re-raise
+            for job, _, _ in part:
+                job.error = e
+        finally:
+            for job, _, _ in part:
+                job.launched.set()
 
     def _launch(self, part: list) -> None:
         t_start = time.perf_counter()
@@ -331,17 +336,39 @@ class DeviceSideDecoder:
         return out
 
     def close(self) -> None:
-        if self._launcher.is_alive():
+        with self._lock:  # jobs never handed to the launcher fail instead of waiting forever
+            closed = RuntimeError("DeviceSideDecoder closed before the side decode was launched")
+            for job, _, _ in self._pool:
+                job.pending = False
+                job.error = closed
+                job.launched.set()
+            self._pool.clear()
+        if self._launcher.is_alive():  # the launcher finishes the parts queued before the sentinel
             self._parts.put(None)
             self._launcher.join()
         if self.timing:
             import sys
             print("side launches (ms, images):", self.launch_ms(), file=sys.stderr)
         with self._lock:
-            self._pool.clear()
             for e in self._engines:
                 e.close()
             self._engines.clear()
+
+
+def _launcher_loop(ref, parts: "queue.Queue") -> None:
+    """The side decoder's launcher thread: runs the pools handed over by ``flush`` until the
+    sentinel, or until its decoder is gone."""
+    while True:
+        part = parts.get()
+        dec = ref() if part is not None else None
+        if dec is None:
+            if part is not None:  # the decoder was collected with a pool queued: fail its jobs
+                for job, _, _ in part:
+                    job.error = RuntimeError("DeviceSideDecoder collected before the side decode was launched")
+                    job.launched.set()
+            return
+        dec._run_part(part)
+        del dec
 
 
 def side_mask(info: np.ndarray) -> np.ndarray:

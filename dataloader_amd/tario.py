@@ -355,12 +355,26 @@ class ShmShardCache:
         if not self._node_master:
             wait_ready(shm, self.shard_timeout_s)
             return shm
+        from concurrent.futures import Future
         with self._lock:
             fut = self._in_flight.get(shard_path)
-        if fut is not None:  # a background load of this shard: wait for it (reference get_view, :588-595)
+            mine = fut is None and not is_ready(shm)
+            if mine:  # a synchronous load registers like a background one: prefetch() and other
+                fut = self._in_flight[shard_path] = Future()  # callers of this shard wait for it
+        if fut is None:  # loaded between the first check and the lock
+            return shm
+        if not mine:  # a load of this shard is running: wait for it (reference get_view, :588-595)
             fut.result()
             return shm
-        self._load(shard_path)
+        try:
+            self._load(shard_path)
+            fut.set_result(None)
+        except BaseException as e:
+            fut.set_exception(e)
+            raise
+        finally:
+            with self._lock:
+                self._in_flight.pop(shard_path, None)
         return shm
 
     def _load(self, shard_path: str) -> None:
@@ -384,6 +398,7 @@ class ShmShardCache:
                 self._drop(old)
         write_shm_shard(shm, data)
         with self._lock:
+            self._total -= self._lru.pop(shard_path, 0)  # a rewrite replaces the size already counted
             self._lru[shard_path] = n
             self._total += n
         self._check_utilisation()

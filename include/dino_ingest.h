@@ -309,8 +309,9 @@ int dino_kernel_times(dino_ctx* ctx, double* total_ms, int64_t* counts, int32_t 
 /* Debug / test introspection of the last decoded batch: copy image `index`'s
  * region (0 descriptor, 1 destuffed entropy bytes, 2 sparse DCT coefficient entries + block info,
  * 3 component planes, 4 RGB, 5 speculative Huffman lane records: 68 bytes per lane =
- * start state, range result, first-decode result, checkpoints, first block) into d_dst
- * (<= max_bytes).  Synchronises the stream. */
+ * start state, range result, first-decode result, checkpoints, first block, 6 the scan-list
+ * header of a kind-1 image: 832 bytes, int32 at byte 776 = 1 when the lane decoder took it)
+ * into d_dst (<= max_bytes).  Synchronises the stream. */
 int dino_debug_region(dino_ctx* ctx, int32_t index, int32_t region, void* d_dst, int64_t max_bytes, void* stream);
 
 /* Per-dataset normalisation (reference NormSource, pipeline.py:109-180, and

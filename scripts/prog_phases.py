@@ -54,7 +54,7 @@ def main():
     for i in range(n):
         meta = int(ph[0, i, 2])
         ss, se, ah, al = (meta >> 8) & 255, (meta >> 16) & 255, (meta >> 24) & 15, (meta >> 28) & 15
-        cyc = dur[:, i].max() * 2100 / max(sym[i], 1)
+        cyc = dur[:, i].max() * 2400 / max(sym[i], 1)
         print(f"  scan {i}: level {meta & 255} band {ss}-{se} ah {ah} al {al}  {dur[0, i]:8.1f} us (max {dur[:, i].max():8.1f})"
               f"  symbols {sym[i]:6d}  ~{cyc:6.0f} cycles/symbol")
     for level in range(int(lv[:n].max()) + 1):

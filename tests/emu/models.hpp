@@ -15,6 +15,7 @@
 #include "../../dataloader_amd/csrc/jpeg_parse.hpp"
 #include "../../dataloader_amd/csrc/progressive.hpp"
 #include "../../dataloader_amd/csrc/pscan.hpp"
+#include "../../dataloader_amd/csrc/lscan.hpp"
 
 namespace dino {
 
@@ -235,6 +236,93 @@ inline int host_model_decode_multiscan(const uint8_t* p, int64_t len, ImgDesc& d
   return model_idct_color(d, coef, out_rgb, cap);
 }
 
+// k_pwalk + k_plscan + k_papply (lscan.hpp): every scan through lane_scan_decode with the
+// refinements deferred to side records, then applied block by block in scan order.
+// Returns 1 (not decoded) when lane_plan leaves the image to the wave decoder.
+struct HostLaneOut {
+  int16_t* coef;
+  uint8_t* side;
+  int slot;
+  int64_t blk0 = 0;
+  int32_t bw = 0, mcx = 1;
+  void set(int64_t e, int16_t v) { coef[e] = v; }
+  void begin_ac(int64_t b0, int32_t w, int32_t mx, int32_t, bool) {
+    blk0 = b0;
+    bw = w;
+    mcx = mx;
+  }
+  void maintain(int32_t) {}
+  uint64_t mask(int32_t m) const {
+    const int64_t b = blk0 + (int64_t)(m / mcx) * bw + m % mcx;
+    return *(const uint64_t*)(side + b * kLSideBytes);
+  }
+  void mask_or(int64_t b, uint64_t bits) { *(uint64_t*)(side + b * kLSideBytes) |= bits; }
+  void ac_ops(int64_t b, uint64_t seq, uint64_t nzn, uint64_t neg) {
+    uint64_t* tr = (uint64_t*)(side + b * kLSideBytes + kLTripleOff + 24 * slot);
+    tr[0] = seq;
+    tr[1] = nzn;
+    tr[2] = neg;
+  }
+  void dc_op(int64_t b) { side[b * kLSideBytes + kLDcOff + slot] = 1; }
+};
+
+inline int host_model_decode_lane(const uint8_t* p, int64_t len, ImgDesc& d, uint8_t* out_rgb, int32_t* stats,
+                                  StageCapture* cap) {
+  std::vector<ScanRec> scans(kMaxScans);
+  HostMarkerFinder find;
+  if (prog_walk(p, len, &d, scans.data(), find) != DINO_IMG_OK) return d.status;
+  std::vector<int32_t> slot(kMaxScans, -1);
+  LanePlan lp;
+  if (!lane_plan(scans.data(), d.n_scans, d.progressive != 0, slot.data(), &lp)) return 1;
+  std::vector<int32_t> slot_off(kPMaxTabs);
+  std::vector<uint8_t> slot_dc(kPMaxTabs);
+  std::vector<uint64_t> ts(kMaxScans);
+  const int ntab = prog_table_slots(scans.data(), d.n_scans, slot_off.data(), slot_dc.data(), ts.data(), kPMaxTabs);
+  if (ntab < 0) return DINO_IMG_UNSUPPORTED;
+  std::vector<PTab> tabs(ntab > 0 ? ntab : 1);
+  for (int s = 0; s < ntab; ++s) {
+    ProgTable t;
+    if (!huff_build_derived(p + slot_off[s], slot_dc[s] != 0, &t)) return DINO_IMG_CORRUPT;
+    ptab_fill_derived(&t, &tabs[s]);
+    for (int i = 0; i < (1 << kPLookBits); ++i) tabs[s].look[i] = ptab_look_entry(&t, i);
+  }
+  const int64_t nblk = d.coef_bytes / 128;
+  std::vector<int16_t> coef(d.coef_bytes / 2, 0);
+  std::vector<uint8_t> side((size_t)nblk * kLSideBytes, 0);
+  std::vector<uint8_t> clean(len + 16, 0);
+  // the kernels run the scans level by level; file order gives the same result (a scan only
+  // reads the history of earlier levels, which file order has finished too)
+  for (int i = 0; i < d.n_scans; ++i) {
+    const ScanRec& sr = scans[i];
+    HostLaneOut o{coef.data(), side.data(), slot[i]};
+    HostLaneTabs tb;
+    tb.tabs = tabs.data();
+    tb.ts = ts[i];
+    HostLaneClean r;
+    r.s = clean.data();
+    r.n = host_destuff(p, len, sr.data_off, clean.data());
+    lane_scan_decode(r, tb, &d, sr, o);
+    std::fill(clean.begin(), clean.end(), 0);
+  }
+  uint32_t nac, ndc, al_dc;
+  uint64_t al_ac, band_ac[kMaxComp];
+  lane_pack(lp, &nac, &al_ac, band_ac, &ndc, &al_dc);
+  for (int c = 0; c < d.ncomp; ++c) {
+    const int64_t b0 = d.comp[c].coef_off / 128, nb = (int64_t)d.comp[c].bw * d.comp[c].bh;
+    for (int64_t b = b0; b < b0 + nb; ++b)
+      lane_apply_block(coef.data() + b * 64, side.data() + b * kLSideBytes, c, nac, al_ac, band_ac, ndc, al_dc);
+  }
+  if (stats) {
+    stats[0] = d.n_scans;
+    stats[1] = lp.ndc;
+  }
+  if (cap) {
+    cap->desc = d;
+    cap->coef = coef;
+  }
+  return model_idct_color(d, coef, out_rgb, cap);
+}
+
 inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes, uint8_t* out_rgb, int32_t* stats,
                              StageCapture* cap = nullptr) {
   ImgDesc d;
@@ -243,6 +331,7 @@ inline int host_model_decode(const uint8_t* p, int64_t len, int mode, int lanes,
     memcpy(out_rgb, p + 16, (size_t)d.width * d.height * 3);
     return DINO_IMG_OK;
   }
+  if (d.kind == 1 && mode == 4) return host_model_decode_lane(p, len, d, out_rgb, stats, cap);
   if (d.kind == 1) return host_model_decode_multiscan(p, len, d, out_rgb, stats, cap);
   Destuffed ds = model_destuff(p + d.scan_off, d.scan_len);
   if (cap) {
