@@ -75,16 +75,38 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// How the feed reads a shard-cache file (DINO_FEED_IO):
+//   "mmap" (default)  index and copies over a mapping of the file;
+//   "index"           the tar index reads only the 512-byte headers (dino_tar_index_fd: the
+//                     openers never fault a shard in), copies from the mapping;
+//   "pread"           header-only index, and the copier threads pread each JPEG straight into
+//                     the pinned slot (no mapping: no faults, no unmap per shard).
+// At 8 ranks on one node (scripts/gpu_host_feed.sh, profiles/r06_host/): the openers' time fell
+// 6.3 -> 3.2 (index) / 2.2 s (pread) of 8, but the slowest feed stayed 108-109k (index) or fell
+// to 100-105k img/s (pread) against 107-115k (mmap): the node's copy bandwidth, not the
+// openers, bounds 8 feeds (~85 GB/s of /dev/shm reads in all).
+enum FeedIo { kIoMmap = 0, kIoIndex = 1, kIoPread = 2 };
+FeedIo feed_io_mode() {
+  static const FeedIo m = [] {
+    const char* e = getenv("DINO_FEED_IO");
+    if (e && !strcmp(e, "pread")) return kIoPread;
+    return e && !strcmp(e, "index") ? kIoIndex : kIoMmap;
+  }();
+  return m;
+}
+
 struct Shard {
   std::string path;
   void* map = nullptr;
   size_t map_len = 0;
+  int fd = -1;       // pread mode: the file stays open while its samples are packed
   const uint8_t* tar = nullptr;
   int64_t tar_len = 0;
   std::vector<dino_tar_sample> samples;
   size_t next = 0;   // next sample the packer takes
   ~Shard() {
     if (map) munmap(map, map_len);
+    if (fd >= 0) close(fd);
   }
 };
 
@@ -161,7 +183,7 @@ void shuffle_samples(std::vector<dino_tar_sample>& v, uint64_t seed, uint64_t ep
   }
 }
 
-// Opens, pre-faults and indexes one shard-cache file; "" on success, else the reason.
+// Opens and indexes one shard-cache file (feed_io_mode); "" on success, else the reason.
 std::string open_shard(Shard& s) {
   const int fd = open(s.path.c_str(), O_RDONLY | O_CLOEXEC);
   if (fd < 0) return "open " + s.path + ": " + strerror(errno);
@@ -169,6 +191,39 @@ std::string open_shard(Shard& s) {
   if (fstat(fd, &st) != 0 || st.st_size < 16) {
     close(fd);
     return "shard " + s.path + ": too short";
+  }
+  const FeedIo io = feed_io_mode();
+  if (io != kIoMmap) {
+    uint64_t hdr[2] = {0, 0};
+    if (pread(fd, hdr, 16, 0) != 16 || hdr[1] != kShardMagic) {
+      close(fd);
+      return "shard " + s.path + ": corrupt header (not ready)";  // reference shard_cache.py:331-340
+    }
+    if ((int64_t)hdr[0] > st.st_size - 16) {
+      close(fd);
+      return "shard " + s.path + ": data length past the file";
+    }
+    s.tar_len = (int64_t)hdr[0];
+    const int64_t cap = s.tar_len / 1024 + 16;  // a sample's member takes >= 1024 bytes
+    s.samples.resize((size_t)cap);
+    int64_t ns = 0, nm = 0;
+    const int rc = dino_tar_index_fd(fd, 16, s.tar_len, s.samples.data(), cap, nullptr, 0, &ns, &nm);
+    if (rc < 0) {
+      close(fd);
+      return "shard " + s.path + ": " + dino_tar_last_error();
+    }
+    s.samples.resize((size_t)ns);
+    if (io == kIoPread) {
+      s.fd = fd;
+      return "";
+    }
+    void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);  // copies fault it in
+    close(fd);
+    if (m == MAP_FAILED) return "mmap " + s.path + ": " + strerror(errno);
+    s.map = m;
+    s.map_len = (size_t)st.st_size;
+    s.tar = (const uint8_t*)m + 16;
+    return "";
   }
   void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fd, 0);
   close(fd);
@@ -217,11 +272,14 @@ class CopyPool {
     for (auto& t : th_) t.join();
   }
   // Pack n images into dst at offs (offs[n] = total) and probe them; returns ws / aws sums.
-  void run(const uint64_t* ptrs, const int64_t* lens, const int64_t* offs, int32_t n, uint8_t* dst,
+  // fds (nullable): image i is read with pread(fds[i], ..., offset ptrs[i]) instead of copied
+  // from address ptrs[i]
+  void run(const uint64_t* ptrs, const int32_t* fds, const int64_t* lens, const int64_t* offs, int32_t n, uint8_t* dst,
            int32_t max_dim, const dino_aug_config* cfg, int32_t* info, int64_t* ws, int64_t* aws) {
     {
       std::lock_guard<std::mutex> g(m_);
-      ptrs_ = ptrs, lens_ = lens, offs_ = offs, n_img_ = n, dst_ = dst, max_dim_ = max_dim, cfg_ = cfg, info_ = info;
+      ptrs_ = ptrs, fds_ = fds, lens_ = lens, offs_ = offs, n_img_ = n, dst_ = dst, max_dim_ = max_dim, cfg_ = cfg,
+      info_ = info;
       left_ = n_ - 1;
       ++gen_;
     }
@@ -264,9 +322,21 @@ class CopyPool {
     };
     int64_t w = 0, a = 0;
     for (int32_t i = first(k), e = first(k + 1); i < e; ++i) {
+      int64_t len = lens_[i];
+      if (fds_) {  // pread into the slot, then probe the slot's copy
+        int64_t got = 0;
+        while (got < len) {
+          const ssize_t r = pread(fds_[i], dst_ + offs_[i] + got, (size_t)(len - got), (off_t)(ptrs_[i] + got));
+          if (r <= 0) break;
+          got += r;
+        }
+        if (got < len) memset(dst_ + offs_[i] + got, 0, (size_t)(len - got));  // (a shard truncated under us)
+        probe_one(dst_ + offs_[i], len, false, max_dim_, cfg_, scans.data(), info_ + 4 * i, &w, &a);
+        continue;
+      }
       const uint8_t* src = (const uint8_t*)(uintptr_t)ptrs_[i];
-      if (lens_[i]) stream_copy(dst_ + offs_[i], src, lens_[i]);
-      probe_one(src, lens_[i], false, max_dim_, cfg_, scans.data(), info_ + 4 * i, &w, &a);
+      if (len) stream_copy(dst_ + offs_[i], src, len);
+      probe_one(src, len, false, max_dim_, cfg_, scans.data(), info_ + 4 * i, &w, &a);
     }
     stream_fence();
     ws_[k] = w;
@@ -283,6 +353,7 @@ class CopyPool {
   bool stop_ = false;
   int left_ = 0;
   const uint64_t* ptrs_ = nullptr;
+  const int32_t* fds_ = nullptr;
   const int64_t* lens_ = nullptr;
   const int64_t* offs_ = nullptr;
   int32_t n_img_ = 0;
@@ -445,6 +516,7 @@ int dino_feed::free_slot_locked(std::unique_lock<std::mutex>& lk) {
 
 void dino_feed::packer_loop() {
   std::vector<uint64_t> ptrs;
+  std::vector<int32_t> fds;
   std::vector<int64_t> lens;
   std::vector<std::shared_ptr<Shard>> used;  // keeps the batch's mappings alive while it is packed
   std::unique_lock<std::mutex> lk(m);
@@ -477,7 +549,9 @@ void dino_feed::packer_loop() {
     Slot& sl = slots[k];
     sl.state = kFilling;
     ptrs.resize(batch);
+    fds.resize(batch);
     lens.resize(batch);
+    bool by_fd = false;
     sl.offs.resize(batch + 1);
     sl.info.assign((size_t)batch * 4, 0);
     int32_t i = 0;
@@ -487,7 +561,13 @@ void dino_feed::packer_loop() {
       if (i < batch && s->next < s->samples.size()) used.push_back(s);
       while (i < batch && s->next < s->samples.size()) {
         const dino_tar_sample& r = s->samples[s->next++];
-        ptrs[i] = (uint64_t)(uintptr_t)(s->tar + r.img_off);
+        if (s->fd >= 0) {  // pread mode: file offset of the image
+          ptrs[i] = (uint64_t)(16 + r.img_off);
+          by_fd = true;
+        } else {
+          ptrs[i] = (uint64_t)(uintptr_t)(s->tar + r.img_off);
+        }
+        fds[i] = s->fd;
         lens[i] = r.img_len;
         sl.offs[i + 1] = sl.offs[i] + r.img_len;
         ++i;
@@ -510,8 +590,8 @@ void dino_feed::packer_loop() {
       else ok = false;
     }
     if (ok) {
-      pool->run(ptrs.data(), lens.data(), sl.offs.data(), batch, sl.host, max_dim, cfgp, sl.info.data(), &sl.ws,
-                &sl.aws);
+      pool->run(ptrs.data(), by_fd ? fds.data() : nullptr, lens.data(), sl.offs.data(), batch, sl.host, max_dim, cfgp,
+                sl.info.data(), &sl.ws, &sl.aws);
       memcpy(sl.offs_pinned, sl.offs.data(), sizeof(int64_t) * (batch + 1));
     }
     const double dt = now_s() - t0;

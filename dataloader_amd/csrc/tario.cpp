@@ -19,6 +19,7 @@
 // extension = the rest, lower-cased; consecutive members with one key form a sample.
 #include <stdint.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <string>
@@ -131,15 +132,38 @@ bool split_key(const std::string& name, std::string* key, std::string* ext) {
   return true;
 }
 
-}  // namespace
+// The tar walk over any byte source.  Src::at(pos, n): a pointer to n bytes at pos (n <=
+// the bytes left), valid until the next call.  Memory: the mapped shard itself; file
+// (dino_tar_index_fd): pread of the 512-byte headers and of pax / long-name data only, so that
+// an index never touches (faults in) the members' data.
+struct MemSrc {
+  const uint8_t* tar;
+  const uint8_t* at(int64_t pos, int64_t) { return tar + pos; }
+};
+struct FdSrc {
+  int fd;
+  int64_t base;
+  std::vector<uint8_t> buf;
+  bool ok = true;
+  const uint8_t* at(int64_t pos, int64_t n) {
+    if ((int64_t)buf.size() < n) buf.resize((size_t)n);
+    int64_t got = 0;
+    while (got < n) {
+      const ssize_t r = pread(fd, buf.data() + got, (size_t)(n - got), (off_t)(base + pos + got));
+      if (r <= 0) {
+        ok = false;
+        memset(buf.data() + got, 0, (size_t)(n - got));  // read as an end-of-archive block
+        break;
+      }
+      got += r;
+    }
+    return buf.data();
+  }
+};
 
-extern "C" {
-
-const char* dino_tar_last_error(void) { return g_tar_err.c_str(); }
-
-int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_t cap, char* keys, int64_t keys_cap,
-                   int64_t* n_samples, int64_t* n_members) {
-  if ((!tar && len > 0) || len < 0 || !n_samples || (cap > 0 && !out)) return tar_fail(DINO_EINVAL, "dino_tar_index: bad args");
+template <typename Src>
+int tar_index(Src& src, int64_t len, dino_tar_sample* out, int64_t cap, char* keys, int64_t keys_cap,
+              int64_t* n_samples, int64_t* n_members) {
   *n_samples = 0;
   if (n_members) *n_members = 0;
   int64_t pos = 0, ns = 0, nm = 0, kpos = 0;
@@ -166,8 +190,9 @@ int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_
     out[ns++] = cur;
     return DINO_OK;
   };
+  uint8_t h[512];
   while (pos + 512 <= len) {
-    const uint8_t* h = tar + pos;
+    memcpy(h, src.at(pos, 512), 512);
     if (is_zero_block(h)) break;  // end-of-archive marker
     if (!checksum_ok(h)) {
       if (pos == 0) return tar_fail(DINO_EFORMAT, "dino_tar_index: invalid tar header at offset 0");
@@ -189,9 +214,10 @@ int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_
     }
     const int64_t next = data + ((size + 511) / 512) * 512;
     if (type == 'L') {
-      long_name = cstr(tar + data, (int)std::min<int64_t>(size, 1 << 20));
+      const int64_t n = std::min<int64_t>(size, 1 << 20);
+      long_name = cstr(src.at(data, n), (int)n);
     } else if (type == 'x') {
-      parse_pax(tar + data, size, &pax_path, &pax_size);
+      parse_pax(src.at(data, size), size, &pax_path, &pax_size);
     } else if (type == 'g' || type == 'K') {
       // global pax header / GNU long link name: nothing per member
     } else {
@@ -239,6 +265,28 @@ int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_
   if (n_members) *n_members = nm;
   if (status != DINO_OK) g_tar_err = status == DINO_TAR_TRUNCATED ? "truncated member" : "bad header after offset 0";
   return status;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dino_tar_last_error(void) { return g_tar_err.c_str(); }
+
+int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_t cap, char* keys, int64_t keys_cap,
+                   int64_t* n_samples, int64_t* n_members) {
+  if ((!tar && len > 0) || len < 0 || !n_samples || (cap > 0 && !out)) return tar_fail(DINO_EINVAL, "dino_tar_index: bad args");
+  MemSrc src{tar};
+  return tar_index(src, len, out, cap, keys, keys_cap, n_samples, n_members);
+}
+
+int dino_tar_index_fd(int32_t fd, int64_t base, int64_t len, dino_tar_sample* out, int64_t cap, char* keys,
+                      int64_t keys_cap, int64_t* n_samples, int64_t* n_members) {
+  if (fd < 0 || base < 0 || len < 0 || !n_samples || (cap > 0 && !out)) return tar_fail(DINO_EINVAL, "dino_tar_index_fd: bad args");
+  FdSrc src{fd, base, {}};
+  const int rc = tar_index(src, len, out, cap, keys, keys_cap, n_samples, n_members);
+  if (!src.ok && rc >= 0) return tar_fail(DINO_EFORMAT, "dino_tar_index_fd: read error");
+  return rc;
 }
 
 int dino_gather(const uint64_t* src_ptrs, const int64_t* lens, int64_t n, uint8_t* dst, int64_t dst_cap,

@@ -109,6 +109,24 @@ def index_tar(buf) -> TarIndex:
     rc = lib.dino_tar_index(ctypes.c_void_p(addr), n, ctypes.c_void_p(out.ctypes.data), cap,
                             ctypes.c_void_p(keys.ctypes.data), keys.size, ctypes.byref(ns), ctypes.byref(nm))
     del keep
+    return _index_result(lib, rc, out, keys, ns, nm)
+
+
+def index_tar_fd(fd: int, base: int, length: int) -> TarIndex:
+    """Index the tar bytes [base, base + length) of an open file by reading only its headers
+    (``dino_tar_index_fd``: pread, the members' data is never read); offsets are relative to
+    ``base``, as ``index_tar`` of those bytes reports them."""
+    lib = _lib.load()
+    cap = max(16, int(length) // 1024 + 16)
+    out = np.zeros(cap, SAMPLE_DTYPE)
+    keys = np.zeros(max(256, cap * 64), np.uint8)
+    ns, nm = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib.dino_tar_index_fd(int(fd), int(base), int(length), ctypes.c_void_p(out.ctypes.data), cap,
+                               ctypes.c_void_p(keys.ctypes.data), keys.size, ctypes.byref(ns), ctypes.byref(nm))
+    return _index_result(lib, rc, out, keys, ns, nm)
+
+
+def _index_result(lib, rc, out, keys, ns, nm) -> TarIndex:
     if rc < 0:
         raise _lib.DinoError(f"dino_tar_index failed ({rc}): {lib.dino_tar_last_error().decode(errors='replace')}")
     s = out[:ns.value].copy()

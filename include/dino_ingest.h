@@ -350,6 +350,11 @@ typedef struct dino_tar_sample {
  * a positive DINO_TAR_* warning (samples before the fault are valid), or < 0. */
 int dino_tar_index(const uint8_t* tar, int64_t len, dino_tar_sample* out, int64_t cap, char* keys, int64_t keys_cap,
                    int64_t* n_samples, int64_t* n_members);
+/* The same walk over a file (the shard-cache file's fd, tar bytes [base, base + len)): only
+ * the 512-byte headers and pax / long-name records are read (pread), so indexing a shard
+ * never faults its members' data in (the native feed's openers). */
+int dino_tar_index_fd(int32_t fd, int64_t base, int64_t len, dino_tar_sample* out, int64_t cap, char* keys,
+                      int64_t keys_cap, int64_t* n_samples, int64_t* n_members);
 const char* dino_tar_last_error(void);
 
 /* Pack n byte ranges (absolute host addresses, e.g. JPEG members of mapped shards)

@@ -67,11 +67,26 @@ def oracle_samples(tar: bytes) -> list[tuple[str, bytes, bytes | None]]:
     return res
 
 
+def _index_via_file(tar: bytes) -> tario.TarIndex:
+    """dino_tar_index_fd over the bytes written after a 16-byte shard-cache header."""
+    import tempfile
+    with tempfile.TemporaryFile() as f:
+        f.write(b"H" * 16 + tar)
+        f.flush()
+        return tario.index_tar_fd(f.fileno(), 16, len(tar))
+
+
+@pytest.fixture(params=["memory", "fd"])
+def index_any(request):
+    """Both forms of the tar walk: over mapped bytes, and over a file reading headers only."""
+    return tario.index_tar if request.param == "memory" else _index_via_file
+
+
 @pytest.mark.parametrize("fmt", [tarfile.GNU_FORMAT, tarfile.PAX_FORMAT, tarfile.USTAR_FORMAT])
 @pytest.mark.parametrize("prefix", ["", "d" * 140 + "/"])
-def test_tar_index_matches_tarfile(fmt, prefix):
+def test_tar_index_matches_tarfile(fmt, prefix, index_any):
     tar = make_shard(37, fmt=fmt, seed=3, prefix=prefix)
-    idx = tario.index_tar(tar)
+    idx = index_any(tar)
     ref = oracle_samples(tar)
     assert idx.status == 0 and len(idx) == len(ref) == 37
     assert idx.n_members == 74
@@ -81,7 +96,7 @@ def test_tar_index_matches_tarfile(fmt, prefix):
         assert tar[row["meta_off"]:row["meta_off"] + row["meta_len"]] == rjson
 
 
-def test_tar_index_grouping_edge_cases():
+def test_tar_index_grouping_edge_cases(index_any):
     buf = io.BytesIO()
     with tarfile.open(fileobj=buf, mode="w") as tf:
         _add(tf, "a.json", b"{}")                # sample without an image: skipped
@@ -95,31 +110,31 @@ def test_tar_index_grouping_edge_cases():
         tf.addfile(ti)
         _add(tf, "e.jpg", b"")                   # empty image member
     tar = buf.getvalue()
-    idx = tario.index_tar(tar)
+    idx = index_any(tar)
     assert idx.keys == ["b", "dir/c", "e"]
     got = [tar[r["img_off"]:r["img_off"] + r["img_len"]] for r in idx.samples]
     assert got == [b"B", b"C2", b""]
     assert [(k, i) for k, i, _ in oracle_samples(tar)] == list(zip(idx.keys, got))
 
 
-def test_tar_index_truncation_and_bad_headers():
+def test_tar_index_truncation_and_bad_headers(index_any):
     tar = make_shard(6, seed=1)
-    full = tario.index_tar(tar)
+    full = index_any(tar)
     # truncated inside the 4th jpg's data: 3 samples, truncation status
     cut = int(full.samples[3]["img_off"]) + 5
-    t = tario.index_tar(tar[:cut])
+    t = index_any(tar[:cut])
     assert t.status == tario.TAR_TRUNCATED and len(t) == 3
     # corrupt checksum of a later header: iteration stops there (tarfile semantics)
     bad = bytearray(tar)
     h = int(full.samples[2]["img_off"]) - 512
     bad[h + 148:h + 156] = b"0000000\x00"
-    t = tario.index_tar(bytes(bad))
+    t = index_any(bytes(bad))
     assert t.status == tario.TAR_BAD_HEADER and len(t) == 2
     # corrupt first header: error, like tarfile.ReadError
     with pytest.raises(tario._lib.DinoError):
-        tario.index_tar(b"\x01" * 2048)
-    assert len(tario.index_tar(b"")) == 0
-    assert len(tario.index_tar(b"\x00" * 1024)) == 0
+        index_any(b"\x01" * 2048)
+    assert len(index_any(b"")) == 0
+    assert len(index_any(b"\x00" * 1024)) == 0
 
 
 def test_extract_jpegs_with_meta_records():
