@@ -862,8 +862,23 @@ def _procs(args, world: int) -> int:
     return max(2, min(16, share // max(1, world)))
 
 
+def _maps_at_exit(path: str) -> None:
+    """Study hook (DINO_EXIT_MAPS=path): the process's library map written at interpreter exit,
+    to resolve the PCs of a crash during library finalization (VERDICT r5 weak #6)."""
+    import atexit
+
+    def dump():
+        try:
+            Path(path).write_text(Path("/proc/self/maps").read_text())
+        except OSError:
+            pass
+    atexit.register(dump)
+
+
 def main(argv: list[str] | None = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
+    if os.environ.get("DINO_EXIT_MAPS"):
+        _maps_at_exit(os.environ["DINO_EXIT_MAPS"])
     args = build_parser().parse_args(argv)
     launched = "WORLD_SIZE" in os.environ
     if not launched and (args.gpus or 1) > 1:

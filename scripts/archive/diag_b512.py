@@ -5,7 +5,7 @@ from pathlib import Path
 import numpy as np
 import torch
 
-ROOT = Path(__file__).resolve().parents[1]
+ROOT = Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 from dataloader_amd.config import DINOAugConfig  # noqa: E402

@@ -6,7 +6,7 @@ import pstats
 import sys
 from pathlib import Path
 
-sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+sys.path.insert(0, str(Path(__file__).resolve().parents[2]))
 import bench  # noqa: E402
 
 if __name__ == "__main__":  # the encoder pool spawns workers that import this file

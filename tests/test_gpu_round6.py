@@ -140,3 +140,139 @@ def test_damaged_progressive_scans_both_decoders(gpu_device, lane):
             bad.append((i, int((got != np.asarray(ref)).sum())))
     eng.close()
     assert not bad, bad[:10]
+
+
+# ----------------------------------------------------------------------------- the drop-in route at B = 512
+B = 512
+
+
+class _Recording:
+    """A callable source with the reference's conventions (_batch_size, _resolution_src;
+    _ReaderAdapter.__call__, shard_reader.py:346-376) that keeps every batch it hands out."""
+
+    def __init__(self, src):
+        self._src = src
+        self._batch_size = src._batch_size
+        self._resolution_src = None
+        self.batches = []
+
+    def __call__(self):
+        b = self._src()
+        self.batches.append(b)
+        return b
+
+
+def _check_handed(pipe, out, batch_jpegs, k, sample_rng, tdtype, n_sampled=36):
+    """The batch just handed over by the iterator (its slot still holds it): every decode
+    bit-exact with Pillow, >= 32 sampled images x 10 views against the oracle replay of their
+    records (tests/test_gpu_parity.py _check_views: bit-exact except blur)."""
+    from dataloader_amd.config import DINOAugConfig
+    from dataloader_amd.engine import params_from_device
+    from dataloader_amd.params import RECORD_BYTES
+    from tests.test_gpu_parity import _check_views
+    torch.cuda.synchronize()
+    sl = pipe._handed
+    assert sl.batch_index == k
+    info = sl.info.cpu().numpy()
+    assert (info[:, 0] == 0).all(), np.unique(info[:, 0], return_counts=True)
+    bad = []
+    for i, j in enumerate(batch_jpegs):
+        arr = np.asarray(cpu_ref.decode_rgb(j))
+        assert (info[i, 1], info[i, 2]) == (arr.shape[1], arr.shape[0]), i
+        got = sl.engine.copy_rgb(i, arr.shape[1], arr.shape[0]).cpu().numpy()
+        if not np.array_equal(got, arr):
+            bad.append((i, int((got != arr).sum())))
+    assert not bad, f"batch {k}: decode mismatches (image, bytes): {bad[:16]}"
+    cfg = DINOAugConfig()
+    nv = cfg.n_views
+    recs = params_from_device(sl.params[: B * nv * RECORD_BYTES])
+    views = [out[0][name] for name in pipe._names]
+    assert all(v.dtype == tdtype and v.shape[0] == B for v in views)
+    prog = [i for i, j in enumerate(batch_jpegs) if b"\xff\xc2" in j[:4096]]
+    pick = list(range(8)) + list(range(B - 16, B)) + prog[:6]
+    rest = [i for i in range(B) if i not in pick]
+    pick += [int(x) for x in sample_rng.choice(rest, size=max(0, n_sampled - len(set(pick))), replace=False)]
+    pick = sorted(set(pick))
+    assert len(pick) >= 32
+    sel_views = [v[pick] for v in views]
+    sel_recs = np.concatenate([recs[b * nv:(b + 1) * nv] for b in pick])
+    worst = _check_views([batch_jpegs[b] for b in pick], sel_views, sel_recs, nv, tdtype, cfg.mean, cfg.std)
+    assert worst <= 0.005
+    return len(pick), len(prog)
+
+
+@pytest.mark.parametrize("fp8", [False, True], ids=["bf16", "fp8"])
+def test_dropin_side_route_b512_from_a_host_source(gpu_device, fp8):
+    """MI355XBackend.build_pipeline + build_pipeline_iterator, as DINODataLoader
+    drives them (PipelineConfig.gpu_queue 3 batches in flight), from a host list source with one
+    progressive JPEG in 16 (the default route: prefetch thread -> dino_gather_probe -> side
+    look-ahead staged in HBM -> side decoder -> raw containers merged into the batch), at
+    B = 512: a batch with its progressive images checked whole against Pillow and 36 sampled
+    images x 10 views against the oracle; FP8 (PipelineConfig.dali_fp8_output, memory.py:193-214)
+    the same way."""
+    import bench
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import DINOAugConfig, DinoV2AugSpec, PipelineConfig
+    uniq = bench.make_unique(256, 640, 480, 1, False, 16)
+    uniq_prog = bench.make_unique(32, 640, 480, 31, False, 16, 1.0)
+    src = _Recording(bench._ProgMixSource(uniq, uniq_prog, B, 1.0 / 16, 80))
+    pcfg = PipelineConfig(device_id=0, seed=77, gpu_queue=3, dali_fp8_output=fp8)
+    backend = MI355XBackend()
+    spec = DinoV2AugSpec(aug_cfg=DINOAugConfig())
+    pipe = backend.build_pipeline(src, spec, pcfg, None)
+    try:
+        assert pipe._multiscan_route == "side" and pipe.depth == 3
+        it = backend.build_pipeline_iterator(pipe, spec, spec.output_map, B)
+        k_check = 6
+        for k in range(k_check + 1):
+            out = next(it)
+        n, n_prog = _check_handed(pipe, out, src.batches[k_check], k_check, np.random.default_rng(8),
+                                  torch.float8_e4m3fn if fp8 else torch.bfloat16)
+        assert n_prog == B // 16
+        st = pipe.flush_stats()
+        assert st["side_decoded"] >= (k_check + 1) * (B // 16) and st["host_decoded"] == 0
+        assert set(st["status"]) == {0}
+    finally:
+        pipe.close()
+
+
+def test_dropin_native_feed_b512(gpu_device, tmp_path):
+    """the e2e path's host half (/dev/shm shard-cache files, reference
+    shard_cache.py:584-609 -> NativeShardFeed: C++ openers + packer, pinned slots, probe) through
+    MI355XBackend.build_pipeline + build_pipeline_iterator at B = 512, depth 3: a batch that
+    straddles two shards checked whole against Pillow and 36 images x 10 views against the
+    oracle."""
+    import bench
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import DINOAugConfig, DinoV2AugSpec, PipelineConfig
+    from dataloader_amd.tario import NativeShardFeed, ShmShardCache
+    uniq = bench.make_unique(256, 640, 480, 3, False, 16)
+    per = 700
+    n_shards = 8
+    order = [uniq[(k * 7919 + i) % len(uniq)] for k in range(n_shards) for i in range(per)]
+    blobs = [bench.make_shards(order[k * per:(k + 1) * per], per)[0] for k in range(n_shards)]
+    cache = ShmShardCache(job_id=f"r6_dropin_{os.getpid()}", base_dir="/dev/shm", max_gb=16.0)
+    paths = [f"/synthetic/r6/shard-{k:05d}.tar" for k in range(n_shards)]
+    try:
+        for p, blob in zip(paths, blobs):
+            cache.put(p, blob)
+        feed = NativeShardFeed(cache, paths, B, nthreads=8, slots=6, shuffle=False)
+        pcfg = PipelineConfig(device_id=0, seed=78, gpu_queue=3)
+        backend = MI355XBackend()
+        spec = DinoV2AugSpec(aug_cfg=DINOAugConfig())
+        pipe = backend.build_pipeline(feed, spec, pcfg, None)
+        try:
+            assert pipe._feed and pipe.depth == 3
+            it = backend.build_pipeline_iterator(pipe, spec, spec.output_map, B)
+            k_check = 5  # images 2560 .. 3071: shards 3 and 4
+            for k in range(k_check + 1):
+                out = next(it)
+            _check_handed(pipe, out, order[k_check * B:(k_check + 1) * B], k_check, np.random.default_rng(9),
+                          torch.bfloat16)
+            st = pipe.flush_stats()
+            assert set(st["status"]) == {0} and st["host_decoded"] == 0
+        finally:
+            pipe.close()
+            feed.close()
+    finally:
+        cache.close(remove=True)
