@@ -875,10 +875,12 @@ def _maps_at_exit(path: str) -> None:
     atexit.register(dump)
 
 
+if os.environ.get("DINO_EXIT_MAPS"):  # every process of the run, spawn workers included ({pid})
+    _maps_at_exit(os.environ["DINO_EXIT_MAPS"].replace("{pid}", str(os.getpid())))
+
+
 def main(argv: list[str] | None = None) -> int:
     argv = list(sys.argv[1:] if argv is None else argv)
-    if os.environ.get("DINO_EXIT_MAPS"):
-        _maps_at_exit(os.environ["DINO_EXIT_MAPS"])
     args = build_parser().parse_args(argv)
     launched = "WORLD_SIZE" in os.environ
     if not launched and (args.gpus or 1) > 1:

@@ -1689,6 +1689,9 @@ __device__ __forceinline__ void fast_ac_first(CleanReader& r, const VTab& t, con
   int32_t bx = 0;
   int64_t rowe = plane;  // element of block (0, by)
   for (int32_t by = 0; by < mcy; ++by, rowe += (int64_t)bw * 64) {
+    // an AC first scan follows the earlier scans that may write its coefficients (a corrupt
+    // neighbour band's run, progressive.hpp scan_write_end) row by row
+    pp.need((by + 1) * mcx);
     for (bx = 0; bx < mcx; ++bx) {
       if (eobrun > 0) {
         --eobrun;

@@ -276,3 +276,41 @@ def test_dropin_native_feed_b512(gpu_device, tmp_path):
             feed.close()
     finally:
         cache.close(remove=True)
+
+
+def test_role_streams_released_before_exit(gpu_device, tmp_path):
+    """a process that used depth-3 pipelines (role streams from
+    dino_stream_create) ends with those streams destroyed by the pipeline module's atexit hook,
+    before library finalization, and exits 0 -- whether it closed its pipeline or not."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    script = tmp_path / "child.py"
+    script.write_text(f"""
+import atexit, sys
+sys.path.insert(0, {str(root)!r})
+import torch
+from dataloader_amd import pipeline as P
+from dataloader_amd.config import DINOAugConfig
+from dataloader_amd.engine import pack_jpegs
+from dataloader_amd.synthetic import make_jpeg
+jp = [make_jpeg(96, 80, s) for s in range(8)]
+hb, off = pack_jpegs(jp, pin=True)
+dev = torch.device("cuda", 0)
+pipe = P.MI355XAugPipeline(None, DINOAugConfig(global_crop_size=64, local_crop_size=32, n_local_crops=2), 8,
+                           depth=3)
+for k in range(4):
+    pipe.run_device_batch(hb.to(dev), off.to(dev), 8)
+torch.cuda.synchronize()
+assert P._RAW_ROLE_STREAMS, "no dino_stream_create role stream was made"
+if sys.argv[1] == "close":
+    pipe.close()
+# registered after the module's own hook, so it runs first (atexit is LIFO): report after it
+atexit.register(lambda: None)
+""")
+    for mode in ("close", "leave_open"):
+        r = subprocess.run([sys.executable, str(script), mode], capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, (mode, r.stderr[-2000:])
+    from dataloader_amd import pipeline as P
+    assert callable(P.release_role_streams)
