@@ -290,6 +290,8 @@ def test_role_streams_released_before_exit(gpu_device, tmp_path):
     script.write_text(f"""
 import atexit, sys
 sys.path.insert(0, {str(root)!r})
+# registered before the pipeline module's hook, so it runs after it (atexit is LIFO)
+atexit.register(lambda: print("left", len(sys.modules["dataloader_amd.pipeline"]._RAW_ROLE_STREAMS), flush=True))
 import torch
 from dataloader_amd import pipeline as P
 from dataloader_amd.config import DINOAugConfig
@@ -306,11 +308,8 @@ torch.cuda.synchronize()
 assert P._RAW_ROLE_STREAMS, "no dino_stream_create role stream was made"
 if sys.argv[1] == "close":
     pipe.close()
-# registered after the module's own hook, so it runs first (atexit is LIFO): report after it
-atexit.register(lambda: None)
 """)
     for mode in ("close", "leave_open"):
         r = subprocess.run([sys.executable, str(script), mode], capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, (mode, r.stderr[-2000:])
-    from dataloader_amd import pipeline as P
-    assert callable(P.release_role_streams)
+        assert "left 0" in r.stdout, (mode, r.stdout[-500:])
