@@ -4176,8 +4176,10 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s, KernelTimer* tm) {
                                                                a.geom.prog_lane)));
   TIMED(tm, kKProg, s, (k_pscan<<<a.geom.grid_ps, kPScanThreads, 0, s>>>(a.bytes, a.offsets, a.lengths, a.desc, a.ws, a.pctl,
                                                                              a.geom.scan_prio)));
-  TIMED(tm, kKPlscan, s, (k_plscan<<<a.geom.grid_ls, 64, kPLscanLds, s>>>(a.desc, a.ws, a.pctl, a.geom.scan_prio)));
-  TIMED(tm, kKPapply, s, (k_papply<<<dim3(kPApplyWgs, B), 256, 0, s>>>(a.desc, a.ws, a.pctl)));
+  if (a.geom.prog_lane) {  // the lane decoder (opt-in): k_pwalk registers no lane image otherwise
+    TIMED(tm, kKPlscan, s, (k_plscan<<<a.geom.grid_ls, 64, kPLscanLds, s>>>(a.desc, a.ws, a.pctl, a.geom.scan_prio)));
+    TIMED(tm, kKPapply, s, (k_papply<<<dim3(kPApplyWgs, B), 256, 0, s>>>(a.desc, a.ws, a.pctl)));
+  }
   TIMED(tm, kKHseg, s, (k_hseg<<<1, 1024, 0, s>>>(a.desc, B)));
   TIMED(tm, kKHuff1, s, (k_huff1<<<grid1, kHuffThreads, kHuffLdsBytes, s>>>(a.desc, B, a.ws)));
   TIMED(tm, kKHuff2, s, (k_huff2<<<B, kHuff2Threads, 0, s>>>(a.desc, a.ws)));
