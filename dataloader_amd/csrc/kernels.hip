@@ -2506,15 +2506,26 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
   const int64_t npx = (int64_t)W * d.height;
   const int64_t nq = (npx + 3) >> 2;  // npx < 2^31 (max_image_dim <= 16384 is enforced by k_parse limits)
   // (y, x) of the lane's first quad by one division; later quads advance by the
-  // grid stride (dy rows + dx pixels) without dividing again
+  // stride (dy rows + dx pixels) without dividing again.
+#ifdef DINO_COLOR_STRIDED
+  // grid-strided: workgroup x takes every gridDim.x-th run of 256 quads
   const int64_t q0 = (int64_t)bk.x * blockDim.x + threadIdx.x, qs = (int64_t)gridDim.x * blockDim.x;
+  const int64_t qend = nq;
+#else
+  // one contiguous band of rows per workgroup: the chroma rows an output row pair shares
+  // with its neighbours are read by the same workgroup (one XCD's L2) instead of by up to
+  // five workgroups on different XCDs, each fetching them again
+  const int64_t band = ((nq + gridDim.x - 1) / gridDim.x + blockDim.x - 1) / blockDim.x * blockDim.x;
+  const int64_t q0 = (int64_t)bk.x * band + threadIdx.x, qs = blockDim.x;
+  const int64_t qend = min(nq, (int64_t)(bk.x + 1) * band);
+#endif
   const uint32_t pstride = (uint32_t)(qs * 4);
   const int dy = (int)(pstride / (uint32_t)W), dx = (int)(pstride - (uint32_t)dy * (uint32_t)W);
   int yq = (int)((uint32_t)(q0 * 4) / (uint32_t)W), xq = (int)((uint32_t)(q0 * 4) - (uint32_t)yq * (uint32_t)W);
   // kColorBatch quads per lane per iteration: every load of the batch is issued before
   // any of its quads is converted (the RGB stores may alias the planes for the compiler,
   // so it would not move the next quad's loads above this quad's stores by itself)
-  for (int64_t qb = q0; qb < nq; qb += kColorBatch * qs) {
+  for (int64_t qb = q0; qb < qend; qb += kColorBatch * qs) {
     int ys[kColorBatch], xs[kColorBatch];
     bool fast[kColorBatch];
     uint32_t yw0[kColorBatch], yw1[kColorBatch], cw[kColorBatch][8];
@@ -2532,7 +2543,7 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
       // every 4:2:0 quad inside one row (row edges included: the fancy upsampler's edge
       // columns are clamps, applied to the loaded samples below) takes the vector path;
       // a lane on the generic per-pixel path would make its whole wave run that too
-      fast[k] = fast420 && qb + k * qs < nq && x + 3 < W;
+      fast[k] = fast420 && qb + k * qs < qend && x + 3 < W;
       if (fast[k]) {  // raw words: Y at x, Cb / Cr at column x/2 - 1 of the nearer and the farther row
         const int r = y >> 1;
         const int rf = (y & 1) ? min(r + 1, p1.dh - 1) : max(r - 1, 0);
@@ -2554,7 +2565,7 @@ __global__ void __launch_bounds__(256) k_color(const uint8_t* __restrict__ bytes
 #pragma unroll
     for (int k = 0; k < kColorBatch; ++k) {
       const int64_t q = qb + k * qs;
-      if (q >= nq) break;
+      if (q >= qend) break;
       int y = ys[k], x = xs[k];
       const int64_t i0 = q * 4;
       union {
