@@ -759,8 +759,9 @@ def run_prog_leg(args, uniq, uniq_prog, rank: int, world: int, cfg, B: int, dist
     pcfg = PipelineConfig(device_id=torch.cuda.current_device(), seed=4321 + rank, gpu_queue=args.gpu_queue)
     backend = MI355XBackend()
     # the warm-up fills the side look-ahead; the timed window spans several side pools
-    warm = max(args.warmup, backend.side_look_ahead(pcfg, None, 3) + 16)
-    steps = max(args.steps, 96)
+    ahead = backend.side_look_ahead(pcfg, None, 3)
+    warm = max(args.warmup, ahead + 16)
+    steps = max(args.steps, 96, 2 * ahead)
     src = _ProgMixSource(uniq, uniq_prog, B, args.prog_mix, warm + steps + 64)
     spec = DinoV2AugSpec(aug_cfg=cfg)
     pipe = backend.build_pipeline(src, spec, pcfg, None)

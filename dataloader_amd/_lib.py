@@ -90,6 +90,7 @@ def load() -> ctypes.CDLL:
         "dino_bf16_to_fp8": (i32, [vp, vp, i64, vp]),
         "dino_debug_region": (i32, [vp, i32, i32, vp, i64, vp]),
         "dino_set_timing": (i32, [vp, i32]),
+        "dino_ctx_set_prog_decoder": (i32, [vp, i32]),
         "dino_kernel_times": (i32, [vp, vp, vp, i32]),
         "dino_tar_index": (i32, [vp, i64, vp, i64, vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "dino_tar_index_fd": (i32, [i32, i64, i64, vp, i64, vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
@@ -123,7 +124,7 @@ def exported_symbols() -> list[str]:
     return ["dino_abi_version", "dino_last_error", "dino_ctx_create", "dino_ctx_destroy", "dino_decode",
             "dino_copy_rgb", "dino_pixel_ops_all", "dino_sample_params", "dino_augment", "dino_run_batch", "dino_masks",
             "dino_bf16_to_fp8", "dino_debug_region", "dino_set_timing", "dino_kernel_times",
-            "dino_tar_index", "dino_tar_index_fd", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
+            "dino_ctx_set_prog_decoder", "dino_tar_index", "dino_tar_index_fd", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
             "dino_probe", "dino_reserve", "dino_workspace_sizes", "dino_masks_host", "dino_resize_batch",
             "dino_augment_need", "dino_decode_spans", "dino_run_batch_spans", "dino_probe_spans",
             "dino_host_register", "dino_host_unregister", "dino_copy_h2d", "dino_gather_probe",

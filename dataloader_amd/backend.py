@@ -23,6 +23,7 @@ runs Stage 3 on the GPU.  Method-by-method:
 from __future__ import annotations
 
 import contextlib
+import os
 from dataclasses import dataclass
 from typing import TYPE_CHECKING, Any
 
@@ -131,10 +132,14 @@ class MI355XBackend:
         self._multiscan_route = multiscan_route
         self._side_ahead = side_ahead  # None: SIDE_AHEAD (see side_look_ahead)
 
-    # side look-ahead in batches (measured, scripts/route_study.py, B = 512 with 32 progressive:
-    # 16 -> 84.8k img/s, 48 -> 92.2-94.9k; profiles/r04_side_ahead.jsonl): a side decode pool
-    # takes ~45 ms, about 13 batch launches, so the look-ahead must cover several of them
-    SIDE_AHEAD = 48
+    # side look-ahead in batches.  Round 4 (scripts/route_study.py, B = 512 with 32 progressive:
+    # 16 -> 84.8k img/s, 48 -> 92.2-94.9k; profiles/r04_side_ahead.jsonl): a wave-decoder pool
+    # takes ~45 ms alone, so the look-ahead must cover several of them.  Round 6 (c2_prog,
+    # profiles/r06_side_plan/): 256 batches let the side decoder run the lane decoder on pools
+    # of 4096 images (progside.side_plan), which costs the batches less GPU time per image:
+    # c2_prog 72k -> 89-112k img/s.  The look-ahead's batches wait in HBM (~43 MB per C2
+    # batch: ~11 GB of the 288 at 256)
+    SIDE_AHEAD = 256
     PREFETCH = 1  # host-half batches prepared ahead by the pipeline's prefetch thread
 
     def side_look_ahead(self, pipeline_cfg: Any, source: Any, depth: int) -> int:
@@ -144,9 +149,9 @@ class MI355XBackend:
         so that everything pulled and not yet handed over (look-ahead + prefetch queue + batches
         in flight) fits the source's metadata FIFO (``_ReaderAdapter._meta_queue``, 64 slots,
         shard_reader.py:98, 357-375: an overflow raises).  The look-ahead's batches wait in HBM
-        (MI355XAugPipeline._stage_on_device): 48 C2 batches take ~2 GB of the 288."""
+        (MI355XAugPipeline._stage_on_device): 256 C2 batches take ~11 GB of the 288."""
         want = self._side_ahead if self._side_ahead is not None else \
-            max(self.SIDE_AHEAD, int(getattr(pipeline_cfg, "cpu_queue", 16) or 16))
+            max(int(os.environ.get("DINO_SIDE_AHEAD", self.SIDE_AHEAD)), int(getattr(pipeline_cfg, "cpu_queue", 16) or 16))
         mq = getattr(source, "_meta_queue", None)
         cap = getattr(mq, "maxsize", 0) or 0
         if cap > 0:

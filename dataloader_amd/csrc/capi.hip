@@ -529,6 +529,14 @@ int dino_masks_host(int32_t height, int32_t width, int32_t num_masking_patches, 
   return DINO_OK;
 }
 
+int dino_ctx_set_prog_decoder(dino_ctx* c, int32_t decoder) {
+  if (!c) return fail(DINO_EINVAL, "dino_ctx_set_prog_decoder: null ctx%s%lld");
+  if (decoder != DINO_PROG_WAVE && decoder != DINO_PROG_LANES)
+    return fail(DINO_EINVAL, "dino_ctx_set_prog_decoder: unknown decoder%s %lld", "", (long long)decoder);
+  c->geom.prog_lane = decoder == DINO_PROG_LANES;  // read at each launch (launch_decode)
+  return DINO_OK;
+}
+
 int dino_set_timing(dino_ctx* c, int32_t enable) {
   if (!c) return fail(DINO_EINVAL, "dino_set_timing: null ctx%s%lld");
   if (!c->timer) c->timer = new KernelTimer();

@@ -1842,8 +1842,13 @@ static_assert(kLRowHv + 64 <= kLLookWords && kLSlowLens == 8, "lane table row");
 // (all lanes that have room load a chunk at once, one memory wait per phase), so the decode
 // steps themselves never wait on global memory: on gfx9 a load's wait also waits for every
 // store issued before it, and the lanes' triggers would otherwise never line up.
+#ifdef DINO_LANE_SMALL_RINGS  // (A/B: half-size rings, 79 KiB of LDS per wave instead of 103.5)
+constexpr int kLRing = 64, kLChunk = 16, kLLow = 16;
+constexpr int kLMRing = 16, kLMChunk = 8, kLMLow = 4;
+#else
 constexpr int kLRing = 128, kLChunk = 32, kLLow = 16;   // dwords (kLLow: > a DC MCU's 10 blocks x 32 bits)
 constexpr int kLMRing = 32, kLMChunk = 16, kLMLow = 4;  // masks
+#endif
 constexpr int kPLscanLds = 64 * kLLookWords * 4 + kLRing * 64 * 4 + kLMRing * 64 * 8 + 80;
 
 struct LaneReader {

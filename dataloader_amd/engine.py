@@ -63,6 +63,7 @@ class IngestEngine:
                                                 ctypes.byref(self._ctx)), "dino_ctx_create")
         self.last_batch = 0
         self.stream = stream  # None: launch on torch's current stream
+        self.prog_lanes: bool | None = None  # set_prog_decoder's choice (None: the library default)
 
     def _s(self) -> ctypes.c_void_p:
         return _stream_handle(self.device, self.stream)
@@ -120,6 +121,12 @@ class IngestEngine:
                     "k_rcoeffs", "k_hresize", "k_final_global", "k_final_local", "k_vert_global", "k_vert_local",
                     "k_dcscan", "k_htab", "k_hseg", "k_huff2", "k_huff3", "k_prog", "k_pwalk", "k_plscan",
                     "k_papply"]
+
+    def set_prog_decoder(self, lanes: bool) -> None:
+        """Decode this context's coefficient-buffer images with the lane decoder (``True``:
+        64 images per wave, for large pools decoded well ahead) or the wave decoder."""
+        _lib.check(self.lib.dino_ctx_set_prog_decoder(self._ctx, int(bool(lanes))), "dino_ctx_set_prog_decoder")
+        self.prog_lanes = bool(lanes)
 
     def set_timing(self, enable: bool) -> None:
         _lib.check(self.lib.dino_set_timing(self._ctx, int(enable)), "dino_set_timing")

@@ -763,8 +763,10 @@ class MI355XAugPipeline:
         if not len(idx):
             return
         if self._side is None:
-            self._side = progside.DeviceSideDecoder(self.device, max_image_dim=self._max_image_dim,
-                                                    stream_set=self._stream_set)
+            lanes, pool = progside.side_plan(self._side_ahead)
+            self._side = progside.DeviceSideDecoder(self.device, max_images=pool, max_image_dim=self._max_image_dim,
+                                                    stream_set=self._stream_set, lanes=lanes)
+            self.stats["side_lanes"] = lanes
         if pb.jpegs is not None:
             imgs = {int(i): pb.jpegs[i] for i in idx}
         elif pb.feed is not None:

@@ -123,12 +123,13 @@ class _SideEngine:
     Consecutive launches of a context are ordered by the dedicated stream itself."""
 
     def __init__(self, device: torch.device, max_images: int, max_image_dim: int, cu_count: int = 0,
-                 dedicated: bool = True, index: int = 0, stream_set: int = 0):
+                 dedicated: bool = True, index: int = 0, stream_set: int = 0, lanes: bool = False):
         from .pipeline import role_stream
         self.raw = _create_stream(device.index or 0, int(cu_count)) if dedicated else None
         self.stream = self.raw if dedicated else role_stream(device, "side", index, stream_set)
         self.eng = IngestEngine(device, max_batch=max_images, max_views=1, max_crop_size=8,
                                 max_image_dim=max_image_dim, workspace_bytes=64 << 20, stream=self.stream)
+        self.eng.set_prog_decoder(lanes)
         self.copy = role_stream(device, "side_copy", index, stream_set)  # this context's torch stream (allocations, copies)
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
         self.keep = None                             # host / device inputs of the mini-batch in flight
@@ -147,6 +148,30 @@ class _SideEngine:
             self.raw = None
 
 
+# Side decoder plan by look-ahead (c2_prog: B = 512 C2 batches, one image in 16 progressive;
+# RESULTS.md round 6, profiles/r06_side_plan/).  The wave decoder (k_pscan) finishes a pool
+# sooner but costs the batches more GPU time per image; the lane decoder (k_plscan) costs
+# little per image and its launch time barely grows with the pool (one 64-image group per
+# wave), but a launch takes ~250-450 ms under a running pipeline.  So with a look-ahead
+# that can hold two pools of 4096 images decoding at once (>= LANES_MIN_AHEAD batches) the
+# lane decoder on large pools wins (lane, look-ahead 256, pools of 4096: 89-112k img/s;
+# wave, look-ahead 48, pools of 512: 72k; wave, look-ahead 256, pools of 2048: 77k); a
+# shorter look-ahead (a source whose metadata FIFO caps it, backend.side_look_ahead) keeps
+# the wave decoder on pools of 512.
+LANES_MIN_AHEAD = 128
+LANE_POOL = 4096
+WAVE_POOL = 512
+
+
+def side_plan(side_ahead: int) -> tuple[bool, int]:
+    """(lane decoder?, pool size in images) for a side look-ahead of ``side_ahead`` batches;
+    ``DINO_SIDE_DECODER=wave|lanes`` and ``DINO_SIDE_MAX`` override."""
+    import os
+    want = os.environ.get("DINO_SIDE_DECODER", "")
+    lanes = want == "lanes" if want in ("wave", "lanes") else int(side_ahead) >= LANES_MIN_AHEAD
+    return lanes, int(os.environ.get("DINO_SIDE_MAX", LANE_POOL if lanes else WAVE_POOL))
+
+
 class DeviceSideDecoder:
     """Pending pool + ``engines`` side contexts (created on demand).  ``add`` queues a
     batch's images and hands the pool to the launcher once it holds ``min_images``;
@@ -156,8 +181,8 @@ class DeviceSideDecoder:
     mini-batch in flight) run on a launcher thread of their own: on the pipeline's launch
     thread they cost the c2_prog leg ~3 ms per batch (``scripts/prof_leg.py``)."""
 
-    def __init__(self, device: torch.device, max_images: int = 512, min_images: int | None = None,
-                 engines: int | None = None, max_image_dim: int = 0, stream_set: int = 0):
+    def __init__(self, device: torch.device, max_images: int = WAVE_POOL, min_images: int | None = None,
+                 engines: int | None = None, max_image_dim: int = 0, stream_set: int = 0, lanes: bool = False):
         import os
         # measured (scripts/route_study.py, 16 progressive per 256-image batch, dedicated queues,
         # look-ahead 64, profiles/r03_side_pools.jsonl): pools of 16 images on 2 contexts 11.2k img/s,
@@ -177,6 +202,7 @@ class DeviceSideDecoder:
         self.cap = max(1, int(engines))
         self.max_image_dim = int(max_image_dim)
         self.stream_set = int(stream_set)  # the owning pipeline's role streams (pipeline.acquire_stream_set)
+        self.lanes = bool(lanes)           # the side contexts' decoder (side_plan)
         self._engines: list[_SideEngine] = []
         self._rr = 0
         self._pool: list = []   # (job, batch index, JPEG bytes)
@@ -217,7 +243,7 @@ class DeviceSideDecoder:
                 return e
         if len(self._engines) < self.cap:
             e = _SideEngine(self.device, self.max_images, self.max_image_dim, self.cu_count, self.dedicated,
-                            index=len(self._engines), stream_set=self.stream_set)
+                            index=len(self._engines), stream_set=self.stream_set, lanes=self.lanes)
             self._engines.append(e)
             return e
         e = self._engines[self._rr % len(self._engines)]

@@ -296,6 +296,18 @@ int dino_masks_host(int32_t height, int32_t width, int32_t num_masking_patches, 
                     int32_t max_num_patches, double log_aspect_min, double log_aspect_max, int32_t n_masks,
                     uint32_t* py_state, uint32_t* np_state, uint8_t* out);
 
+/* Decoder of this ctx's coefficient-buffer (progressive / multi-scan) images, from the next
+ * call on (round 6): DINO_PROG_WAVE (the default, or DINO_PROG_LANE=1 in the environment at
+ * dino_ctx_create) decodes one scan per wave (k_pscan, ~28 ms per libjpeg-default 640x480
+ * file); DINO_PROG_LANES decodes scan j of 64 images in the lanes of one wave (k_plscan +
+ * k_papply) where the image's scan script allows it (else the wave decoder): lower GPU cost
+ * per image, several times the latency, so it pays for large pools decoded well ahead of
+ * their batches (the side route's look-ahead).  Results are identical.  No reference
+ * counterpart: Pillow decodes one image at a time on a CPU thread (cpu.py:251). */
+#define DINO_PROG_WAVE 0
+#define DINO_PROG_LANES 1
+int dino_ctx_set_prog_decoder(dino_ctx* ctx, int32_t decoder);
+
 /* Per-kernel HIP-event timing of this ctx's launches (bench / profiling).
  * Kernel ids: 0 parse, 1 plan, 2 destuff, 3 huff1, 4 idct, 5 color, 6 params,
  * 7 vplan, 8 rcoeffs, 9 hresize, 10 final(global views), 11 final(local views),

@@ -5,7 +5,7 @@ OUT=gpurun_out/${R6TAG:-r6d}
 mkdir -p $OUT
 run() {  # name, env...
   local name=$1; shift
-  env "$@" DINO_SIDE_TIMING=1 timeout -k 10 240 python -u bench.py --only-leg c2_prog --steps 96 --warmup 5 > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; return 1; }
+  env "$@" DINO_SIDE_TIMING=1 timeout -k 10 240 python -u bench.py --only-leg c2_prog --steps ${STEPS:-96} --warmup 5 > $OUT/$name.json 2> $OUT/$name.err || { echo "$name failed"; tail -5 $OUT/$name.err; return 1; }
   python - "$name" "$OUT/$name.json" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

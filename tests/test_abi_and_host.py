@@ -189,7 +189,7 @@ def test_integration_ctypes_argtypes_match_header_and_binding():
 
 
 def test_backend_side_look_ahead_fits_the_metadata_fifo():
-    """The side route pulls max(PipelineConfig.cpu_queue, 48) batches ahead (DALI's CPU prefetch
+    """The side route pulls max(PipelineConfig.cpu_queue, 256) batches ahead (DALI's CPU prefetch
     queue, reference config.py:166), never more than the source's metadata FIFO holds
     (_ReaderAdapter._meta_queue, 64 slots, shard_reader.py:98, 357-375: an overflow raises)."""
     import queue
@@ -207,11 +207,12 @@ def test_backend_side_look_ahead_fits_the_metadata_fifo():
     # worst case pulled and not handed over: look-ahead + prefetch queue (1 + min(ahead, 4)) +
     # 1 being prepared + the batches in flight; one FIFO entry stays spare
     assert MI355XAugPipeline.pulled_bound(3, 1, 48) == 48 + 5 + 1 + 3
-    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 48
-    assert be.side_look_ahead(PipelineConfig(), object(), 3) == 48
+    assert be.SIDE_AHEAD == 256
+    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7
+    assert be.side_look_ahead(PipelineConfig(), object(), 3) == 256
     assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 7
     assert be.side_look_ahead(PipelineConfig(cpu_queue=60), Src(64), 3) == 64 - 3 - 7
-    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), object(), 3) == 60
+    assert be.side_look_ahead(PipelineConfig(cpu_queue=300), object(), 3) == 300
     assert MI355XBackend(side_ahead=8).side_look_ahead(PipelineConfig(), Src(64), 3) == 8
     assert MI355XBackend(side_ahead=80).side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7
     for cap in (12, 20, 64):
@@ -220,6 +221,33 @@ def test_backend_side_look_ahead_fits_the_metadata_fifo():
                 a = be.side_look_ahead(PipelineConfig(cpu_queue=cq), Src(cap), depth)
                 if a > 1:
                     assert MI355XAugPipeline.pulled_bound(depth, be.PREFETCH, a) + 1 <= cap, (cap, depth, cq)
+
+
+def test_side_plan_follows_the_look_ahead(monkeypatch):
+    """The side decoder runs the lane decoder on pools of 4096 when the look-ahead holds two
+    such pools in flight (>= 128 batches), the wave decoder on pools of 512 otherwise (a source
+    whose metadata FIFO caps the look-ahead); DINO_SIDE_DECODER / DINO_SIDE_MAX override."""
+    from dataloader_amd import progside
+    from dataloader_amd.backend import MI355XBackend
+    from dataloader_amd.config import PipelineConfig
+
+    monkeypatch.delenv("DINO_SIDE_DECODER", raising=False)
+    monkeypatch.delenv("DINO_SIDE_MAX", raising=False)
+    be = MI355XBackend()
+    assert progside.side_plan(be.side_look_ahead(PipelineConfig(), object(), 3)) == (True, 4096)
+
+    class Fifo:
+        def __init__(self):
+            import queue
+            self._meta_queue = queue.Queue(maxsize=64)
+
+    assert progside.side_plan(be.side_look_ahead(PipelineConfig(), Fifo(), 3)) == (False, 512)
+    assert progside.side_plan(127) == (False, 512) and progside.side_plan(128) == (True, 4096)
+    monkeypatch.setenv("DINO_SIDE_DECODER", "wave")
+    assert progside.side_plan(256) == (False, 512)
+    monkeypatch.setenv("DINO_SIDE_DECODER", "lanes")
+    monkeypatch.setenv("DINO_SIDE_MAX", "1024")
+    assert progside.side_plan(8) == (True, 1024)
 
 
 def test_side_look_ahead_engages_only_with_coefficient_buffer_images():

@@ -335,11 +335,15 @@ def test_output_views_reused_only_after_the_caller_drops_them(gpu_device):
             assert torch.equal(a[k], b[k]), k
 
 
-def test_side_route_matches_in_batch_device_route(gpu_device):
+@pytest.mark.parametrize("side_decoder", ["wave", "lanes"])
+def test_side_route_matches_in_batch_device_route(gpu_device, side_decoder, monkeypatch):
     """multiscan_route="side": progressive / multi-scan images decoded on the device ahead of
     their batch (progside.py) give every view bit-identical to the in-batch k_prog route
     ("device"), with a CMYK file (Pillow hand-over) and a cut progressive file (undecodable:
-    it stays in its batch and comes back zero-filled, as the reference's) in the mix."""
+    it stays in its batch and comes back zero-filled, as the reference's) in the mix.  The side
+    contexts run either decoder (round 6: the lane decoder is the side plan's choice at the
+    default look-ahead; the in-batch route keeps the wave decoder)."""
+    monkeypatch.setenv("DINO_SIDE_DECODER", side_decoder)
     from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
     rng = np.random.default_rng(57)
     uniq = [encode_jpeg(textured_rgb(240 + 8 * s, 180 + 4 * s, rng)) for s in range(5)]
@@ -366,6 +370,7 @@ def test_side_route_matches_in_batch_device_route(gpu_device):
 
     (ref, st0), (got, st1) = run("device"), run("side")
     assert len(ref) == len(got) == nb
+    assert st1.get("side_lanes") == (side_decoder == "lanes"), st1
     assert st1["side_decoded"] == nb + 3 and st0["side_decoded"] == 0, (st0, st1)  # the cut file fails on the side too
     assert st0["status"] == st1["status"] and st0["host_decoded"] == st1["host_decoded"] == 1
     for k, (a, b) in enumerate(zip(ref, got)):

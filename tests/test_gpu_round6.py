@@ -232,6 +232,9 @@ def test_dropin_side_route_b512_from_a_host_source(gpu_device, fp8):
         st = pipe.flush_stats()
         assert st["side_decoded"] >= (k_check + 1) * (B // 16) and st["host_decoded"] == 0
         assert set(st["status"]) == {0}
+        # the default look-ahead (256 batches, a source without a metadata FIFO) puts the side
+        # contexts on the lane decoder (progside.side_plan)
+        assert pipe._side_ahead == 256 and st["side_lanes"] is True
     finally:
         pipe.close()
 
