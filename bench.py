@@ -735,7 +735,8 @@ def _side_stats(pipe) -> dict | None:
     sd = getattr(pipe, "_side", None)
     if sd is None:
         return None
-    out = {"launches": sd.launches, "images": sd.images, "urgent_flushes": pipe.stats.get("side_urgent", 0),
+    out = {"launches": sd.launches, "lane_launches": sd.lane_launches, "images": sd.images,
+           "urgent_flushes": pipe.stats.get("side_urgent", 0),
            "launcher_s": {k: round(v, 3) for k, v in sd.phase_seconds.items()},
            "per_batch_ms": {k: round(v * 1e3 / max(1, sd.lead["jobs"]), 2) for k, v in sd.lead.items() if k != "jobs"}}
     if sd.timing:

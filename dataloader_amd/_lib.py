@@ -81,6 +81,7 @@ def load() -> ctypes.CDLL:
         "dino_stream_create": (i32, [i32, i32, ctypes.POINTER(vp)]),
         "dino_stream_destroy": (i32, [vp]),
         "dino_copy_rgb": (i32, [vp, i32, vp, vp]),
+        "dino_copy_rgb_packed": (i32, [vp, i32, vp, vp, vp, vp]),
         "dino_pixel_ops_all": (i32, [i32, i32, vp, vp]),
         "dino_sample_params": (i32, [vp, ctypes.POINTER(DinoAugConfig), u64, u64, vp, vp]),
         "dino_augment": (i32, [vp, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(vp), vp]),
@@ -124,7 +125,7 @@ def exported_symbols() -> list[str]:
     return ["dino_abi_version", "dino_last_error", "dino_ctx_create", "dino_ctx_destroy", "dino_decode",
             "dino_copy_rgb", "dino_pixel_ops_all", "dino_sample_params", "dino_augment", "dino_run_batch", "dino_masks",
             "dino_bf16_to_fp8", "dino_debug_region", "dino_set_timing", "dino_kernel_times",
-            "dino_ctx_set_prog_decoder", "dino_tar_index", "dino_tar_index_fd", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
+            "dino_ctx_set_prog_decoder", "dino_copy_rgb_packed", "dino_tar_index", "dino_tar_index_fd", "dino_tar_last_error", "dino_gather", "dino_set_norm", "dino_batch_info",
             "dino_probe", "dino_reserve", "dino_workspace_sizes", "dino_masks_host", "dino_resize_batch",
             "dino_augment_need", "dino_decode_spans", "dino_run_batch_spans", "dino_probe_spans",
             "dino_host_register", "dino_host_unregister", "dino_copy_h2d", "dino_gather_probe",

@@ -165,6 +165,16 @@ int dino_copy_rgb(dino_ctx* c, int32_t index, uint8_t* d_rgb, void* stream) {
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_copy_rgb");
 }
 
+int dino_copy_rgb_packed(dino_ctx* c, int32_t n, const int32_t* d_index, const int64_t* d_offset, uint8_t* d_base,
+                         void* stream) {
+  if (!c || n < 0 || (n > 0 && (!d_index || !d_offset || !d_base)))
+    return fail(DINO_EINVAL, "dino_copy_rgb_packed: bad arguments%s%lld");
+  if (n > 65535) return fail(DINO_EINVAL, "dino_copy_rgb_packed: n %s%lld > 65535", "", (long long)n);
+  hipError_t e = launch_copy_rgb_packed(c->d_desc, c->last_batch, n, d_index, d_offset, c->d_ws, d_base,
+                                        (hipStream_t)stream);
+  return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_copy_rgb_packed");
+}
+
 int dino_pixel_ops_all(int32_t op, int32_t param, uint8_t* d_out, void* stream) {
   if (!d_out || op < 0 || op > 2) return fail(DINO_EINVAL, "dino_pixel_ops_all: bad args%s%lld");
   hipError_t e = launch_pixel_ops(op, param & 255, d_out, (hipStream_t)stream);

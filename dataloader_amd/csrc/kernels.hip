@@ -4032,6 +4032,30 @@ __global__ void k_copy_rgb(const ImgDesc* __restrict__ desc, int idx, const uint
     dst[i] = ws[d.rgb_off + i];
 }
 
+// Decoded images -> slices of one buffer (the side decoder's raw containers): image idx[k]'s
+// RGB to base + off[k], grid (x, n).  16-byte copies when source and destination are both
+// 16-byte aligned (the workspace's RGB areas are; the containers' data starts 16 bytes into a
+// 16-byte aligned slice), the tail and unaligned cases bytewise.
+__global__ void k_copy_rgb_packed(const ImgDesc* __restrict__ desc, int B, const int32_t* __restrict__ idx,
+                                  const int64_t* __restrict__ off, const uint8_t* __restrict__ ws,
+                                  uint8_t* __restrict__ base) {
+  const int k = blockIdx.y, i = idx[k];
+  if (i < 0 || i >= B) return;
+  const ImgDesc& d = desc[i];
+  if (d.status != DINO_IMG_OK) return;
+  const int64_t n = (int64_t)d.width * d.height * 3;
+  const uint8_t* src = ws + d.rgb_off;
+  uint8_t* dst = base + off[k];
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, ts = (int64_t)gridDim.x * blockDim.x;
+  int64_t head = 0;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const int64_t n16 = n >> 4;
+    for (int64_t q = t0; q < n16; q += ts) ((uint4*)dst)[q] = ((const uint4*)src)[q];
+    head = n16 << 4;
+  }
+  for (int64_t q = head + t0; q < n; q += ts) dst[q] = src[q];
+}
+
 __global__ void k_info(const ImgDesc* __restrict__ desc, int B, int32_t* __restrict__ info) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= B) return;
@@ -4298,6 +4322,13 @@ hipError_t launch_pixel_ops(int op, int param, uint8_t* out, hipStream_t s) {
 
 hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s) {
   k_copy_rgb<<<256, 256, 0, s>>>(desc, idx, ws, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_rgb_packed(const ImgDesc* desc, int B, int n, const int32_t* idx, const int64_t* off,
+                                  const uint8_t* ws, uint8_t* base, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  k_copy_rgb_packed<<<dim3(16, n), 256, 0, s>>>(desc, B, idx, off, ws, base);
   return hipGetLastError();
 }
 

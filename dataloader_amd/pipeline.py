@@ -372,6 +372,9 @@ class _Prefetcher:
         self._thread.join(timeout=5.0)
 
 
+SIDE_URGENT_SHORT = 8  # side look-ahead batches flushed at once while the look-ahead is short (_pull_side)
+
+
 class MI355XAugPipeline:
     """``depth`` > 1 keeps that many batches in flight: each slot owns a ctx and a
     HIP stream, consecutive batches alternate slots, so one batch's entropy
@@ -870,8 +873,14 @@ class MI355XAugPipeline:
                 raise StopIteration
             # the pool launches when it holds min_images, or once its oldest batch is within
             # half the look-ahead of its own launch (a decode then has those batches' time to
-            # finish; flushing at launch would make the batch wait for it)
-            urgent = min(len(self._ahead), max(1, self._side_ahead // 2))
+            # finish; flushing at launch would make the batch wait for it).  With the lane plan,
+            # while the look-ahead is shorter than that (the host half fell behind), only the next SIDE_URGENT_SHORT
+            # batches are urgent: flushing every batch as it arrived made pools of one batch's
+            # images, whose launches starved the batches and kept the look-ahead short (c2_prog
+            # 50-78k img/s in that state, profiles/r06_side_plan/r6q)
+            half = max(1, self._side_ahead // 2)
+            short = self._side is not None and self._side.lanes and len(self._ahead) <= half
+            urgent = min(len(self._ahead), SIDE_URGENT_SHORT if short else half)
             if self._side is not None and any(pb.side is not None and pb.side.pending
                                               for pb in itertools.islice(self._ahead, urgent)):
                 self._side.flush()

@@ -32,7 +32,8 @@ import numpy as np
 import torch
 
 from . import _lib, fallback
-from .engine import IngestEngine, pack_jpegs
+from .engine import IngestEngine
+from .tario import gather
 
 
 class SideJob:
@@ -133,6 +134,7 @@ class _SideEngine:
         self.copy = role_stream(device, "side_copy", index, stream_set)  # this context's torch stream (allocations, copies)
         self.last: torch.cuda.Event | None = None   # the engine's workspace is free once this completes
         self.keep = None                             # host / device inputs of the mini-batch in flight
+        self.hbuf: torch.Tensor | None = None        # pinned pack buffer, reused once `last` completes
 
     def idle(self) -> bool:
         return self.last is None or self.last.query()
@@ -161,6 +163,11 @@ class _SideEngine:
 LANES_MIN_AHEAD = 128
 LANE_POOL = 4096
 WAVE_POOL = 512
+# A pool flushed before it filled (the look-ahead ran short: the host half fell behind the
+# batches) goes to the wave decoder when it is smaller than this: a lane-decoder launch takes
+# ~120 ms even for a few images, and small lane pools launched back to back starved the
+# batches (c2_prog 50k img/s with pools of 32-500 images, profiles/r06_side_plan/r6n).
+LANE_MIN_POOL = 1024
 
 
 def side_plan(side_ahead: int) -> tuple[bool, int]:
@@ -203,10 +210,12 @@ class DeviceSideDecoder:
         self.max_image_dim = int(max_image_dim)
         self.stream_set = int(stream_set)  # the owning pipeline's role streams (pipeline.acquire_stream_set)
         self.lanes = bool(lanes)           # the side contexts' decoder (side_plan)
+        self.lane_min = int(os.environ.get("DINO_SIDE_LANE_MIN", LANE_MIN_POOL))  # smaller pools: wave decoder
         self._engines: list[_SideEngine] = []
         self._rr = 0
         self._pool: list = []   # (job, batch index, JPEG bytes)
         self.launches = 0
+        self.lane_launches = 0  # launches the lane decoder took (the rest: the wave decoder)
         self.images = 0
         self.host_seconds = 0.0   # spent in _launch (pack, probe, launches; waits for a free context)
         self.phase_seconds = {"engine": 0.0, "pack": 0.0, "probe": 0.0, "decode": 0.0, "containers": 0.0}
@@ -279,8 +288,20 @@ class DeviceSideDecoder:
         t1 = time.perf_counter()
         ph["engine"] += t1 - t_start
         eng = se.eng
+        lanes = self.lanes and len(part) >= self.lane_min
+        if eng.prog_lanes != lanes:
+            eng.set_prog_decoder(lanes)
+        self.lane_launches += int(lanes)
         items = [j for _, _, j in part]
-        hb, off = pack_jpegs(items, pin=True)
+        # the pool's bytes go into this context's own pinned buffer (reused: the context is idle,
+        # so its last upload has completed) by the native gather's threads (no GIL): a fresh
+        # pinned buffer per pool (pack_jpegs) cost a pinned allocation of the pool's size
+        # (~350 MB for 4096 C2 images) and a Python-loop copy on this thread
+        total = sum(len(j) for j in items)
+        if se.hbuf is None or se.hbuf.numel() < total + 16:
+            se.hbuf = torch.empty(total * 5 // 4 + 4096, dtype=torch.uint8, pin_memory=True)
+        hb = se.hbuf
+        off = torch.from_numpy(gather(items, hb, 4))
         t2 = time.perf_counter()
         ph["pack"] += t2 - t1
         info, ws, _ = fallback.probe(hb.data_ptr(), off.numpy(), len(items), self.max_image_dim)
@@ -299,13 +320,13 @@ class DeviceSideDecoder:
             if self.timing:
                 t0 = torch.cuda.Event(enable_timing=True)
                 t0.record(es)
-            d_bytes = hb.to(self.device, non_blocking=True)
+            d_bytes = hb[:max(total, 1) + 16].to(self.device, non_blocking=True)
             d_off = off.to(self.device, non_blocking=True)
             d_info = torch.empty((len(items), 4), dtype=torch.int32, device=self.device)
             # every decoded image's container is a 16-byte aligned slice of one device buffer;
             # the headers go over in one copy and one scatter (per-image pinned headers and
             # copies cost the launch thread ~10 us each)
-            big = None
+            big = d_idx = d_dst = None
             if keep:
                 start = np.zeros(len(keep) + 1, np.int64)
                 start[1:] = np.cumsum([(16 + w * h * 3 + 15) & ~15 for _, _, _, w, h in keep])
@@ -316,8 +337,14 @@ class DeviceSideDecoder:
                 hdr[:, 2] = [h for _, _, _, _, h in keep]
                 h_hdr = torch.from_numpy(hdr.view(np.uint8).reshape(-1)).pin_memory()
                 h_pos = torch.from_numpy((start[:-1, None] + np.arange(16)).reshape(-1)).pin_memory()
-                heads.extend((h_hdr, h_pos))
+                # the pixel copies: one dino_copy_rgb_packed launch for the pool (mini-batch row k
+                # -> its container's data, 16 bytes past the header)
+                h_idx = torch.from_numpy(np.array([k for k, _, _, _, _ in keep], np.int32)).pin_memory()
+                h_dst = torch.from_numpy(start[:-1] + 16).pin_memory()
+                heads.extend((h_hdr, h_pos, h_idx, h_dst))
                 big[h_pos.to(self.device, non_blocking=True)] = h_hdr.to(self.device, non_blocking=True)
+                d_idx = h_idx.to(self.device, non_blocking=True)
+                d_dst = h_dst.to(self.device, non_blocking=True)
             # the library's kernels on the dedicated stream, after the inputs (and after any
             # earlier use of the memory the allocator just handed out, on this torch stream)
             ready = torch.cuda.Event()
@@ -326,10 +353,13 @@ class DeviceSideDecoder:
             eng.decode(d_bytes, d_off, len(items), info=d_info)
             t4 = time.perf_counter()
             ph["decode"] += t4 - t3
+            if keep:
+                _lib.check(eng.lib.dino_copy_rgb_packed(eng._ctx, len(keep), ctypes.c_void_p(d_idx.data_ptr()),
+                                                        ctypes.c_void_p(d_dst.data_ptr()),
+                                                        ctypes.c_void_p(big.data_ptr()), eng._s()),
+                           "dino_copy_rgb_packed")
             for (k, job, i, w, h), o in zip(keep, start[:-1] if keep else []):
                 o = int(o)
-                _lib.check(eng.lib.dino_copy_rgb(eng._ctx, k, ctypes.c_void_p(big.data_ptr() + o + 16), eng._s()),
-                           "dino_copy_rgb")
                 job.containers[i] = big[o:o + 16 + w * h * 3]
             # the status copy and the completion event on the decode's own stream: a torch stream
             # made to wait for the decode would hold its hardware queue (shared with other
@@ -348,7 +378,7 @@ class DeviceSideDecoder:
         for job, _, _ in part:
             job.event, job.status, job.t_launch = ev, status, t_end
         se.last = ev
-        se.keep = (hb, off, d_bytes, d_off, heads, d_info, big)
+        se.keep = (hb, off, d_bytes, d_off, heads, d_info, big, d_idx, d_dst)
         self.launches += 1
         self.images += len(part)
         self.host_seconds += time.perf_counter() - t_start

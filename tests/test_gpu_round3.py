@@ -344,6 +344,7 @@ def test_side_route_matches_in_batch_device_route(gpu_device, side_decoder, monk
     contexts run either decoder (round 6: the lane decoder is the side plan's choice at the
     default look-ahead; the in-batch route keeps the wave decoder)."""
     monkeypatch.setenv("DINO_SIDE_DECODER", side_decoder)
+    monkeypatch.setenv("DINO_SIDE_LANE_MIN", "1")  # this test's pools are a few images
     from dataloader_amd.pipeline import MI355XAugPipeline, MI355XPipelineIterator
     rng = np.random.default_rng(57)
     uniq = [encode_jpeg(textured_rgb(240 + 8 * s, 180 + 4 * s, rng)) for s in range(5)]
@@ -359,18 +360,23 @@ def test_side_route_matches_in_batch_device_route(gpu_device, side_decoder, monk
     batches[5][6] = cut
     cfg = DINOAugConfig(global_crop_size=96, local_crop_size=48)
 
+    side_lane_launches = [0]
+
     def run(route):
         src = _ListSource(batches)
         pipe = MI355XAugPipeline(src, cfg, B, seed=9, depth=3, multiscan_route=route, host_workers=2, side_ahead=4)
         it = MI355XPipelineIterator(pipe, [f"view_{i}" for i in range(cfg.n_views)], B)
         outs = _collect(it)
         st = pipe.flush_stats()
+        if pipe._side is not None:
+            side_lane_launches[0] = pipe._side.lane_launches
         pipe.close()
         return outs, st
 
     (ref, st0), (got, st1) = run("device"), run("side")
     assert len(ref) == len(got) == nb
     assert st1.get("side_lanes") == (side_decoder == "lanes"), st1
+    assert (side_lane_launches[0] > 0) == (side_decoder == "lanes")
     assert st1["side_decoded"] == nb + 3 and st0["side_decoded"] == 0, (st0, st1)  # the cut file fails on the side too
     assert st0["status"] == st1["status"] and st0["host_decoded"] == st1["host_decoded"] == 1
     for k, (a, b) in enumerate(zip(ref, got)):

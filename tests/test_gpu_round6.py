@@ -32,17 +32,11 @@ def _wave_cases(rng):
 
 
 def _engine(dev, n: int, lane: bool) -> IngestEngine:
-    """An engine whose progressive images take the lane decoder (DINO_PROG_LANE=1, read when
-    the context is created) or the wave decoder."""
-    old = os.environ.get("DINO_PROG_LANE")
-    os.environ["DINO_PROG_LANE"] = "1" if lane else "0"
-    try:
-        return IngestEngine(dev, max_batch=n, max_views=1, max_crop_size=8)
-    finally:
-        if old is None:
-            os.environ.pop("DINO_PROG_LANE")
-        else:
-            os.environ["DINO_PROG_LANE"] = old
+    """An engine whose progressive images take the lane decoder or the wave decoder
+    (dino_ctx_set_prog_decoder)."""
+    eng = IngestEngine(dev, max_batch=n, max_views=1, max_crop_size=8)
+    eng.set_prog_decoder(lane)
+    return eng
 
 
 def _decode(dev, jpegs, lane: bool):
@@ -61,6 +55,29 @@ def _decode(dev, jpegs, lane: bool):
         else:
             flags.append(-1)
     rgb = [eng.copy_rgb(i, int(info[i, 1]), int(info[i, 2])).cpu().numpy() for i in range(len(jpegs))]
+    # dino_copy_rgb_packed (the side decoder's containers): every image, in reverse order, into
+    # one buffer at odd and 16-byte aligned offsets, gaps left untouched
+    import ctypes
+    sizes = [int(info[i, 1]) * int(info[i, 2]) * 3 for i in range(len(jpegs))]
+    order = list(range(len(jpegs)))[::-1]
+    offs, pos = [], 0
+    for k, i in enumerate(order):
+        pos += 16 + (k & 1)
+        offs.append(pos)
+        pos += sizes[i]
+    big = torch.full((pos + 16,), 0xA5, dtype=torch.uint8, device=dev)
+    d_idx = torch.tensor(order, dtype=torch.int32, device=dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    assert eng.lib.dino_copy_rgb_packed(eng._ctx, len(order), ctypes.c_void_p(d_idx.data_ptr()),
+                                        ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(big.data_ptr()),
+                                        eng._s()) == 0
+    torch.cuda.synchronize()
+    hb_big = big.cpu().numpy()
+    for k, i in enumerate(order):
+        if st[i, 0] == 0:  # (an image that did not decode is skipped)
+            assert np.array_equal(hb_big[offs[k]:offs[k] + sizes[i]], rgb[i].reshape(-1)), i
+        assert (hb_big[offs[k] - 16 - (k & 1):offs[k]] == 0xA5).all(), i
     eng.close()
     return st, flags, rgb
 
@@ -234,7 +251,7 @@ def test_dropin_side_route_b512_from_a_host_source(gpu_device, fp8):
         assert set(st["status"]) == {0}
         # the default look-ahead (256 batches, a source without a metadata FIFO) puts the side
         # contexts on the lane decoder (progside.side_plan)
-        assert pipe._side_ahead == 256 and st["side_lanes"] is True
+        assert pipe._side_ahead == 256 and st["side_lanes"] is True and pipe._side.lane_launches > 0
     finally:
         pipe.close()
 
