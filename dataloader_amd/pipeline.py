@@ -340,6 +340,7 @@ class _Prefetcher:
         try:
             while not self._stop.is_set():
                 pb = self._pipe._prepare_next()
+                self._pipe._stage_early(pb)
                 if not self._put(pb):
                     self._pipe._drop(pb)
                     return
@@ -781,6 +782,19 @@ class MI355XAugPipeline:
             hb, o = pb.staging.buf.numpy(), pb.offsets
             imgs = {int(i): hb[o[i]:o[i + 1]].tobytes() for i in idx}
         pb.side = self._side.add(imgs)
+
+    def _stage_early(self, pb: _Prepared) -> None:
+        """On the prefetch thread: a batch bound for the side look-ahead (the route is engaged,
+        or the batch carries coefficient-buffer images) goes to HBM right after its pack, so
+        its staging buffer returns to the ring when the copy retires instead of when the
+        launch thread pulls the batch (the prefetch thread waited ~1-2 ms per batch for a free
+        staging buffer, c2_prog).  Only batches whose images the source handed over as a list
+        (``pb.jpegs``, what the side decoder reads them from later)."""
+        if not self._side_ahead or pb.jpegs is None or pb.futures or pb.dev is not None:
+            return
+        from . import progside
+        if self._side_hot > 0 or progside.side_mask(pb.info).any():
+            self._stage_on_device(pb)
 
     def _stage_on_device(self, pb: _Prepared) -> None:
         """Copy a batch that joins the side look-ahead to HBM now, on the copy stream, and free
