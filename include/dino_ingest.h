@@ -42,7 +42,10 @@
  *    host gather; dino_host_register / dino_host_unregister / dino_copy_h2d to page-lock
  *    those mappings and DMA from them; dino_gather_probe (pack + probe in one threaded
  *    pass); the native shard feed dino_feed_* (the host half of a batch off the Python
- *    interpreter).
+ *    interpreter).  Round 6, still additive within ABI 4: dino_tar_index_fd (header-only
+ *    tar index over a file descriptor), dino_ctx_set_prog_decoder (wave / lane decoder of
+ *    progressive images per context), dino_copy_rgb_packed (a pool's images into one
+ *    buffer in one launch).
  */
 #ifndef DINO_INGEST_H
 #define DINO_INGEST_H
