@@ -10,7 +10,10 @@ namespace dino {
 constexpr int kHuffThreads = 256;
 // Bits of entropy-coded stream per Huffman work item (kHuffThreads lanes); an image
 // larger than this is decoded by several workgroups (k_huff1 / k_huff3).
-constexpr int64_t kHuffSegBits = (int64_t)2048 * 1024;
+#ifndef DINO_HUFF_SEG_KBITS
+#define DINO_HUFF_SEG_KBITS 2048
+#endif
+constexpr int64_t kHuffSegBits = (int64_t)DINO_HUFF_SEG_KBITS * 1024;
 
 // LDS of k_hresize: taps (when they fit in kHresizeTapLds) + planar rows of one band.
 constexpr int kHresizeLds = 26 * 1024;
