@@ -312,34 +312,75 @@ def release_role_streams() -> None:
         pass
 
 
+RAW_AHEAD = 2  # pulled, not yet packed batches the prefetcher's puller thread holds (list sources)
+
+
 class _Prefetcher:
-    """The host half of the pipeline on a worker thread (DALI's prefetch queue, reference
+    """The host half of the pipeline on worker threads (DALI's prefetch queue, reference
     pipeline.py:317 ``prefetch_queue_depth``): pull the next batch from the source, pack it
     into pinned staging (``dino_gather``), ``dino_probe`` it and submit its Pillow
     hand-overs, up to ``ahead`` batches ahead of the launches.  The GIL is released inside
-    the native calls, so this overlaps the launch thread and the GPU."""
+    the native calls, so this overlaps the launch thread and the GPU.  For a source that
+    hands over JPEG lists (the reference's ``_ReaderAdapter``) the pull runs on a thread of
+    its own, up to ``RAW_AHEAD`` batches ahead of the pack: the source's Python call and the
+    native pack overlap instead of adding up (c2_prog: ~0.8 + 1.2-3 ms per batch)."""
 
     def __init__(self, pipe: "MI355XAugPipeline", ahead: int):
         self._pipe = pipe
         self._q: queue.Queue = queue.Queue(maxsize=max(1, ahead))
         self._stop = threading.Event()
         self.finished = False       # the source raised StopIteration (the END marker is queued)
+        self._raw: queue.Queue | None = None
+        self._puller = None
+        if not pipe._spans_feed and not pipe._native:
+            self._raw = queue.Queue(maxsize=RAW_AHEAD)
+            self._puller = threading.Thread(target=self._pull_loop, name="dino-pull", daemon=True)
+            self._puller.start()
         self._thread = threading.Thread(target=self._run, name="dino-prefetch", daemon=True)
         self._thread.start()
 
-    def _put(self, item) -> bool:
+    def _put(self, item, q: queue.Queue | None = None) -> bool:
+        q = self._q if q is None else q
         while not self._stop.is_set():
             try:
-                self._q.put(item, timeout=0.1)
+                q.put(item, timeout=0.1)
                 return True
             except queue.Full:
                 continue
         return False
 
+    def _pull_loop(self) -> None:
+        try:
+            while not self._stop.is_set():
+                if not self._put(self._pipe._pull_raw(), self._raw):
+                    return
+        except StopIteration:
+            self._put(_END, self._raw)
+        except BaseException as e:  # noqa: BLE001 - handed to the pack thread, then the launch thread
+            self._put(e, self._raw)
+
+    def _next(self) -> _Prepared | None:
+        """The next prepared batch (None once stopped); StopIteration at the source's end."""
+        if self._raw is None:
+            return self._pipe._prepare_next()
+        while not self._stop.is_set():
+            try:
+                item = self._raw.get(timeout=0.1)
+            except queue.Empty:
+                continue
+            if item is _END:
+                raise StopIteration
+            if isinstance(item, BaseException):
+                raise item
+            return self._pipe._pack_raw(item)
+        return None
+
     def _run(self) -> None:
         try:
             while not self._stop.is_set():
-                pb = self._pipe._prepare_next()
+                pb = self._next()
+                if pb is None:
+                    return
                 self._pipe._stage_early(pb)
                 if not self._put(pb):
                     self._pipe._drop(pb)
@@ -363,14 +404,17 @@ class _Prefetcher:
 
     def close(self) -> None:
         self._stop.set()
-        while True:  # unblock a pending put, free staging of batches never launched
-            try:
-                item = self._q.get_nowait()
-            except queue.Empty:
-                break
-            if isinstance(item, _Prepared):
-                self._pipe._drop(item)
+        for q in (self._q, self._raw):  # unblock pending puts, free staging of batches never launched
+            while q is not None:
+                try:
+                    item = q.get_nowait()
+                except queue.Empty:
+                    break
+                if isinstance(item, _Prepared):
+                    self._pipe._drop(item)
         self._thread.join(timeout=5.0)
+        if self._puller is not None:
+            self._puller.join(timeout=5.0)
 
 
 SIDE_URGENT_SHORT = 8  # side look-ahead batches flushed at once while the look-ahead is short (_pull_side)
@@ -499,11 +543,11 @@ class MI355XAugPipeline:
     @staticmethod
     def pulled_bound(depth: int, prefetch_ahead: int, side_ahead: int) -> int:
         """Most batches pulled from the source and not yet handed over, on the side route: the
-        look-ahead, the prefetch queue, one being prepared on the prefetch thread and the
-        batches in flight.  A source whose metadata FIFO pairs each pulled batch with its
+        look-ahead, the prefetch queue, one being packed on the prefetch thread, the puller's
+        queue and the batch it holds, and the batches in flight.  A source whose metadata FIFO pairs each pulled batch with its
         hand-over (reference _ReaderAdapter._meta_queue, shard_reader.py:98, 357-375) must
         hold this many."""
-        return side_ahead + MI355XAugPipeline.side_queue(prefetch_ahead, side_ahead) + 1 + depth
+        return side_ahead + MI355XAugPipeline.side_queue(prefetch_ahead, side_ahead) + 1 + RAW_AHEAD + 1 + depth
 
     @property
     def engine(self) -> IngestEngine:
@@ -640,12 +684,16 @@ class MI355XAugPipeline:
         routed to the host (``fallback.route_mask``).  A page-locked spans feed batch that
         needs no hand-over is not packed at all (its shard ranges are DMA'd at launch).
         Runs on the prefetch thread (or inline at prefetch 0)."""
+        return self._pack_raw(self._pull_raw())
+
+    def _pull_raw(self) -> tuple:
+        """The pull half of ``_prepare_next``: the source's next batch as (spans batch or None,
+        JPEG list or None, pointers, lengths, references keeping the bytes alive)."""
         from .tario import spans_of
-        B = self._batch_size
-        hs = self.host_seconds
         t0 = time.perf_counter()
         bs = None
         jpegs = None
+        keep = None
         if self._spans_feed:
             bs = self._source.next_batch_spans()  # may raise StopIteration (end of epoch)
             ptrs, lens = bs.ptrs, bs.lens
@@ -653,7 +701,15 @@ class MI355XAugPipeline:
             ptrs, lens, _ = spans_of(self._source.next_spans())  # may raise StopIteration
         else:
             jpegs = self._source()  # may raise StopIteration (end of epoch)
-            ptrs, lens, _keep = spans_of(jpegs)
+            ptrs, lens, keep = spans_of(jpegs)
+        self.host_seconds["pull"] += time.perf_counter() - t0
+        return bs, jpegs, ptrs, lens, keep
+
+    def _pack_raw(self, raw: tuple) -> _Prepared:
+        """The pack half of ``_prepare_next`` (see there)."""
+        bs, jpegs, ptrs, lens, _keep = raw
+        B = self._batch_size
+        hs = self.host_seconds
         try:
             if len(lens) != B:
                 raise ValueError(f"source returned {len(lens)} samples, expected {B}")
@@ -667,7 +723,6 @@ class MI355XAugPipeline:
                     st.fit(0, B)
                     st.off.numpy()[: B + 1] = bs.offsets
                     st.lens.numpy()[:B] = lens
-                    hs["pull"] += t1 - t0
                     hs["probe"] += time.perf_counter() - t1
                     return _Prepared(st, None, bs.offsets, info, ws, aws, sizes, {}, spans=bs)
             st = self._ring.acquire()
@@ -677,9 +732,7 @@ class MI355XAugPipeline:
                 off, info, ws, aws = fallback.gather_probe(ptrs, lens, st.buf, self._gather_threads,
                                                            self._max_image_dim, cfg)
                 st.off.numpy()[: B + 1] = off
-                t2 = time.perf_counter()
-                hs["pull"] += t1 - t0
-                hs["pack"] += t2 - t1
+                hs["pack"] += time.perf_counter() - t1
                 if bs is not None:  # packed: the shard ranges are no longer read
                     self._source.retire(bs, None)
                     bs = None
