@@ -151,7 +151,8 @@ class MI355XBackend:
         shard_reader.py:98, 357-375: an overflow raises).  The look-ahead's batches wait in HBM
         (MI355XAugPipeline._stage_on_device): 256 C2 batches take ~11 GB of the 288."""
         want = self._side_ahead if self._side_ahead is not None else \
-            max(int(os.environ.get("DINO_SIDE_AHEAD", self.SIDE_AHEAD)), int(getattr(pipeline_cfg, "cpu_queue", 16) or 16))
+            max(int(os.environ.get("DINO_SIDE_AHEAD", self.SIDE_AHEAD)),
+                int(getattr(pipeline_cfg, "cpu_queue", 16) or 16))
         mq = getattr(source, "_meta_queue", None)
         cap = getattr(mq, "maxsize", 0) or 0
         if cap > 0:

@@ -544,9 +544,9 @@ class MI355XAugPipeline:
     def pulled_bound(depth: int, prefetch_ahead: int, side_ahead: int) -> int:
         """Most batches pulled from the source and not yet handed over, on the side route: the
         look-ahead, the prefetch queue, one being packed on the prefetch thread, the puller's
-        queue and the batch it holds, and the batches in flight.  A source whose metadata FIFO pairs each pulled batch with its
-        hand-over (reference _ReaderAdapter._meta_queue, shard_reader.py:98, 357-375) must
-        hold this many."""
+        queue and the batch it holds, and the batches in flight.  A source whose metadata FIFO
+        pairs each pulled batch with its hand-over (reference _ReaderAdapter._meta_queue,
+        shard_reader.py:98, 357-375) must hold this many."""
         return side_ahead + MI355XAugPipeline.side_queue(prefetch_ahead, side_ahead) + 1 + RAW_AHEAD + 1 + depth
 
     @property
@@ -940,11 +940,11 @@ class MI355XAugPipeline:
                 raise StopIteration
             # the pool launches when it holds min_images, or once its oldest batch is within
             # half the look-ahead of its own launch (a decode then has those batches' time to
-            # finish; flushing at launch would make the batch wait for it).  With the lane plan,
-            # while the look-ahead is shorter than that (the host half fell behind), only the next SIDE_URGENT_SHORT
-            # batches are urgent: flushing every batch as it arrived made pools of one batch's
-            # images, whose launches starved the batches and kept the look-ahead short (c2_prog
-            # 50-78k img/s in that state, profiles/r06_side_plan/r6q)
+            # finish; flushing at launch would make the batch wait for it).  With the lane
+            # plan, while the look-ahead is shorter than that (the host half fell behind), only
+            # the next SIDE_URGENT_SHORT batches are urgent: flushing every batch as it arrived
+            # made pools of one batch's images, whose launches starved the batches and kept the
+            # look-ahead short (c2_prog 50-78k img/s in that state, profiles/r06_side_plan/r6q)
             half = max(1, self._side_ahead // 2)
             short = self._side is not None and self._side.lanes and len(self._ahead) <= half
             urgent = min(len(self._ahead), SIDE_URGENT_SHORT if short else half)
