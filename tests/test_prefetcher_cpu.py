@@ -1,0 +1,110 @@
+"""The pipeline's host-half prefetcher (pipeline._Prefetcher) on CPU: with a list source its
+pull runs on a thread of its own ahead of the pack (round 6); batches still come out in the
+source's order, the source's end and its errors reach the launch thread in place, and close()
+frees every prepared batch that was never handed out."""
+
+from __future__ import annotations
+
+import threading
+import time
+
+import pytest
+
+from dataloader_amd import pipeline as P
+
+
+class _FakePipe:
+    """What _Prefetcher calls on its pipeline: _pull_raw, _pack_raw, _stage_early, _drop."""
+
+    def __init__(self, n: int, fail_at: int | None = None, spans: bool = False):
+        self._spans_feed = spans
+        self._native = False
+        self.n, self.fail_at = n, fail_at
+        self.k = 0
+        self.pull_threads, self.pack_threads = set(), set()
+        self.dropped, self.staged = [], []
+        self.lock = threading.Lock()
+
+    def _pull_raw(self):
+        self.pull_threads.add(threading.current_thread().name)
+        if self.k == self.fail_at:
+            self.k += 1
+            raise ValueError("source broke")
+        if self.k >= self.n:
+            raise StopIteration
+        k, self.k = self.k, self.k + 1
+        time.sleep(0.001)
+        return k
+
+    def _pack_raw(self, raw):
+        self.pack_threads.add(threading.current_thread().name)
+        time.sleep(0.002)
+        pb = P._Prepared(None, None, None, None, 0, 0, (0, 0), {})
+        pb.k = raw
+        return pb
+
+    def _prepare_next(self):
+        return self._pack_raw(self._pull_raw())
+
+    def _stage_early(self, pb):
+        with self.lock:
+            self.staged.append(pb.k)
+
+    def _drop(self, pb):
+        with self.lock:
+            self.dropped.append(pb.k)
+
+
+def _drain(pf):
+    got = []
+    while True:
+        try:
+            got.append(pf.get().k)
+        except StopIteration:
+            return got
+
+
+def test_list_source_pull_runs_on_its_own_thread_in_order():
+    pipe = _FakePipe(40)
+    pf = P._Prefetcher(pipe, 3)
+    try:
+        assert _drain(pf) == list(range(40))
+        assert pf.finished
+    finally:
+        pf.close()
+    assert pipe.pull_threads == {"dino-pull"} and pipe.pack_threads == {"dino-prefetch"}
+    assert sorted(pipe.staged) == list(range(40))
+
+
+def test_spans_sources_keep_one_thread():
+    pipe = _FakePipe(10, spans=True)
+    pf = P._Prefetcher(pipe, 2)
+    try:
+        assert _drain(pf) == list(range(10))
+    finally:
+        pf.close()
+    assert pipe.pull_threads == {"dino-prefetch"} == pipe.pack_threads
+
+
+def test_source_error_reaches_the_launch_thread_after_the_batches_before_it():
+    pipe = _FakePipe(20, fail_at=7)
+    pf = P._Prefetcher(pipe, 2)
+    try:
+        got = [pf.get().k for _ in range(7)]
+        assert got == list(range(7))
+        with pytest.raises(ValueError, match="source broke"):
+            pf.get()
+    finally:
+        pf.close()
+
+
+def test_close_drops_prepared_batches_never_handed_out():
+    pipe = _FakePipe(1000)
+    pf = P._Prefetcher(pipe, 4)
+    first = pf.get().k
+    time.sleep(0.05)  # let the queues fill
+    pf.close()
+    assert first == 0
+    # everything prepared after the first hand-out was either dropped or never made
+    assert set(pipe.dropped) <= set(range(1, 1000)) and len(pipe.dropped) >= 1
+    assert not pf._thread.is_alive() and not pf._puller.is_alive()
