@@ -2263,7 +2263,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int kIdctWgs = 32;  // workgroups per image (grid-stride over its blocks)
+#ifndef DINO_IDCT_WGS
+#define DINO_IDCT_WGS 32
+#endif
+constexpr int kIdctWgs = DINO_IDCT_WGS;  // workgroups per image (grid-stride over its blocks)
 
 // The steps of one 8-lane group's block (k_idct).  sb: the group's LDS block,
 // rows of 9 words, all zero on entry.
@@ -2473,7 +2476,10 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, uint32
   out[3] = odd ? o3 : e3;
 }
 
-constexpr int kColorWgs = 16;  // workgroups per image
+#ifndef DINO_COLOR_WGS
+#define DINO_COLOR_WGS 16
+#endif
+constexpr int kColorWgs = DINO_COLOR_WGS;  // workgroups per image
 constexpr int kColorBatch = 1;  // quads whose loads a lane issues together (measured: 4 and 8 slower)
 
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;

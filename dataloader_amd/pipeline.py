@@ -313,6 +313,7 @@ def release_role_streams() -> None:
 
 
 RAW_AHEAD = 2  # pulled, not yet packed batches the prefetcher's puller thread holds (list sources)
+PACK_THREADS = 2  # pack threads of a list source's prefetcher (DINO_PACK_THREADS)
 
 
 class _Prefetcher:
@@ -320,82 +321,124 @@ class _Prefetcher:
     pipeline.py:317 ``prefetch_queue_depth``): pull the next batch from the source, pack it
     into pinned staging (``dino_gather``), ``dino_probe`` it and submit its Pillow
     hand-overs, up to ``ahead`` batches ahead of the launches.  The GIL is released inside
-    the native calls, so this overlaps the launch thread and the GPU.  For a source that
-    hands over JPEG lists (the reference's ``_ReaderAdapter``) the pull runs on a thread of
-    its own, up to ``RAW_AHEAD`` batches ahead of the pack: the source's Python call and the
-    native pack overlap instead of adding up (c2_prog: ~0.8 + 1.2-3 ms per batch)."""
+    the native calls, so this overlaps the launch thread and the GPU.
+
+    For a source that hands over JPEG lists (the reference's ``_ReaderAdapter``) the pull
+    runs on a thread of its own, up to ``RAW_AHEAD`` batches ahead, and ``PACK_THREADS``
+    threads pack the pulled batches concurrently: the source's Python call and the native
+    packs overlap instead of adding up (c2_prog: ~0.8 ms pull + 1.2-3 ms pack per batch).
+    Batches are handed out in the source's order (sequence numbers, a reorder buffer of at
+    most ``ahead`` batches); the source's end and its errors arrive in place."""
 
     def __init__(self, pipe: "MI355XAugPipeline", ahead: int):
         self._pipe = pipe
-        self._q: queue.Queue = queue.Queue(maxsize=max(1, ahead))
+        self._ahead = max(1, ahead)
         self._stop = threading.Event()
         self.finished = False       # the source raised StopIteration (the END marker is queued)
+        self._cv = threading.Condition()
+        self._out: dict = {}        # sequence number -> _Prepared, _END or an exception
+        self._next = 0              # sequence number get() hands out next
         self._raw: queue.Queue | None = None
-        self._puller = None
+        self._threads: list[threading.Thread] = []
         if not pipe._spans_feed and not pipe._native:
             self._raw = queue.Queue(maxsize=RAW_AHEAD)
-            self._puller = threading.Thread(target=self._pull_loop, name="dino-pull", daemon=True)
-            self._puller.start()
-        self._thread = threading.Thread(target=self._run, name="dino-prefetch", daemon=True)
-        self._thread.start()
+            n = max(1, int(os.environ.get("DINO_PACK_THREADS", PACK_THREADS)))
+            self._threads.append(threading.Thread(target=self._pull_loop, name="dino-pull", daemon=True))
+            self._threads += [threading.Thread(target=self._pack_loop, name=f"dino-prefetch-{k}", daemon=True)
+                              for k in range(n)]
+        else:
+            self._threads.append(threading.Thread(target=self._run, name="dino-prefetch", daemon=True))
+        for t in self._threads:
+            t.start()
 
-    def _put(self, item, q: queue.Queue | None = None) -> bool:
-        q = self._q if q is None else q
+    # ---- producers
+    def _emit(self, seq: int, item) -> bool:
+        """Place item `seq` in the reorder buffer once it is within `ahead` of the next hand-out."""
+        with self._cv:
+            while seq - self._next >= self._ahead and not self._stop.is_set():
+                self._cv.wait(0.1)
+            if self._stop.is_set():
+                return False
+            self._out[seq] = item
+            self._cv.notify_all()
+            return True
+
+    def _settle(self, seq: int, item) -> bool:
+        """Emit a prepared batch, or drop it if the prefetcher is closing."""
+        if isinstance(item, _Prepared) and not self._emit(seq, item):
+            self._pipe._drop(item)
+            return False
+        return isinstance(item, _Prepared) or self._emit(seq, item)
+
+    def _run(self) -> None:  # one thread pulls and packs (spans / native sources)
+        seq = 0
+        try:
+            while not self._stop.is_set():
+                pb = self._pipe._prepare_next()
+                self._pipe._stage_early(pb)
+                if not self._settle(seq, pb):
+                    return
+                seq += 1
+        except StopIteration:
+            self.finished = True
+            self._emit(seq, _END)
+        except BaseException as e:  # noqa: BLE001 - handed to the launch thread
+            self._emit(seq, e)
+
+    def _put_raw(self, item) -> bool:
         while not self._stop.is_set():
             try:
-                q.put(item, timeout=0.1)
+                self._raw.put(item, timeout=0.1)
                 return True
             except queue.Full:
                 continue
         return False
 
     def _pull_loop(self) -> None:
+        seq = 0
         try:
             while not self._stop.is_set():
-                if not self._put(self._pipe._pull_raw(), self._raw):
+                if not self._put_raw((seq, self._pipe._pull_raw())):
                     return
+                seq += 1
         except StopIteration:
-            self._put(_END, self._raw)
-        except BaseException as e:  # noqa: BLE001 - handed to the pack thread, then the launch thread
-            self._put(e, self._raw)
+            self._put_raw((seq, _END))
+        except BaseException as e:  # noqa: BLE001 - handed to a pack thread, then the launch thread
+            self._put_raw((seq, e))
 
-    def _next(self) -> _Prepared | None:
-        """The next prepared batch (None once stopped); StopIteration at the source's end."""
-        if self._raw is None:
-            return self._pipe._prepare_next()
+    def _pack_loop(self) -> None:
         while not self._stop.is_set():
             try:
-                item = self._raw.get(timeout=0.1)
+                seq, raw = self._raw.get(timeout=0.1)
             except queue.Empty:
                 continue
-            if item is _END:
-                raise StopIteration
-            if isinstance(item, BaseException):
-                raise item
-            return self._pipe._pack_raw(item)
-        return None
-
-    def _run(self) -> None:
-        try:
-            while not self._stop.is_set():
-                pb = self._next()
-                if pb is None:
-                    return
+            if raw is _END or isinstance(raw, BaseException):
+                if raw is _END:
+                    self.finished = True
+                self._put_raw((seq, raw))  # the other pack threads see the end too
+                self._emit(seq, raw)
+                return
+            try:
+                pb = self._pipe._pack_raw(raw)
                 self._pipe._stage_early(pb)
-                if not self._put(pb):
-                    self._pipe._drop(pb)
-                    return
-        except StopIteration:
-            self.finished = True
-            self._put(_END)
-        except BaseException as e:  # noqa: BLE001 - handed to the launch thread
-            self._put(e)
+            except BaseException as e:  # noqa: BLE001 - handed to the launch thread in place
+                self._emit(seq, e)
+                continue
+            if not self._settle(seq, pb):
+                return
 
+    # ---- consumer
     def get(self, block: bool = True) -> _Prepared | None:
-        try:
-            item = self._q.get(block=block)
-        except queue.Empty:
-            return None
+        with self._cv:
+            while self._next not in self._out:
+                if not block or self._stop.is_set():
+                    return None
+                self._cv.wait(0.1)
+            item = self._out[self._next]
+            if item is not _END and not isinstance(item, BaseException):
+                del self._out[self._next]
+                self._next += 1
+                self._cv.notify_all()
         if item is _END:
             raise StopIteration
         if isinstance(item, BaseException):
@@ -404,17 +447,20 @@ class _Prefetcher:
 
     def close(self) -> None:
         self._stop.set()
-        for q in (self._q, self._raw):  # unblock pending puts, free staging of batches never launched
-            while q is not None:
-                try:
-                    item = q.get_nowait()
-                except queue.Empty:
-                    break
-                if isinstance(item, _Prepared):
-                    self._pipe._drop(item)
-        self._thread.join(timeout=5.0)
-        if self._puller is not None:
-            self._puller.join(timeout=5.0)
+        with self._cv:
+            self._cv.notify_all()
+        for t in self._threads:
+            t.join(timeout=5.0)
+        with self._cv:  # free staging of batches never launched
+            items, self._out = list(self._out.values()), {}
+        for item in items:
+            if isinstance(item, _Prepared):
+                self._pipe._drop(item)
+        while self._raw is not None:
+            try:
+                self._raw.get_nowait()
+            except queue.Empty:
+                break
 
 
 SIDE_URGENT_SHORT = 8  # side look-ahead batches flushed at once while the look-ahead is short (_pull_side)
@@ -480,7 +526,9 @@ class MI355XAugPipeline:
             self.prefetch_ahead = max(1, self.prefetch_ahead)
         self._prefetcher: _Prefetcher | None = None
         # the side look-ahead holds its batches in HBM (``_stage_on_device``), not in staging
-        self._ring = _StagingRing(self.depth + self.prefetch_ahead + (4 if self._side_ahead else 0) + 2)
+        # (+ PACK_THREADS: a pack thread holds a buffer while the batch the launch waits for is
+        # still being packed by another)
+        self._ring = _StagingRing(self.depth + self.prefetch_ahead + (4 if self._side_ahead else 0) + 2 + PACK_THREADS)
         # copier threads of the host half's pack (dino_gather_probe): the source's own count
         # (the native feeds) or DINO_GATHER_THREADS (default 8)
         self._gather_threads = int(getattr(source, "nthreads", 0) or os.environ.get("DINO_GATHER_THREADS", 8))
@@ -543,11 +591,12 @@ class MI355XAugPipeline:
     @staticmethod
     def pulled_bound(depth: int, prefetch_ahead: int, side_ahead: int) -> int:
         """Most batches pulled from the source and not yet handed over, on the side route: the
-        look-ahead, the prefetch queue, one being packed on the prefetch thread, the puller's
-        queue and the batch it holds, and the batches in flight.  A source whose metadata FIFO
+        look-ahead, the prefetch queue, the batches being packed (one per pack thread), the
+        puller's queue and the batch it holds, and the batches in flight.  A source whose metadata FIFO
         pairs each pulled batch with its hand-over (reference _ReaderAdapter._meta_queue,
         shard_reader.py:98, 357-375) must hold this many."""
-        return side_ahead + MI355XAugPipeline.side_queue(prefetch_ahead, side_ahead) + 1 + RAW_AHEAD + 1 + depth
+        return (side_ahead + MI355XAugPipeline.side_queue(prefetch_ahead, side_ahead) + PACK_THREADS + RAW_AHEAD + 1 +
+                depth)
 
     @property
     def engine(self) -> IngestEngine:

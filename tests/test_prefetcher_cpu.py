@@ -1,10 +1,12 @@
 """The pipeline's host-half prefetcher (pipeline._Prefetcher) on CPU: with a list source its
-pull runs on a thread of its own ahead of the pack (round 6); batches still come out in the
-source's order, the source's end and its errors reach the launch thread in place, and close()
-frees every prepared batch that was never handed out."""
+pull runs on a thread of its own and PACK_THREADS threads pack concurrently (round 6);
+batches still come out in the source's order, the source's end and its errors (pull or
+pack) reach the launch thread in place, and close() frees every prepared batch that was
+never handed out."""
 
 from __future__ import annotations
 
+import random
 import threading
 import time
 
@@ -16,8 +18,10 @@ from dataloader_amd import pipeline as P
 class _FakePipe:
     """What _Prefetcher calls on its pipeline: _pull_raw, _pack_raw, _stage_early, _drop."""
 
-    def __init__(self, n: int, fail_at: int | None = None, spans: bool = False):
+    def __init__(self, n: int, fail_at: int | None = None, spans: bool = False, pack_fail_at: int | None = None):
         self._spans_feed = spans
+        self.pack_fail_at = pack_fail_at
+        self.rng = random.Random(7)
         self._native = False
         self.n, self.fail_at = n, fail_at
         self.k = 0
@@ -38,7 +42,9 @@ class _FakePipe:
 
     def _pack_raw(self, raw):
         self.pack_threads.add(threading.current_thread().name)
-        time.sleep(0.002)
+        time.sleep(0.004 * self.rng.random())  # uneven packs: batches finish out of order
+        if raw == self.pack_fail_at:
+            raise RuntimeError("pack broke")
         pb = P._Prepared(None, None, None, None, 0, 0, (0, 0), {})
         pb.k = raw
         return pb
@@ -72,7 +78,8 @@ def test_list_source_pull_runs_on_its_own_thread_in_order():
         assert pf.finished
     finally:
         pf.close()
-    assert pipe.pull_threads == {"dino-pull"} and pipe.pack_threads == {"dino-prefetch"}
+    assert pipe.pull_threads == {"dino-pull"}
+    assert pipe.pack_threads == {f"dino-prefetch-{k}" for k in range(P.PACK_THREADS)}
     assert sorted(pipe.staged) == list(range(40))
 
 
@@ -107,4 +114,15 @@ def test_close_drops_prepared_batches_never_handed_out():
     assert first == 0
     # everything prepared after the first hand-out was either dropped or never made
     assert set(pipe.dropped) <= set(range(1, 1000)) and len(pipe.dropped) >= 1
-    assert not pf._thread.is_alive() and not pf._puller.is_alive()
+    assert not any(t.is_alive() for t in pf._threads)
+
+
+def test_pack_error_arrives_in_place():
+    pipe = _FakePipe(30, pack_fail_at=11)
+    pf = P._Prefetcher(pipe, 3)
+    try:
+        assert [pf.get().k for _ in range(11)] == list(range(11))
+        with pytest.raises(RuntimeError, match="pack broke"):
+            pf.get()
+    finally:
+        pf.close()
