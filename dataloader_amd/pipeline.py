@@ -313,7 +313,9 @@ def release_role_streams() -> None:
 
 
 RAW_AHEAD = 2  # pulled, not yet packed batches the prefetcher's puller thread holds (list sources)
-PACK_THREADS = 2  # pack threads of a list source's prefetcher (DINO_PACK_THREADS)
+# pack threads of a list source's prefetcher (DINO_PACK_THREADS): two measured no faster than
+# one on c2_prog (the packs then contend for the job's CPU share, profiles/r06_side_plan/r6x)
+PACK_THREADS = 1
 
 
 class _Prefetcher:
@@ -325,8 +327,8 @@ class _Prefetcher:
 
     For a source that hands over JPEG lists (the reference's ``_ReaderAdapter``) the pull
     runs on a thread of its own, up to ``RAW_AHEAD`` batches ahead, and ``PACK_THREADS``
-    threads pack the pulled batches concurrently: the source's Python call and the native
-    packs overlap instead of adding up (c2_prog: ~0.8 ms pull + 1.2-3 ms pack per batch).
+    threads pack the pulled batches: the source's Python call and the native pack overlap
+    instead of adding up (c2_prog: ~0.8 ms pull + 1.2-3 ms pack per batch).
     Batches are handed out in the source's order (sequence numbers, a reorder buffer of at
     most ``ahead`` batches); the source's end and its errors arrive in place."""
 

@@ -208,16 +208,16 @@ def test_backend_side_look_ahead_fits_the_metadata_fifo():
     # the batches being packed (PACK_THREADS) + the puller's queue (RAW_AHEAD) and the batch it
     # holds + the batches in flight; one FIFO entry stays spare
     from dataloader_amd.pipeline import PACK_THREADS, RAW_AHEAD
-    assert RAW_AHEAD == 2 and PACK_THREADS == 2
-    assert MI355XAugPipeline.pulled_bound(3, 1, 48) == 48 + 5 + 2 + 3 + 3
+    assert RAW_AHEAD == 2 and PACK_THREADS == 1
+    assert MI355XAugPipeline.pulled_bound(3, 1, 48) == 48 + 5 + 1 + 3 + 3
     assert be.SIDE_AHEAD == 256
-    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7 - 4
+    assert be.side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7 - 3
     assert be.side_look_ahead(PipelineConfig(), object(), 3) == 256
-    assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 7 - 4
-    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), Src(64), 3) == 64 - 3 - 7 - 4
+    assert be.side_look_ahead(PipelineConfig(), Src(20), 3) == 20 - 3 - 7 - 3
+    assert be.side_look_ahead(PipelineConfig(cpu_queue=60), Src(64), 3) == 64 - 3 - 7 - 3
     assert be.side_look_ahead(PipelineConfig(cpu_queue=300), object(), 3) == 300
     assert MI355XBackend(side_ahead=8).side_look_ahead(PipelineConfig(), Src(64), 3) == 8
-    assert MI355XBackend(side_ahead=80).side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7 - 4
+    assert MI355XBackend(side_ahead=80).side_look_ahead(PipelineConfig(), Src(64), 3) == 64 - 3 - 7 - 3
     for cap in (12, 20, 64):
         for depth in (1, 3, 6):
             for cq in (1, 16, 60, 200):

@@ -70,7 +70,9 @@ def _drain(pf):
             return got
 
 
-def test_list_source_pull_runs_on_its_own_thread_in_order():
+@pytest.mark.parametrize("packers", [1, 2, 3])
+def test_list_source_pull_runs_on_its_own_thread_in_order(packers, monkeypatch):
+    monkeypatch.setenv("DINO_PACK_THREADS", str(packers))
     pipe = _FakePipe(40)
     pf = P._Prefetcher(pipe, 3)
     try:
@@ -79,7 +81,7 @@ def test_list_source_pull_runs_on_its_own_thread_in_order():
     finally:
         pf.close()
     assert pipe.pull_threads == {"dino-pull"}
-    assert pipe.pack_threads == {f"dino-prefetch-{k}" for k in range(P.PACK_THREADS)}
+    assert pipe.pack_threads <= {f"dino-prefetch-{k}" for k in range(packers)} and pipe.pack_threads
     assert sorted(pipe.staged) == list(range(40))
 
 
@@ -93,7 +95,9 @@ def test_spans_sources_keep_one_thread():
     assert pipe.pull_threads == {"dino-prefetch"} == pipe.pack_threads
 
 
-def test_source_error_reaches_the_launch_thread_after_the_batches_before_it():
+@pytest.mark.parametrize("packers", [1, 2])
+def test_source_error_reaches_the_launch_thread_after_the_batches_before_it(packers, monkeypatch):
+    monkeypatch.setenv("DINO_PACK_THREADS", str(packers))
     pipe = _FakePipe(20, fail_at=7)
     pf = P._Prefetcher(pipe, 2)
     try:
@@ -105,7 +109,9 @@ def test_source_error_reaches_the_launch_thread_after_the_batches_before_it():
         pf.close()
 
 
-def test_close_drops_prepared_batches_never_handed_out():
+@pytest.mark.parametrize("packers", [1, 2])
+def test_close_drops_prepared_batches_never_handed_out(packers, monkeypatch):
+    monkeypatch.setenv("DINO_PACK_THREADS", str(packers))
     pipe = _FakePipe(1000)
     pf = P._Prefetcher(pipe, 4)
     first = pf.get().k
@@ -117,7 +123,9 @@ def test_close_drops_prepared_batches_never_handed_out():
     assert not any(t.is_alive() for t in pf._threads)
 
 
-def test_pack_error_arrives_in_place():
+@pytest.mark.parametrize("packers", [1, 2])
+def test_pack_error_arrives_in_place(packers, monkeypatch):
+    monkeypatch.setenv("DINO_PACK_THREADS", str(packers))
     pipe = _FakePipe(30, pack_fail_at=11)
     pf = P._Prefetcher(pipe, 3)
     try:
