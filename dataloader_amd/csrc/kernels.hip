@@ -3020,7 +3020,10 @@ __device__ __forceinline__ void hresize_item(const ImgDesc* __restrict__ desc, c
                                              const ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int nc, int c,
                                              const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws, uint8_t* smem);
 
-__global__ void __launch_bounds__(256) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
+#ifndef DINO_HRESIZE_WAVES  // (A/B: minimum waves per SIMD the register allocation must allow)
+#define DINO_HRESIZE_WAVES 1
+#endif
+__global__ void __launch_bounds__(256, DINO_HRESIZE_WAVES) k_hresize(const ImgDesc* __restrict__ desc, const dino_view_params* __restrict__ prm,
                                                  ViewPlan* __restrict__ plan, int nv, int v0, int nvc, int B,
                                                  const uint8_t* __restrict__ ws, uint8_t* __restrict__ aws) {
   main_prio();
