@@ -521,7 +521,12 @@ def summarize(leg: dict, ab: dict, B: int, steps: int, world: int, tag: str) -> 
                           "per step over the mean launch time (the same ratio). path_frac: the whole timed step "
                           "against the same bytes. traffic: PMC HBM bytes per launch (rocprofv3, "
                           "traffic_source); traffic_over_interface: that over the kernel's own interface bytes",
-            "traffic_source": f"profiles/{traffic_src}" if traffic_src else None}
+            "traffic_source": f"profiles/{traffic_src}" if traffic_src else None,
+            "ceiling_note": "SURVEY 8(d): the algorithmic bytes (JPEG in + views out, ~1.1 MB per C2 image) "
+                            "put the whole path at ~1-3 % of HBM even at ~200k img/s; it is bound by serial "
+                            "entropy decode and per-pixel integer work, so a 70 % HBM-roofline target is out "
+                            "of reach by this definition (SURVEY 8(d) 'Honest expectation'). frac and "
+                            "path_frac are reported as measured, not rescaled"}
         roof_all = {}
         for k, v in per_kernel.items():
             if ab.get(k) and v["avg_ms"] > 0:
