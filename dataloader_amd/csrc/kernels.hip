@@ -2281,7 +2281,10 @@ __device__ __forceinline__ void idct_group_dense(int32_t* sb, int l, const uint8
 // l, l + 8, .. (kIdctPre of them) already loaded into pre[]; halfword entries
 // (zigzag | int10 value << 6), then u32 entries from the next even halfword (see
 // SparseSink); the DC is int16 (absolute after k_dcscan).
-constexpr int kIdctPre = 4;  // halfword entries per lane loaded a block ahead (8 lanes: 8 kIdctPre)
+#ifndef DINO_IDCT_PRE
+#define DINO_IDCT_PRE 4
+#endif
+constexpr int kIdctPre = DINO_IDCT_PRE;  // halfword entries per lane loaded a block ahead (8 lanes: 8 kIdctPre)
 __device__ __forceinline__ void idct_load_pre(uint32_t* pre, int l, uint2 bi, const uint16_t* ent16) {
   const uint32_t c = bi.y & 0x7Fu;
 #pragma unroll
@@ -2480,7 +2483,10 @@ __device__ __forceinline__ void h2v2_quad(uint32_t n, uint32_t f, int x0, uint32
 #define DINO_COLOR_WGS 16
 #endif
 constexpr int kColorWgs = DINO_COLOR_WGS;  // workgroups per image
-constexpr int kColorBatch = 1;  // quads whose loads a lane issues together (measured: 4 and 8 slower)
+#ifndef DINO_COLOR_BATCH
+#define DINO_COLOR_BATCH 1
+#endif
+constexpr int kColorBatch = DINO_COLOR_BATCH;  // quads whose loads a lane issues together (measured: 4 and 8 slower)
 
 // Four consecutive pixels per lane (12 output bytes = three aligned dword stores;
 // the RGB area is padded by 16 bytes, so the last partial quad may store whole words).
