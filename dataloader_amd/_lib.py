@@ -20,6 +20,7 @@ IMG_STATUS = {0: "ok", -1: "corrupt", -2: "truncated", -3: "bad-data", -4: "too-
               1: "unsupported", 2: "multi-scan", 3: "no-space", 4: "over max_image_dim (handed to Pillow)"}
 ABI_VERSION = 4
 RAW_MAGIC = 0x42475244  # "DRGB": pre-decoded RGB container (include/dino_ingest.h)
+COPY_HEADER = 1  # dino_copy_rgb_packed flags: write the container header in front of each image
 
 _lib = None
 FEED_END, FEED_TIMEOUT, FEED_SHARD_ERROR = 1, 2, 3
@@ -81,7 +82,7 @@ def load() -> ctypes.CDLL:
         "dino_stream_create": (i32, [i32, i32, ctypes.POINTER(vp)]),
         "dino_stream_destroy": (i32, [vp]),
         "dino_copy_rgb": (i32, [vp, i32, vp, vp]),
-        "dino_copy_rgb_packed": (i32, [vp, i32, vp, vp, vp, vp]),
+        "dino_copy_rgb_packed": (i32, [vp, i32, vp, vp, vp, i32, vp]),
         "dino_pixel_ops_all": (i32, [i32, i32, vp, vp]),
         "dino_sample_params": (i32, [vp, ctypes.POINTER(DinoAugConfig), u64, u64, vp, vp]),
         "dino_augment": (i32, [vp, ctypes.POINTER(DinoAugConfig), vp, ctypes.POINTER(vp), vp]),

@@ -166,12 +166,12 @@ int dino_copy_rgb(dino_ctx* c, int32_t index, uint8_t* d_rgb, void* stream) {
 }
 
 int dino_copy_rgb_packed(dino_ctx* c, int32_t n, const int32_t* d_index, const int64_t* d_offset, uint8_t* d_base,
-                         void* stream) {
-  if (!c || n < 0 || (n > 0 && (!d_index || !d_offset || !d_base)))
+                         int32_t flags, void* stream) {
+  if (!c || n < 0 || (n > 0 && (!d_index || !d_offset)) || (flags & ~DINO_COPY_HEADER))
     return fail(DINO_EINVAL, "dino_copy_rgb_packed: bad arguments%s%lld");
   if (n > 65535) return fail(DINO_EINVAL, "dino_copy_rgb_packed: n %s%lld > 65535", "", (long long)n);
   hipError_t e = launch_copy_rgb_packed(c->d_desc, c->last_batch, n, d_index, d_offset, c->d_ws, d_base,
-                                        (hipStream_t)stream);
+                                        (flags & DINO_COPY_HEADER) != 0, (hipStream_t)stream);
   return e == hipSuccess ? DINO_OK : hip_fail(e, "dino_copy_rgb_packed");
 }
 

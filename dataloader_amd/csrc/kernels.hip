@@ -4047,20 +4047,27 @@ __global__ void k_copy_rgb(const ImgDesc* __restrict__ desc, int idx, const uint
     dst[i] = ws[d.rgb_off + i];
 }
 
-// Decoded images -> slices of one buffer (the side decoder's raw containers): image idx[k]'s
-// RGB to base + off[k], grid (x, n).  16-byte copies when source and destination are both
-// 16-byte aligned (the workspace's RGB areas are; the containers' data starts 16 bytes into a
-// 16-byte aligned slice), the tail and unaligned cases bytewise.
+// Decoded images -> raw containers (the side decoder): image idx[k]'s RGB to base + off[k]
+// (base null: off[k] is the destination's device address), grid (x, n).  16-byte copies when
+// source and destination are both 16-byte aligned (the workspace's RGB areas are; the
+// containers' data starts 16 bytes into a 16-byte aligned slice), the tail and unaligned
+// cases bytewise.  With `header`, the 16 bytes before the data get the container header
+// {DINO_RAW_MAGIC, width, height, 0} (little-endian words).
 __global__ void k_copy_rgb_packed(const ImgDesc* __restrict__ desc, int B, const int32_t* __restrict__ idx,
                                   const int64_t* __restrict__ off, const uint8_t* __restrict__ ws,
-                                  uint8_t* __restrict__ base) {
+                                  uint8_t* __restrict__ base, int header) {
   const int k = blockIdx.y, i = idx[k];
   if (i < 0 || i >= B) return;
   const ImgDesc& d = desc[i];
   if (d.status != DINO_IMG_OK) return;
   const int64_t n = (int64_t)d.width * d.height * 3;
   const uint8_t* src = ws + d.rgb_off;
-  uint8_t* dst = base + off[k];
+  uint8_t* dst = base ? base + off[k] : reinterpret_cast<uint8_t*>(static_cast<uintptr_t>(off[k]));
+  if (header && blockIdx.x == 0 && threadIdx.x < 16) {
+    const uint32_t w[4] = {DINO_RAW_MAGIC, (uint32_t)d.width, (uint32_t)d.height, 0u};
+    const int j = threadIdx.x;
+    dst[j - 16] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+  }
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, ts = (int64_t)gridDim.x * blockDim.x;
   int64_t head = 0;
   if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
@@ -4341,9 +4348,9 @@ hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint
 }
 
 hipError_t launch_copy_rgb_packed(const ImgDesc* desc, int B, int n, const int32_t* idx, const int64_t* off,
-                                  const uint8_t* ws, uint8_t* base, hipStream_t s) {
+                                  const uint8_t* ws, uint8_t* base, int header, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  k_copy_rgb_packed<<<dim3(16, n), 256, 0, s>>>(desc, B, idx, off, ws, base);
+  k_copy_rgb_packed<<<dim3(16, n), 256, 0, s>>>(desc, B, idx, off, ws, base, header);
   return hipGetLastError();
 }
 

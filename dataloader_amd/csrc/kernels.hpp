@@ -135,7 +135,7 @@ hipError_t launch_augment(const AugmentArgs& a, hipStream_t s, KernelTimer* tm =
 hipError_t launch_info(const ImgDesc* desc, int batch, int32_t* info, hipStream_t s);
 hipError_t launch_copy_rgb(const ImgDesc* desc, int idx, const uint8_t* ws, uint8_t* dst, hipStream_t s);
 hipError_t launch_copy_rgb_packed(const ImgDesc* desc, int B, int n, const int32_t* idx, const int64_t* off,
-                                  const uint8_t* ws, uint8_t* base, hipStream_t s);
+                                  const uint8_t* ws, uint8_t* base, int header, hipStream_t s);
 hipError_t launch_pixel_ops(int op, int param, uint8_t* out, hipStream_t s);
 hipError_t launch_masks(int H, int W, int target, int minp, int maxp, double la0, double la1, int n, uint32_t* py,
                         uint32_t* np, uint8_t* out, hipStream_t s);

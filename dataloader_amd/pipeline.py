@@ -184,6 +184,7 @@ class _Prepared:
         self.spans = spans            # tario.BatchSpans: the batch stays in its page-locked shard ranges
         self.feed = feed              # tario.FeedBatch: the batch is packed in a native feed slot
         self.side = None              # progside.SideJob: its coefficient-buffer images, decoded ahead
+        self.room: dict = {}          # batch index -> offset of room for its container in the HBM copy
         self.side_submitted = False   # _side_submit ran (on the prefetch thread, or at the pull)
         self.jpegs = jpegs            # the source's list (None for the native feed)
         self.offsets = offsets
@@ -885,7 +886,10 @@ class MI355XAugPipeline:
         else:
             hb, o = pb.staging.buf.numpy(), pb.offsets
             imgs = {int(i): hb[o[i]:o[i + 1]].tobytes() for i in idx}
-        pb.side = self._side.add(imgs)
+        room = {}
+        if pb.dev is not None and pb.room:
+            room = {i: (pb.dev[0], pb.room[i]) for i in imgs if i in pb.room}
+        pb.side = self._side.add(imgs, room, pb.copied if room else None)
 
     def _stage_early(self, pb: _Prepared) -> None:
         """On the prefetch thread: a batch bound for the side look-ahead (the route is engaged,
@@ -936,7 +940,16 @@ class MI355XAugPipeline:
             else:
                 st = pb.staging
                 nbytes = int(pb.offsets[-1])
-                d_bytes = st.buf[:max(nbytes, 1)].to(self.device, non_blocking=True)
+                # room after the batch's bytes for the raw containers of its coefficient-buffer
+                # images: the side decoder writes them there, so the launch needs no merge copy
+                from . import progside
+                pos = (nbytes + 15) & ~15
+                for i in np.flatnonzero(progside.side_mask(pb.info)):
+                    if int(i) not in pb.futures:
+                        pb.room[int(i)] = pos
+                        pos += (16 + int(pb.info[i, 1]) * int(pb.info[i, 2]) * 3 + 15) & ~15
+                d_bytes = torch.empty(max(pos, 1) + 64, dtype=torch.uint8, device=self.device)
+                d_bytes[:max(nbytes, 1)].copy_(st.buf[:max(nbytes, 1)], non_blocking=True)
                 d_off = st.off[: B + 1].to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(cs)
@@ -1224,6 +1237,17 @@ class MI355XAugPipeline:
         off = np.asarray(base_off, np.int64)[: B + 1].copy()
         lens = np.asarray(base_lens, np.int64)[:B].copy()
         rawm = raw.cpu().numpy().astype(np.uint8) if raw is not None else np.zeros(B, np.uint8)
+        base, cap = d_bytes.data_ptr(), d_bytes.numel()
+        if all(base <= c.data_ptr() and c.data_ptr() + c.numel() <= base + cap for c in conts.values()):
+            # every container was written into the room after the batch's bytes: no copy
+            for i, c in conts.items():
+                off[i], lens[i], rawm[i] = c.data_ptr() - base, int(c.numel()), 1
+            off[B] = cap
+            h_off = torch.from_numpy(off).pin_memory()
+            h_len = torch.from_numpy(lens.astype(np.int64)).pin_memory()
+            h_raw = torch.from_numpy(rawm).pin_memory()
+            return (d_bytes, h_off.to(self.device, non_blocking=True), h_len.to(self.device, non_blocking=True),
+                    h_raw.to(self.device, non_blocking=True))
         pos = (nbytes + 15) & ~15
         total = pos + sum((int(c.numel()) + 15) & ~15 for c in conts.values())
         merged = torch.empty(total + 64, dtype=torch.uint8, device=self.device)

@@ -41,9 +41,11 @@ class SideJob:
     ``event`` (None until the pool holding its images is launched)."""
 
     __slots__ = ("containers", "event", "status", "rows", "pending", "launched", "error", "t_add", "t_launch",
-                 "owner")
+                 "owner", "room", "room_ready")
 
-    def __init__(self):
+    def __init__(self, room: dict | None = None, room_ready: torch.cuda.Event | None = None):
+        self.room = room or {}                    # batch index -> (device buffer, offset): where its
+        self.room_ready = room_ready              # container goes in the batch's own input buffer
         self.containers: dict = {}
         self.event: torch.cuda.Event | None = None
         self.status: torch.Tensor | None = None   # pinned int32[n][4] of the mini-batch
@@ -234,10 +236,13 @@ class DeviceSideDecoder:
         if getattr(self, "_parts", None) is not None:
             self._parts.put(None)
 
-    def add(self, imgs: dict) -> SideJob | None:
+    def add(self, imgs: dict, room: dict | None = None, room_ready=None) -> SideJob | None:
+        """Queue a batch's images (batch index -> JPEG bytes).  ``room``: batch index -> (device
+        tensor, offset) of space reserved for the image's container in the batch's own input
+        buffer, usable once ``room_ready`` has completed; the others get containers of their own."""
         if not imgs:
             return None
-        job = SideJob()
+        job = SideJob(room, room_ready)
         job.owner = self
         with self._lock:
             for i in sorted(imgs):
@@ -323,26 +328,29 @@ class DeviceSideDecoder:
             d_bytes = hb[:max(total, 1) + 16].to(self.device, non_blocking=True)
             d_off = off.to(self.device, non_blocking=True)
             d_info = torch.empty((len(items), 4), dtype=torch.int32, device=self.device)
-            # every decoded image's container is a 16-byte aligned slice of one device buffer;
-            # the headers go over in one copy and one scatter (per-image pinned headers and
-            # copies cost the launch thread ~10 us each)
+            # every decoded image's container: the room reserved for it in its batch's input
+            # buffer when the batch has some (_stage_on_device), else a 16-byte aligned slice of
+            # one pool buffer; one dino_copy_rgb_packed launch writes all their headers and pixels
+            # at absolute addresses
             big = d_idx = d_dst = None
             if keep:
-                start = np.zeros(len(keep) + 1, np.int64)
-                start[1:] = np.cumsum([(16 + w * h * 3 + 15) & ~15 for _, _, _, w, h in keep])
-                big = torch.empty(int(start[-1]), dtype=torch.uint8, device=self.device)
-                hdr = np.zeros((len(keep), 4), np.uint32)
-                hdr[:, 0] = _lib.RAW_MAGIC
-                hdr[:, 1] = [w for _, _, _, w, _ in keep]
-                hdr[:, 2] = [h for _, _, _, _, h in keep]
-                h_hdr = torch.from_numpy(hdr.view(np.uint8).reshape(-1)).pin_memory()
-                h_pos = torch.from_numpy((start[:-1, None] + np.arange(16)).reshape(-1)).pin_memory()
-                # the pixel copies: one dino_copy_rgb_packed launch for the pool (mini-batch row k
-                # -> its container's data, 16 bytes past the header)
+                own = [(job, i) for _, job, i, _, _ in keep if i not in job.room]
+                sizes = {(id(job), i): (16 + w * h * 3 + 15) & ~15 for _, job, i, w, h in keep}
+                if own:
+                    big = torch.empty(sum(sizes[(id(j), i)] for j, i in own), dtype=torch.uint8, device=self.device)
+                dst, conts, o = [], [], 0
+                for k, job, i, w, h in keep:
+                    if i in job.room:
+                        buf, pos = job.room[i]
+                        c = buf[pos:pos + 16 + w * h * 3]
+                    else:
+                        c = big[o:o + 16 + w * h * 3]
+                        o += sizes[(id(job), i)]
+                    conts.append(c)
+                    dst.append(c.data_ptr() + 16)
                 h_idx = torch.from_numpy(np.array([k for k, _, _, _, _ in keep], np.int32)).pin_memory()
-                h_dst = torch.from_numpy(start[:-1] + 16).pin_memory()
-                heads.extend((h_hdr, h_pos, h_idx, h_dst))
-                big[h_pos.to(self.device, non_blocking=True)] = h_hdr.to(self.device, non_blocking=True)
+                h_dst = torch.from_numpy(np.array(dst, np.int64)).pin_memory()
+                heads.extend((h_idx, h_dst))
                 d_idx = h_idx.to(self.device, non_blocking=True)
                 d_dst = h_dst.to(self.device, non_blocking=True)
             # the library's kernels on the dedicated stream, after the inputs (and after any
@@ -354,13 +362,16 @@ class DeviceSideDecoder:
             t4 = time.perf_counter()
             ph["decode"] += t4 - t3
             if keep:
+                waited = set()
+                for _, job, i, _, _ in keep:  # the batches' input buffers hold their bytes (and are ours)
+                    if i in job.room and job.room_ready is not None and id(job) not in waited:
+                        es.wait_event(job.room_ready)
+                        waited.add(id(job))
                 _lib.check(eng.lib.dino_copy_rgb_packed(eng._ctx, len(keep), ctypes.c_void_p(d_idx.data_ptr()),
-                                                        ctypes.c_void_p(d_dst.data_ptr()),
-                                                        ctypes.c_void_p(big.data_ptr()), eng._s()),
-                           "dino_copy_rgb_packed")
-            for (k, job, i, w, h), o in zip(keep, start[:-1] if keep else []):
-                o = int(o)
-                job.containers[i] = big[o:o + 16 + w * h * 3]
+                                                        ctypes.c_void_p(d_dst.data_ptr()), None, _lib.COPY_HEADER,
+                                                        eng._s()), "dino_copy_rgb_packed")
+                for (k, job, i, w, h), c in zip(keep, conts):
+                    job.containers[i] = c
             # the status copy and the completion event on the decode's own stream: a torch stream
             # made to wait for the decode would hold its hardware queue (shared with other
             # streams, GPU_MAX_HW_QUEUES) for the whole decode -- the batches' H2D copies

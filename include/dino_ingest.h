@@ -177,10 +177,13 @@ int dino_copy_rgb(dino_ctx* ctx, int32_t index, uint8_t* d_rgb, void* stream);
 
 /* Copy n decoded images at once (round 6, the side decoder's raw containers): image
  * d_index[k] of the last call (device int32[n]) to d_base + d_offset[k] (device int64[n]),
- * one launch for the whole pool.  Images that did not decode, and indices outside the last
- * call's batch, are skipped.  n <= 65535. */
+ * one launch for the whole pool; with d_base NULL, d_offset[k] is the destination's device
+ * address.  flags DINO_COPY_HEADER: the 16 bytes before each destination get the raw
+ * container header {DINO_RAW_MAGIC, width, height, 0}.  Images that did not decode, and
+ * indices outside the last call's batch, are skipped.  n <= 65535. */
+#define DINO_COPY_HEADER 1
 int dino_copy_rgb_packed(dino_ctx* ctx, int32_t n, const int32_t* d_index, const int64_t* d_offset, uint8_t* d_base,
-                         void* stream);
+                         int32_t flags, void* stream);
 
 /* The per-pixel colour operators of the ColorJitter hue op over all 2^24 inputs
  * (index = a << 16 | b << 8 | c; d_out: 3 * 2^24 bytes, out[3 * index + k]): op 0 RGB -> HSV

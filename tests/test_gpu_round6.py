@@ -70,7 +70,7 @@ def _decode(dev, jpegs, lane: bool):
     d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     assert eng.lib.dino_copy_rgb_packed(eng._ctx, len(order), ctypes.c_void_p(d_idx.data_ptr()),
-                                        ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(big.data_ptr()),
+                                        ctypes.c_void_p(d_off.data_ptr()), ctypes.c_void_p(big.data_ptr()), 0,
                                         eng._s()) == 0
     torch.cuda.synchronize()
     hb_big = big.cpu().numpy()
@@ -78,6 +78,20 @@ def _decode(dev, jpegs, lane: bool):
         if st[i, 0] == 0:  # (an image that did not decode is skipped)
             assert np.array_equal(hb_big[offs[k]:offs[k] + sizes[i]], rgb[i].reshape(-1)), i
         assert (hb_big[offs[k] - 16 - (k & 1):offs[k]] == 0xA5).all(), i
+    # absolute destinations (null base) with the container header written in front
+    from dataloader_amd import _lib as L
+    big.fill_(0xA5)
+    d_abs = d_off + big.data_ptr()
+    torch.cuda.synchronize()
+    assert eng.lib.dino_copy_rgb_packed(eng._ctx, len(order), ctypes.c_void_p(d_idx.data_ptr()),
+                                        ctypes.c_void_p(d_abs.data_ptr()), None, L.COPY_HEADER, eng._s()) == 0
+    torch.cuda.synchronize()
+    hb_big = big.cpu().numpy()
+    for k, i in enumerate(order):
+        if st[i, 0] == 0:
+            assert np.array_equal(hb_big[offs[k]:offs[k] + sizes[i]], rgb[i].reshape(-1)), i
+            hdr = hb_big[offs[k] - 16:offs[k]].copy().view("<u4")
+            assert list(hdr) == [L.RAW_MAGIC, int(info[i, 1]), int(info[i, 2]), 0], (i, hdr)
     eng.close()
     return st, flags, rgb
 
