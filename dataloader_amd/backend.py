@@ -138,7 +138,8 @@ class MI355XBackend:
     # profiles/r06_side_plan/): 256 batches let the side decoder run the lane decoder on pools
     # of 4096 images (progside.side_plan), which costs the batches less GPU time per image:
     # c2_prog 72k -> 89-112k img/s.  The look-ahead's batches wait in HBM (~43 MB per C2
-    # batch: ~11 GB of the 288 at 256)
+    # batch, plus room for its progressive images' containers: ~19 GB of the 288 at 256 with 32
+    # progressive images per batch)
     SIDE_AHEAD = 256
     PREFETCH = 1  # host-half batches prepared ahead by the pipeline's prefetch thread
 
@@ -149,7 +150,8 @@ class MI355XBackend:
         so that everything pulled and not yet handed over (look-ahead + prefetch queue + batches
         in flight) fits the source's metadata FIFO (``_ReaderAdapter._meta_queue``, 64 slots,
         shard_reader.py:98, 357-375: an overflow raises).  The look-ahead's batches wait in HBM
-        (MI355XAugPipeline._stage_on_device): 256 C2 batches take ~11 GB of the 288."""
+        (MI355XAugPipeline._stage_on_device): 256 C2 batches with 32 progressive images each
+        take ~19 GB of the 288 (their bytes and their containers)."""
         want = self._side_ahead if self._side_ahead is not None else \
             max(int(os.environ.get("DINO_SIDE_AHEAD", self.SIDE_AHEAD)),
                 int(getattr(pipeline_cfg, "cpu_queue", 16) or 16))
